@@ -1,0 +1,219 @@
+"""Multi-replica / multi-rank process launcher for one MI355X node.
+
+Replaces what Vertex AI Training does for ``CustomTrainingJob.run(replica_count=3,
+accelerator_count=2, ...)`` (pytorch-pipeline.ipynb nb:181-188): start the user script on
+every replica with the rendezvous env contract task.py consumes — ``WORLD_SIZE``
+(replicas), ``RANK`` (replica index), ``MASTER_ADDR``, ``MASTER_PORT``, ``AIP_MODEL_DIR``
+(task.py:61, 80, 98, 141, 289) — and, in ``nproc_per_node`` mode, the torchrun contract
+(``RANK``/``LOCAL_RANK``/``WORLD_SIZE``/``LOCAL_WORLD_SIZE`` per GPU rank).
+
+MI355X specifics: each replica is pinned to a disjoint slice of the node's GPUs through
+``HIP_VISIBLE_DEVICES`` (one process per GPU is the RCCL/xGMI sweet spot);
+``HSA_ENABLE_IPC_MODE_LEGACY=0`` is forced so RCCL's dmabuf IPC works.
+
+Failure semantics: fail-fast — the first replica that exits non-zero causes
+every other replica's process group to get SIGTERM, then SIGKILL after a grace period; the
+launcher returns that first non-zero exit code.  An optional wall-clock ``timeout`` turns a
+hang into a failure (exit code 124).
+"""
+from __future__ import annotations
+
+import os
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+__all__ = ["LaunchSpec", "launch", "free_port", "visible_gpu_ids", "ReplicaResult"]
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def visible_gpu_ids() -> List[str]:
+    """GPU ids this launcher may hand out (honours an outer HIP/CUDA_VISIBLE_DEVICES)."""
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None and v.strip() != "":
+            return [x.strip() for x in v.split(",") if x.strip() != ""]
+    n = _count_gpus()
+    return [str(i) for i in range(n)]
+
+
+def _count_gpus() -> int:
+    n = os.environ.get("MIPIPE_NUM_GPUS")
+    if n is not None:
+        return int(n)
+    # Count render nodes of AMD GPUs without initialising HIP in this process.
+    try:
+        import glob
+        cnt = 0
+        for d in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+            with open(d) as f:
+                props = f.read()
+            if "simd_count" in props and "simd_count 0" not in props:
+                cnt += 1
+        return cnt
+    except Exception:
+        return 0
+
+
+@dataclass
+class LaunchSpec:
+    command: List[str]                      # e.g. [sys.executable, "task.py", "--dist-url=env://"]
+    replica_count: int = 1
+    accelerator_count: int = 0              # GPUs per replica
+    nproc_per_node: Optional[int] = None    # None: one process per replica (Vertex mode)
+    env: Dict[str, str] = field(default_factory=dict)
+    model_dir: Optional[str] = None         # AIP_MODEL_DIR
+    checkpoint_dir: Optional[str] = None
+    tensorboard_dir: Optional[str] = None
+    master_addr: str = "127.0.0.1"
+    master_port: Optional[int] = None
+    log_dir: Optional[str] = None
+    echo: bool = True
+    timeout: Optional[float] = None
+    grace_period: float = 10.0
+    cwd: Optional[str] = None
+
+
+@dataclass
+class ReplicaResult:
+    rank: int
+    returncode: Optional[int]
+    log_path: Optional[str]
+
+
+def _pump(proc: subprocess.Popen, prefix: str, log_path: Optional[str], echo: bool) -> None:
+    logf = open(log_path, "a") if log_path else None
+    try:
+        for line in proc.stdout:
+            if logf:
+                logf.write(line)
+                logf.flush()
+            if echo:
+                sys.stdout.write(f"{prefix}{line}")
+                sys.stdout.flush()
+    finally:
+        if logf:
+            logf.close()
+
+
+def _kill_group(p: subprocess.Popen, sig) -> None:
+    try:
+        os.killpg(p.pid, sig)
+    except (ProcessLookupError, PermissionError):
+        pass
+
+
+def build_envs(spec: LaunchSpec) -> List[Dict[str, str]]:
+    """Environment of every process the launch starts (exposed for tests)."""
+    gpus = visible_gpu_ids()
+    per_replica = spec.accelerator_count
+    nproc = spec.nproc_per_node
+    total_needed = spec.replica_count * per_replica
+    if per_replica and total_needed > len(gpus):
+        raise RuntimeError(f"job needs {spec.replica_count}x{per_replica}={total_needed} GPUs, "
+                           f"node exposes {len(gpus)} ({gpus})")
+    port = spec.master_port or free_port()
+    envs = []
+    procs_per_replica = nproc or 1
+    world = spec.replica_count * procs_per_replica
+    for r in range(spec.replica_count):
+        slice_ = gpus[r * per_replica:(r + 1) * per_replica] if per_replica else []
+        for lr in range(procs_per_replica):
+            e = dict(os.environ)
+            e.update(spec.env)
+            e["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+            e["MASTER_ADDR"] = spec.master_addr
+            e["MASTER_PORT"] = str(port)
+            if nproc:
+                e["WORLD_SIZE"] = str(world)
+                e["RANK"] = str(r * procs_per_replica + lr)
+                e["LOCAL_RANK"] = str(lr)
+                e["LOCAL_WORLD_SIZE"] = str(procs_per_replica)
+                e["GROUP_RANK"] = str(r)
+                dev = slice_[lr:lr + 1] if per_replica else []
+                if per_replica and not dev:
+                    raise RuntimeError(f"nproc_per_node={nproc} exceeds accelerator_count={per_replica}")
+                vis = ",".join(dev)
+            else:
+                e["WORLD_SIZE"] = str(spec.replica_count)
+                e["RANK"] = str(r)
+                vis = ",".join(slice_)
+            if per_replica:
+                e["HIP_VISIBLE_DEVICES"] = vis
+                e.pop("CUDA_VISIBLE_DEVICES", None)
+                e.pop("ROCR_VISIBLE_DEVICES", None)
+            else:
+                e["HIP_VISIBLE_DEVICES"] = ""
+                e["MIPIPE_FORCE_CPU"] = "1"
+            if spec.model_dir:
+                e["AIP_MODEL_DIR"] = spec.model_dir
+            if spec.checkpoint_dir:
+                e["AIP_CHECKPOINT_DIR"] = spec.checkpoint_dir
+            if spec.tensorboard_dir:
+                e["AIP_TENSORBOARD_LOG_DIR"] = spec.tensorboard_dir
+            e["CLUSTER_SPEC"] = (
+                '{"cluster": {"workerpool0": ["%s:%d"]}, "task": {"type": "workerpool0", "index": %d}}'
+                % (spec.master_addr, port, r))
+            envs.append(e)
+    return envs
+
+
+def launch(spec: LaunchSpec) -> int:
+    """Run the job; return 0 or the first failing process' exit code."""
+    envs = build_envs(spec)
+    if spec.log_dir:
+        os.makedirs(spec.log_dir, exist_ok=True)
+    procs: List[subprocess.Popen] = []
+    pumps: List[threading.Thread] = []
+    for i, e in enumerate(envs):
+        log_path = os.path.join(spec.log_dir, f"rank{i}.log") if spec.log_dir else None
+        p = subprocess.Popen(spec.command, env=e, cwd=spec.cwd, stdout=subprocess.PIPE,
+                             stderr=subprocess.STDOUT, text=True, bufsize=1,
+                             start_new_session=True)
+        procs.append(p)
+        th = threading.Thread(target=_pump, args=(p, f"[rank{i}] ", log_path, spec.echo),
+                              daemon=True)
+        th.start()
+        pumps.append(th)
+    t0 = time.time()
+    first_fail: Optional[int] = None
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad and first_fail is None:
+                first_fail = bad[0]
+                break
+            if all(c is not None for c in codes):
+                break
+            if spec.timeout is not None and time.time() - t0 > spec.timeout:
+                first_fail = 124
+                break
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        first_fail = 130
+    if first_fail is not None:
+        for p in procs:
+            if p.poll() is None:
+                _kill_group(p, signal.SIGTERM)
+        deadline = time.time() + spec.grace_period
+        while time.time() < deadline and any(p.poll() is None for p in procs):
+            time.sleep(0.05)
+        for p in procs:
+            if p.poll() is None:
+                _kill_group(p, signal.SIGKILL)
+        for p in procs:
+            p.wait()
+    for th in pumps:
+        th.join(timeout=5)
+    return 0 if first_fail is None else int(first_fail)

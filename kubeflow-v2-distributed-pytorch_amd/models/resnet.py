@@ -1,0 +1,189 @@
+"""ResNet family on mipipe's fused NHWC kernels, torchvision-compatible ``state_dict``.
+
+The reference builds ``torchvision.models.__dict__[arch]()`` (task.py:166-171; default
+``resnet18``, 1000-class head).  Parameter/buffer names and shapes here match torchvision's
+(``conv1.weight``, ``bn1.running_mean``, ``layer2.0.downsample.0.weight``, ``fc.bias`` ...)
+so checkpoints load either way.
+
+Execution is fused per conv: ``conv -> BN -> [+identity | +BN(downsample conv)] -> ReLU`` is
+one implicit-GEMM launch (BN statistics accumulated in its epilogue), a tiny finalize and one
+elementwise pass; the downsample branch is normalised inside the residual pass.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Type, Union
+
+import torch
+import torch.nn as tnn
+
+from mipipe import nn as mnn
+from mipipe.ops import kernels as K
+from mipipe.ops import functional as MF
+
+__all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50",
+           "resnet101", "resnet152", "wide_resnet50_2", "wide_resnet101_2"]
+
+
+def _conv3x3(cin, cout, stride=1):
+    return mnn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
+
+
+def _conv1x1(cin, cout, stride=1):
+    return mnn.Conv2d(cin, cout, 1, stride=stride, padding=0, bias=False)
+
+
+class BasicBlock(tnn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, base_width=64):
+        super().__init__()
+        self.conv1 = _conv3x3(inplanes, planes, stride)
+        self.bn1 = mnn.BatchNorm2d(planes)
+        self.relu = mnn.ReLU(inplace=True)
+        self.conv2 = _conv3x3(planes, planes)
+        self.bn2 = mnn.BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        out = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        if self.downsample is not None:
+            ds_conv, ds_bn = self.downsample[0], self.downsample[1]
+            return mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, branch=(x, ds_conv, ds_bn))
+        return mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=x)
+
+
+class Bottleneck(tnn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, base_width=64):
+        super().__init__()
+        width = int(planes * (base_width / 64.0))
+        self.conv1 = _conv1x1(inplanes, width)
+        self.bn1 = mnn.BatchNorm2d(width)
+        self.conv2 = _conv3x3(width, width, stride)
+        self.bn2 = mnn.BatchNorm2d(width)
+        self.conv3 = _conv1x1(width, planes * self.expansion)
+        self.bn3 = mnn.BatchNorm2d(planes * self.expansion)
+        self.relu = mnn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        out = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        out = mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
+        if self.downsample is not None:
+            ds_conv, ds_bn = self.downsample[0], self.downsample[1]
+            return mnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, branch=(x, ds_conv, ds_bn))
+        return mnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=x)
+
+
+class _StemConv(mnn.Conv2d):
+    """7x7/2 stem: input channels zero-padded 3 -> 8 so every 16-byte operand load is one tap."""
+
+    CIN_PAD = 8
+
+    def compute_weight(self, dtype):
+        w = self.weight.detach().permute(0, 2, 3, 1)
+        ci = w.shape[-1]
+        if ci % self.CIN_PAD:
+            w = torch.nn.functional.pad(w, (0, self.CIN_PAD - ci % self.CIN_PAD))
+        return w.to(dtype).contiguous()
+
+
+class ResNet(tnn.Module):
+    def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: List[int],
+                 num_classes: int = 1000, zero_init_residual: bool = False,
+                 width_per_group: int = 64, in_chans: int = 3,
+                 compute_dtype: Optional[torch.dtype] = None):
+        super().__init__()
+        self.inplanes = 64
+        self.base_width = width_per_group
+        self.in_chans = in_chans
+        self.compute_dtype = compute_dtype
+        self.conv1 = _StemConv(in_chans, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = mnn.BatchNorm2d(64)
+        self.relu = mnn.ReLU(inplace=True)
+        self.maxpool = mnn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
+        self.avgpool = mnn.AdaptiveAvgPool2d((1, 1))
+        self.fc = mnn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, mnn.Conv2d):
+                tnn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, tnn.BatchNorm2d):
+                tnn.init.ones_(m.weight)
+                tnn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    tnn.init.zeros_(m.bn3.weight)
+                elif isinstance(m, BasicBlock):
+                    tnn.init.zeros_(m.bn2.weight)
+
+    def _make_layer(self, block, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = tnn.Sequential(_conv1x1(self.inplanes, planes * block.expansion, stride),
+                                        mnn.BatchNorm2d(planes * block.expansion))
+        layers = [block(self.inplanes, planes, stride, downsample, self.base_width)]
+        self.inplanes = planes * block.expansion
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, planes, base_width=self.base_width))
+        return tnn.Sequential(*layers)
+
+    def activation_dtype(self, x: torch.Tensor) -> torch.dtype:
+        if self.compute_dtype is not None:
+            return self.compute_dtype
+        return torch.bfloat16 if x.is_cuda else torch.float32
+
+    def forward_features(self, x: torch.Tensor) -> torch.Tensor:
+        """NCHW float input -> NHWC features of layer4."""
+        x = K.nchw_to_nhwc(x, self.activation_dtype(x), _StemConv.CIN_PAD)
+        x = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        x = self.maxpool(x)
+        x = self.layer1(x)
+        x = self.layer2(x)
+        x = self.layer3(x)
+        return self.layer4(x)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.forward_features(x)
+        x = self.avgpool(x)
+        return self.fc(x)
+
+
+def _resnet(block, layers, **kw) -> ResNet:
+    kw.pop("pretrained", None)  # no network: pretrained weights cannot be fetched
+    return ResNet(block, layers, **kw)
+
+
+def resnet18(**kw) -> ResNet:
+    return _resnet(BasicBlock, [2, 2, 2, 2], **kw)
+
+
+def resnet34(**kw) -> ResNet:
+    return _resnet(BasicBlock, [3, 4, 6, 3], **kw)
+
+
+def resnet50(**kw) -> ResNet:
+    return _resnet(Bottleneck, [3, 4, 6, 3], **kw)
+
+
+def resnet101(**kw) -> ResNet:
+    return _resnet(Bottleneck, [3, 4, 23, 3], **kw)
+
+
+def resnet152(**kw) -> ResNet:
+    return _resnet(Bottleneck, [3, 8, 36, 3], **kw)
+
+
+def wide_resnet50_2(**kw) -> ResNet:
+    return _resnet(Bottleneck, [3, 4, 6, 3], width_per_group=128, **kw)
+
+
+def wide_resnet101_2(**kw) -> ResNet:
+    return _resnet(Bottleneck, [3, 4, 23, 3], width_per_group=128, **kw)

@@ -1,0 +1,167 @@
+"""Layers with torch.nn-compatible state (same parameter/buffer names and shapes), executed
+by mipipe's fused kernels.
+
+Checkpoints therefore stay interchangeable with torchvision / torch.nn models (the reference
+saves ``model.state_dict()``, task.py:282-294).  Differences in *execution*:
+
+* activations are NHWC in the model's compute dtype (bf16 on MI355X);
+* conv weights are stored ``channels_last`` so their physical order is ``[Cout,KH,KW,Cin]``,
+  the K-contiguous operand layout the implicit-GEMM kernels read;
+* each weighted layer reads a compute-dtype *shadow* of its fp32 master weight, refreshed by
+  the fused optimizer step (:mod:`mipipe.optim`) instead of a per-layer cast each forward.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as tnn
+
+from mipipe.ops import functional as MF
+from mipipe.ops import kernels as K
+
+__all__ = ["Conv2d", "BatchNorm2d", "Linear", "ReLU", "MaxPool2d", "AdaptiveAvgPool2d",
+           "Embedding", "LayerNorm", "Dropout", "ShadowMixin", "conv_bn_act"]
+
+
+class ShadowMixin:
+    """Provides ``compute_weight(dtype)``: the compute-dtype operand view of ``self.weight``."""
+
+    _shadow: Optional[torch.Tensor] = None
+
+    def operand_view(self, w: torch.Tensor) -> torch.Tensor:
+        return w
+
+    def compute_weight(self, dtype: torch.dtype) -> torch.Tensor:
+        sh = self.__dict__.get("_shadow")
+        if sh is not None and sh.dtype == dtype and sh.device == self.weight.device:
+            return sh
+        w = self.operand_view(self.weight.detach())
+        if w.dtype == dtype and w.is_contiguous():
+            return w
+        return w.to(dtype).contiguous()
+
+    def set_shadow(self, t: Optional[torch.Tensor]) -> None:
+        self.__dict__["_shadow"] = t
+
+
+class Conv2d(ShadowMixin, tnn.Module):
+    """``torch.nn.Conv2d``-compatible (groups=1, dilation=1, square kernel/stride/pad)."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int, stride: int = 1,
+                 padding: int = 0, bias: bool = False):
+        super().__init__()
+        k = kernel_size if isinstance(kernel_size, int) else kernel_size[0]
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size = (k, k)
+        self.stride = (stride, stride) if isinstance(stride, int) else tuple(stride)
+        self.padding = (padding, padding) if isinstance(padding, int) else tuple(padding)
+        w = torch.empty(out_channels, in_channels, k, k).to(memory_format=torch.channels_last)
+        self.weight = tnn.Parameter(w)
+        self.bias = tnn.Parameter(torch.zeros(out_channels)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        tnn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if self.bias is not None:
+            fan_in = self.in_channels * self.kernel_size[0] * self.kernel_size[1]
+            bound = 1 / math.sqrt(fan_in)
+            tnn.init.uniform_(self.bias, -bound, bound)
+
+    def operand_view(self, w):
+        return w.permute(0, 2, 3, 1)  # [Co,KH,KW,Ci]; contiguous when w is channels_last
+
+    def _apply(self, fn, *args, **kwargs):
+        r = super()._apply(fn, *args, **kwargs)
+        # keep channels_last physical order after .to()/.cuda()
+        if not self.weight.is_contiguous(memory_format=torch.channels_last):
+            self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
+        return r
+
+    def forward(self, x: torch.Tensor, stats_shift: Optional[torch.Tensor] = None):
+        """x: NHWC.  Returns y, or (y, psum, psumsq) when ``stats_shift`` is given."""
+        w_c = self.compute_weight(x.dtype)
+        y, ps, pss = MF.conv2d(x, self.weight, w_c, self.stride[0], self.padding[0], stats_shift)
+        if self.bias is not None:
+            y = y + self.bias.to(y.dtype)
+        return y if stats_shift is None else (y, ps, pss)
+
+    def extra_repr(self) -> str:
+        return (f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, "
+                f"stride={self.stride}, padding={self.padding}, bias={self.bias is not None}")
+
+
+class BatchNorm2d(tnn.BatchNorm2d):
+    """Same state as ``torch.nn.BatchNorm2d``; standalone forward on NHWC input."""
+
+    def forward(self, y: torch.Tensor) -> torch.Tensor:  # NHWC
+        training = self.training and self.track_running_stats is not None
+        use_batch = self.training or not self.track_running_stats
+        if use_batch:
+            ps, pss = MF.channel_partials(y, self.running_mean if self.running_mean is not None
+                                          else torch.zeros(y.shape[-1], device=y.device))
+            st = MF.bn_stats_from_partials(ps, pss, y.numel() // y.shape[-1], self, True)
+        else:
+            st = MF.bn_stats_from_partials(None, None, y.numel() // y.shape[-1], self, False)
+        return MF.batchnorm_act(y, st, self, relu=False)
+
+
+def conv_bn_act(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d, relu: bool = True,
+                residual: Optional[torch.Tensor] = None,
+                branch: Optional[tuple] = None) -> torch.Tensor:
+    """Fused conv -> BN -> [+residual | +BN(conv(branch_x))] -> ReLU on NHWC activations.
+
+    ``branch`` = (x_b, conv_b, bn_b): the ResNet downsample path, normalised and added in the
+    same elementwise pass as the main path.
+    """
+    use_batch = bn.training
+    y, ps, pss = conv(x, bn.running_mean if use_batch else None) if use_batch else (conv(x), None, None)
+    count = y.numel() // y.shape[-1]
+    st = MF.bn_stats_from_partials(ps, pss, count, bn, use_batch)
+    if branch is not None:
+        xb, convb, bnb = branch
+        yb, psb, pssb = convb(xb, bnb.running_mean) if bnb.training else (convb(xb), None, None)
+        stb = MF.bn_stats_from_partials(psb, pssb, count, bnb, bnb.training)
+        return MF.batchnorm_act(y, st, bn, relu, y2=yb, st2=stb, bn2=bnb)
+    return MF.batchnorm_act(y, st, bn, relu, residual=residual)
+
+
+class ReLU(tnn.ReLU):
+    pass
+
+
+class MaxPool2d(tnn.MaxPool2d):
+    def forward(self, x):  # NHWC
+        k = self.kernel_size if isinstance(self.kernel_size, int) else self.kernel_size[0]
+        s = self.stride if isinstance(self.stride, int) else self.stride[0]
+        p = self.padding if isinstance(self.padding, int) else self.padding[0]
+        return MF.max_pool2d(x, k, s, p)
+
+
+class AdaptiveAvgPool2d(tnn.AdaptiveAvgPool2d):
+    def forward(self, x):  # NHWC -> [N, C]
+        return MF.global_avg_pool(x)
+
+
+class Linear(ShadowMixin, tnn.Linear):
+    """``torch.nn.Linear`` state; GEMM on the MFMA kernel with the bias in the epilogue."""
+
+    def forward(self, x: torch.Tensor, act: str = "none") -> torch.Tensor:
+        w_c = self.compute_weight(x.dtype)
+        b = None if self.bias is None else self.bias
+        return MF.linear(x, self.weight, w_c, b, act)
+
+
+class Embedding(ShadowMixin, tnn.Embedding):
+    def forward(self, idx: torch.Tensor, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+        return MF.embedding(idx, self.weight, self.compute_weight(dtype or self.weight.dtype))
+
+
+class LayerNorm(tnn.LayerNorm):
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return MF.layer_norm(x, self.weight, self.bias, self.eps, residual)
+
+
+class Dropout(tnn.Dropout):
+    pass

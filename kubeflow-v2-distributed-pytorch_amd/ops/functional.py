@@ -1,0 +1,316 @@
+"""Autograd functions over the fused kernel contracts (see :mod:`mipipe.ops.kernels`).
+
+The training step of the reference (task.py:308-312: zero_grad, forward, CE loss,
+backward, SGD step) decomposes into these units, each one or two HIP launches:
+
+* :func:`conv2d` — implicit-GEMM convolution (MFMA) whose epilogue also emits the
+  per-channel partial sums BatchNorm needs, so BN never re-reads the conv output for stats;
+* :func:`batchnorm_act` — BN normalize/affine + optional residual add (raw identity or a
+  second BN'd branch) + ReLU in one pass; backward = one reduce pass + one apply pass that
+  also produces the residual gradient;
+* :func:`linear`, :func:`cross_entropy`, :func:`max_pool2d`, :func:`global_avg_pool`,
+  :func:`layer_norm`, :func:`gelu`, :func:`attention`, :func:`embedding`.
+
+Master weights stay fp32 (``nn.Parameter``); kernels consume a compute-dtype *shadow*
+(bf16 on the GPU) passed as a separate, non-differentiable argument; weight gradients come
+back in fp32.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+from torch.autograd import Function
+
+from . import kernels as K
+
+Tensor = torch.Tensor
+
+
+# ----------------------------------------------------------------------------- conv
+class _ConvFn(Function):
+    @staticmethod
+    def forward(ctx, x, weight, w_c, stride, pad, shift):
+        y, psum, psumsq = K.conv_fwd(x, w_c, stride, pad, shift)
+        ctx.save_for_backward(x, w_c)
+        ctx.conf = (stride, pad, weight.shape[2], weight.shape[3], weight.shape[1])
+        if psum is not None:
+            ctx.mark_non_differentiable(psum, psumsq)
+        return y, psum, psumsq
+
+    @staticmethod
+    def backward(ctx, dy, _g1, _g2):
+        x, w_c = ctx.saved_tensors
+        stride, pad, kh, kw, ci = ctx.conf
+        dy = dy.contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = K.conv_dgrad(dy, w_c, x.shape, stride, pad)
+        if ctx.needs_input_grad[1]:
+            dw = K.conv_wgrad(dy, x, kh, kw, stride, pad)
+            if dw.shape[-1] != ci:  # input channels were zero-padded for the kernel
+                dw = dw[..., :ci]
+            dw = dw.permute(0, 3, 1, 2)
+        return dx, dw, None, None, None, None
+
+
+def conv2d(x: Tensor, weight: Tensor, w_c: Tensor, stride: int, pad: int,
+           stats_shift: Optional[Tensor] = None):
+    """NHWC conv.  Returns (y, psum, psumsq); the partials are None unless ``stats_shift``."""
+    return _ConvFn.apply(x, weight, w_c, stride, pad, stats_shift)
+
+
+# ----------------------------------------------------------------------------- batchnorm
+@dataclass
+class BNStats:
+    mean: Tensor
+    invstd: Tensor
+    scale: Tensor
+    bias: Tensor
+    count: int
+    batch_stats: bool
+
+
+def bn_stats_from_partials(psum, psumsq, count, bn, training: bool) -> BNStats:
+    """Finalize batch statistics (training) or use running statistics (eval)."""
+    if training:
+        mom = 0.1 if bn.momentum is None else bn.momentum
+        mean, invstd, scale, bias = K.bn_finalize(
+            psum, psumsq, count, bn.running_mean, bn.weight.detach(), bn.bias.detach(),
+            bn.running_mean if bn.track_running_stats else None,
+            bn.running_var if bn.track_running_stats else None, mom, bn.eps)
+        if bn.track_running_stats:
+            bn.num_batches_tracked.add_(1)
+        return BNStats(mean, invstd, scale, bias, count, True)
+    invstd = torch.rsqrt(bn.running_var.float() + bn.eps)
+    scale = bn.weight.detach().float() * invstd
+    bias = bn.bias.detach().float() - bn.running_mean.float() * scale
+    return BNStats(bn.running_mean.float(), invstd, scale, bias, count, False)
+
+
+class _BNActFn(Function):
+    @staticmethod
+    def forward(ctx, y, gamma, beta, residual, y2, gamma2, beta2, st, st2, relu):
+        z = K.bn_act_fwd(y, st.scale, st.bias, relu,
+                         residual if y2 is None else y2,
+                         None if st2 is None else st2.scale, None if st2 is None else st2.bias)
+        ctx.save_for_backward(y, z, y2, gamma, gamma2)
+        ctx.st, ctx.st2, ctx.relu = st, st2, relu
+        ctx.has_res = residual is not None
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        y, z, y2, gamma, gamma2 = ctx.saved_tensors
+        st, st2, relu = ctx.st, ctx.st2, ctx.relu
+        dz = dz.contiguous()
+        sg, sgx, sgx2 = K.bn_act_bwd_reduce(dz, z, y, st.mean, st.invstd, relu, y2,
+                                            None if st2 is None else st2.mean,
+                                            None if st2 is None else st2.invstd)
+        zero = torch.zeros_like(sg)
+        a_g, a_gx = (sg, sgx) if st.batch_stats else (zero, zero)
+        a_gx2 = None
+        if st2 is not None:
+            a_gx2 = sgx2 if st2.batch_stats else zero
+        dy, other = K.bn_act_bwd_apply(
+            dz, z, y, st.mean, st.invstd, gamma.detach(), a_g, a_gx, st.count, relu,
+            want_dres=ctx.has_res, y2=y2, mean2=None if st2 is None else st2.mean,
+            invstd2=None if st2 is None else st2.invstd,
+            gamma2=None if gamma2 is None else gamma2.detach(), sum_gx2=a_gx2)
+        dres = other if ctx.has_res else None
+        dy2 = other if y2 is not None else None
+        dgamma2 = sgx2 if y2 is not None else None
+        dbeta2 = sg if y2 is not None else None
+        return (dy, sgx.to(gamma.dtype), sg.to(gamma.dtype), dres, dy2,
+                None if dgamma2 is None else dgamma2.to(gamma2.dtype),
+                None if dbeta2 is None else dbeta2.to(gamma2.dtype), None, None, None)
+
+
+def batchnorm_act(y: Tensor, st: BNStats, bn, relu: bool, residual: Optional[Tensor] = None,
+                  y2: Optional[Tensor] = None, st2: Optional[BNStats] = None, bn2=None) -> Tensor:
+    """z = relu?( bn(y) [+ residual | + bn2(y2)] )."""
+    return _BNActFn.apply(y, bn.weight, bn.bias, residual, y2,
+                          None if bn2 is None else bn2.weight,
+                          None if bn2 is None else bn2.bias, st, st2, relu)
+
+
+def channel_partials(y: Tensor, shift: Tensor) -> Tuple[Tensor, Tensor]:
+    """Shifted per-channel sums of an NHWC tensor (BN without a producing conv)."""
+    C = y.shape[-1]
+    d = y.detach().reshape(-1, C).float() - shift.float()
+    return d.sum(0, keepdim=True), (d * d).sum(0, keepdim=True)
+
+
+# ----------------------------------------------------------------------------- pooling
+class _MaxPoolFn(Function):
+    @staticmethod
+    def forward(ctx, x, k, stride, pad):
+        y, idx = K.maxpool_fwd(x, k, stride, pad)
+        ctx.save_for_backward(idx)
+        ctx.xshape = tuple(x.shape)
+        ctx.mark_non_differentiable(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        return K.maxpool_bwd(dy.contiguous(), idx, ctx.xshape), None, None, None
+
+
+def max_pool2d(x: Tensor, k: int, stride: int, pad: int) -> Tensor:
+    return _MaxPoolFn.apply(x, k, stride, pad)
+
+
+class _AvgPoolFn(Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.xshape = tuple(x.shape)
+        return K.avgpool_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return K.avgpool_bwd(dy.contiguous(), ctx.xshape)
+
+
+def global_avg_pool(x: Tensor) -> Tensor:
+    """NHWC [N,H,W,C] -> [N,C] (AdaptiveAvgPool2d((1,1)) + flatten)."""
+    return _AvgPoolFn.apply(x)
+
+
+# ----------------------------------------------------------------------------- linear
+class _LinearFn(Function):
+    @staticmethod
+    def forward(ctx, x, weight, w_c, bias, act):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        if act == "gelu":
+            h = K.gemm(x2, w_c, False, True, bias, "none", x.dtype)
+            y = K.gelu_fwd(h)
+            ctx.save_for_backward(x2, w_c, h)
+        else:
+            y = K.gemm(x2, w_c, False, True, bias, act, x.dtype)
+            ctx.save_for_backward(x2, w_c, y if act == "relu" else None)
+        ctx.act, ctx.shp, ctx.has_bias = act, shp, bias is not None
+        return y.reshape(*shp[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w_c, aux = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        if ctx.act == "gelu":
+            dy2 = K.gelu_bwd(dy2, aux)
+        elif ctx.act == "relu":
+            dy2 = (dy2.float() * (aux > 0)).to(dy2.dtype)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = K.gemm(dy2, w_c, False, False, None, "none", dy2.dtype).reshape(ctx.shp)
+        if ctx.needs_input_grad[1]:
+            dw = K.gemm(dy2, x2, True, False, None, "none", torch.float32)
+        if ctx.has_bias and ctx.needs_input_grad[3]:
+            db = dy2.float().sum(0)
+        return dx, dw, None, db, None
+
+
+def linear(x: Tensor, weight: Tensor, w_c: Tensor, bias: Optional[Tensor], act: str = "none"):
+    return _LinearFn.apply(x, weight, w_c, bias, act)
+
+
+# ----------------------------------------------------------------------------- loss
+class _CrossEntropyFn(Function):
+    @staticmethod
+    def forward(ctx, logits, labels, label_smoothing, ignore_index):
+        loss, grad = K.cross_entropy_fwd_bwd(logits.contiguous(), labels.contiguous(),
+                                             label_smoothing, ignore_index)
+        ctx.save_for_backward(grad)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return (grad * g.to(grad.dtype)), None, None, None
+
+
+def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0,
+                  ignore_index: int = -100) -> Tensor:
+    """Fused log-softmax + NLL (mean) whose backward costs one scale."""
+    return _CrossEntropyFn.apply(logits, labels, label_smoothing, ignore_index)
+
+
+# ----------------------------------------------------------------------------- transformer ops
+class _LayerNormFn(Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps, residual):
+        y, mean, rstd, xs = K.layernorm_fwd(x, gamma, beta, eps, residual)
+        ctx.save_for_backward(x if xs is None else xs, mean, rstd, gamma)
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd, gamma = ctx.saved_tensors
+        dx, dgamma, dbeta = K.layernorm_bwd(dy.contiguous(), x, mean, rstd, gamma)
+        return dx, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), None, (dx if ctx.has_res else None)
+
+
+def layer_norm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float = 1e-12,
+               residual: Optional[Tensor] = None) -> Tensor:
+    """LN(x [+ residual]) — the BERT post-LN residual add fused into the norm."""
+    return _LayerNormFn.apply(x, gamma, beta, eps, residual)
+
+
+class _GeluFn(Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return K.gelu_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        return K.gelu_bwd(dy.contiguous(), x)
+
+
+def gelu(x: Tensor) -> Tensor:
+    return _GeluFn.apply(x)
+
+
+class _AttentionFn(Function):
+    @staticmethod
+    def forward(ctx, q, k, v, mask_bias, scale):
+        o, lse = K.attention_fwd(q, k, v, mask_bias, scale)
+        ctx.save_for_backward(q, k, v, o, lse, mask_bias)
+        ctx.scale = scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, mask_bias = ctx.saved_tensors
+        dq, dk, dv = K.attention_bwd(do.contiguous(), q, k, v, o, lse, mask_bias, ctx.scale)
+        return dq, dk, dv, None, None
+
+
+def attention(q: Tensor, k: Tensor, v: Tensor, mask_bias: Optional[Tensor] = None,
+              scale: Optional[float] = None) -> Tensor:
+    """Flash-style softmax(QKᵀ·scale + mask)·V; q,k,v [B,H,S,D]."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    return _AttentionFn.apply(q, k, v, mask_bias, scale)
+
+
+class _EmbeddingFn(Function):
+    @staticmethod
+    def forward(ctx, idx, weight, w_c):
+        ctx.save_for_backward(idx)
+        ctx.rows = weight.shape[0]
+        return w_c[idx]
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        return None, K.embedding_bwd(dy.contiguous(), idx, ctx.rows), None
+
+
+def embedding(idx: Tensor, weight: Tensor, w_c: Tensor) -> Tensor:
+    return _EmbeddingFn.apply(idx, weight, w_c)
