@@ -34,9 +34,17 @@ class ShadowMixin:
         return w
 
     def compute_weight(self, dtype: torch.dtype) -> torch.Tensor:
-        sh = self.__dict__.get("_shadow")
-        if sh is not None and sh.dtype == dtype and sh.device == self.weight.device:
-            return sh
+        from mipipe.optim.flat import flat_space_for
+        fs = flat_space_for(self.weight)
+        if fs is not None and fs.shadow is not None and fs.shadow.dtype == dtype:
+            fs.sync_shadow(self.weight)
+            sh = self.__dict__.get("_shadow")
+            if sh is None or sh.data_ptr() != fs.shadow_view(self.weight).data_ptr():
+                sh = self.operand_view(fs.shadow_view(self.weight))
+                sh = sh if sh.is_contiguous() else None
+                self.__dict__["_shadow"] = sh
+            if sh is not None:
+                return sh
         w = self.operand_view(self.weight.detach())
         if w.dtype == dtype and w.is_contiguous():
             return w

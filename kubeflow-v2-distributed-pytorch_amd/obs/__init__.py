@@ -1,1 +1,1 @@
-
+"""Observability: throughput meter, roctx ranges, structured logs, profiler helpers."""

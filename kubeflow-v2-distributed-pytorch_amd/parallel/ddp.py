@@ -1,0 +1,265 @@
+"""DistributedDataParallel over RCCL with flat in-place gradient buckets.
+
+Replaces ``torch.nn.parallel.DistributedDataParallel(model, device_ids=[gpu])`` used by the
+reference (task.py:189, 194) and reproduces its collective contract:
+
+* C2 — at construction, all ranks agree on parameter shapes (all-gather of a digest);
+* C3 — at construction, parameters and buffers are broadcast from rank 0 (the flat
+  parameter buffer goes in ONE collective);
+* C4 — before every grad-enabled forward, module buffers (BN running stats) are broadcast
+  from rank 0 (``broadcast_buffers=True``, DDP's default);
+* C5 — during backward, gradients are averaged with bucketed all-reduce overlapped with the
+  remaining backward kernels.
+
+MI355X design: gradients already live in one flat fp32 buffer in gradient-ready order
+(:mod:`mipipe.optim.flat`), so a bucket is a contiguous slice that RCCL all-reduces *in place*
+— no copy into/out of bucket staging buffers.  Buckets are launched strictly in index order
+(every rank issues the same collective sequence) from post-accumulate-grad hooks, on the
+process group's communication stream; the step's end waits on them with stream semantics only
+(no host sync).  Bucket size defaults to 32 MiB (≈7 links × ~4.5 MiB chunks per ring step on
+the 8-GPU xGMI mesh) with a small first bucket so communication starts early; the optional
+``comm_dtype=torch.bfloat16`` halves the bytes on the wire.
+
+Debug aid (SURVEY §5.2 hazard): ``check_collectives=True`` (or ``MIPIPE_CHECK_COLLECTIVES=1``)
+hashes every collective this wrapper issues and compares the digests across ranks every
+``check_every`` steps, turning a mismatched collective sequence into an immediate error.
+"""
+from __future__ import annotations
+
+import contextlib
+import hashlib
+import os
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+import torch.nn as tnn
+
+from mipipe.optim.flat import FlatParamSpace, get_flat_space
+
+__all__ = ["DistributedDataParallel", "CollectiveSequenceError", "Bucket"]
+
+
+class CollectiveSequenceError(RuntimeError):
+    pass
+
+
+class Bucket:
+    __slots__ = ("index", "start", "end", "params", "pending", "work", "launched", "tmp")
+
+    def __init__(self, index: int, start: int, end: int, params: List[tnn.Parameter]):
+        self.index, self.start, self.end, self.params = index, start, end, params
+        self.pending = len(params)
+        self.work = None
+        self.launched = False
+        self.tmp = None
+
+    @property
+    def nbytes(self) -> int:
+        return (self.end - self.start) * 4
+
+
+class _CollectiveLog:
+    def __init__(self):
+        self.h = hashlib.sha1()
+        self.count = 0
+
+    def record(self, op: str, t: torch.Tensor) -> None:
+        self.h.update(f"{op}:{t.numel()}:{t.dtype};".encode())
+        self.count += 1
+
+    def digest(self) -> bytes:
+        return self.h.digest()
+
+
+class DistributedDataParallel(tnn.Module):
+    def __init__(self, module: tnn.Module, device_ids: Optional[List[int]] = None,
+                 output_device=None, broadcast_buffers: bool = True,
+                 process_group=None, bucket_cap_mb: float = 32.0, first_bucket_mb: float = 1.0,
+                 comm_dtype: Optional[torch.dtype] = None, find_unused_parameters: bool = False,
+                 check_collectives: Optional[bool] = None, check_every: int = 50,
+                 gradient_as_bucket_view: bool = True, static_graph: bool = False):
+        super().__init__()
+        self.module = module
+        self.device_ids = device_ids
+        self.broadcast_buffers = broadcast_buffers
+        self.process_group = process_group
+        self.comm_dtype = comm_dtype
+        self.require_forward_param_sync = True
+        self._sync_enabled = True
+        if check_collectives is None:
+            check_collectives = os.environ.get("MIPIPE_CHECK_COLLECTIVES", "0") == "1"
+        self.check_collectives = check_collectives
+        self.check_every = check_every
+        self._clog = _CollectiveLog()
+        self._steps = 0
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        params = [p for p in module.parameters() if p.requires_grad]
+        dev = params[0].device
+        shadow = torch.bfloat16 if dev.type == "cuda" else None
+        self.space: FlatParamSpace = get_flat_space(params, shadow, module)
+        backend = dist.get_backend(process_group) if dist.is_initialized() else "none"
+        self._avg_supported = backend == "nccl"
+        if self.world > 1:
+            self._verify_shapes(params)
+            self._sync_module_states()
+        self.buckets = self._build_buckets(bucket_cap_mb * 2 ** 20, first_bucket_mb * 2 ** 20)
+        self._bucket_of = {}
+        for b in self.buckets:
+            for p in b.params:
+                self._bucket_of[id(p)] = b
+        self._next_bucket = 0
+        self._callback_queued = False
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(p)) for p in params]
+
+    # ------------------------------------------------------------------ construction
+    def _verify_shapes(self, params) -> None:
+        h = hashlib.sha1(";".join(f"{tuple(p.shape)}:{p.dtype}" for p in params).encode()).hexdigest()
+        out: List[Optional[str]] = [None] * self.world
+        dist.all_gather_object(out, h, group=self.process_group)
+        if any(o != h for o in out):
+            raise RuntimeError(f"DDP: parameter shapes differ across ranks: {out}")
+
+    def _broadcast(self, t: torch.Tensor, src: int = 0) -> None:
+        self._clog.record("broadcast", t)
+        dist.broadcast(t, src, group=self.process_group)
+
+    def _sync_module_states(self) -> None:
+        self._broadcast(self.space.flat)
+        self.space.sync_shadow()
+        self._broadcast_buffers_now()
+
+    def _module_buffers(self) -> List[torch.Tensor]:
+        return [b for b in self.module.buffers()]
+
+    def _broadcast_buffers_now(self) -> None:
+        bufs = self._module_buffers()
+        if not bufs:
+            return
+        # coalesce per dtype into one flat tensor per dtype
+        by_dtype = {}
+        for b in bufs:
+            by_dtype.setdefault(b.dtype, []).append(b)
+        for dt, lst in by_dtype.items():
+            flat = torch.cat([b.reshape(-1) for b in lst])
+            self._broadcast(flat)
+            off = 0
+            for b in lst:
+                n = b.numel()
+                b.copy_(flat[off:off + n].view_as(b))
+                off += n
+
+    def _build_buckets(self, cap_bytes: float, first_bytes: float) -> List[Bucket]:
+        buckets: List[Bucket] = []
+        cur: List[tnn.Parameter] = []
+        start = None
+        end = 0
+        limit = first_bytes
+        for (s, e, p) in self.space.ranges():
+            if start is None:
+                start = s
+            cur.append(p)
+            end = e
+            if (end - start) * 4 >= limit:
+                buckets.append(Bucket(len(buckets), start, end, cur))
+                cur, start = [], None
+                limit = cap_bytes
+        if cur:
+            buckets.append(Bucket(len(buckets), start, end, cur))
+        return buckets
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, *args, **kwargs):
+        if self.world > 1 and torch.is_grad_enabled() and self.broadcast_buffers \
+                and self.require_forward_param_sync:
+            self._broadcast_buffers_now()
+        if torch.is_grad_enabled() and self.module.training:
+            self._prepare_backward()
+            self.require_forward_param_sync = True
+        else:
+            self.require_forward_param_sync = False
+        return self.module(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self._sync_enabled
+        self._sync_enabled = False
+        try:
+            yield
+        finally:
+            self._sync_enabled = old
+
+    # ------------------------------------------------------------------ backward / comm
+    def _prepare_backward(self) -> None:
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.work = None
+            b.launched = False
+            b.tmp = None
+        self._next_bucket = 0
+        self._callback_queued = False
+        self.space.ensure_grad_views()
+
+    def _make_hook(self, p):
+        def hook(param):
+            if self.world <= 1 or not self._sync_enabled:
+                return
+            if not self._callback_queued:
+                self._callback_queued = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+            b = self._bucket_of[id(param)]
+            b.pending -= 1
+            self._launch_ready()
+        return hook
+
+    def _launch(self, b: Bucket) -> None:
+        g = self.space.flat_grad[b.start:b.end]
+        if self.comm_dtype is not None and self.comm_dtype != g.dtype:
+            b.tmp = g.to(self.comm_dtype)
+            t = b.tmp
+        else:
+            t = g
+        self._clog.record("all_reduce", t)
+        op = dist.ReduceOp.AVG if self._avg_supported else dist.ReduceOp.SUM
+        b.work = dist.all_reduce(t, op=op, group=self.process_group, async_op=True)
+        b.launched = True
+
+    def _launch_ready(self) -> None:
+        while self._next_bucket < len(self.buckets) and self.buckets[self._next_bucket].pending <= 0:
+            self._launch(self.buckets[self._next_bucket])
+            self._next_bucket += 1
+
+    def _finalize(self) -> None:
+        # unused parameters: their (zero) gradients still take part in the average
+        while self._next_bucket < len(self.buckets):
+            self._launch(self.buckets[self._next_bucket])
+            self._next_bucket += 1
+        for b in self.buckets:
+            if b.work is not None:
+                b.work.wait()
+                g = self.space.flat_grad[b.start:b.end]
+                if b.tmp is not None:
+                    g.copy_(b.tmp)
+                    if not self._avg_supported:
+                        g.div_(self.world)
+                elif not self._avg_supported:
+                    g.div_(self.world)
+                b.work = None
+                b.tmp = None
+        self._steps += 1
+        if self.check_collectives and self._steps % self.check_every == 0:
+            self.verify_collective_sequence()
+
+    # ------------------------------------------------------------------ debugging
+    def verify_collective_sequence(self) -> None:
+        """All-gather the per-rank digest of collectives issued so far; raise on mismatch."""
+        d = (self._clog.digest().hex(), self._clog.count)
+        out: List[Optional[Tuple[str, int]]] = [None] * self.world
+        dist.all_gather_object(out, d, group=self.process_group)
+        if any(o != out[0] for o in out):
+            raise CollectiveSequenceError(
+                f"collective sequences diverged across ranks: {out} (an op ran on a subset of "
+                "ranks — e.g. evaluating the DDP wrapper on rank 0 only, SURVEY §5.2)")
+
+    def state_dict(self, *args, **kwargs):
+        return super().state_dict(*args, **kwargs)

@@ -1,0 +1,359 @@
+"""Distributed training entry point — flag-compatible with the reference's ``task.py``.
+
+Reference: /root/reference/task.py (318 lines).  Same CLI flags with the same names and
+defaults (task.py:55-95) so the compiled pipeline's args
+(``--dist-url=env:// --multiprocessing-distributed --num_epochs=2``, nb:159-163) work
+unchanged, the same env contract (``WORLD_SIZE``/``RANK``/``MASTER_*``/``AIP_MODEL_DIR``) and
+the same process structure: ``main()`` resolves the distributed mode (task.py:97-113) and
+either ``mp.spawn``s one worker per local GPU (task.py:117-124) or runs ``main_worker``
+in-process (task.py:127); ``main_worker`` does rank math + rendezvous (task.py:132-150),
+seeding (161-162), model construction (165-171), DDP wrapping (173-208), loss/optimizer
+(210-214), resume (216-242), data (246-267), the epoch loop with periodic eval + export
+(272-312).
+
+Deliberate fixes of reference quirks, each noted inline:
+  * evaluation runs on the *unwrapped* model, sharded over all ranks (no rank-0-only
+    collective mismatch, §5.2); the model is also evaluated and saved after training;
+  * ``--resume`` takes a path (or ``auto``) and ``start_epoch`` is honoured;
+  * ``DistributedSampler.set_epoch`` is called; ``--dist-url`` defaults to ``env://``;
+  * per-process batch = ``--batch_size`` (what the reference effectively does), reported
+    together with the global batch;
+  * data is synthetic and generated on the GPU (no download race, no CPU decode).
+Additions: ``--dtype``, ``--dataset``, ``--steps``, ``--bench``, ``--num_classes``,
+``--eval-every``, metrics JSON with samples/sec, fault injection for tests.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import sys
+import time
+from datetime import datetime
+
+if __package__ in (None, ""):  # executed as a plain script (the pipeline stages it as task.py)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+import numpy as np
+import torch
+import torch.multiprocessing as mp
+
+from mipipe.models import create_model, model_names
+from mipipe.parallel import DataParallel, DistributedDataParallel, DistributedSampler
+from mipipe.parallel import dist_utils
+from mipipe.data.synthetic import DATASET_SHAPES, DeviceBatchLoader, SyntheticImageDataset
+from mipipe.optim import SGD
+from mipipe.ops import functional as MF
+from mipipe.train import checkpoint as ckpt
+from mipipe.obs.meter import ThroughputMeter
+
+best_acc1 = 0.0
+
+
+def set_random_seeds(random_seed: int = 0) -> None:
+    """task.py:22-28.  Deterministic kernel choice is the default here (fixed tile tables,
+    no autotuning), so the reference's later ``cudnn.benchmark = True`` override has no
+    analogue."""
+    torch.manual_seed(random_seed)
+    np.random.seed(random_seed)
+    random.seed(random_seed)
+
+
+class CrossEntropyLoss(torch.nn.Module):
+    """``nn.CrossEntropyLoss()`` (task.py:211) on the fused log-softmax+NLL kernel."""
+
+    def __init__(self, label_smoothing: float = 0.0, ignore_index: int = -100):
+        super().__init__()
+        self.label_smoothing = label_smoothing
+        self.ignore_index = ignore_index
+
+    def forward(self, logits, labels):
+        return MF.cross_entropy(logits, labels, self.label_smoothing, self.ignore_index)
+
+
+def _unwrap(model):
+    return model.module if isinstance(model, (DistributedDataParallel, torch.nn.DataParallel)) else model
+
+
+@torch.no_grad()
+def evaluate(model, device, test_loader) -> float:
+    """Top-1 accuracy (task.py:30-46) — argmax + correct count stay on the device and the
+    host reads ONE value at the end instead of a ``.item()`` per batch.  Sharded over ranks
+    (each rank's loader holds its shard) and summed with one all-reduce."""
+    m = _unwrap(model)
+    was_training = m.training
+    m.eval()
+    correct = torch.zeros((), dtype=torch.int64, device=device)
+    total = torch.zeros((), dtype=torch.int64, device=device)
+    for images, labels in test_loader:
+        images, labels = images.to(device), labels.to(device)
+        outputs = m(images)
+        predicted = outputs.float().argmax(1)
+        total += labels.numel()
+        correct += (predicted == labels).sum()
+    if dist_utils.get_world_size() > 1:
+        t = torch.stack([correct, total])
+        torch.distributed.all_reduce(t)
+        correct, total = t[0], t[1]
+    if was_training:
+        m.train()
+    return float(correct.item()) / max(1, int(total.item()))
+
+
+def build_parser() -> argparse.ArgumentParser:
+    names = model_names()
+    p = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter,
+                                description="mipipe distributed trainer (task.py compatible)")
+    # --- reference flags (task.py:56-94), same names and defaults -------------------------
+    p.add_argument("--local_rank", type=int, help="Local rank (torch.distributed.launch compat).")
+    p.add_argument("--num_epochs", type=int, default=100, help="Number of training epochs.")
+    p.add_argument("--batch_size", type=int, default=1024, help="Training batch size for one process.")
+    p.add_argument("--learning_rate", dest="learning_rate", type=float, default=0.1, help="Learning rate.")
+    p.add_argument("--random_seed", type=int, default=0, help="Random seed.")
+    p.add_argument("--model_dir", type=str, default=os.environ.get("AIP_MODEL_DIR", ""),
+                   help="Directory (or gs:// URI) for saving models.")
+    p.add_argument("--model_filename", type=str, default="resnet_distributed.pth", help="Model filename.")
+    p.add_argument("-a", "--arch", metavar="ARCH", default="resnet18", choices=names,
+                   help="model architecture: " + " | ".join(names) + " (default: resnet18)")
+    p.add_argument("--momentum", default=0.9, type=float, metavar="M", help="momentum")
+    p.add_argument("--wd", "--weight-decay", default=1e-4, type=float, metavar="W",
+                   dest="weight_decay", help="weight decay (default: 1e-4)")
+    p.add_argument("--pretrained", dest="pretrained", action="store_true",
+                   help="use pre-trained model (no network here: warns and random-inits)")
+    p.add_argument("--local_training", dest="local_training", action="store_true",
+                   help="save to --model_dir instead of AIP_MODEL_DIR")
+    p.add_argument("--rank", default=-1, type=int, help="node rank for distributed training")
+    p.add_argument("--resume", nargs="?", const="auto", default="",
+                   help="resume from checkpoint PATH ('auto' = <model_dir>/checkpoint.pth.tar)")
+    p.add_argument("--world-size", default=int(os.getenv("WORLD_SIZE", -1)), type=int,
+                   help="number of nodes for distributed training")
+    p.add_argument("--dist-url", default="env://", type=str,
+                   help="url used to set up distributed training (reference default "
+                        "http://localhost:8082 is not a valid init method)")
+    p.add_argument("--dist-backend", default="nccl", type=str,
+                   help="distributed backend (nccl = RCCL on ROCm; gloo on CPU)")
+    p.add_argument("--multiprocessing-distributed", action="store_true",
+                   help="launch one process per local GPU (N per node)")
+    p.add_argument("--gpu", default=None, type=int, help="GPU id to use.")
+    p.add_argument("--workers", default=4, type=int, metavar="N",
+                   help="data loading workers (data is generated on the device; kept for compat)")
+    # --- additions ------------------------------------------------------------------------
+    p.add_argument("--dataset", default="cifar10", choices=sorted(DATASET_SHAPES),
+                   help="synthetic dataset shape")
+    p.add_argument("--image-size", type=int, default=None, help="override image H=W")
+    p.add_argument("--train-samples", type=int, default=None)
+    p.add_argument("--test-samples", type=int, default=None)
+    p.add_argument("--num_classes", type=int, default=None,
+                   help="classifier width (reference keeps torchvision's 1000)")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                   help="compute dtype on GPU (master weights stay fp32); CPU runs fp32")
+    p.add_argument("--steps", type=int, default=0, help="max training steps per epoch (0 = all)")
+    p.add_argument("--eval-every", type=int, default=10, help="evaluate every N epochs (task.py:279)")
+    p.add_argument("--log-every", type=int, default=20)
+    p.add_argument("--warmup-steps", type=int, default=2, help="steps excluded from samples/sec")
+    p.add_argument("--bucket-cap-mb", type=float, default=32.0)
+    p.add_argument("--no-broadcast-buffers", action="store_true")
+    p.add_argument("--dist-timeout", type=float, default=1800.0, help="collective timeout (s)")
+    p.add_argument("--compat-nested-model-dir", action="store_true",
+                   help="export to AIP_MODEL_DIR/model/<file> like task.py:291")
+    p.add_argument("--metrics-file", default="", help="write final metrics JSON here")
+    p.add_argument("--cpu-procs", type=int, default=1,
+                   help="processes per node when no GPU is visible (gloo)")
+    return p
+
+
+def _ngpus() -> int:
+    if os.environ.get("MIPIPE_FORCE_CPU") == "1":
+        return 0
+    return torch.cuda.device_count()
+
+
+def main(argv=None) -> int:
+    argv = build_parser().parse_args(argv)
+    if argv.dist_url == "env://" and argv.world_size == -1:
+        argv.world_size = int(os.environ.get("WORLD_SIZE", 1))
+    argv.distributed = argv.world_size > 1 or argv.multiprocessing_distributed
+    ngpus_per_node = _ngpus()
+    procs_per_node = ngpus_per_node if ngpus_per_node > 0 else argv.cpu_procs
+    if ngpus_per_node == 0:
+        argv.dist_backend = "gloo"
+    # debugging (task.py:104-113)
+    print(f"os WORLD_SIZE={os.getenv('WORLD_SIZE', -1)}")
+    print(f"os RANK={os.getenv('RANK', 0)}")
+    print(f"os MASTER_ADDR={os.getenv('MASTER_ADDR', 'localhost')}")
+    print(f"os MASTER_PORT={os.getenv('MASTER_PORT', '8082')}")
+    print(f"Arg - distributed={argv.distributed}")
+    print(f"Arg - multiprocessing_distributed={argv.multiprocessing_distributed}")
+    print(f"Arg - dist_backend={argv.dist_backend}")
+    print(f"Arg - dist_url={argv.dist_url}")
+    print(f"ngpus_per_node={ngpus_per_node}")
+    start = datetime.now().strftime("%Y_%m_%d_%H_%M_%S")
+    print(f"Starting training: {start}", flush=True)
+    if argv.multiprocessing_distributed:
+        argv.world_size = procs_per_node * argv.world_size  # task.py:120
+        print(f"GPU x WORLD SIZE = {argv.world_size}")
+        mp.spawn(main_worker, nprocs=procs_per_node, args=(procs_per_node, argv))
+    else:
+        main_worker(argv.gpu, procs_per_node, argv)
+    end = datetime.now().strftime("%Y_%m_%d_%H_%M_%S")
+    print(f"Training complete: {end}", flush=True)
+    return 0
+
+
+def _fault_check(rank: int, step: int) -> None:
+    spec = os.environ.get("MIPIPE_FAULT_INJECT")  # "rank:step[:code]"
+    if not spec:
+        return
+    parts = spec.split(":")
+    if int(parts[0]) == rank and int(parts[1]) == step:
+        code = int(parts[2]) if len(parts) > 2 else 17
+        print(f"[fault-injection] rank {rank} exiting with {code} at step {step}", flush=True)
+        sys.stdout.flush()
+        os._exit(code)
+
+
+def main_worker(gpu, ngpus_per_node, args) -> dict:
+    global best_acc1
+    args.gpu = gpu
+    if args.gpu is not None:
+        print(f"Use GPU: {args.gpu} for training")
+    if args.distributed:
+        if args.dist_url == "env://" and args.rank == -1:
+            args.rank = int(os.environ.get("RANK", 0))
+            print(f"Distributed and getting rank from os.environ: rank={args.rank}")
+        if args.multiprocessing_distributed:
+            args.rank = dist_utils.global_rank(args.rank, ngpus_per_node, gpu)  # task.py:146
+            print(f"Distributed and Multiprocesing. Setting rank for each worker. rank={args.rank}")
+    else:
+        args.rank = 0
+    use_gpu = _ngpus() > 0
+    if use_gpu:
+        local = args.gpu if args.gpu is not None else int(os.environ.get("LOCAL_RANK", 0))
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if args.distributed:
+        dist_utils.init_distributed(args.dist_backend, args.dist_url, args.world_size, args.rank,
+                                    args.dist_timeout, device if use_gpu else None)
+        print("Process group initialized", flush=True)
+    world = dist_utils.get_world_size()
+    set_random_seeds(args.random_seed)  # same seed on every rank -> identical init (task.py:161)
+
+    if args.pretrained:
+        print(f"=> pre-trained weights for '{args.arch}' need network access; random init instead")
+    print(f"=> creating model '{args.arch}'")
+    C, H, W, K, N = DATASET_SHAPES[args.dataset]
+    if args.image_size:
+        H = W = args.image_size
+    kw = {}
+    if args.num_classes is not None:
+        kw["num_classes"] = args.num_classes
+    if args.arch == "mnist_cnn":
+        kw.setdefault("num_classes", K)
+        kw["in_chans"] = C
+    elif args.arch.startswith(("resnet", "wide_resnet")):
+        kw["in_chans"] = C
+    model = create_model(args.arch, **kw)
+    compute_dtype = torch.bfloat16 if (use_gpu and args.dtype == "bf16") else torch.float32
+    if hasattr(model, "compute_dtype"):
+        model.compute_dtype = compute_dtype
+    model = model.to(device)
+    if args.distributed:
+        model = DistributedDataParallel(model, device_ids=[device.index] if use_gpu else None,
+                                        bucket_cap_mb=args.bucket_cap_mb,
+                                        broadcast_buffers=not args.no_broadcast_buffers)
+    elif use_gpu and args.gpu is None and torch.cuda.device_count() > 1:
+        model = DataParallel(model)  # task.py:201-208 path (d)
+    criterion = CrossEntropyLoss().to(device)
+    optimizer = SGD(model.parameters(), args.learning_rate, momentum=args.momentum,
+                    weight_decay=args.weight_decay,
+                    shadow_dtype=compute_dtype if compute_dtype != torch.float32 else None)
+
+    start_epoch = 0
+    if args.resume:
+        path = ckpt.resolve_resume_path(args.resume, args.model_dir)
+        if path and os.path.isfile(path):
+            print(f"=> loading checkpoint '{path}'")
+            state = ckpt.load_checkpoint(path, device)
+            start_epoch = int(state["epoch"])
+            best_acc1 = float(state.get("best_acc1", 0.0))
+            ckpt.load_model_state(model, state["state_dict"])
+            optimizer.load_state_dict(state["optimizer"])
+            print(f"=> loaded checkpoint '{path}' (epoch {start_epoch})")
+        else:
+            print(f"=> no checkpoint found at '{path}'")
+
+    train_n = args.train_samples or N
+    test_n = args.test_samples or min(N, 10000)
+    train_set = SyntheticImageDataset(args.dataset, train_n, seed=args.random_seed,
+                                      shape=(C, H, W), num_classes=K)
+    test_set = SyntheticImageDataset(args.dataset, test_n, seed=args.random_seed,
+                                     shape=(C, H, W), num_classes=K)
+    train_sampler = DistributedSampler(train_set, seed=args.random_seed)
+    test_sampler = DistributedSampler(test_set, shuffle=False)
+    train_loader = DeviceBatchLoader(train_set, args.batch_size, train_sampler, device)
+    test_loader = DeviceBatchLoader(test_set, 128, test_sampler, device)
+
+    meter = ThroughputMeter(device, warmup_steps=args.warmup_steps)
+    global_step = 0
+    last_loss = float("nan")
+    accuracy = None
+    for epoch in range(start_epoch, args.num_epochs):
+        epoch_start = datetime.now().strftime("%Y_%m_%d_%H_%M_%S")
+        print(f"Rank: {args.rank}, Epoch: {epoch}, Training start: {epoch_start}", flush=True)
+        train_sampler.set_epoch(epoch)
+        if epoch % args.eval_every == 0:
+            accuracy = evaluate(model, device, test_loader)
+            if args.rank == 0:
+                ckpt.export_model(model, args, epoch, accuracy)
+                print("-" * 75)
+                print(f"Epoch: {epoch}, Accuracy: {accuracy}, Time: "
+                      f"{datetime.now().strftime('%Y_%m_%d_%H_%M_%S')}")
+                print("-" * 75, flush=True)
+        model.train()
+        for i, (inputs, labels) in enumerate(train_loader):
+            if args.steps and i >= args.steps:
+                break
+            _fault_check(args.rank, global_step)
+            meter.step_begin()
+            optimizer.zero_grad()
+            outputs = model(inputs)
+            loss = criterion(outputs, labels)
+            loss.backward()
+            optimizer.step()
+            meter.step_end(inputs.shape[0])
+            global_step += 1
+            if args.log_every and global_step % args.log_every == 0:
+                last_loss = float(loss.detach().float().item())
+                if args.rank == 0:
+                    print(f"epoch {epoch} step {global_step} loss {last_loss:.4f} "
+                          f"{meter.samples_per_sec() * world:.1f} samples/s (job)", flush=True)
+        if args.rank == 0:
+            ckpt.save_checkpoint(model, optimizer, args, epoch + 1, best_acc1)
+    # fixed quirk: evaluate and save the *trained* model at the end as well
+    accuracy = evaluate(model, device, test_loader)
+    best_acc1 = max(best_acc1, accuracy)
+    last_loss = float(loss.detach().float().item()) if global_step else last_loss
+    metrics = {"accuracy": accuracy, "loss": last_loss, "epochs": args.num_epochs,
+               "steps": global_step, "world_size": world, "arch": args.arch,
+               "batch_per_process": args.batch_size, "global_batch": args.batch_size * world,
+               "samples_per_sec_per_rank": meter.samples_per_sec(),
+               "samples_per_sec_job": meter.samples_per_sec() * world,
+               "dtype": str(compute_dtype).replace("torch.", ""), "device": str(device)}
+    if args.rank == 0:
+        ckpt.export_model(model, args, args.num_epochs, accuracy)
+        ckpt.save_checkpoint(model, optimizer, args, args.num_epochs, best_acc1)
+        print("MIPIPE_METRICS " + json.dumps(metrics), flush=True)
+        if args.metrics_file:
+            ckpt.write_json(args.metrics_file, metrics)
+    epoch_end = datetime.now().strftime("%Y_%m_%d_%H_%M_%S")
+    print(f"Epoch complete: {epoch_end}", flush=True)
+    dist_utils.barrier(device if use_gpu else None)
+    dist_utils.cleanup()
+    return metrics
+
+
+if __name__ == "__main__":
+    sys.exit(main())
