@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: task.py-style DDP training throughput (samples/sec, whole node).
+
+BASELINE.json metric: "samples/sec (whole node) task.py DDP at 1/2/4/8 MI355X; scaling
+efficiency"; config: ResNet-50, ImageNet shape (3x224x224, 1000 classes), 256 images per GPU
+(weak scaling), bf16 compute with fp32 master weights, SGD(lr=0.1, momentum=0.9, wd=1e-4)
+exactly as task.py:212-214, synthetic data generated on the device, random-init weights.
+
+One timed step = zero_grad + forward + cross-entropy + backward (with the bucketed RCCL
+gradient all-reduce overlapped) + optimizer step — the reference hot loop (task.py:308-312).
+W untimed warmup steps, then exactly K steps bracketed by barrier + device sync on both
+sides; the reported time is the MAX over ranks.
+
+Single GPU:   python bench.py --gpus 1 --steps 20 --warmup 5
+Multi GPU:    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+                  --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "samples/sec (whole node) task.py DDP at 1/2/4/8 MI355X; scaling efficiency"
+# Measured comparator: stock PyTorch-ROCm 2.10 (MIOpen + hipBLASLt, channels_last,
+# bf16 autocast, torch SGD) on ONE MI355X, ResNet-50 b256 224x224: 6580.1 samples/s.
+# vs_baseline = value / (comparator_per_gpu * n_gpus)  (ideal linear scaling of the comparator).
+STOCK_1GPU = {"resnet50": 6580.1, "resnet18_32": 76880.3}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--res", type=int, default=224)
+    ap.add_argument("--classes", type=int, default=1000)
+    ap.add_argument("--bucket-cap-mb", type=float, default=32.0)
+    ap.add_argument("--impl", default="mipipe", choices=["mipipe", "stock"],
+                    help="stock = torch DDP + MIOpen comparator")
+    return ap.parse_args()
+
+
+def main() -> int:
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    torch.manual_seed(0)
+
+    from mipipe.data.synthetic import synthetic_batch
+    idx = [torch.arange(i * a.batch, (i + 1) * a.batch, device=dev) + rank * 10_000_000
+           for i in range(2)]
+    batches = [synthetic_batch(t, (3, a.res, a.res), a.classes, seed=0) for t in idx]
+
+    if a.impl == "mipipe":
+        from mipipe.models import create_model
+        from mipipe.optim import SGD
+        from mipipe.parallel import DistributedDataParallel
+        from mipipe.ops.functional import cross_entropy
+        model = create_model(a.model, num_classes=a.classes).to(dev)
+        model.compute_dtype = torch.bfloat16
+        if world > 1:
+            model = DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=a.bucket_cap_mb)
+        opt = SGD(model.parameters(), 0.1, momentum=0.9, weight_decay=1e-4)
+
+        def step(x, y):
+            opt.zero_grad()
+            loss = cross_entropy(model(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+    else:
+        from mipipe.models.reference import ref_resnet
+        model = ref_resnet(a.model, num_classes=a.classes).to(dev).to(memory_format=torch.channels_last)
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local])
+        opt = torch.optim.SGD(model.parameters(), 0.1, momentum=0.9, weight_decay=1e-4)
+        crit = torch.nn.CrossEntropyLoss()
+        torch.backends.cudnn.benchmark = True
+        batches = [(x.contiguous(memory_format=torch.channels_last), y) for x, y in batches]
+
+        def step(x, y):
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = crit(model(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+
+    model.train()
+    for i in range(a.warmup):
+        loss = step(*batches[i % 2])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(*batches[i % 2])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    value = a.batch * world * a.steps / dt
+    key = a.model if a.res == 224 else f"{a.model}_{a.res}"
+    base = STOCK_1GPU.get(key)
+    loss_v = float(loss.detach().float().item())
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / (base * world), 4) if base else None,
+            "dtype": "bf16", "data": "synthetic (on-device, random-init weights)",
+            "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": None,
+                       "image_size": a.res, "batch_per_gpu": a.batch,
+                       "parallelism": f"dp{world}", "impl": a.impl,
+                       "optimizer": "SGD(lr=0.1,momentum=0.9,wd=1e-4)"},
+            "final_loss": loss_v}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,544 @@
+// Python bindings of mipipe's gfx950 kernels (module ``mipipe._C``).
+//
+// Every entry validates dtypes, contiguity and the shape constraints the kernels and their
+// grids assume (NHWC, channels % 8 == 0, K % 8 == 0 ...) on the HOST before launching, so a bad
+// call raises a Python error instead of faulting the GPU.  Outputs are allocated with the torch
+// caching allocator and kernels run on the current HIP stream (graph-capturable).
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "kernels/launchers.hpp"
+
+using torch::Tensor;
+using c10::optional;
+
+namespace {
+
+hipStream_t stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_bf16(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16, got ", t.scalar_type());
+}
+void check_f32(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32, got ", t.scalar_type());
+}
+void check_vec(const Tensor& t, int64_t C, const char* name) {
+  check_f32(t, name);
+  TORCH_CHECK(t.numel() == C, name, " must have ", C, " elements, got ", t.numel());
+}
+const void* ptr_or_null(const optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int pad) {
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv expects NHWC x and [Co,KH,KW,Ci] w");
+  mipipe::ConvShape s;
+  s.N = (int)x.size(0); s.H = (int)x.size(1); s.W = (int)x.size(2); s.Ci = (int)x.size(3);
+  s.Co = (int)w.size(0); s.KH = (int)w.size(1); s.KW = (int)w.size(2);
+  TORCH_CHECK(w.size(3) == s.Ci, "weight Ci ", w.size(3), " != input channels ", s.Ci);
+  TORCH_CHECK(stride >= 1 && pad >= 0, "bad stride/pad");
+  s.stride = stride; s.pad = pad;
+  s.Ho = (s.H + 2 * pad - s.KH) / stride + 1;
+  s.Wo = (s.W + 2 * pad - s.KW) / stride + 1;
+  TORCH_CHECK(s.Ho > 0 && s.Wo > 0, "empty conv output");
+  TORCH_CHECK(s.Ci % 8 == 0, "conv kernels need Ci % 8 == 0 (pad channels), got ", s.Ci);
+  TORCH_CHECK(s.Co % 8 == 0, "conv kernels need Co % 8 == 0, got ", s.Co);
+  TORCH_CHECK((int64_t)s.N * s.H * s.W * s.Ci < (1ll << 31) &&
+                  (int64_t)s.N * s.Ho * s.Wo * s.Co < (1ll << 31),
+              "conv tensors beyond 2^31 elements are not supported");
+  return s;
+}
+
+// ------------------------------------------------------------------------------- conv
+std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor w, int stride,
+                                                                int pad, optional<Tensor> shift) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  c10::DeviceGuard g(x.device());
+  auto s = conv_shape(x, w, stride, pad);
+  auto y = torch::empty({s.N, s.Ho, s.Wo, s.Co}, x.options());
+  optional<Tensor> ps, pss;
+  float *psp = nullptr, *pssp = nullptr;
+  const float* sh = nullptr;
+  if (shift.has_value()) {
+    check_vec(*shift, s.Co, "stats_shift");
+    int P = mipipe::conv_fwd_stat_rows(s);
+    ps = torch::empty({P, s.Co}, x.options().dtype(at::kFloat));
+    pss = torch::empty({P, s.Co}, x.options().dtype(at::kFloat));
+    psp = ps->data_ptr<float>();
+    pssp = pss->data_ptr<float>();
+    sh = shift->data_ptr<float>();
+  }
+  mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), psp, pssp, sh, s, stream());
+  return {y, ps, pss};
+}
+
+Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride, int pad) {
+  check_bf16(dy, "dy");
+  check_bf16(w, "w");
+  c10::DeviceGuard g(dy.device());
+  TORCH_CHECK(x_shape.size() == 4, "x_shape must be [N,H,W,Ci]");
+  auto xmeta = torch::empty({0}, dy.options());
+  mipipe::ConvShape s;
+  s.N = (int)x_shape[0]; s.H = (int)x_shape[1]; s.W = (int)x_shape[2]; s.Ci = (int)x_shape[3];
+  s.Co = (int)w.size(0); s.KH = (int)w.size(1); s.KW = (int)w.size(2);
+  TORCH_CHECK(w.size(3) == s.Ci, "weight/input channel mismatch");
+  s.stride = stride; s.pad = pad;
+  s.Ho = (s.H + 2 * pad - s.KH) / stride + 1;
+  s.Wo = (s.W + 2 * pad - s.KW) / stride + 1;
+  TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo && dy.size(3) == s.Co,
+              "dy shape does not match the convolution");
+  TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv dgrad needs Ci, Co % 8 == 0");
+  auto dx = torch::empty({s.N, s.H, s.W, s.Ci}, dy.options());
+  mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream());
+  return dx;
+}
+
+Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  c10::DeviceGuard g(dy.device());
+  mipipe::ConvShape s;
+  s.N = (int)x.size(0); s.H = (int)x.size(1); s.W = (int)x.size(2); s.Ci = (int)x.size(3);
+  s.Co = (int)dy.size(3); s.KH = kh; s.KW = kw; s.stride = stride; s.pad = pad;
+  s.Ho = (s.H + 2 * pad - kh) / stride + 1;
+  s.Wo = (s.W + 2 * pad - kw) / stride + 1;
+  TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo, "dy/x mismatch");
+  TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv wgrad needs Ci, Co % 8 == 0");
+  auto dw = torch::zeros({s.Co, kh, kw, s.Ci}, x.options().dtype(at::kFloat));
+  mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream());
+  return dw;
+}
+
+// ------------------------------------------------------------------------------- batchnorm
+std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(Tensor psum, Tensor psq, int64_t count,
+                                                       Tensor shift, Tensor gamma, Tensor beta,
+                                                       optional<Tensor> rm, optional<Tensor> rv,
+                                                       double momentum, double eps) {
+  check_f32(psum, "psum");
+  check_f32(psq, "psumsq");
+  c10::DeviceGuard g(psum.device());
+  int64_t C = psum.size(-1);
+  int64_t P = psum.numel() / C;
+  check_vec(shift, C, "shift");
+  check_vec(gamma, C, "gamma");
+  check_vec(beta, C, "beta");
+  if (rm.has_value()) {
+    check_vec(*rm, C, "running_mean");
+    check_vec(*rv, C, "running_var");
+  }
+  auto o = psum.options();
+  auto mean = torch::empty({C}, o), invstd = torch::empty({C}, o), scale = torch::empty({C}, o),
+       bias = torch::empty({C}, o);
+  auto work = torch::empty({3 * 32 * C}, o);
+  mipipe::bn_finalize(psum.data_ptr<float>(), psq.data_ptr<float>(), (int)P, (int)C, count,
+                      shift.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                      rm.has_value() ? rm->data_ptr<float>() : nullptr,
+                      rv.has_value() ? rv->data_ptr<float>() : nullptr, (float)momentum,
+                      (float)eps, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                      scale.data_ptr<float>(), bias.data_ptr<float>(), work.data_ptr<float>(),
+                      stream());
+  return {mean, invstd, scale, bias};
+}
+
+Tensor bn_act_fwd(Tensor y, Tensor scale, Tensor bias, bool relu, optional<Tensor> r,
+                  optional<Tensor> rscale, optional<Tensor> rbias) {
+  check_bf16(y, "y");
+  c10::DeviceGuard g(y.device());
+  int64_t C = y.size(-1), M = y.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bn_act_fwd needs C % 8 == 0");
+  check_vec(scale, C, "scale");
+  check_vec(bias, C, "bias");
+  if (r.has_value()) {
+    check_bf16(*r, "residual");
+    TORCH_CHECK(r->sizes() == y.sizes(), "residual shape mismatch");
+  }
+  if (rscale.has_value()) {
+    check_vec(*rscale, C, "res_scale");
+    check_vec(*rbias, C, "res_bias");
+  }
+  auto z = torch::empty_like(y);
+  mipipe::bn_act_fwd(y.data_ptr(), scale.data_ptr<float>(), bias.data_ptr<float>(), ptr_or_null(r),
+                     rscale.has_value() ? rscale->data_ptr<float>() : nullptr,
+                     rbias.has_value() ? rbias->data_ptr<float>() : nullptr, z.data_ptr(), M,
+                     (int)C, relu, stream());
+  return z;
+}
+
+std::tuple<Tensor, Tensor, optional<Tensor>> bn_act_bwd_reduce(
+    Tensor dz, Tensor z, Tensor y, Tensor mean, Tensor invstd, bool relu, optional<Tensor> y2,
+    optional<Tensor> mean2, optional<Tensor> invstd2) {
+  check_bf16(dz, "dz");
+  check_bf16(z, "z");
+  check_bf16(y, "y");
+  c10::DeviceGuard g(dz.device());
+  int64_t C = y.size(-1), M = y.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && dz.sizes() == y.sizes() && z.sizes() == y.sizes(), "shape mismatch");
+  check_vec(mean, C, "mean");
+  check_vec(invstd, C, "invstd");
+  if (y2.has_value()) {
+    check_bf16(*y2, "y2");
+    TORCH_CHECK(y2->sizes() == y.sizes(), "y2 shape mismatch");
+    check_vec(*mean2, C, "mean2");
+    check_vec(*invstd2, C, "invstd2");
+  }
+  auto o = y.options().dtype(at::kFloat);
+  auto sg = torch::empty({C}, o), sgx = torch::empty({C}, o);
+  optional<Tensor> sgx2;
+  if (y2.has_value()) sgx2 = torch::empty({C}, o);
+  int G = mipipe::bn_bwd_partials(M, (int)C);
+  auto work = torch::empty({(3L * G + 3L * 32) * C}, o);
+  mipipe::bn_act_bwd_reduce(dz.data_ptr(), z.data_ptr(), y.data_ptr(), mean.data_ptr<float>(),
+                            invstd.data_ptr<float>(), ptr_or_null(y2),
+                            mean2.has_value() ? mean2->data_ptr<float>() : nullptr,
+                            invstd2.has_value() ? invstd2->data_ptr<float>() : nullptr, relu, M,
+                            (int)C, sg.data_ptr<float>(), sgx.data_ptr<float>(),
+                            sgx2.has_value() ? sgx2->data_ptr<float>() : nullptr,
+                            work.data_ptr<float>(), stream());
+  return {sg, sgx, sgx2};
+}
+
+std::tuple<Tensor, optional<Tensor>> bn_act_bwd_apply(
+    Tensor dz, Tensor z, Tensor y, Tensor mean, Tensor invstd, Tensor gamma, Tensor sum_g,
+    Tensor sum_gx, int64_t count, bool relu, bool want_dres, optional<Tensor> y2,
+    optional<Tensor> mean2, optional<Tensor> invstd2, optional<Tensor> gamma2,
+    optional<Tensor> sum_gx2) {
+  check_bf16(dz, "dz");
+  check_bf16(z, "z");
+  check_bf16(y, "y");
+  c10::DeviceGuard g(dz.device());
+  int64_t C = y.size(-1), M = y.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && dz.sizes() == y.sizes() && z.sizes() == y.sizes(), "shape mismatch");
+  for (auto* t : {&mean, &invstd, &gamma, &sum_g, &sum_gx}) check_vec(*t, C, "bn vector");
+  if (y2.has_value()) {
+    check_bf16(*y2, "y2");
+    TORCH_CHECK(y2->sizes() == y.sizes(), "y2 shape mismatch");
+    check_vec(*mean2, C, "mean2");
+    check_vec(*invstd2, C, "invstd2");
+    check_vec(*gamma2, C, "gamma2");
+    check_vec(*sum_gx2, C, "sum_gx2");
+  }
+  auto dy = torch::empty_like(y);
+  optional<Tensor> other;
+  if (y2.has_value() || want_dres) other = torch::empty_like(y);
+  mipipe::bn_act_bwd_apply(
+      dz.data_ptr(), z.data_ptr(), y.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+      gamma.data_ptr<float>(), sum_g.data_ptr<float>(), sum_gx.data_ptr<float>(), ptr_or_null(y2),
+      mean2.has_value() ? mean2->data_ptr<float>() : nullptr,
+      invstd2.has_value() ? invstd2->data_ptr<float>() : nullptr,
+      gamma2.has_value() ? gamma2->data_ptr<float>() : nullptr,
+      sum_gx2.has_value() ? sum_gx2->data_ptr<float>() : nullptr, count, relu, want_dres,
+      dy.data_ptr(), other.has_value() ? other->data_ptr() : nullptr, M, (int)C, stream());
+  return {dy, other};
+}
+
+// ------------------------------------------------------------------------------- pooling
+std::tuple<Tensor, Tensor> maxpool_fwd(Tensor x, int k, int s, int p) {
+  check_bf16(x, "x");
+  c10::DeviceGuard g(x.device());
+  int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && k <= 15, "maxpool needs C % 8 == 0 and k <= 15");
+  int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
+  auto y = torch::empty({N, Ho, Wo, C}, x.options());
+  auto idx = torch::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
+  mipipe::maxpool_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, k, s,
+                      p, stream());
+  return {y, idx};
+}
+
+Tensor maxpool_bwd(Tensor dy, Tensor idx, std::vector<int64_t> xs, int k, int s, int p) {
+  check_bf16(dy, "dy");
+  check_cuda(idx, "idx");
+  c10::DeviceGuard g(dy.device());
+  int N = xs[0], H = xs[1], W = xs[2], C = xs[3];
+  int Ho = dy.size(1), Wo = dy.size(2);
+  TORCH_CHECK(idx.sizes() == dy.sizes() && dy.size(3) == C, "maxpool_bwd shape mismatch");
+  auto dx = torch::empty({N, H, W, C}, dy.options());
+  mipipe::maxpool_bwd(dy.data_ptr(), idx.data_ptr<uint8_t>(), dx.data_ptr(), N, H, W, C, Ho, Wo, k,
+                      s, p, stream());
+  return dx;
+}
+
+Tensor avgpool_fwd(Tensor x) {
+  check_bf16(x, "x");
+  c10::DeviceGuard g(x.device());
+  int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0, "avgpool needs C % 8 == 0");
+  auto y = torch::empty({N, C}, x.options());
+  mipipe::avgpool_fwd(x.data_ptr(), y.data_ptr(), N, HW, C, stream());
+  return y;
+}
+
+Tensor avgpool_bwd(Tensor dy, std::vector<int64_t> xs) {
+  check_bf16(dy, "dy");
+  c10::DeviceGuard g(dy.device());
+  int N = xs[0], H = xs[1], W = xs[2], C = xs[3];
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == C, "avgpool_bwd shape mismatch");
+  auto dx = torch::empty({N, H, W, C}, dy.options());
+  mipipe::avgpool_bwd(dy.data_ptr(), dx.data_ptr(), N, H * W, C, stream());
+  return dx;
+}
+
+// ------------------------------------------------------------------------------- GEMM
+Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bias,
+            std::string act, at::ScalarType out_dtype, optional<Tensor> c, double beta) {
+  check_bf16(a, "A");
+  check_bf16(b, "B");
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm expects 2-D operands");
+  int64_t M = trans_a ? a.size(1) : a.size(0);
+  int64_t K = trans_a ? a.size(0) : a.size(1);
+  int64_t N = trans_b ? b.size(0) : b.size(1);
+  int64_t Kb = trans_b ? b.size(1) : b.size(0);
+  TORCH_CHECK(K == Kb, "gemm inner dims differ: ", K, " vs ", Kb);
+  TORCH_CHECK(M % 8 == 0 || !trans_a, "A^T operand needs M % 8 == 0");
+  TORCH_CHECK(K % 8 == 0 || (trans_a && !trans_b), "K-contiguous operands need K % 8 == 0");
+  TORCH_CHECK(N % 8 == 0, "gemm needs N % 8 == 0, got ", N);
+  TORCH_CHECK(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31), "gemm dims too large");
+  int act_i = act == "relu" ? 1 : 0;
+  TORCH_CHECK(act == "none" || act == "relu", "gemm epilogue act must be none|relu");
+  const float* bias_p = nullptr;
+  if (bias.has_value()) {
+    check_vec(*bias, N, "bias");
+    bias_p = bias->data_ptr<float>();
+  }
+  Tensor out;
+  int mode;
+  if (c.has_value() && beta != 0.0) {
+    TORCH_CHECK(beta == 1.0, "gemm supports beta in {0, 1}");
+    check_f32(*c, "C");
+    TORCH_CHECK(c->size(0) == M && c->size(1) == N, "C shape mismatch");
+    TORCH_CHECK(bias_p == nullptr && act_i == 0, "accumulating gemm has no epilogue");
+    out = *c;
+    mode = 2;
+  } else if (out_dtype == at::kFloat) {
+    out = torch::empty({M, N}, a.options().dtype(at::kFloat));
+    mode = 1;
+    TORCH_CHECK(act_i == 0, "fp32 gemm output has no activation epilogue");
+  } else {
+    TORCH_CHECK(out_dtype == at::kBFloat16, "gemm out dtype must be bf16 or fp32");
+    out = torch::empty({M, N}, a.options());
+    mode = 0;
+  }
+  mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b,
+               out.data_ptr(), N, (int)M, (int)N, (int)K, bias_p, act_i, mode, stream());
+  return out;
+}
+
+// ------------------------------------------------------------------------------- loss / optim
+std::tuple<Tensor, Tensor> cross_entropy_fwd_bwd(Tensor logits, Tensor labels, double smoothing,
+                                                 int64_t ignore_index) {
+  check_bf16(logits, "logits");
+  check_cuda(labels, "labels");
+  c10::DeviceGuard g(logits.device());
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  TORCH_CHECK(logits.dim() == 2 && labels.numel() == logits.size(0), "CE shape mismatch");
+  int R = logits.size(0), V = logits.size(1);
+  auto loss = torch::empty({}, logits.options().dtype(at::kFloat));
+  auto grad = torch::empty_like(logits);
+  auto work = torch::empty({4}, logits.options().dtype(at::kInt));
+  mipipe::cross_entropy_fwd_bwd(logits.data_ptr(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                                grad.data_ptr(), R, V, (float)smoothing, ignore_index,
+                                work.data_ptr<int>(), stream());
+  return {loss, grad};
+}
+
+void check_flat(const Tensor& t, int64_t n, const char* name) {
+  check_f32(t, name);
+  TORCH_CHECK(t.numel() == n, name, " size mismatch");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-B aligned");
+}
+
+void sgd_step(Tensor p, Tensor g, Tensor m, optional<Tensor> shadow, double lr, double momentum,
+              double dampening, double wd, bool nesterov, bool first, double grad_scale) {
+  int64_t n = p.numel();
+  TORCH_CHECK(n % 4 == 0, "flat buffer size must be a multiple of 4");
+  check_flat(p, n, "param");
+  check_flat(g, n, "grad");
+  check_flat(m, n, "momentum");
+  c10::DeviceGuard gd(p.device());
+  void* sh = nullptr;
+  if (shadow.has_value()) {
+    check_cuda(*shadow, "shadow");
+    TORCH_CHECK(shadow->numel() == n && shadow->scalar_type() == at::kBFloat16, "shadow mismatch");
+    sh = shadow->data_ptr();
+  }
+  mipipe::sgd_step(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), sh, n, (float)lr,
+                   (float)momentum, (float)dampening, (float)wd, nesterov, first,
+                   (float)grad_scale, stream());
+}
+
+void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, optional<Tensor> shadow, double lr,
+                double b1, double b2, double eps, double wd, int64_t step, double grad_scale) {
+  int64_t n = p.numel();
+  TORCH_CHECK(n % 4 == 0, "flat buffer size must be a multiple of 4");
+  check_flat(p, n, "param");
+  check_flat(g, n, "grad");
+  check_flat(m, n, "exp_avg");
+  check_flat(v, n, "exp_avg_sq");
+  c10::DeviceGuard gd(p.device());
+  void* sh = nullptr;
+  if (shadow.has_value()) {
+    TORCH_CHECK(shadow->numel() == n && shadow->scalar_type() == at::kBFloat16, "shadow mismatch");
+    sh = shadow->data_ptr();
+  }
+  double bc1 = 1.0 - std::pow(b1, (double)step), bc2 = 1.0 - std::pow(b2, (double)step);
+  mipipe::adamw_step(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
+                     v.data_ptr<float>(), sh, n, (float)lr, (float)b1, (float)b2, (float)eps,
+                     (float)wd, (float)bc1, (float)bc2, (float)grad_scale, stream());
+}
+
+Tensor nchw_to_nhwc(Tensor x, at::ScalarType dtype, int64_t pad_to) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(dtype == at::kBFloat16, "nchw_to_nhwc produces bf16");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be fp32/bf16");
+  TORCH_CHECK(x.dim() == 4, "x must be NCHW");
+  int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  int Cp = C;
+  if (pad_to > 0 && C % pad_to) Cp = (int)((C + pad_to - 1) / pad_to * pad_to);
+  Cp = (Cp + 7) / 8 * 8;
+  auto y = torch::empty({N, H, W, Cp}, x.options().dtype(at::kBFloat16));
+  mipipe::nchw_to_nhwc(x.data_ptr(), x.scalar_type() == at::kBFloat16, y.data_ptr(), N, C, H, W, Cp,
+                       stream());
+  return y;
+}
+
+std::tuple<Tensor, Tensor> synthetic_batch(Tensor idx, int C, int H, int W, int classes, int seed,
+                                           at::ScalarType dtype) {
+  check_cuda(idx, "indices");
+  c10::DeviceGuard g(idx.device());
+  TORCH_CHECK(idx.scalar_type() == at::kLong, "indices must be int64");
+  int n = idx.numel();
+  bool bf = dtype == at::kBFloat16;
+  TORCH_CHECK(bf || dtype == at::kFloat, "synthetic dtype must be fp32 or bf16");
+  auto x = torch::empty({n, C, H, W}, idx.options().dtype(dtype));
+  auto lab = torch::empty({n}, idx.options().dtype(at::kLong));
+  mipipe::synthetic_batch(idx.data_ptr<int64_t>(), n, C, H, W, classes, seed, x.data_ptr(), bf,
+                          lab.data_ptr<int64_t>(), stream());
+  return {x, lab};
+}
+
+// ------------------------------------------------------------------------------- transformer ops
+Tensor gelu_fwd(Tensor x) {
+  check_bf16(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.numel() % 8 == 0, "gelu needs numel % 8 == 0");
+  auto y = torch::empty_like(x);
+  mipipe::gelu_fwd(x.data_ptr(), y.data_ptr(), x.numel(), stream());
+  return y;
+}
+
+Tensor gelu_bwd(Tensor dy, Tensor x) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.sizes() == dy.sizes() && x.numel() % 8 == 0, "gelu_bwd shape mismatch");
+  auto dx = torch::empty_like(x);
+  mipipe::gelu_bwd(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), x.numel(), stream());
+  return dx;
+}
+
+std::tuple<Tensor, Tensor, Tensor, optional<Tensor>> layernorm_fwd(Tensor x, Tensor gamma,
+                                                                   Tensor beta, double eps,
+                                                                   optional<Tensor> res) {
+  check_bf16(x, "x");
+  c10::DeviceGuard g(x.device());
+  int64_t H = x.size(-1), rows = x.numel() / H;
+  TORCH_CHECK(H % 8 == 0 && H <= 2048, "layernorm needs H % 8 == 0 and H <= 2048");
+  check_vec(gamma, H, "gamma");
+  check_vec(beta, H, "beta");
+  optional<Tensor> xs;
+  if (res.has_value()) {
+    check_bf16(*res, "residual");
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape mismatch");
+    xs = torch::empty_like(x);
+  }
+  auto y = torch::empty_like(x);
+  auto o = x.options().dtype(at::kFloat);
+  auto shp = x.sizes().vec();
+  shp.pop_back();
+  auto mean = torch::empty(shp, o), rstd = torch::empty(shp, o);
+  mipipe::layernorm_fwd(x.data_ptr(), ptr_or_null(res), gamma.data_ptr<float>(),
+                        beta.data_ptr<float>(), y.data_ptr(), xs.has_value() ? xs->data_ptr() : nullptr,
+                        mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, (int)H, (float)eps,
+                        stream());
+  return {y, mean, rstd, xs};
+}
+
+std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd,
+                                                 Tensor gamma) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  c10::DeviceGuard g(x.device());
+  int64_t H = x.size(-1), rows = x.numel() / H;
+  TORCH_CHECK(H % 8 == 0 && H <= 2048 && dy.sizes() == x.sizes(), "layernorm_bwd shape mismatch");
+  check_vec(gamma, H, "gamma");
+  TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "mean/rstd size mismatch");
+  auto dx = torch::empty_like(x);
+  auto o = x.options().dtype(at::kFloat);
+  auto dg = torch::empty({H}, o), db = torch::empty({H}, o);
+  int64_t G = std::max<int64_t>(1, std::min<int64_t>(256, (rows + 15) / 16));
+  auto work = torch::empty({2 * G * H + 128 * H + 64}, o);
+  mipipe::layernorm_bwd(dy.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                        gamma.data_ptr<float>(), dx.data_ptr(), dg.data_ptr<float>(),
+                        db.data_ptr<float>(), work.data_ptr<float>(), rows, (int)H, stream());
+  return {dx, dg, db};
+}
+
+Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows) {
+  check_bf16(dy, "dy");
+  check_cuda(idx, "idx");
+  c10::DeviceGuard g(dy.device());
+  int64_t H = dy.size(-1), n = dy.numel() / H;
+  TORCH_CHECK(idx.numel() == n && idx.scalar_type() == at::kLong, "embedding_bwd idx mismatch");
+  auto out = torch::zeros({num_rows, H}, dy.options().dtype(at::kFloat));
+  mipipe::embedding_bwd(dy.data_ptr(), idx.data_ptr<int64_t>(), out.data_ptr<float>(), n, (int)H,
+                        stream());
+  return out;
+}
+
+Tensor colsum(Tensor x) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  int64_t cols = x.size(-1), rows = x.numel() / cols;
+  auto out = torch::empty({cols}, x.options().dtype(at::kFloat));
+  auto work = torch::empty({64 * cols}, x.options().dtype(at::kFloat));
+  mipipe::colsum_f32(x.data_ptr(), x.scalar_type() == at::kBFloat16, out.data_ptr<float>(), rows,
+                     (int)cols, work.data_ptr<float>(), stream());
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "mipipe gfx950 (MI355X) HIP kernels";
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_act_fwd", &bn_act_fwd);
+  m.def("bn_act_bwd_reduce", &bn_act_bwd_reduce);
+  m.def("bn_act_bwd_apply", &bn_act_bwd_apply);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd_impl", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("gemm", &gemm);
+  m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
+  m.def("sgd_step", &sgd_step);
+  m.def("adamw_step", &adamw_step);
+  m.def("nchw_to_nhwc", &nchw_to_nhwc);
+  m.def("synthetic_batch", &synthetic_batch);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.def("colsum", &colsum);
+}

@@ -1,0 +1,87 @@
+// Shared device helpers for mipipe's gfx950 (MI355X / CDNA4) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+#include <algorithm>
+
+namespace mipipe {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+constexpr int kWave = 64;  // CDNA wavefront width
+
+__device__ __forceinline__ float bf2f(__bf16 v) { return (float)v; }
+__device__ __forceinline__ __bf16 f2bf(float v) { return (__bf16)v; }
+
+__device__ __forceinline__ float bf16_bits_to_f(uint16_t b) {
+  return __uint_as_float(((uint32_t)b) << 16);
+}
+
+// Unpack 8 bf16 held in a uint4 to floats.
+__device__ __forceinline__ void unpack8(const uint4& u, float* f) {
+  f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+  f[4] = __uint_as_float(u.z << 16); f[5] = __uint_as_float(u.z & 0xffff0000u);
+  f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  bf16x2 v = {(__bf16)a, (__bf16)b};
+  return *reinterpret_cast<uint32_t*>(&v);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Fast unsigned division by a runtime constant (Granlund-Montgomery "round-up" variant).
+struct FastDiv {
+  uint32_t d, m, s;
+  __host__ __device__ FastDiv() : d(1), m(0), s(0) {}
+  __host__ __device__ explicit FastDiv(uint32_t div) : d(div) {
+    s = 0;
+    while ((1ull << s) < div) ++s;
+    m = (uint32_t)((((1ull << 32) * ((1ull << s) - div)) / div) + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    uint32_t t = __umulhi(n, m);
+    return (t + ((n - t) >> 1)) >> (s > 0 ? s - 1 : 0);
+  }
+};
+
+// s == 0 (div by 1) special case handled by callers passing d >= 1: for d == 1, s = 0, m = 1
+// gives t = n>>32=0... guard explicitly.
+__device__ __forceinline__ uint32_t fdiv(const FastDiv& f, uint32_t n) {
+  return f.d == 1 ? n : f.div(n);
+}
+
+// XCD-aware bijective remap of a linear workgroup id (guide §5 "XCD swizzle must be
+// bijective"): consecutive logical tiles land on the same XCD (shared L2).
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t wg, uint32_t nwg) {
+  constexpr uint32_t NX = 8;
+  if (nwg < NX) return wg;
+  uint32_t q = nwg / NX, r = nwg % NX;
+  uint32_t x = wg % NX, l = wg / NX;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
+}
+
+}  // namespace mipipe

@@ -1,0 +1,216 @@
+// Implicit-GEMM convolution (forward, data-grad, weight-grad) for NHWC bf16 on gfx950.
+//
+//   forward : M = N*Ho*Wo, N = Co, K = KH*KW*Ci   A = im2col(x) (gathered rows), B = W[Co][K]
+//   dgrad   : M = N*H*W,   N = Ci, K = KH*KW*Co   A = gather(dy), B = W viewed [K=(tap,co)][Ci]
+//   wgrad   : M = Co, N = KH*KW*Ci, K = N*Ho*Wo  A = dy^T (k-major), B = im2col(x)^T, split-K
+//
+// Forward fuses the BatchNorm batch-statistics reduction into its epilogue (shifted per-channel
+// sum / sum-of-squares of the fp32 accumulators), so BN never re-reads y for statistics.
+// 1x1 / stride-1 / pad-0 convolutions take the dense-operand fast path (no gather math).
+#include "epilogue.hpp"
+#include "launchers.hpp"
+
+namespace mipipe {
+namespace gk {
+
+__device__ __attribute__((aligned(64))) uint4 g_conv_zero[8];
+
+template <int BM, int BN>
+constexpr int lds_bytes_bf16() {
+  constexpr int a = 2 * (BM + BN) * BK * 2;
+  constexpr int b = BM * (BN * 2 + 16);
+  return a > b ? a : b;
+}
+template <int BM, int BN>
+constexpr int lds_bytes_f32() {
+  constexpr int a = 2 * (BM + BN) * BK * 2;
+  constexpr int b = BM * (BN * 4 + 16);
+  return a > b ? a : b;
+}
+
+template <int BM, int BN, bool DENSE>
+__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restrict__ x,
+                                                           const __bf16* __restrict__ w,
+                                                           ConvGeom g, uint32_t M, uint32_t tilesN,
+                                                           EpiParams e) {
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_bf16<BM, BN>()];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t tm = id / tilesN, tn = id % tilesN;
+  const uint32_t m0 = tm * BM, n0 = tn * BN;
+  const uint32_t K = (uint32_t)(g.KH * g.KW * g.C);
+  const int nk = (int)((K + BK - 1) / BK);
+  typedef typename std::conditional<DENSE, KCDense<BM>, KCIm2col<BM>>::type OpA;
+  OpA a;
+  if constexpr (DENSE) a.init(x, g.C, M, K, m0, wave, lane, g_conv_zero);
+  else a.init(x, g, M, m0, wave, lane, g_conv_zero);
+  KCDense<BN> b;
+  b.init(w, K, e.N, K, n0, wave, lane, g_conv_zero);
+  f32x4 acc[BM / 32][BN / 32];
+  MainLoop<BM, BN, OpA, KCDense<BN>>::run(smem, a, b, 0, nk, acc, wave, lane);
+  epilogue_bf16<BM, BN>(smem, acc, e, m0, n0, tm * 2, wave, lane);
+}
+
+template <int BM, int BN, bool DENSE>
+__global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const __bf16* __restrict__ dy,
+                                                             const __bf16* __restrict__ w,
+                                                             ConvGeom g, FastDiv fHW, FastDiv fW,
+                                                             uint32_t M, uint32_t tilesN,
+                                                             EpiParams e) {
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_bf16<BM, BN>()];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t tm = id / tilesN, tn = id % tilesN;
+  const uint32_t m0 = tm * BM, n0 = tn * BN;
+  const uint32_t Co = (uint32_t)g.C, Ci = e.N, taps = (uint32_t)(g.KH * g.KW);
+  const uint32_t K = taps * Co;
+  const int nk = (int)((K + BK - 1) / BK);
+  typedef typename std::conditional<DENSE, KCDense<BM>, KCDgrad<BM>>::type OpA;
+  typedef typename std::conditional<DENSE, MCDense<BN>, MCDgradW<BN>>::type OpB;
+  OpA a;
+  OpB b;
+  if constexpr (DENSE) {
+    a.init(dy, Co, M, K, m0, wave, lane, g_conv_zero);
+    b.init(w, Ci, Ci, K, n0, wave, lane, g_conv_zero);
+  } else {
+    a.init(dy, g, fHW, fW, M, m0, wave, lane, g_conv_zero);
+    b.init(w, Co, taps, Ci, g.fC, n0, wave, lane, g_conv_zero);
+  }
+  f32x4 acc[BM / 32][BN / 32];
+  MainLoop<BM, BN, OpA, OpB>::run(smem, a, b, 0, nk, acc, wave, lane);
+  epilogue_bf16<BM, BN>(smem, acc, e, m0, n0, 0, wave, lane);
+}
+
+template <int BM, int BN, bool DENSE>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const __bf16* __restrict__ dy,
+                                                             const __bf16* __restrict__ x,
+                                                             ConvGeom g, uint32_t tilesN,
+                                                             int kt_per_split, EpiParams e) {
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_f32<BM, BN>()];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t tm = id / tilesN, tn = id % tilesN;
+  const uint32_t m0 = tm * BM, n0 = tn * BN;
+  const uint32_t Co = e.M;
+  const uint32_t K = (uint32_t)(g.N * g.Ho * g.Wo);
+  const int nk = (int)((K + BK - 1) / BK);
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int kt1 = min(nk, kt0 + kt_per_split);
+  MCDense<BM> a;
+  a.init(dy, Co, Co, K, m0, wave, lane, g_conv_zero);
+  typedef typename std::conditional<DENSE, MCDense<BN>, MCIm2colT<BN>>::type OpB;
+  OpB b;
+  if constexpr (DENSE) b.init(x, g.C, g.C, K, n0, wave, lane, g_conv_zero);
+  else b.init(x, g, n0, wave, lane, g_conv_zero);
+  f32x4 acc[BM / 32][BN / 32];
+  MainLoop<BM, BN, MCDense<BM>, OpB>::run(smem, a, b, kt0, kt1, acc, wave, lane);
+  epilogue_f32<BM, BN, true>(smem, acc, e, m0, n0, wave, lane);
+}
+
+}  // namespace gk
+
+using namespace gk;
+
+static ConvGeom make_geom(int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int stride,
+                          int pad) {
+  ConvGeom g;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.Ho = Ho; g.Wo = Wo;
+  g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
+  g.fHoWo = FastDiv((uint32_t)(Ho * Wo));
+  g.fWo = FastDiv((uint32_t)Wo);
+  g.fC = FastDiv((uint32_t)C);
+  g.fKW = FastDiv((uint32_t)KW);
+  return g;
+}
+
+static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+static bool is_dense(const ConvShape& s) {
+  return s.KH == 1 && s.KW == 1 && s.stride == 1 && s.pad == 0;
+}
+
+int conv_fwd_stat_rows(const ConvShape& s) {
+  long M = (long)s.N * s.Ho * s.Wo;
+  return (int)cdiv(M, 128) * 2;  // both tile configs use BM = 128
+}
+
+#define MIPIPE_LAUNCH(kern, grid, ...) hipLaunchKernelGGL((kern), (grid), dim3(256), 0, st, __VA_ARGS__)
+
+void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
+              const float* st_shift, const ConvShape& s, hipStream_t st) {
+  ConvGeom g = make_geom(s.N, s.H, s.W, s.Ci, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad);
+  uint32_t M = (uint32_t)s.N * s.Ho * s.Wo;
+  EpiParams e{};
+  e.C = y; e.ldc = s.Co; e.M = M; e.N = s.Co; e.bias = nullptr; e.act = 0;
+  e.st_sum = st_sum; e.st_sq = st_sq; e.st_shift = st_shift; e.st_rows_per_block = 2;
+  const bool dense = is_dense(s);
+  const __bf16* xp = (const __bf16*)x;
+  const __bf16* wp = (const __bf16*)w;
+  if (s.Co <= 64) {
+    uint32_t tN = cdiv(s.Co, 64), tiles = cdiv(M, 128) * tN;
+    if (dense) MIPIPE_LAUNCH((conv_fwd_kernel<128, 64, true>), dim3(tiles), xp, wp, g, M, tN, e);
+    else MIPIPE_LAUNCH((conv_fwd_kernel<128, 64, false>), dim3(tiles), xp, wp, g, M, tN, e);
+  } else {
+    uint32_t tN = cdiv(s.Co, 128), tiles = cdiv(M, 128) * tN;
+    if (dense) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, true>), dim3(tiles), xp, wp, g, M, tN, e);
+    else MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, false>), dim3(tiles), xp, wp, g, M, tN, e);
+  }
+}
+
+void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st) {
+  // geometry seen from the dgrad GEMM: N,H,W = dx dims; C = Co (dy channels); Ho,Wo = dy dims
+  ConvGeom g = make_geom(s.N, s.H, s.W, s.Co, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad);
+  FastDiv fHW((uint32_t)(s.H * s.W)), fW((uint32_t)s.W);
+  uint32_t M = (uint32_t)s.N * s.H * s.W;
+  EpiParams e{};
+  e.C = dx; e.ldc = s.Ci; e.M = M; e.N = s.Ci;
+  const bool dense = is_dense(s);
+  const __bf16* dyp = (const __bf16*)dy;
+  const __bf16* wp = (const __bf16*)w;
+  if (s.Ci <= 64) {
+    uint32_t tN = cdiv(s.Ci, 64), tiles = cdiv(M, 128) * tN;
+    if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 64, true>), dim3(tiles), dyp, wp, g, fHW, fW, M, tN, e);
+    else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 64, false>), dim3(tiles), dyp, wp, g, fHW, fW, M, tN, e);
+  } else {
+    uint32_t tN = cdiv(s.Ci, 128), tiles = cdiv(M, 128) * tN;
+    if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true>), dim3(tiles), dyp, wp, g, fHW, fW, M, tN, e);
+    else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, false>), dim3(tiles), dyp, wp, g, fHW, fW, M, tN, e);
+  }
+}
+
+static int pick_splits(uint32_t tiles, int nk) {
+  int target = 1024;
+  int splits = (int)std::max<uint32_t>(1, target / std::max<uint32_t>(1, tiles));
+  int max_splits = std::max(1, nk / 4);
+  return std::min(splits, max_splits);
+}
+
+void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st) {
+  ConvGeom g = make_geom(s.N, s.H, s.W, s.Ci, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad);
+  uint32_t Ntot = (uint32_t)(s.KH * s.KW * s.Ci);
+  EpiParams e{};
+  e.C = dw; e.ldc = Ntot; e.M = s.Co; e.N = Ntot;
+  const bool dense = is_dense(s);
+  long K = (long)s.N * s.Ho * s.Wo;
+  int nk = (int)cdiv(K, BK);
+  const __bf16* dyp = (const __bf16*)dy;
+  const __bf16* xp = (const __bf16*)x;
+  if (s.Co <= 64) {
+    uint32_t tN = cdiv(Ntot, 128), tiles = cdiv(s.Co, 64) * tN;
+    int splits = pick_splits(tiles, nk), per = (int)cdiv(nk, splits);
+    splits = (int)cdiv(nk, per);
+    if (dense) MIPIPE_LAUNCH((conv_wgrad_kernel<64, 128, true>), dim3(tiles, splits), dyp, xp, g, tN, per, e);
+    else MIPIPE_LAUNCH((conv_wgrad_kernel<64, 128, false>), dim3(tiles, splits), dyp, xp, g, tN, per, e);
+  } else {
+    uint32_t tN = cdiv(Ntot, 128), tiles = cdiv(s.Co, 128) * tN;
+    int splits = pick_splits(tiles, nk), per = (int)cdiv(nk, splits);
+    splits = (int)cdiv(nk, per);
+    if (dense) MIPIPE_LAUNCH((conv_wgrad_kernel<128, 128, true>), dim3(tiles, splits), dyp, xp, g, tN, per, e);
+    else MIPIPE_LAUNCH((conv_wgrad_kernel<128, 128, false>), dim3(tiles, splits), dyp, xp, g, tN, per, e);
+  }
+}
+
+}  // namespace mipipe

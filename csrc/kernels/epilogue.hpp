@@ -1,0 +1,156 @@
+// GEMM epilogues: bf16 store (+bias, +ReLU, +BatchNorm partial statistics) and fp32
+// store / split-K atomic accumulate.  All stage the tile through LDS so global traffic is
+// whole 16-B (bf16) or 256-B-contiguous (fp32 atomics) row segments.
+#pragma once
+#include "gemm_core.hpp"
+
+namespace mipipe {
+namespace gk {
+
+struct EpiParams {
+  void* C;           // bf16 or fp32 output
+  long ldc;
+  uint32_t M, N;
+  const float* bias;  // per column, may be null
+  int act;            // 0 none, 1 relu
+  // BatchNorm partials (per column, shifted): slab[prow][N] sum / sumsq; null if unused
+  float* st_sum;
+  float* st_sq;
+  const float* st_shift;
+  int st_rows_per_block;  // 2 (one per wave row)
+};
+
+// bf16 output.  acc layout: lane holds C[m][n..n+3] for tile (i, j).
+template <int BM, int BN>
+__device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const EpiParams& e,
+                              uint32_t m0, uint32_t n0, uint32_t prow_base, int wave, int lane) {
+  constexpr int MT = BM / 32, NT = BN / 32;
+  const int wr = wave >> 1, wc = wave & 1;
+  const uint32_t ml0 = wr * (BM / 2) + (lane & 15);
+  const uint32_t nl0 = wc * (BN / 2) + (lane >> 4) * 4;
+  // bias / activation
+  if (e.bias != nullptr || e.act) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      uint32_t n = n0 + nl0 + j * 16;
+      float b[4] = {0.f, 0.f, 0.f, 0.f};
+      if (e.bias != nullptr) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b[q] = (n + q < e.N) ? e.bias[n + q] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v = acc[i][j][q] + b[q];
+          acc[i][j][q] = e.act == 1 ? fmaxf(v, 0.f) : v;
+        }
+    }
+  }
+  // BatchNorm partial statistics from the fp32 accumulators
+  if (e.st_sum != nullptr) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      uint32_t n = n0 + nl0 + j * 16;
+      float sh[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sh[q] = (n + q < e.N) ? e.st_shift[n + q] : 0.f;
+      float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        uint32_t m = m0 + ml0 + i * 16;
+        if (m < e.M) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float d = acc[i][j][q] - sh[q];
+            s[q] += d;
+            ss[q] += d * d;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s[q] += __shfl_xor(s[q], o);
+          ss[q] += __shfl_xor(ss[q], o);
+        }
+      }
+      if ((lane & 15) == 0 && n < e.N) {
+        uint32_t prow = prow_base + wr;
+        *reinterpret_cast<float4*>(e.st_sum + (long)prow * e.N + n) = make_float4(s[0], s[1], s[2], s[3]);
+        *reinterpret_cast<float4*>(e.st_sq + (long)prow * e.N + n) = make_float4(ss[0], ss[1], ss[2], ss[3]);
+      }
+    }
+  }
+  // stage bf16 tile in LDS: pitch BN*2 + 16 bytes
+  constexpr int P = BN * 2 + 16;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      uint32_t ml = ml0 + i * 16, nl = nl0 + j * 16;
+      uint2 v = make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+      *reinterpret_cast<uint2*>(smem + ml * P + nl * 2) = v;
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 16-B chunks per row
+  __bf16* C = reinterpret_cast<__bf16*>(e.C);
+  for (int c = threadIdx.x; c < BM * CPR; c += kThreads) {
+    uint32_t r = c / CPR, cc = c % CPR;
+    uint32_t m = m0 + r, n = n0 + cc * 8;
+    if (m < e.M && n < e.N) {
+      uint4 v = *reinterpret_cast<const uint4*>(smem + r * P + cc * 16);
+      *reinterpret_cast<uint4*>(C + (long)m * e.ldc + n) = v;
+    }
+  }
+}
+
+// fp32 output; ATOMIC accumulates into C (split-K), otherwise plain store (beta = 0).
+template <int BM, int BN, bool ATOMIC>
+__device__ void epilogue_f32(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const EpiParams& e,
+                             uint32_t m0, uint32_t n0, int wave, int lane) {
+  constexpr int MT = BM / 32, NT = BN / 32;
+  const int wr = wave >> 1, wc = wave & 1;
+  const uint32_t ml0 = wr * (BM / 2) + (lane & 15);
+  const uint32_t nl0 = wc * (BN / 2) + (lane >> 4) * 4;
+  // stage fp32 tile: pitch BN*4 + 16 bytes (BM*(BN*4+16) <= LDS of the main loop)
+  constexpr int P = BN * 4 + 16;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      uint32_t ml = ml0 + i * 16, nl = nl0 + j * 16;
+      *reinterpret_cast<float4*>(smem + ml * P + nl * 4) =
+          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  __syncthreads();
+  float* C = reinterpret_cast<float*>(e.C);
+  if constexpr (ATOMIC) {
+    // each wave-instruction: 64 lanes x 4 B = 256 contiguous bytes of one row
+    for (int c = threadIdx.x; c < BM * BN; c += kThreads) {
+      uint32_t r = c / BN, cc = c % BN;
+      uint32_t m = m0 + r, n = n0 + cc;
+      if (m < e.M && n < e.N) {
+        float v = *reinterpret_cast<const float*>(smem + r * P + cc * 4);
+        atomicAdd(C + (long)m * e.ldc + n, v);
+      }
+    }
+  } else {
+    constexpr int CPR = BN / 4;
+    for (int c = threadIdx.x; c < BM * CPR; c += kThreads) {
+      uint32_t r = c / CPR, cc = c % CPR;
+      uint32_t m = m0 + r, n = n0 + cc * 4;
+      if (m < e.M && n < e.N) {
+        float4 v = *reinterpret_cast<const float4*>(smem + r * P + cc * 16);
+        if (e.bias != nullptr) {
+          v.x += e.bias[n]; v.y += e.bias[n + 1]; v.z += e.bias[n + 2]; v.w += e.bias[n + 3];
+        }
+        *reinterpret_cast<float4*>(C + (long)m * e.ldc + n) = v;
+      }
+    }
+  }
+}
+
+}  // namespace gk
+}  // namespace mipipe

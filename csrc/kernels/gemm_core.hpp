@@ -1,0 +1,417 @@
+// Implicit-GEMM core on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), shared by convolution
+// forward / data-grad / weight-grad and the Linear (GEMM) kernels.
+//
+//   C[m][n] = sum_k A(m,k) * B(k,n),  bf16 operands, fp32 accumulation.
+//
+// Structure (cdna_hip_programming.md §5 "minimum 2-phase" + T1/T2/T10):
+//  * 256 threads = 4 waves (2x2), block tile BM x BN x 64, wave tile (BM/2) x (BN/2) made of
+//    16x16 MFMA tiles; LDS double buffer, one barrier per K-step.
+//  * Operands reach LDS with global_load_lds_dwordx4 (16 B per lane, 1 KiB per wave-instruction,
+//    lane-linear LDS destination).  Each operand policy computes a per-lane *source* address, so
+//    im2col / data-grad gathers are free, and padding taps point at a zero page.
+//  * Two LDS image formats:
+//      KC ("K-contiguous"): [rows][64 k] 128-B rows, 16-B chunk c stored at c ^ (row & 7);
+//          fragments by ds_read_b128 (conflict-free for the 16x16x32 lane map).
+//      MC ("M/N-contiguous"): [64 k][W cols] (W = 64 or 128) with an XOR chunk swizzle chosen so
+//          ds_read_b64_tr_b16 (hardware transpose, guide T10) is conflict-free; used when the
+//          operand is stored k-major in memory (weight-grad, Linear backward, dgrad weights).
+//    The swizzle is applied on the SOURCE address (glds writes linearly; guide rule 21).
+//  * MFMA runs in the swapped orientation D = B^T A^T so each lane ends with 4 consecutive
+//    output columns of one row -> 8-byte LDS writes in the epilogue, then fully coalesced 16-B
+//    global stores (or 256-B-contiguous fp32 atomics for split-K).
+//  * Workgroup ids are remapped XCD-aware (guide T1) so blocks sharing A-rows share an L2.
+#pragma once
+#include "common.hpp"
+
+namespace mipipe {
+namespace gk {
+
+constexpr int BK = 64;
+constexpr int kThreads = 256;
+
+// ---------------------------------------------------------------------------------------------
+// LDS image addressing
+__device__ __forceinline__ uint32_t kc_off(uint32_t row, uint32_t chunk) {
+  return row * 128u + ((chunk ^ (row & 7u)) << 4);
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t mc_swz(uint32_t row) {
+  if constexpr (W == 128) return ((row & 3u) << 2) | ((row >> 2) & 3u);
+  else return (((row >> 1) & 1u) << 1) | (((row >> 3) & 1u) << 2);
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t mc_off(uint32_t row, uint32_t chunk) {
+  return row * (uint32_t)(W * 2) + ((chunk ^ mc_swz<W>(row)) << 4);
+}
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Operand policies.  Each describes one operand (A: rows = M, or B: rows = N) and exposes
+//   static constexpr bool KC;               // image format
+//   __device__ void init(const P&, uint32_t tile_origin, int wave, int lane);
+//   __device__ const void* src(int kt, int i) const;   // i-th glds of this wave at k-step kt
+// KC: NI = R/32 instructions per wave, row = (wave*NI+i)*8 + lane/8, chunk = (lane&7)^(lane>>3)
+// MC: NI = W/32, RPI = 512/W rows per instruction, row = (wave*NI+i)*RPI + lane/(W/8)
+
+template <int R>
+struct KCGeom {
+  static constexpr int NI = R / 32;
+  __device__ static uint32_t row(int wave, int i, int lane) { return (wave * NI + i) * 8 + (lane >> 3); }
+  __device__ static uint32_t chunk(int lane) { return (lane & 7) ^ (lane >> 3); }
+};
+
+template <int W>
+struct MCGeom {
+  static constexpr int NI = W / 32;
+  static constexpr int RPI = 512 / W;
+  static constexpr int LPR = W / 8;
+  __device__ static uint32_t row(int wave, int i, int lane) { return (wave * NI + i) * RPI + lane / LPR; }
+  __device__ static uint32_t chunk(int wave, int i, int lane) {
+    return (uint32_t)(lane % LPR) ^ mc_swz<W>(row(wave, i, lane));
+  }
+};
+
+// Dense K-contiguous rows: element (r, k) at base[r*ld + k].
+template <int R>
+struct KCDense {
+  static constexpr bool KC = true;
+  static constexpr int NI = R / 32;
+  const __bf16* ptr[NI];
+  uint32_t kcol;
+  uint32_t K;
+  const void* zero;
+  __device__ void init(const __bf16* base, long ld, uint32_t rows_total, uint32_t K_,
+                       uint32_t origin, int wave, int lane, const void* zero_page) {
+    K = K_;
+    zero = zero_page;
+    kcol = KCGeom<R>::chunk(lane) * 8;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      uint32_t r = origin + KCGeom<R>::row(wave, i, lane);
+      ptr[i] = r < rows_total ? base + (long)r * ld + kcol : nullptr;
+    }
+  }
+  __device__ const void* src(int kt, int i) const {
+    uint32_t k = (uint32_t)kt * BK + kcol;
+    return (ptr[i] != nullptr && k < K) ? (const void*)(ptr[i] + (long)kt * BK) : zero;
+  }
+};
+
+// Conv forward A operand: im2col of NHWC x.  row m -> (img, ho, wo); k -> (kh, kw, ci).
+struct ConvGeom {
+  int N, H, W, C;        // input
+  int Ho, Wo;            // output
+  int KH, KW, stride, pad;
+  FastDiv fHoWo, fWo, fC, fKW;
+};
+
+template <int R>
+struct KCIm2col {
+  static constexpr bool KC = true;
+  static constexpr int NI = R / 32;
+  const __bf16* x;
+  int hi0[NI], wi0[NI];
+  long pix[NI];   // (img*H + hi0)*W + wi0 ; -1 when row invalid
+  uint32_t kcol, K;
+  ConvGeom g;
+  const void* zero;
+  __device__ void init(const __bf16* x_, const ConvGeom& g_, uint32_t M, uint32_t origin, int wave,
+                       int lane, const void* zero_page) {
+    x = x_;
+    g = g_;
+    zero = zero_page;
+    K = (uint32_t)(g.KH * g.KW * g.C);
+    kcol = KCGeom<R>::chunk(lane) * 8;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      uint32_t m = origin + KCGeom<R>::row(wave, i, lane);
+      if (m < M) {
+        uint32_t img = fdiv(g.fHoWo, m);
+        uint32_t rem = m - img * (uint32_t)(g.Ho * g.Wo);
+        uint32_t ho = fdiv(g.fWo, rem);
+        uint32_t wo = rem - ho * (uint32_t)g.Wo;
+        hi0[i] = (int)ho * g.stride - g.pad;
+        wi0[i] = (int)wo * g.stride - g.pad;
+        pix[i] = ((long)img * g.H + hi0[i]) * g.W + wi0[i];
+      } else {
+        hi0[i] = wi0[i] = -100000;
+        pix[i] = -1;
+      }
+    }
+  }
+  __device__ const void* src(int kt, int i) const {
+    uint32_t k = (uint32_t)kt * BK + kcol;
+    if (k >= K) return zero;  // invalid rows carry hi0 = -100000 -> fail the bounds check
+    uint32_t tap = fdiv(g.fC, k);
+    uint32_t ci = k - tap * (uint32_t)g.C;
+    uint32_t kh = fdiv(g.fKW, tap);
+    uint32_t kw = tap - kh * (uint32_t)g.KW;
+    int hi = hi0[i] + (int)kh, wi = wi0[i] + (int)kw;
+    if ((unsigned)hi >= (unsigned)g.H || (unsigned)wi >= (unsigned)g.W) return zero;
+    return x + (pix[i] + (long)kh * g.W + kw) * g.C + ci;
+  }
+};
+
+// Conv data-grad A operand: gather of NHWC dy.  row m -> (img, h, w) of dx; k -> (kh, kw, co);
+// source dy[img, (h+p-kh)/s, (w+p-kw)/s, co] when divisible and in range.
+template <int R>
+struct KCDgrad {
+  static constexpr bool KC = true;
+  static constexpr int NI = R / 32;
+  const __bf16* dy;
+  int h[NI], w[NI];
+  long imgbase[NI];  // img*Ho*Wo ; -1 invalid
+  uint32_t kcol, K;
+  ConvGeom g;  // here C = Co (dy channels); N,H,W describe dx; Ho,Wo describe dy
+  const void* zero;
+  FastDiv fHW, fW;
+  __device__ void init(const __bf16* dy_, const ConvGeom& g_, const FastDiv& fHW_, const FastDiv& fW_,
+                       uint32_t M, uint32_t origin, int wave, int lane, const void* zero_page) {
+    dy = dy_;
+    g = g_;
+    fHW = fHW_;
+    fW = fW_;
+    zero = zero_page;
+    K = (uint32_t)(g.KH * g.KW * g.C);
+    kcol = KCGeom<R>::chunk(lane) * 8;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      uint32_t m = origin + KCGeom<R>::row(wave, i, lane);
+      if (m < M) {
+        uint32_t img = fdiv(fHW, m);
+        uint32_t rem = m - img * (uint32_t)(g.H * g.W);
+        uint32_t hh = fdiv(fW, rem);
+        h[i] = (int)hh + g.pad;
+        w[i] = (int)(rem - hh * (uint32_t)g.W) + g.pad;
+        imgbase[i] = (long)img * g.Ho * g.Wo;
+      } else {
+        h[i] = w[i] = 0;
+        imgbase[i] = -1;
+      }
+    }
+  }
+  __device__ const void* src(int kt, int i) const {
+    uint32_t k = (uint32_t)kt * BK + kcol;
+    if (k >= K || imgbase[i] < 0) return zero;
+    uint32_t tap = fdiv(g.fC, k);
+    uint32_t co = k - tap * (uint32_t)g.C;
+    uint32_t kh = fdiv(g.fKW, tap);
+    uint32_t kw = tap - kh * (uint32_t)g.KW;
+    int hn = h[i] - (int)kh, wn = w[i] - (int)kw;
+    if (hn < 0 || wn < 0) return zero;
+    int ho = hn, wo = wn;
+    if (g.stride != 1) {
+      if ((hn % g.stride) | (wn % g.stride)) return zero;
+      ho = hn / g.stride;
+      wo = wn / g.stride;
+    }
+    if (ho >= g.Ho || wo >= g.Wo) return zero;
+    return dy + (imgbase[i] + (long)ho * g.Wo + wo) * g.C + co;
+  }
+};
+
+// Dense MN-contiguous operand: element (k, col) at base[k*ld + col]; W columns per tile.
+template <int W>
+struct MCDense {
+  static constexpr bool KC = false;
+  static constexpr int NI = W / 32;
+  const __bf16* colptr[NI];
+  uint32_t krow[NI];
+  long ld;
+  uint32_t K;
+  const void* zero;
+  __device__ void init(const __bf16* base, long ld_, uint32_t cols_total, uint32_t K_,
+                       uint32_t origin, int wave, int lane, const void* zero_page) {
+    ld = ld_;
+    K = K_;
+    zero = zero_page;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      krow[i] = MCGeom<W>::row(wave, i, lane);
+      uint32_t col = origin + MCGeom<W>::chunk(wave, i, lane) * 8;
+      colptr[i] = col < cols_total ? base + col : nullptr;
+    }
+  }
+  __device__ const void* src(int kt, int i) const {
+    uint32_t k = (uint32_t)kt * BK + krow[i];
+    return (colptr[i] != nullptr && k < K) ? (const void*)(colptr[i] + (long)k * ld) : zero;
+  }
+};
+
+// Conv data-grad B operand: B(k = (kh,kw,co), n = ci) = Wt[co][kh][kw][ci] (weights [Co,KH,KW,Ci]).
+template <int W>
+struct MCDgradW {
+  static constexpr bool KC = false;
+  static constexpr int NI = W / 32;
+  const __bf16* colptr[NI];
+  uint32_t krow[NI];
+  uint32_t K, Co, taps, Ci;
+  FastDiv fCo;
+  const void* zero;
+  __device__ void init(const __bf16* w, uint32_t Co_, uint32_t taps_, uint32_t Ci_, FastDiv fCo_,
+                       uint32_t origin, int wave, int lane, const void* zero_page) {
+    Co = Co_; taps = taps_; Ci = Ci_; fCo = fCo_;
+    K = Co * taps;
+    zero = zero_page;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      krow[i] = MCGeom<W>::row(wave, i, lane);
+      uint32_t col = origin + MCGeom<W>::chunk(wave, i, lane) * 8;
+      colptr[i] = col < Ci ? w + col : nullptr;
+    }
+  }
+  __device__ const void* src(int kt, int i) const {
+    uint32_t k = (uint32_t)kt * BK + krow[i];
+    if (colptr[i] == nullptr || k >= K) return zero;
+    uint32_t tap = fdiv(fCo, k);
+    uint32_t co = k - tap * Co;
+    return colptr[i] + ((long)co * taps + tap) * Ci;
+  }
+};
+
+// Conv weight-grad B operand: B(k = output pixel, n = (kh,kw,ci)) = x[img, ho*s-p+kh, wo*s-p+kw, ci].
+template <int W>
+struct MCIm2colT {
+  static constexpr bool KC = false;
+  static constexpr int NI = W / 32;
+  const __bf16* x;
+  uint32_t krow[NI];
+  int kh[NI], kw[NI], ci[NI];
+  bool colok[NI];
+  uint32_t K;
+  ConvGeom g;
+  const void* zero;
+  __device__ void init(const __bf16* x_, const ConvGeom& g_, uint32_t origin, int wave, int lane,
+                       const void* zero_page) {
+    x = x_;
+    g = g_;
+    zero = zero_page;
+    K = (uint32_t)(g.N * g.Ho * g.Wo);
+    uint32_t Ntot = (uint32_t)(g.KH * g.KW * g.C);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      krow[i] = MCGeom<W>::row(wave, i, lane);
+      uint32_t n = origin + MCGeom<W>::chunk(wave, i, lane) * 8;
+      colok[i] = n < Ntot;
+      uint32_t tap = fdiv(g.fC, n);
+      ci[i] = (int)(n - tap * (uint32_t)g.C);
+      uint32_t a = fdiv(g.fKW, tap);
+      kh[i] = (int)a;
+      kw[i] = (int)(tap - a * (uint32_t)g.KW);
+    }
+  }
+  __device__ const void* src(int kt, int i) const {
+    uint32_t k = (uint32_t)kt * BK + krow[i];
+    if (!colok[i] || k >= K) return zero;
+    uint32_t img = fdiv(g.fHoWo, k);
+    uint32_t rem = k - img * (uint32_t)(g.Ho * g.Wo);
+    uint32_t ho = fdiv(g.fWo, rem);
+    uint32_t wo = rem - ho * (uint32_t)g.Wo;
+    int hi = (int)ho * g.stride - g.pad + kh[i];
+    int wi = (int)wo * g.stride - g.pad + kw[i];
+    if ((unsigned)hi >= (unsigned)g.H || (unsigned)wi >= (unsigned)g.W) return zero;
+    return x + (((long)img * g.H + hi) * g.W + wi) * g.C + ci[i];
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Fragment loads from an LDS stage.
+template <bool KC, int R>
+struct FragLoader;
+
+template <int R>
+struct FragLoader<true, R> {  // KC image: ds_read_b128
+  __device__ static bf16x8 load(const char* img, uint32_t row0, int ks, int lane) {
+    uint32_t row = row0 + (lane & 15);
+    uint32_t chunk = ks * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + kc_off(row, chunk));
+  }
+};
+
+template <int W>
+struct FragLoader<false, W> {  // MC image: 2 x ds_read_b64_tr_b16
+  __device__ static bf16x8 load(const char* img, uint32_t col0, int ks, int lane) {
+    uint32_t g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    uint32_t c = (col0 >> 3) + (p >> 1);
+    uint32_t k0 = ks * 32 + 8 * g + q;
+    const char* a0 = img + mc_off<W>(k0, c) + 8 * (p & 1);
+    const char* a1 = img + mc_off<W>(k0 + 4, c) + 8 * (p & 1);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Main loop.  Returns accumulators acc[MT][NT] (swapped orientation: lane holds C[m][n..n+3]).
+template <int BM, int BN, class OpA, class OpB>
+struct MainLoop {
+  static constexpr int MT = BM / 32;  // 16-row tiles per wave (wave tile BM/2)
+  static constexpr int NT = BN / 32;
+  static constexpr int A_BYTES = BM * BK * 2;
+  static constexpr int B_BYTES = BN * BK * 2;
+  static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  static constexpr int LDS_BYTES = 2 * STAGE_BYTES;
+
+  __device__ static void stage(char* buf, const OpA& a, const OpB& b, int kt, int wave) {
+#pragma unroll
+    for (int i = 0; i < OpA::NI; ++i)
+      glds16(a.src(kt, i), buf + (wave * OpA::NI + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < OpB::NI; ++i)
+      glds16(b.src(kt, i), buf + A_BYTES + (wave * OpB::NI + i) * 1024);
+  }
+
+  __device__ static void run(char* smem, const OpA& a, const OpB& b, int kt0, int kt1,
+                             f32x4 (&acc)[MT][NT], int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (kt0 >= kt1) return;
+    const int wr = wave >> 1, wc = wave & 1;
+    const uint32_t arow0 = wr * (BM / 2), bcol0 = wc * (BN / 2);
+    stage(smem, a, b, kt0, wave);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      char* cbuf = smem + cur * STAGE_BYTES;
+      if (kt + 1 < kt1) stage(smem + (cur ^ 1) * STAGE_BYTES, a, b, kt + 1, wave);
+      const char* aimg = cbuf;
+      const char* bimg = cbuf + A_BYTES;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[MT], bfr[NT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          af[i] = FragLoader<OpA::KC, BM>::load(aimg, arow0 + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          bfr[j] = FragLoader<OpB::KC, BN>::load(bimg, bcol0 + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+};
+
+// Row/col of acc element: lane holds C[m][n + e], e = 0..3, for tile (i, j):
+//   m = block_m0 + wr*(BM/2) + i*16 + (lane & 15)
+//   n = block_n0 + wc*(BN/2) + j*16 + (lane >> 4)*4
+
+}  // namespace gk
+}  // namespace mipipe

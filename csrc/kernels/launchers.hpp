@@ -1,0 +1,97 @@
+// Host-side launch API of mipipe's gfx950 kernels (raw pointers + shapes + stream).
+// Bound to Python in csrc/bindings.cpp.  Every launcher is graph-capture safe: no
+// allocation, no synchronisation (cdna_hip_programming.md Guideline 9).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mipipe {
+
+// ---- convolution (NHWC activations, weights [Co][KH][KW][Ci]) --------------------------------
+struct ConvShape {
+  int N, H, W, Ci;   // input
+  int Co, KH, KW, stride, pad;
+  int Ho, Wo;        // output
+};
+
+// Number of BN-partial rows the forward kernel writes (stats slab height).
+int conv_fwd_stat_rows(const ConvShape& s);
+void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
+              const float* st_shift, const ConvShape& s, hipStream_t st);
+void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st);
+// dw must be zero-filled by the caller (split-K accumulates with fp32 atomics)
+void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st);
+
+// ---- dense GEMM: C[M][N] = op(A) op(B) --------------------------------------------------------
+//  a_kc: A stored [M][K] (else [K][M]);  b_kc: B stored [N][K] (else [K][N]).
+//  out: 0 = bf16 store (bias/act), 1 = fp32 store (bias), 2 = fp32 atomic accumulate (split-K).
+void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
+          long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st);
+
+// ---- BatchNorm ------------------------------------------------------------------------------
+// Reduce a [P][C] partial slab pair (shifted sums) and finalize: mean, invstd, scale, bias and
+// running-stat update.  work: >= 2*64*C floats scratch.
+void bn_finalize(const float* psum, const float* psq, int P, int C, long count, const float* shift,
+                 const float* gamma, const float* beta, float* run_mean, float* run_var,
+                 float momentum, float eps, float* mean, float* invstd, float* scale, float* bias,
+                 float* work, hipStream_t st);
+// z = act(y*scale + bias [+ r | + r*rscale + rbias])   (M rows of C channels, bf16)
+void bn_act_fwd(const void* y, const float* scale, const float* bias, const void* r,
+                const float* rscale, const float* rbias, void* z, long M, int C, bool relu,
+                hipStream_t st);
+// sums: out_g[C], out_gx[C], out_gx2[C] (if y2); work >= 3*P*C floats where P = partial rows
+int bn_bwd_partials(long M, int C);
+void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float* mean,
+                       const float* invstd, const void* y2, const float* mean2,
+                       const float* invstd2, bool relu, long M, int C, float* out_g,
+                       float* out_gx, float* out_gx2, float* work, hipStream_t st);
+void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float* mean,
+                      const float* invstd, const float* gamma, const float* sum_g,
+                      const float* sum_gx, const void* y2, const float* mean2,
+                      const float* invstd2, const float* gamma2, const float* sum_gx2, long count,
+                      bool relu, bool want_dres, void* dy, void* dother, long M, int C,
+                      hipStream_t st);
+
+// ---- pooling ----------------------------------------------------------------------------------
+void maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
+                 int k, int stride, int pad, hipStream_t st);
+void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C, int Ho,
+                 int Wo, int k, int stride, int pad, hipStream_t st);
+void avgpool_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st);
+void avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
+
+// ---- loss / optimizer / data -----------------------------------------------------------------
+void cross_entropy_fwd_bwd(const void* logits, const int64_t* labels, float* loss, void* grad,
+                           int R, int V, float smoothing, int64_t ignore_index, int* work,
+                           hipStream_t st);
+void sgd_step(float* p, const float* g, float* m, void* shadow, long n, float lr, float momentum,
+              float dampening, float wd, bool nesterov, bool first, float grad_scale,
+              hipStream_t st);
+void adamw_step(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr,
+                float b1, float b2, float eps, float wd, float bc1, float bc2, float grad_scale,
+                hipStream_t st);
+void nchw_to_nhwc(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int Cp,
+                  hipStream_t st);
+void synthetic_batch(const int64_t* idx, int n, int C, int H, int W, int classes, int seed,
+                     void* x, bool bf16_out, int64_t* labels, hipStream_t st);
+
+// ---- transformer ops ------------------------------------------------------------------------
+void layernorm_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y,
+                   void* xsum, float* mean, float* rstd, long rows, int H, float eps,
+                   hipStream_t st);
+void layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd,
+                   const float* gamma, void* dx, float* dgamma, float* dbeta, float* work,
+                   long rows, int H, hipStream_t st);
+void gelu_fwd(const void* x, void* y, long n, hipStream_t st);
+void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st);
+void attention_fwd(const void* q, const void* k, const void* v, const float* mask_bias, void* o,
+                   float* lse, int B, int H, int S, int D, float scale, hipStream_t st);
+void attention_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
+                   const float* lse, const float* mask_bias, void* dq, void* dk, void* dv,
+                   float* delta, float* dq_acc, int B, int H, int S, int D, float scale,
+                   hipStream_t st);
+void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, hipStream_t st);
+void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
+                hipStream_t st);
+
+}  // namespace mipipe

@@ -1,0 +1,548 @@
+// Memory-bound kernels of the training step: fused cross-entropy (fwd+bwd in one pass over
+// the logits), flat-buffer SGD-momentum / AdamW (one launch for the whole model, also emitting
+// the bf16 weight shadow), NCHW->NHWC input conversion, on-device synthetic data, GELU,
+// LayerNorm, embedding-grad scatter and column sums.  16-B vector accesses throughout
+// (cdna_hip_programming.md Guideline 13).
+#include "common.hpp"
+#include "launchers.hpp"
+
+namespace mipipe {
+
+static int grid1d(long work, int per_thread = 1, int cap = 8192) {
+  long g = (work / per_thread + 255) / 256;
+  return (int)std::max<long>(1, std::min<long>(g, cap));
+}
+
+// ------------------------------------------------------------------------------ cross-entropy
+__global__ void ce_count_kernel(const int64_t* __restrict__ labels, int R, int64_t ignore,
+                                int* __restrict__ out) {
+  __shared__ int red[256];
+  int c = 0;
+  for (int i = threadIdx.x; i < R; i += 256) c += labels[i] != ignore;
+  red[threadIdx.x] = c;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+__device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
+  v = is_max ? wave_max(v) : wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  float r = sh[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = is_max ? fmaxf(r, sh[i]) : r + sh[i];
+  return r;
+}
+
+// one block per row; logits bf16 [R][V]
+__global__ __launch_bounds__(256) void ce_kernel(const __bf16* __restrict__ logits,
+                                                 const int64_t* __restrict__ labels,
+                                                 float* __restrict__ loss, __bf16* __restrict__ grad,
+                                                 int V, float eps, int64_t ignore,
+                                                 const int* __restrict__ nvalid) {
+  __shared__ float sh[8];
+  const long row = blockIdx.x;
+  const __bf16* x = logits + row * V;
+  __bf16* g = grad + row * V;
+  const int64_t lab = labels[row];
+  const bool valid = lab != ignore;
+  const bool vec = (V % 8) == 0;
+  float mx = -INFINITY, sx = 0.f;
+  if (vec) {
+    for (int c = threadIdx.x; c < V / 8; c += 256) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + c * 8), v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        mx = fmaxf(mx, v[q]);
+        sx += v[q];
+      }
+    }
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) {
+      float v = (float)x[c];
+      mx = fmaxf(mx, v);
+      sx += v;
+    }
+  }
+  mx = block_reduce(mx, sh, true);
+  sx = block_reduce(sx, sh, false);
+  float se = 0.f;
+  if (vec) {
+    for (int c = threadIdx.x; c < V / 8; c += 256) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + c * 8), v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) se += __expf(v[q] - mx);
+    }
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) se += __expf((float)x[c] - mx);
+  }
+  se = block_reduce(se, sh, false);
+  const float lse = mx + __logf(se);
+  const float inv_n = 1.f / (float)max(1, nvalid[0]);
+  if (threadIdx.x == 0 && valid) {
+    float xl = (float)x[lab];
+    float l = (1.f - eps) * (lse - xl) + eps * (lse - sx / (float)V);
+    atomicAdd(loss, l * inv_n);
+  }
+  const float scale = valid ? inv_n : 0.f;
+  const float inv_se = 1.f / se;
+  const float base_t = eps / (float)V;
+  if (vec) {
+    for (int c = threadIdx.x; c < V / 8; c += 256) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + c * 8), v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        int col = c * 8 + q;
+        float t = base_t + (col == lab ? 1.f - eps : 0.f);
+        v[q] = (__expf(v[q] - mx) * inv_se - t) * scale;
+      }
+      *reinterpret_cast<uint4*>(g + c * 8) = pack8(v);
+    }
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) {
+      float t = base_t + (c == lab ? 1.f - eps : 0.f);
+      g[c] = (__bf16)((__expf((float)x[c] - mx) * inv_se - t) * scale);
+    }
+  }
+}
+
+void cross_entropy_fwd_bwd(const void* logits, const int64_t* labels, float* loss, void* grad,
+                           int R, int V, float smoothing, int64_t ignore_index, int* work,
+                           hipStream_t st) {
+  hipMemsetAsync(loss, 0, sizeof(float), st);
+  hipLaunchKernelGGL(ce_count_kernel, dim3(1), dim3(256), 0, st, labels, R, ignore_index, work);
+  hipLaunchKernelGGL(ce_kernel, dim3(R), dim3(256), 0, st, (const __bf16*)logits, labels, loss,
+                     (__bf16*)grad, V, smoothing, ignore_index, (const int*)work);
+}
+
+// ------------------------------------------------------------------------------ optimizers
+// SGD ([torch] optim/sgd.py:354-380): g += wd*p; m = momentum*m + (1-damp)*g (m = g first);
+// p -= lr * (nesterov ? g + momentum*m : m).  Flat fp32 buffers, n % 4 == 0.
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ m, __bf16* __restrict__ sh,
+                                                  long n4, float lr, float mom, float damp, float wd,
+                                                  bool nesterov, bool first, float gs) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (long)gridDim.x * blockDim.x) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float pa[4] = {pv.x, pv.y, pv.z, pv.w};
+    float ga[4] = {gv.x * gs, gv.y * gs, gv.z * gs, gv.w * gs};
+    if (mom != 0.f) {
+      float4 mv = reinterpret_cast<float4*>(m)[i];
+      float ma[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float d = ga[q] + wd * pa[q];
+        ma[q] = first ? d : mom * ma[q] + (1.f - damp) * d;
+        float upd = nesterov ? d + mom * ma[q] : ma[q];
+        pa[q] -= lr * upd;
+      }
+      reinterpret_cast<float4*>(m)[i] = make_float4(ma[0], ma[1], ma[2], ma[3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pa[q] -= lr * (ga[q] + wd * pa[q]);
+    }
+    reinterpret_cast<float4*>(p)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
+    if (sh != nullptr)
+      reinterpret_cast<uint2*>(sh)[i] = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));
+  }
+}
+
+void sgd_step(float* p, const float* g, float* m, void* shadow, long n, float lr, float momentum,
+              float dampening, float wd, bool nesterov, bool first, float grad_scale,
+              hipStream_t st) {
+  long n4 = n / 4;
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid1d(n4, 4)), dim3(256), 0, st, p, g, m, (__bf16*)shadow,
+                     n4, lr, momentum, dampening, wd, nesterov, first, grad_scale);
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    __bf16* __restrict__ sh, long n4, float lr,
+                                                    float b1, float b2, float eps, float wd,
+                                                    float bc1, float bc2, float gs) {
+  const float rbc2 = rsqrtf(bc2);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (long)gridDim.x * blockDim.x) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 mv = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float pa[4] = {pv.x, pv.y, pv.z, pv.w}, ga[4] = {gv.x, gv.y, gv.z, gv.w};
+    float ma[4] = {mv.x, mv.y, mv.z, mv.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float gq = ga[q] * gs;
+      pa[q] *= 1.f - lr * wd;
+      ma[q] = b1 * ma[q] + (1.f - b1) * gq;
+      va[q] = b2 * va[q] + (1.f - b2) * gq * gq;
+      float denom = sqrtf(va[q]) * rbc2 + eps;
+      pa[q] -= (lr / bc1) * ma[q] / denom;
+    }
+    reinterpret_cast<float4*>(p)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
+    reinterpret_cast<float4*>(m)[i] = make_float4(ma[0], ma[1], ma[2], ma[3]);
+    reinterpret_cast<float4*>(v)[i] = make_float4(va[0], va[1], va[2], va[3]);
+    if (sh != nullptr)
+      reinterpret_cast<uint2*>(sh)[i] = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));
+  }
+}
+
+void adamw_step(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr,
+                float b1, float b2, float eps, float wd, float bc1, float bc2, float grad_scale,
+                hipStream_t st) {
+  long n4 = n / 4;
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid1d(n4, 4)), dim3(256), 0, st, p, g, m, v,
+                     (__bf16*)shadow, n4, lr, b1, b2, eps, wd, bc1, bc2, grad_scale);
+}
+
+// ------------------------------------------------------------------------------ layout / data
+// x [N][C][H][W] (fp32 or bf16) -> y [N][H][W][Cp] bf16 (channels >= C zero)
+template <bool BF16IN>
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const void* __restrict__ xin,
+                                                           __bf16* __restrict__ y, int N, int C,
+                                                           int H, int W, int Cp) {
+  long total = (long)N * H * W;
+  long hw = (long)H * W;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long)gridDim.x * blockDim.x) {
+    long n = t / hw, pix = t % hw;
+    for (int c0 = 0; c0 < Cp; c0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        int c = c0 + q;
+        if (c < C) {
+          long src = (n * C + c) * hw + pix;
+          v[q] = BF16IN ? (float)reinterpret_cast<const __bf16*>(xin)[src]
+                        : reinterpret_cast<const float*>(xin)[src];
+        } else {
+          v[q] = 0.f;
+        }
+      }
+      *reinterpret_cast<uint4*>(y + t * Cp + c0) = pack8(v);
+    }
+  }
+}
+
+void nchw_to_nhwc(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int Cp,
+                  hipStream_t st) {
+  long total = (long)N * H * W;
+  if (x_is_bf16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<true>, dim3(grid1d(total)), dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, Cp);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<false>, dim3(grid1d(total)), dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, Cp);
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85EBCA77u;
+  x ^= x >> 13;
+  x *= 0xC2B2AE3Du;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ float u01(uint32_t h) { return ((float)(h >> 8) + 0.5f) * (1.f / 16777216.f); }
+
+// Same hash / Box-Muller as mipipe.data.synthetic.synthetic_batch (CPU reference).
+__global__ __launch_bounds__(256) void synthetic_kernel(const int64_t* __restrict__ idx, int n,
+                                                        int P, int classes, int seed,
+                                                        void* __restrict__ x, bool bf16_out,
+                                                        int64_t* __restrict__ labels) {
+  long total = (long)n * P;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long)gridDim.x * blockDim.x) {
+    int i = (int)(t / P);
+    uint32_t pos = (uint32_t)(t % P);
+    uint32_t id = (uint32_t)idx[i];
+    uint32_t lab = mix32(id * 0x9E3779B1u + (uint32_t)seed * 7919u + 17u) % (uint32_t)classes;
+    if (pos == 0) labels[i] = lab;
+    uint32_t tk = mix32(lab * 0x27D4EB2Fu + pos * 0x9E3779B1u + (uint32_t)seed * 31u + 1u);
+    float t1 = u01(tk), t2 = u01(mix32(tk + 0x165667B1u));
+    float templ = sqrtf(-2.f * logf(t1)) * cosf(6.283185307179586f * t2);
+    uint32_t nk = mix32(id * 0x632BE5ABu + pos * 0x85EBCA77u + (uint32_t)seed * 131u + 7u);
+    float u1 = u01(nk), u2 = u01(mix32(nk + 0x27D4EB2Fu));
+    float noise = sqrtf(-2.f * logf(u1)) * cosf(6.283185307179586f * u2);
+    float v = 0.5f * templ + noise;
+    if (bf16_out) reinterpret_cast<__bf16*>(x)[t] = (__bf16)v;
+    else reinterpret_cast<float*>(x)[t] = v;
+  }
+}
+
+void synthetic_batch(const int64_t* idx, int n, int C, int H, int W, int classes, int seed,
+                     void* x, bool bf16_out, int64_t* labels, hipStream_t st) {
+  int P = C * H * W;
+  hipLaunchKernelGGL(synthetic_kernel, dim3(grid1d((long)n * P)), dim3(256), 0, st, idx, n, P,
+                     classes, seed, x, bf16_out, labels);
+}
+
+// ------------------------------------------------------------------------------ GELU (erf)
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const __bf16* __restrict__ x,
+                                                       __bf16* __restrict__ y, long n8) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (long)gridDim.x * blockDim.x) {
+    float v[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = 0.5f * v[q] * (1.f + erff(v[q] * 0.70710678118654752f));
+    reinterpret_cast<uint4*>(y)[i] = pack8(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const __bf16* __restrict__ dy,
+                                                       const __bf16* __restrict__ x,
+                                                       __bf16* __restrict__ dx, long n8) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (long)gridDim.x * blockDim.x) {
+    float g[8], v[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[i], g);
+    unpack8(reinterpret_cast<const uint4*>(x)[i], v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float cdf = 0.5f * (1.f + erff(v[q] * 0.70710678118654752f));
+      float pdf = 0.3989422804014327f * __expf(-0.5f * v[q] * v[q]);
+      g[q] *= cdf + v[q] * pdf;
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(g);
+  }
+}
+
+void gelu_fwd(const void* x, void* y, long n, hipStream_t st) {
+  long n8 = n / 8;
+  hipLaunchKernelGGL(gelu_fwd_kernel, dim3(grid1d(n8)), dim3(256), 0, st, (const __bf16*)x,
+                     (__bf16*)y, n8);
+}
+
+void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st) {
+  long n8 = n / 8;
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(grid1d(n8)), dim3(256), 0, st, (const __bf16*)dy,
+                     (const __bf16*)x, (__bf16*)dx, n8);
+}
+
+// ------------------------------------------------------------------------------ column sums
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const void* __restrict__ x, bool bf16,
+                                                             float* __restrict__ part, long rows,
+                                                             int cols, long chunk) {
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rp = threadIdx.x >> 6;
+  __shared__ float red[4][64];
+  long r0 = (long)blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
+  float acc = 0.f;
+  if (col < cols)
+    for (long r = r0 + rp; r < r1; r += 4)
+      acc += bf16 ? (float)reinterpret_cast<const __bf16*>(x)[r * cols + col]
+                  : reinterpret_cast<const float*>(x)[r * cols + col];
+  red[rp][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rp == 0 && col < cols)
+    part[(long)blockIdx.y * cols + col] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ part, int S, int cols,
+                                    float* __restrict__ out) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float a = 0.f;
+  for (int s = 0; s < S; ++s) a += part[(long)s * cols + c];
+  out[c] = a;
+}
+
+void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
+                hipStream_t st) {
+  int S = (int)std::max<long>(1, std::min<long>(64, (rows + 255) / 256));
+  long chunk = (rows + S - 1) / S;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + 63) / 64, S), dim3(256), 0, st, x, bf16,
+                     work, rows, cols, chunk);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, st, work, S, cols,
+                     out);
+}
+
+// ------------------------------------------------------------------------------ embedding grad
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(const __bf16* __restrict__ dy,
+                                                            const int64_t* __restrict__ idx,
+                                                            float* __restrict__ out, long n, int H) {
+  long total = n * H;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long)gridDim.x * blockDim.x) {
+    long r = t / H;
+    int c = (int)(t % H);
+    atomicAdd(out + idx[r] * H + c, (float)dy[t]);
+  }
+}
+
+void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, hipStream_t st) {
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(grid1d(n * H)), dim3(256), 0, st,
+                     (const __bf16*)dy, idx, out, n, H);
+}
+
+// ------------------------------------------------------------------------------ LayerNorm
+// One wave per row, up to 4 x 8 elements per lane (H <= 2048), H % 8 == 0.
+constexpr int LN_MAXC = 4;
+
+__global__ __launch_bounds__(256) void layernorm_fwd_kernel(const __bf16* __restrict__ x,
+                                                            const __bf16* __restrict__ res,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta,
+                                                            __bf16* __restrict__ y,
+                                                            __bf16* __restrict__ xsum,
+                                                            float* __restrict__ mean,
+                                                            float* __restrict__ rstd, long rows,
+                                                            int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nc = H / 8;
+  float v[LN_MAXC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < LN_MAXC; ++k) {
+    int c = lane + k * 64;
+    if (c < nc) {
+      unpack8(*reinterpret_cast<const uint4*>(x + row * H + c * 8), v[k]);
+      if (res != nullptr) {
+        float r[8];
+        unpack8(*reinterpret_cast<const uint4*>(res + row * H + c * 8), r);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[k][q] += r[q];
+        *reinterpret_cast<uint4*>(xsum + row * H + c * 8) = pack8(v[k]);
+        unpack8(pack8(v[k]), v[k]);  // normalise the bf16-rounded sum that backward will see
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += v[k][q];
+    }
+  }
+  const float mu = wave_sum(s) / (float)H;
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < LN_MAXC; ++k) {
+    int c = lane + k * 64;
+    if (c < nc) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float d = v[k][q] - mu;
+        ss += d * d;
+      }
+    }
+  }
+  const float rs = rsqrtf(wave_sum(ss) / (float)H + eps);
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+#pragma unroll
+  for (int k = 0; k < LN_MAXC; ++k) {
+    int c = lane + k * 64;
+    if (c < nc) {
+      float o[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = (v[k][q] - mu) * rs * gamma[c * 8 + q] + beta[c * 8 + q];
+      *reinterpret_cast<uint4*>(y + row * H + c * 8) = pack8(o);
+    }
+  }
+}
+
+void layernorm_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y,
+                   void* xsum, float* mean, float* rstd, long rows, int H, float eps,
+                   hipStream_t st) {
+  hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, st,
+                     (const __bf16*)x, (const __bf16*)res, gamma, beta, (__bf16*)y,
+                     (__bf16*)xsum, mean, rstd, rows, H, eps);
+}
+
+// dx = rstd*(g*γ - mean(g*γ) - x̂*mean(g*γ*x̂)); per-block partials of Σg·x̂ and Σg for dγ, dβ.
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __restrict__ dy,
+                                                            const __bf16* __restrict__ x,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            const float* __restrict__ gamma,
+                                                            __bf16* __restrict__ dx,
+                                                            float* __restrict__ pg,
+                                                            float* __restrict__ pb, long rows,
+                                                            int H, int rows_per_block) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nc = H / 8;
+  float accg[LN_MAXC][8], accb[LN_MAXC][8];
+#pragma unroll
+  for (int k = 0; k < LN_MAXC; ++k)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) accg[k][q] = accb[k][q] = 0.f;
+  long r0 = (long)blockIdx.x * rows_per_block;
+  long r1 = min(rows, r0 + rows_per_block);
+  for (long row = r0 + w; row < r1; row += 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float g[LN_MAXC][8], xh[LN_MAXC][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < LN_MAXC; ++k) {
+      int c = lane + k * 64;
+      if (c < nc) {
+        unpack8(*reinterpret_cast<const uint4*>(dy + row * H + c * 8), g[k]);
+        unpack8(*reinterpret_cast<const uint4*>(x + row * H + c * 8), xh[k]);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          xh[k][q] = (xh[k][q] - mu) * rs;
+          accg[k][q] += g[k][q] * xh[k][q];
+          accb[k][q] += g[k][q];
+          float gg = g[k][q] * gamma[c * 8 + q];
+          s1 += gg;
+          s2 += gg * xh[k][q];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / (float)H;
+    s2 = wave_sum(s2) / (float)H;
+#pragma unroll
+    for (int k = 0; k < LN_MAXC; ++k) {
+      int c = lane + k * 64;
+      if (c < nc) {
+        float o[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = rs * (g[k][q] * gamma[c * 8 + q] - s1 - xh[k][q] * s2);
+        *reinterpret_cast<uint4*>(dx + row * H + c * 8) = pack8(o);
+      }
+    }
+  }
+  // block partial of dγ/dβ: reduce the 4 waves through LDS
+  __shared__ float red[4][LN_MAXC * 64 * 8 / 8];  // reused per array
+  for (int arr = 0; arr < 2; ++arr) {
+#pragma unroll
+    for (int k = 0; k < LN_MAXC; ++k) {
+      int c = lane + k * 64;
+      for (int q = 0; q < 8; ++q) {
+        __syncthreads();
+        if (c < nc) red[w][c] = arr == 0 ? accg[k][q] : accb[k][q];
+        __syncthreads();
+        if (w == 0 && c < nc) {
+          float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+          (arr == 0 ? pg : pb)[(long)blockIdx.x * H + c * 8 + q] = v;
+        }
+      }
+    }
+  }
+}
+
+void layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd,
+                   const float* gamma, void* dx, float* dgamma, float* dbeta, float* work,
+                   long rows, int H, hipStream_t st) {
+  int G = (int)std::max<long>(1, std::min<long>(256, (rows + 15) / 16));
+  int rpb = (int)((rows + G - 1) / G);
+  G = (int)((rows + rpb - 1) / rpb);
+  float* pg = work;
+  float* pb = work + (long)G * H;
+  float* scratch = work + 2L * G * H;
+  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(G), dim3(256), 0, st, (const __bf16*)dy,
+                     (const __bf16*)x, mean, rstd, gamma, (__bf16*)dx, pg, pb, rows, H, rpb);
+  colsum_f32(pg, false, dgamma, G, H, scratch, st);
+  colsum_f32(pb, false, dbeta, G, H, scratch + 64L * H, st);
+}
+
+}  // namespace mipipe

@@ -150,13 +150,14 @@ class _MaxPoolFn(Function):
         y, idx = K.maxpool_fwd(x, k, stride, pad)
         ctx.save_for_backward(idx)
         ctx.xshape = tuple(x.shape)
+        ctx.conf = (k, stride, pad)
         ctx.mark_non_differentiable(idx)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
-        return K.maxpool_bwd(dy.contiguous(), idx, ctx.xshape), None, None, None
+        return K.maxpool_bwd(dy.contiguous(), idx, ctx.xshape, *ctx.conf), None, None, None
 
 
 def max_pool2d(x: Tensor, k: int, stride: int, pad: int) -> Tensor:

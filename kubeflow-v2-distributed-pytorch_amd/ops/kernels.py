@@ -103,9 +103,9 @@ def maxpool_fwd(x, k, stride, pad):
     return _ref.maxpool_fwd(x, k, stride, pad)
 
 
-def maxpool_bwd(dy, idx, x_shape):
+def maxpool_bwd(dy, idx, x_shape, k, stride, pad):
     if use_native(dy):
-        return native().maxpool_bwd(dy, idx, list(x_shape))
+        return native().maxpool_bwd_impl(dy, idx, list(x_shape), k, stride, pad)
     return _ref.maxpool_bwd(dy, idx, x_shape)
 
 

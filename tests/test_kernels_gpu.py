@@ -1,0 +1,268 @@
+"""Numerics of every gfx950 HIP kernel vs the plain-PyTorch fp32 reference of the same op.
+
+Inputs are random (never zeros; cdna guide rule 25); bf16 inputs are quantised first so both
+sides see identical operands; tolerances are relative to the output magnitude.
+Run on an MI355X:  python -m pytest tests -m gpu
+"""
+import math
+
+import pytest
+import torch
+
+from mipipe.ops import _ref
+from mipipe.ops._native import native, native_available
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def _skip_no_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert native_available(), "mipipe._C must be built for GPU tests (no silent fallback)"
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    _skip_no_gpu()
+    torch.manual_seed(1234)
+    yield
+
+
+def rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+def bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+CONV_CASES = [
+    # N, H, W, Ci, Co, k, s, p
+    (2, 8, 8, 64, 64, 3, 1, 1),
+    (2, 9, 7, 32, 72, 3, 1, 1),
+    (2, 16, 16, 64, 256, 1, 1, 0),
+    (2, 16, 16, 256, 64, 1, 1, 0),
+    (2, 16, 16, 128, 128, 3, 2, 1),
+    (2, 16, 16, 256, 512, 1, 2, 0),
+    (2, 32, 32, 8, 64, 7, 2, 3),
+    (3, 7, 7, 512, 512, 3, 1, 1),
+    (1, 5, 5, 24, 40, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd(case):
+    N, H, W, Ci, Co, k, s, p = case
+    x = bf(N, H, W, Ci)
+    w = bf(Co, k, k, Ci, scale=1.0 / math.sqrt(Ci * k * k))
+    shift = torch.randn(Co, device=dev) * 0.1
+    y, ps, pss = native().conv_fwd(x, w, s, p, shift)
+    yr, psr, pssr = _ref.conv_fwd(x.float(), w.float(), s, p, shift)
+    assert y.shape == yr.shape
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(ps.sum(0), psr[0]) < 2e-3
+    assert rel_err(pss.sum(0), pssr[0]) < 2e-3
+    y2, a, b = native().conv_fwd(x, w, s, p, None)
+    assert a is None and torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_dgrad(case):
+    N, H, W, Ci, Co, k, s, p = case
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = bf(N, Ho, Wo, Co)
+    w = bf(Co, k, k, Ci, scale=1.0 / math.sqrt(Co * k * k))
+    dx = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p)
+    dxr = _ref.conv_dgrad(dy.float(), w.float(), (N, H, W, Ci), s, p)
+    assert rel_err(dx, dxr) < 1e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_wgrad(case):
+    N, H, W, Ci, Co, k, s, p = case
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = bf(N, Ho, Wo, Co)
+    x = bf(N, H, W, Ci)
+    dw = native().conv_wgrad(dy, x, k, k, s, p)
+    dwr = _ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)
+    assert dw.dtype == torch.float32 and dw.shape == dwr.shape
+    assert rel_err(dw, dwr) < 5e-3
+
+
+def test_conv_wgrad_large_k_splitk():
+    # K = N*Ho*Wo large enough to exercise split-K atomics
+    x = bf(16, 28, 28, 64)
+    dy = bf(16, 28, 28, 64)
+    dw = native().conv_wgrad(dy, x, 3, 3, 1, 1)
+    dwr = _ref.conv_wgrad(dy.float(), x.float(), 3, 3, 1, 1)
+    assert rel_err(dw, dwr) < 5e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 72, 200), (64, 1000, 2048),
+                                   (1024, 768, 768), (40, 3072, 768)])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+def test_gemm(M, N, K, ta, tb):
+    if (ta and M % 8) or (not ta and K % 8) or N % 8:
+        pytest.skip("layout constraint")
+    if tb and K % 8:
+        pytest.skip("layout constraint")
+    a = bf(K, M) if ta else bf(M, K)
+    b = bf(N, K) if tb else bf(K, N)
+    bias = torch.randn(N, device=dev)
+    out = native().gemm(a, b, ta, tb, bias, "relu", torch.bfloat16, None, 0.0)
+    ref = _ref.gemm(a.float(), b.float(), ta, tb, bias, "relu", torch.float32)
+    assert rel_err(out, ref) < 1e-2
+    out32 = native().gemm(a, b, ta, tb, None, "none", torch.float32, None, 0.0)
+    ref32 = _ref.gemm(a.float(), b.float(), ta, tb, None, "none", torch.float32)
+    assert rel_err(out32, ref32) < 2e-3
+    acc = torch.randn(M, N, device=dev)
+    acc0 = acc.clone()
+    native().gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0)
+    assert rel_err(acc, acc0 + ref32) < 2e-3
+
+
+def test_gemm_identity_asymmetric():
+    # A = I with asymmetric B catches transposed C writes (cdna guide §3)
+    M = 64
+    a = torch.eye(M, device=dev).to(torch.bfloat16)
+    b = (torch.arange(M * 128, device=dev).reshape(128, M) % 37).to(torch.bfloat16)  # [N][K]
+    out = native().gemm(a, b, False, True, None, "none", torch.float32, None, 0.0)
+    assert torch.equal(out, b.float().t())
+
+
+@pytest.mark.parametrize("C", [64, 256, 2048])
+def test_bn_pipeline(C):
+    M = 5000
+    P = 37
+    psum = torch.randn(P, C, device=dev) * 10
+    psq = torch.rand(P, C, device=dev) * 100 + 400
+    shift = torch.randn(C, device=dev)
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev)
+    rm, rv = torch.randn(C, device=dev), torch.rand(C, device=dev) + 0.5
+    rm2, rv2 = rm.clone(), rv.clone()
+    out = native().bn_finalize(psum, psq, M, shift, gamma, beta, rm, rv, 0.1, 1e-5)
+    ref = _ref.bn_finalize(psum, psq, M, shift, gamma, beta, rm2, rv2, 0.1, 1e-5)
+    for o, r in zip(out, ref):
+        assert rel_err(o, r) < 1e-4
+    assert rel_err(rm, rm2) < 1e-5 and rel_err(rv, rv2) < 1e-5
+    mean, invstd, scale, bias = ref
+    y = bf(M, C)
+    r = bf(M, C)
+    y2 = bf(M, C)
+    for res, rs, rb in [(None, None, None), (r, None, None), (y2, scale * 0.7, bias * 0.3)]:
+        z = native().bn_act_fwd(y, scale, bias, True, res, rs, rb)
+        zr = _ref.bn_act_fwd(y.float(), scale, bias, True, None if res is None else res.float(), rs, rb)
+        assert rel_err(z, zr) < 1e-2
+    dz = bf(M, C)
+    z = native().bn_act_fwd(y, scale, bias, True, None, None, None)
+    sg, sgx, sgx2 = native().bn_act_bwd_reduce(dz, z, y, mean, invstd, True, y2, mean, invstd)
+    rg, rgx = _ref.bn_act_bwd_reduce(dz.float(), z, y.float(), mean, invstd, True)
+    _, rgx2 = _ref.bn_act_bwd_reduce(dz.float(), z, y2.float(), mean, invstd, True)
+    assert rel_err(sg, rg) < 1e-3 and rel_err(sgx, rgx) < 1e-3 and rel_err(sgx2, rgx2) < 1e-3
+    dy, dres = native().bn_act_bwd_apply(dz, z, y, mean, invstd, gamma, sg, sgx, M, True, True,
+                                         None, None, None, None, None)
+    dyr, dresr = _ref.bn_act_bwd_apply(dz.float(), z, y.float(), mean, invstd, gamma, rg, rgx, M,
+                                       True, True)
+    assert rel_err(dy, dyr) < 2e-2 and rel_err(dres, dresr) < 1e-2
+    dy, dy2 = native().bn_act_bwd_apply(dz, z, y, mean, invstd, gamma, sg, sgx, M, True, False,
+                                        y2, mean, invstd, gamma * 0.5, sgx2)
+    dy2r, _ = _ref.bn_act_bwd_apply(dz.float(), z, y2.float(), mean, invstd, gamma * 0.5, rg, rgx2,
+                                    M, True)
+    assert rel_err(dy2, dy2r) < 2e-2
+
+
+def test_maxpool():
+    x = bf(2, 17, 16, 64)
+    y, idx = native().maxpool_fwd(x, 3, 2, 1)
+    yr, _ = _ref.maxpool_fwd(x.float(), 3, 2, 1)
+    assert torch.equal(y.float(), yr)
+    dy = bf(*y.shape)
+    dx = native().maxpool_bwd_impl(dy, idx, list(x.shape), 3, 2, 1)
+    xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    out = torch.nn.functional.max_pool2d(xr, 3, 2, 1)
+    out.backward(dy.float().permute(0, 3, 1, 2))
+    assert rel_err(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_avgpool():
+    x = bf(4, 7, 7, 2048)
+    y = native().avgpool_fwd(x)
+    assert rel_err(y, _ref.avgpool_fwd(x.float())) < 1e-2
+    dy = bf(4, 2048)
+    assert rel_err(native().avgpool_bwd(dy, list(x.shape)), _ref.avgpool_bwd(dy.float(), x.shape)) < 1e-2
+
+
+@pytest.mark.parametrize("V", [1000, 30522])
+def test_cross_entropy(V):
+    R = 257
+    logits = bf(R, V, scale=3.0)
+    labels = torch.randint(0, V, (R,), device=dev)
+    labels[5] = -100
+    for eps in (0.0, 0.1):
+        loss, grad = native().cross_entropy_fwd_bwd(logits, labels, eps, -100)
+        lr_, gr = _ref.cross_entropy_fwd_bwd(logits.float(), labels, eps, -100)
+        assert abs(loss.item() - lr_.item()) / abs(lr_.item()) < 1e-3
+        assert rel_err(grad, gr) < 1e-2
+
+
+def test_sgd_and_adamw():
+    n = 4096 * 3
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    m = torch.randn(n, device=dev)
+    sh = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    p2, m2 = p.clone(), m.clone()
+    for first in (True, False):
+        native().sgd_step(p, g, m, sh, 0.1, 0.9, 0.0, 1e-4, False, first, 1.0)
+        _ref.sgd_step(p2, g, m2, None, 0.1, 0.9, 0.0, 1e-4, False, first)
+        assert rel_err(p, p2) < 1e-6 and rel_err(m, m2) < 1e-6
+    assert torch.equal(sh, p.to(torch.bfloat16))
+    ea, eq = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    ea2, eq2, p3 = ea.clone(), eq.clone(), p.clone()
+    for step in (1, 2, 3):
+        native().adamw_step(p, g, ea, eq, sh, 1e-3, 0.9, 0.999, 1e-8, 0.01, step, 1.0)
+        _ref.adamw_step(p3, g, ea2, eq2, None, 1e-3, 0.9, 0.999, 1e-8, 0.01, step)
+    assert rel_err(p, p3) < 1e-5
+
+
+def test_nchw_to_nhwc_and_synthetic():
+    x = torch.randn(3, 3, 11, 13, device=dev)
+    y = native().nchw_to_nhwc(x, torch.bfloat16, 8)
+    assert y.shape == (3, 11, 13, 8)
+    assert torch.equal(y[..., :3], x.permute(0, 2, 3, 1).to(torch.bfloat16))
+    assert torch.count_nonzero(y[..., 3:]) == 0
+    from mipipe.data.synthetic import synthetic_batch
+    idx = torch.arange(10, 74, device=dev)
+    xg, lg = native().synthetic_batch(idx, 3, 8, 8, 10, 7, torch.float32)
+    xc, lc = synthetic_batch(idx.cpu(), (3, 8, 8), 10, 7)
+    assert torch.equal(lg.cpu(), lc)
+    assert (xg.cpu() - xc).abs().max() < 1e-3
+
+
+def test_layernorm_gelu_embedding():
+    R, H = 300, 768
+    x = bf(R, H)
+    res = bf(R, H)
+    gma = torch.rand(H, device=dev) + 0.5
+    bta = torch.randn(H, device=dev)
+    y, mean, rstd, xs = native().layernorm_fwd(x, gma, bta, 1e-12, res)
+    yr, mr, rr, xsr = _ref.layernorm_fwd(x.float(), gma, bta, 1e-12, res.float())
+    assert rel_err(y, yr) < 1e-2
+    dy = bf(R, H)
+    dx, dg, db = native().layernorm_bwd(dy, xs, mean, rstd, gma)
+    dxr, dgr, dbr = _ref.layernorm_bwd(dy.float(), xs.float(), mean, rstd, gma)
+    assert rel_err(dx, dxr) < 2e-2 and rel_err(dg, dgr) < 1e-2 and rel_err(db, dbr) < 1e-2
+    g = native().gelu_fwd(x)
+    assert rel_err(g, _ref.gelu_fwd(x.float())) < 1e-2
+    gb = native().gelu_bwd(dy, x)
+    assert rel_err(gb, _ref.gelu_bwd(dy.float(), x.float())) < 1e-2
+    idx = torch.randint(0, 50, (R,), device=dev)
+    e = native().embedding_bwd(dy, idx, 50)
+    assert rel_err(e, _ref.embedding_bwd(dy.float(), idx, 50)) < 1e-3
+    cs = native().colsum(dy)
+    assert rel_err(cs, dy.float().sum(0)) < 1e-3

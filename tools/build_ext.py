@@ -1,0 +1,146 @@
+"""Build mipipe's native code for gfx950 with hipcc directly (no hipify, no JIT cache).
+
+Products (in-tree, so they travel to the GPU box with the repo snapshot):
+  mipipe/_C<EXT_SUFFIX>      torch extension: HIP kernels (csrc/kernels/*.hip) + bindings
+  mipipe/_runtime<EXT_SUFFIX> native runtime (csrc/runtime/*.cpp): process supervisor,
+                              DAG scheduler core (CPython API, no torch)
+
+Incremental: an object is rebuilt when its source or any header under csrc/ is newer.
+Usage: python tools/build_ext.py [-j N] [--force] [--only C|runtime]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "csrc")
+PKG = os.path.join(REPO, "kubeflow-v2-distributed-pytorch_amd")
+BUILD = os.path.join(REPO, "build", "obj")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _newest_header() -> float:
+    hs = glob.glob(os.path.join(CSRC, "**", "*.hpp"), recursive=True) + \
+        glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+    return max([os.path.getmtime(h) for h in hs] or [0.0])
+
+
+def _torch_flags():
+    import torch
+    import torch.utils.cpp_extension as ce
+    inc = ce.include_paths(device_type="cuda")
+    flags = [f"-I{p}" for p in inc]
+    flags += [f"-I{sysconfig.get_paths()['include']}"]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    flags += [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H",
+              "-DTORCH_EXTENSION_NAME=_C", "-DUSE_ROCM=1"]
+    libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
+    ldflags = [f"-L{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip",
+               "-ltorch_hip", f"-Wl,-rpath,{libdir}"]
+    return flags, ldflags
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def _compile(src: str, obj: str, flags, force: bool, hdr_time: float) -> str:
+    if not force and os.path.exists(obj):
+        t = os.path.getmtime(obj)
+        if t >= os.path.getmtime(src) and t >= hdr_time:
+            return f"up-to-date {os.path.relpath(src, REPO)}"
+    os.makedirs(os.path.dirname(obj), exist_ok=True)
+    _run([HIPCC] + flags + ["-c", src, "-o", obj])
+    return f"compiled {os.path.relpath(src, REPO)}"
+
+
+def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
+    tflags, ldflags = _torch_flags()
+    common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC}", "-DNDEBUG", "-Wno-unused-result"]
+    hip_flags = common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + tflags
+    cpp_flags = common + tflags
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    cpps = [os.path.join(CSRC, "bindings.cpp")]
+    hdr = _newest_header()
+    jobs_list = []
+    for s in srcs:
+        jobs_list.append((s, os.path.join(BUILD, "C", os.path.basename(s) + ".o"), hip_flags))
+    for s in cpps:
+        jobs_list.append((s, os.path.join(BUILD, "C", os.path.basename(s) + ".o"), cpp_flags))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = [ex.submit(_compile, s, o, f, force, hdr) for (s, o, f) in jobs_list]
+        for fu in futs:
+            msg = fu.result()
+            if verbose:
+                print(msg, flush=True)
+    out = os.path.join(PKG, "_C" + EXT)
+    objs = [o for (_, o, _) in jobs_list]
+    if force or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + ldflags + ["-o", out])
+        if verbose:
+            print(f"linked {os.path.relpath(out, REPO)}", flush=True)
+    return out
+
+
+def build_runtime(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    if not srcs:
+        return ""
+    py_inc = sysconfig.get_paths()["include"]
+    flags = ["-O2", "-std=c++17", "-fPIC", f"-I{py_inc}", f"-I{CSRC}", "-Wall", "-Wno-unused-result"]
+    hdr = _newest_header()
+    objs = []
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = []
+        for s in srcs:
+            o = os.path.join(BUILD, "runtime", os.path.basename(s) + ".o")
+            objs.append(o)
+            futs.append(ex.submit(_compile_cxx, s, o, flags, force, hdr))
+        for fu in futs:
+            msg = fu.result()
+            if verbose:
+                print(msg, flush=True)
+    out = os.path.join(PKG, "_runtime" + EXT)
+    if force or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
+        _run(["g++", "-shared", "-fPIC"] + objs + ["-o", out, "-lpthread"])
+        if verbose:
+            print(f"linked {os.path.relpath(out, REPO)}", flush=True)
+    return out
+
+
+def _compile_cxx(src, obj, flags, force, hdr_time):
+    if not force and os.path.exists(obj):
+        t = os.path.getmtime(obj)
+        if t >= os.path.getmtime(src) and t >= hdr_time:
+            return f"up-to-date {os.path.relpath(src, REPO)}"
+    os.makedirs(os.path.dirname(obj), exist_ok=True)
+    _run(["g++"] + flags + ["-c", src, "-o", obj])
+    return f"compiled {os.path.relpath(src, REPO)}"
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--only", choices=["C", "runtime"], default=None)
+    a = ap.parse_args(argv)
+    if a.only in (None, "runtime"):
+        build_runtime(a.jobs, a.force)
+    if a.only in (None, "C"):
+        build_kernels(a.jobs, a.force)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
