@@ -250,6 +250,12 @@ def _compile_group(ctx: _Ctx, g: _Group, is_root: bool) -> Dict[str, Any]:
     for sub in g.groups:
         sub_name = f"comp-{sub.name}"
         ext = _external_channels(sub)
+        if sub.condition is not None:  # the gate is evaluated on the group task's own inputs
+            have = {_external_name(c) for c in ext}
+            for ch in _channels_of_condition(sub.condition):
+                if _external_name(ch) not in have:
+                    ext.append(ch)
+                    have.add(_external_name(ch))
         sub_dag = _compile_group(ctx, sub, is_root=False)
         indefs: Dict[str, Any] = {}
         task_inputs: Dict[str, Any] = {}

@@ -37,3 +37,4 @@ def install_alias(force: bool = False) -> None:
     sys.modules["kfp.v2.compiler"] = v2.compiler
     sys.modules["kfp.v2.google"] = v2.google
     sys.modules["kfp.v2.google.client"] = v2.google.client
+    sys.modules["kfp.dsl"] = dsl

@@ -1,2 +1,2 @@
-"""``kfp.v2.google.client`` surface."""
-from mipipe import client  # noqa: F401
+"""``kfp.v2.google`` surface."""
+from . import client  # noqa: F401

@@ -140,9 +140,9 @@ def maxpool_fwd(x: Tensor, k: int, stride: int, pad: int) -> Tuple[Tensor, Tenso
 
 def maxpool_bwd(dy: Tensor, idx: Tensor, x_shape) -> Tensor:
     N, H, W, C = x_shape
-    dx = torch.zeros(N, C, H * W, dtype=torch.float32, device=dy.device)
-    dx.scatter_add_(2, _nchw(idx).reshape(N, C, -1).long(),
-                    _nchw(dy).reshape(N, C, -1).float())
+    dyf = _f(_nchw(dy)).reshape(N, C, -1)
+    dx = torch.zeros(N, C, H * W, dtype=dyf.dtype, device=dy.device)
+    dx.scatter_add_(2, _nchw(idx).reshape(N, C, -1).long(), dyf)
     return _nhwc(dx.reshape(N, C, H, W)).to(dy.dtype)
 
 

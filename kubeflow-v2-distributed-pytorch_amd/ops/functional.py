@@ -84,10 +84,11 @@ def bn_stats_from_partials(psum, psumsq, count, bn, training: bool) -> BNStats:
         if bn.track_running_stats:
             bn.num_batches_tracked.add_(1)
         return BNStats(mean, invstd, scale, bias, count, True)
-    invstd = torch.rsqrt(bn.running_var.float() + bn.eps)
-    scale = bn.weight.detach().float() * invstd
-    bias = bn.bias.detach().float() - bn.running_mean.float() * scale
-    return BNStats(bn.running_mean.float(), invstd, scale, bias, count, False)
+    up = (lambda t: t) if bn.running_var.dtype == torch.float64 else (lambda t: t.float())
+    invstd = torch.rsqrt(up(bn.running_var) + bn.eps)
+    scale = up(bn.weight.detach()) * invstd
+    bias = up(bn.bias.detach()) - up(bn.running_mean) * scale
+    return BNStats(up(bn.running_mean), invstd, scale, bias, count, False)
 
 
 class _BNActFn(Function):
@@ -207,10 +208,11 @@ class _LinearFn(Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = K.gemm(dy2, w_c, False, False, None, "none", dy2.dtype).reshape(ctx.shp)
+        gdt = torch.float64 if dy2.dtype == torch.float64 else torch.float32
         if ctx.needs_input_grad[1]:
-            dw = K.gemm(dy2, x2, True, False, None, "none", torch.float32)
+            dw = K.gemm(dy2, x2, True, False, None, "none", gdt)
         if ctx.has_bias and ctx.needs_input_grad[3]:
-            db = dy2.float().sum(0)
+            db = dy2.to(gdt).sum(0)
         return dx, dw, None, db, None
 
 

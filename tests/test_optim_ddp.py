@@ -1,0 +1,123 @@
+"""Fused flat-buffer optimizers vs torch.optim, and DDP over gloo (world size 2)."""
+import copy
+import os
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from mipipe.optim import SGD, AdamW, flat_space_for
+from mipipe.ops import functional as MF
+from mipipe import nn as mnn
+
+
+class MLP(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.fc1 = mnn.Linear(16, 32)
+        self.fc2 = mnn.Linear(32, 8)
+
+    def forward(self, x):
+        return self.fc2(self.fc1(x, act="relu"))
+
+
+def test_sgd_matches_torch():
+    torch.manual_seed(0)
+    m = MLP()
+    m2 = copy.deepcopy(m)
+    o = SGD(m.parameters(), 0.05, momentum=0.9, weight_decay=1e-4)
+    o2 = torch.optim.SGD(m2.parameters(), 0.05, momentum=0.9, weight_decay=1e-4)
+    for _ in range(5):
+        x = torch.randn(8, 16)
+        y = torch.randint(0, 8, (8,))
+        o.zero_grad()
+        MF.cross_entropy(m(x), y).backward()
+        o.step()
+        o2.zero_grad()
+        torch.nn.functional.cross_entropy(m2(x), y).backward()
+        o2.step()
+    for p, q in zip(m.parameters(), m2.parameters()):
+        assert torch.allclose(p, q, atol=1e-6)
+    # flat storage: params are views of one buffer, grads of another
+    sp = flat_space_for(m.fc1.weight)
+    assert sp is not None and m.fc1.weight.data_ptr() >= sp.flat.data_ptr()
+    o2.load_state_dict(o.state_dict())
+    o.load_state_dict(o2.state_dict())
+
+
+def test_adamw_matches_torch():
+    torch.manual_seed(0)
+    m = MLP()
+    m2 = copy.deepcopy(m)
+    o = AdamW(m.parameters(), 1e-2, weight_decay=0.01)
+    o2 = torch.optim.AdamW(m2.parameters(), 1e-2, weight_decay=0.01)
+    for _ in range(4):
+        x = torch.randn(8, 16)
+        y = torch.randint(0, 8, (8,))
+        o.zero_grad()
+        MF.cross_entropy(m(x), y).backward()
+        o.step()
+        o2.zero_grad()
+        torch.nn.functional.cross_entropy(m2(x), y).backward()
+        o2.step()
+    for p, q in zip(m.parameters(), m2.parameters()):
+        assert torch.allclose(p, q, atol=1e-5)
+
+
+def _ddp_worker(rank, world, port, out, check_mismatch):
+    import torch.distributed as dist
+    from mipipe.parallel import DistributedDataParallel, CollectiveSequenceError
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(rank)  # different init per rank: DDP must broadcast rank 0's
+    m = MLP()
+    ddp = DistributedDataParallel(m, bucket_cap_mb=0.0005, first_bucket_mb=0.0001,
+                                  check_collectives=True, check_every=1)
+    opt = SGD(ddp.parameters(), 0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(123)
+    X = torch.randn(4 * world, 16, generator=g)
+    Y = torch.randint(0, 8, (4 * world,), generator=g)
+    for _ in range(3):
+        opt.zero_grad()
+        xs, ys = X[rank * 4:(rank + 1) * 4], Y[rank * 4:(rank + 1) * 4]
+        MF.cross_entropy(ddp(xs), ys).backward()
+        opt.step()
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    ok = True
+    if check_mismatch:
+        try:
+            if rank == 0:  # a collective only rank 0 issues -> digest mismatch
+                ddp._clog.record("broadcast", torch.zeros(3))
+            ddp.verify_collective_sequence()
+            ok = False
+        except CollectiveSequenceError:
+            ok = True
+    out[rank] = (flat, len(ddp.buckets), ok)
+    dist.destroy_process_group()
+
+
+def test_ddp_gloo_matches_single_process():
+    world = 2
+    port = 29000 + os.getpid() % 1000
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_ddp_worker, args=(world, port, out, True), nprocs=world, join=True)
+    f0, nb, ok0 = out[0]
+    f1, _, ok1 = out[1]
+    assert torch.allclose(f0, f1), "replicas diverged"
+    assert nb > 1, "expected several buckets"
+    assert ok0 and ok1, "collective checker missed a mismatched sequence"
+    # single process on the global batch, starting from rank 0's init
+    torch.manual_seed(0)
+    m = MLP()
+    opt = SGD(m.parameters(), 0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(123)
+    X = torch.randn(4 * world, 16, generator=g)
+    Y = torch.randint(0, 8, (4 * world,), generator=g)
+    for _ in range(3):
+        opt.zero_grad()
+        MF.cross_entropy(m(X), Y).backward()
+        opt.step()
+    ref = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    assert torch.allclose(f0, ref, atol=1e-5)

@@ -1,0 +1,77 @@
+"""Local gs:// object store, Google-client aliases, launcher env contract and fail-fast."""
+import os
+import sys
+import time
+
+import pytest
+
+from mipipe.launch import LaunchSpec, build_envs, launch
+from mipipe.storage import gcs
+
+
+def test_gcs_roundtrip(gcs_root, tmp_path):
+    c = gcs.Client()
+    b = c.bucket("test-pkl")
+    b.blob("a/b.txt").upload_from_string("hello")
+    assert gcs.uri_to_local_path("gs://test-pkl/a/b.txt") == str(gcs_root / "test-pkl" / "a" / "b.txt")
+    assert gcs.uri_to_local_path("/gcs/test-pkl/a/b.txt") == gcs.uri_to_local_path("gs://test-pkl/a/b.txt")
+    dst = tmp_path / "x" / "y.txt"
+    b.blob("a/b.txt").download_to_filename(str(dst))
+    assert dst.read_text() == "hello"
+    blob = gcs.blob.Blob.from_string("gs://test-pkl/model/m.pth", client=gcs.Client())
+    blob.upload_from_filename(str(dst))
+    assert [x.name for x in c.list_blobs("test-pkl")] == ["a/b.txt", "model/m.pth"]
+    assert gcs.local_path_to_uri(str(gcs_root / "test-pkl" / "a")) == "gs://test-pkl/a"
+    with pytest.raises(FileNotFoundError):
+        b.blob("missing").download_to_filename(str(tmp_path / "m"))
+
+
+def test_google_alias():
+    from mipipe.storage import install_google_cloud_alias
+    install_google_cloud_alias()
+    from google.cloud import storage, aiplatform  # noqa: F401
+    from google.cloud.aiplatform import gapic as aip
+    assert storage.Client is gcs.Client
+    assert aip.AcceleratorType.NVIDIA_TESLA_V100.name == "NVIDIA_TESLA_V100"
+
+
+def test_env_contract(monkeypatch):
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    envs = build_envs(LaunchSpec(command=["x"], replica_count=3, accelerator_count=2,
+                                 model_dir="gs://b/m/"))
+    assert [e["RANK"] for e in envs] == ["0", "1", "2"]
+    assert all(e["WORLD_SIZE"] == "3" for e in envs)
+    assert [e["HIP_VISIBLE_DEVICES"] for e in envs] == ["0,1", "2,3", "4,5"]
+    assert all(e["AIP_MODEL_DIR"] == "gs://b/m/" for e in envs)
+    assert all(e["MASTER_ADDR"] == "127.0.0.1" for e in envs)
+    assert len({e["MASTER_PORT"] for e in envs}) == 1
+    envs = build_envs(LaunchSpec(command=["x"], replica_count=2, accelerator_count=4,
+                                 nproc_per_node=4))
+    assert [e["RANK"] for e in envs] == [str(i) for i in range(8)]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"] * 2
+    assert envs[5]["HIP_VISIBLE_DEVICES"] == "5"
+    with pytest.raises(RuntimeError):
+        build_envs(LaunchSpec(command=["x"], replica_count=5, accelerator_count=2))
+
+
+def test_fail_fast(tmp_path):
+    script = tmp_path / "s.py"
+    script.write_text(
+        "import os, sys, time\n"
+        "r = int(os.environ['RANK'])\n"
+        "if r == 1:\n    time.sleep(0.3); sys.exit(7)\n"
+        "time.sleep(60)\n")
+    t0 = time.time()
+    rc = launch(LaunchSpec(command=[sys.executable, str(script)], replica_count=3, echo=False,
+                           grace_period=2.0, log_dir=str(tmp_path / "logs")))
+    assert rc == 7
+    assert time.time() - t0 < 20
+    assert (tmp_path / "logs" / "rank0.log").exists()
+
+
+def test_timeout(tmp_path):
+    script = tmp_path / "s.py"
+    script.write_text("import time\ntime.sleep(60)\n")
+    rc = launch(LaunchSpec(command=[sys.executable, str(script)], echo=False, timeout=1.0,
+                           grace_period=1.0))
+    assert rc == 124
