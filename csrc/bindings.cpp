@@ -34,6 +34,11 @@ void check_vec(const Tensor& t, int64_t C, const char* name) {
   TORCH_CHECK(t.numel() == C, name, " must have ", C, " elements, got ", t.numel());
 }
 const void* ptr_or_null(const optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+float* fptr(const optional<Tensor>& t, int64_t n) {
+  if (!t.has_value()) return nullptr;
+  check_vec(*t, n, "gradient accumulator");
+  return t->data_ptr<float>();
+}
 
 mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int pad) {
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv expects NHWC x and [Co,KH,KW,Ci] w");
@@ -56,7 +61,9 @@ mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int p
 
 // ------------------------------------------------------------------------------- conv
 std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor w, int stride,
-                                                                int pad, optional<Tensor> shift) {
+                                                                int pad, optional<Tensor> shift,
+                                                                optional<Tensor> slab_sum,
+                                                                optional<Tensor> slab_sq) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   c10::DeviceGuard g(x.device());
@@ -68,8 +75,17 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
   if (shift.has_value()) {
     check_vec(*shift, s.Co, "stats_shift");
     int P = mipipe::conv_fwd_stat_rows(s);
-    ps = torch::empty({P, s.Co}, x.options().dtype(at::kFloat));
-    pss = torch::empty({P, s.Co}, x.options().dtype(at::kFloat));
+    if (slab_sum.has_value()) {  // persistent zeroed replica slabs (re-zeroed by bn_finalize)
+      check_f32(*slab_sum, "slab_sum");
+      check_f32(*slab_sq, "slab_sq");
+      TORCH_CHECK(slab_sum->numel() == (int64_t)P * s.Co && slab_sq->numel() == (int64_t)P * s.Co,
+                  "stat slabs must be [", P, ", Co]");
+      ps = *slab_sum;
+      pss = *slab_sq;
+    } else {
+      ps = torch::zeros({P, s.Co}, x.options().dtype(at::kFloat));
+      pss = torch::zeros({P, s.Co}, x.options().dtype(at::kFloat));
+    }
     psp = ps->data_ptr<float>();
     pssp = pss->data_ptr<float>();
     sh = shift->data_ptr<float>();
@@ -94,12 +110,13 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo && dy.size(3) == s.Co,
               "dy shape does not match the convolution");
   TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv dgrad needs Ci, Co % 8 == 0");
+  TORCH_CHECK(s.pad < s.KH, "conv dgrad expects pad < kernel size");
   auto dx = torch::empty({s.N, s.H, s.W, s.Ci}, dy.options());
   mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream());
   return dx;
 }
 
-Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad) {
+Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, optional<Tensor> out) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   c10::DeviceGuard g(dy.device());
@@ -110,7 +127,15 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad) {
   s.Wo = (s.W + 2 * pad - kw) / stride + 1;
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo, "dy/x mismatch");
   TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv wgrad needs Ci, Co % 8 == 0");
-  auto dw = torch::zeros({s.Co, kh, kw, s.Ci}, x.options().dtype(at::kFloat));
+  Tensor dw;
+  if (out.has_value()) {  // accumulate straight into an existing gradient (flat DDP bucket view)
+    check_f32(*out, "out");
+    TORCH_CHECK(out->dim() == 4 && out->size(0) == s.Co && out->size(1) == kh && out->size(2) == kw &&
+                    out->size(3) == s.Ci, "wgrad out must be [Co,KH,KW,Ci]");
+    dw = *out;
+  } else {
+    dw = torch::zeros({s.Co, kh, kw, s.Ci}, x.options().dtype(at::kFloat));
+  }
   mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream());
   return dw;
 }
@@ -119,7 +144,8 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad) {
 std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(Tensor psum, Tensor psq, int64_t count,
                                                        Tensor shift, Tensor gamma, Tensor beta,
                                                        optional<Tensor> rm, optional<Tensor> rv,
-                                                       double momentum, double eps) {
+                                                       double momentum, double eps,
+                                                       bool zero_after) {
   check_f32(psum, "psum");
   check_f32(psq, "psumsq");
   c10::DeviceGuard g(psum.device());
@@ -135,14 +161,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(Tensor psum, Tensor psq, 
   auto o = psum.options();
   auto mean = torch::empty({C}, o), invstd = torch::empty({C}, o), scale = torch::empty({C}, o),
        bias = torch::empty({C}, o);
-  auto work = torch::empty({3 * 32 * C}, o);
   mipipe::bn_finalize(psum.data_ptr<float>(), psq.data_ptr<float>(), (int)P, (int)C, count,
                       shift.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
                       rm.has_value() ? rm->data_ptr<float>() : nullptr,
                       rv.has_value() ? rv->data_ptr<float>() : nullptr, (float)momentum,
                       (float)eps, mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                      scale.data_ptr<float>(), bias.data_ptr<float>(), work.data_ptr<float>(),
-                      stream());
+                      scale.data_ptr<float>(), bias.data_ptr<float>(), zero_after, stream());
   return {mean, invstd, scale, bias};
 }
 
@@ -172,7 +196,9 @@ Tensor bn_act_fwd(Tensor y, Tensor scale, Tensor bias, bool relu, optional<Tenso
 
 std::tuple<Tensor, Tensor, optional<Tensor>> bn_act_bwd_reduce(
     Tensor dz, Tensor z, Tensor y, Tensor mean, Tensor invstd, bool relu, optional<Tensor> y2,
-    optional<Tensor> mean2, optional<Tensor> invstd2) {
+    optional<Tensor> mean2, optional<Tensor> invstd2, optional<Tensor> rep,
+    optional<Tensor> dgamma, optional<Tensor> dbeta, optional<Tensor> dgamma2,
+    optional<Tensor> dbeta2) {
   check_bf16(dz, "dz");
   check_bf16(z, "z");
   check_bf16(y, "y");
@@ -191,15 +217,22 @@ std::tuple<Tensor, Tensor, optional<Tensor>> bn_act_bwd_reduce(
   auto sg = torch::empty({C}, o), sgx = torch::empty({C}, o);
   optional<Tensor> sgx2;
   if (y2.has_value()) sgx2 = torch::empty({C}, o);
-  int G = mipipe::bn_bwd_partials(M, (int)C);
-  auto work = torch::empty({(3L * G + 3L * 32) * C}, o);
+  Tensor work;
+  if (rep.has_value()) {  // persistent zeroed [3][R][C] replica slab, left zeroed
+    check_f32(*rep, "rep");
+    TORCH_CHECK(rep->numel() == 3L * mipipe::kStatReplicas * C, "rep must be [3, R, C]");
+    work = *rep;
+  } else {
+    work = torch::zeros({3L * mipipe::kStatReplicas * C}, o);
+  }
   mipipe::bn_act_bwd_reduce(dz.data_ptr(), z.data_ptr(), y.data_ptr(), mean.data_ptr<float>(),
                             invstd.data_ptr<float>(), ptr_or_null(y2),
                             mean2.has_value() ? mean2->data_ptr<float>() : nullptr,
                             invstd2.has_value() ? invstd2->data_ptr<float>() : nullptr, relu, M,
                             (int)C, sg.data_ptr<float>(), sgx.data_ptr<float>(),
                             sgx2.has_value() ? sgx2->data_ptr<float>() : nullptr,
-                            work.data_ptr<float>(), stream());
+                            work.data_ptr<float>(), fptr(dgamma, C), fptr(dbeta, C),
+                            fptr(dgamma2, C), fptr(dbeta2, C), stream());
   return {sg, sgx, sgx2};
 }
 
@@ -518,12 +551,22 @@ Tensor colsum(Tensor x) {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "mipipe gfx950 (MI355X) HIP kernels";
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
+        py::arg("shift") = py::none(), py::arg("slab_sum") = py::none(),
+        py::arg("slab_sq") = py::none());
+  m.attr("STAT_REPLICAS") = mipipe::kStatReplicas;
   m.def("conv_dgrad", &conv_dgrad);
-  m.def("conv_wgrad", &conv_wgrad);
-  m.def("bn_finalize", &bn_finalize);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
+        py::arg("stride"), py::arg("pad"), py::arg("out") = py::none());
+  m.def("bn_finalize", &bn_finalize, py::arg("psum"), py::arg("psq"), py::arg("count"),
+        py::arg("shift"), py::arg("gamma"), py::arg("beta"), py::arg("rm"), py::arg("rv"),
+        py::arg("momentum"), py::arg("eps"), py::arg("zero_after") = true);
   m.def("bn_act_fwd", &bn_act_fwd);
-  m.def("bn_act_bwd_reduce", &bn_act_bwd_reduce);
+  m.def("bn_act_bwd_reduce", &bn_act_bwd_reduce, py::arg("dz"), py::arg("z"), py::arg("y"),
+        py::arg("mean"), py::arg("invstd"), py::arg("relu"), py::arg("y2") = py::none(),
+        py::arg("mean2") = py::none(), py::arg("invstd2") = py::none(),
+        py::arg("rep") = py::none(), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none(),
+        py::arg("dgamma2") = py::none(), py::arg("dbeta2") = py::none());
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd_impl", &maxpool_bwd);

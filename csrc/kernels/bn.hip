@@ -46,18 +46,23 @@ inline int grid_for_rows(long M, int rpb, int cap = 2048) {
 
 }  // namespace
 
-// Per-channel final reduction of an [S][C] slab (S small) + BN statistics.
-__global__ void bn_finalize_kernel(const float* __restrict__ s1, const float* __restrict__ s2,
-                                   int S, int C, float inv_count, float unbias, const float* shift,
+// Per-channel final reduction of a [P][C] slab pair (P = replica rows) + BN statistics.
+// With zero_after the slab is cleared for reuse (replica slabs are persistent and zeroed).
+__global__ void bn_finalize_kernel(float* __restrict__ s1, float* __restrict__ s2, int P, int C,
+                                   float inv_count, float unbias, const float* shift,
                                    const float* gamma, const float* beta, float* run_mean,
                                    float* run_var, float momentum, float eps, float* mean,
-                                   float* invstd, float* scale, float* bias) {
+                                   float* invstd, float* scale, float* bias, bool zero_after) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float a = 0.f, b = 0.f;
-  for (int s = 0; s < S; ++s) {
-    a += s1[(long)s * C + c];
-    b += s2[(long)s * C + c];
+  for (int p = 0; p < P; ++p) {
+    a += s1[(long)p * C + c];
+    b += s2[(long)p * C + c];
+    if (zero_after) {
+      s1[(long)p * C + c] = 0.f;
+      s2[(long)p * C + c] = 0.f;
+    }
   }
   float ms = a * inv_count;
   float var = fmaxf(b * inv_count - ms * ms, 0.f);
@@ -74,67 +79,14 @@ __global__ void bn_finalize_kernel(const float* __restrict__ s1, const float* __
   }
 }
 
-// Two-column-array colsum stage (sum and sq) without pointer arrays.
-__global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ a_in,
-                                                      const float* __restrict__ b_in,
-                                                      const float* __restrict__ c_in,
-                                                      float* a_out, float* b_out, float* c_out,
-                                                      int P, int C, int chunk) {
-  __shared__ float red[3][4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rp = threadIdx.x >> 6;
-  const int p0 = blockIdx.y * chunk, p1 = min(P, p0 + chunk);
-  float x = 0.f, y = 0.f, z = 0.f;
-  if (col < C) {
-    for (int p = p0 + rp; p < p1; p += 4) {
-      long o = (long)p * C + col;
-      x += a_in[o];
-      y += b_in[o];
-      if (c_in != nullptr) z += c_in[o];
-    }
-  }
-  red[0][rp][threadIdx.x & 63] = x;
-  red[1][rp][threadIdx.x & 63] = y;
-  red[2][rp][threadIdx.x & 63] = z;
-  __syncthreads();
-  if (rp == 0 && col < C) {
-    int t = threadIdx.x;
-    long o = (long)blockIdx.y * C + col;
-    a_out[o] = red[0][0][t] + red[0][1][t] + red[0][2][t] + red[0][3][t];
-    b_out[o] = red[1][0][t] + red[1][1][t] + red[1][2][t] + red[1][3][t];
-    if (c_out != nullptr) c_out[o] = red[2][0][t] + red[2][1][t] + red[2][2][t] + red[2][3][t];
-  }
-}
-
-// Reduce up to three [P][C] slabs to [S][C] with S <= 32 rows.  Returns S; outputs in work.
-static int stage_reduce(const float* a, const float* b, const float* c, int P, int C, float* work,
-                        const float** ra, const float** rb, const float** rc, hipStream_t st) {
-  if (P <= 32) {
-    *ra = a; *rb = b; *rc = c;
-    return P;
-  }
-  int S = std::min(32, (P + 15) / 16);
-  int chunk = (P + S - 1) / S;
-  S = (P + chunk - 1) / chunk;
-  float* wa = work;
-  float* wb = work + (long)S * C;
-  float* wc = c ? work + 2L * S * C : nullptr;
-  dim3 grid((C + 63) / 64, S);
-  hipLaunchKernelGGL(colsum2_kernel, grid, dim3(256), 0, st, a, b, c, wa, wb, wc, P, C, chunk);
-  *ra = wa; *rb = wb; *rc = wc;
-  return S;
-}
-
-void bn_finalize(const float* psum, const float* psq, int P, int C, long count, const float* shift,
+void bn_finalize(float* psum, float* psq, int P, int C, long count, const float* shift,
                  const float* gamma, const float* beta, float* run_mean, float* run_var,
                  float momentum, float eps, float* mean, float* invstd, float* scale, float* bias,
-                 float* work, hipStream_t st) {
-  const float *ra, *rb, *rc;
-  int S = stage_reduce(psum, psq, nullptr, P, C, work, &ra, &rb, &rc, st);
+                 bool zero_after, hipStream_t st) {
   float unbias = count > 1 ? (float)count / (float)(count - 1) : 1.f;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ra, rb, S, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, psum, psq, P, C,
                      1.f / (float)count, unbias, shift, gamma, beta, run_mean, run_var, momentum,
-                     eps, mean, invstd, scale, bias);
+                     eps, mean, invstd, scale, bias, zero_after);
 }
 
 // ----------------------------------------------------------------------------- forward apply
@@ -205,23 +157,19 @@ void bn_act_fwd(const void* y, const float* scale, const float* bias, const void
 }
 
 // ----------------------------------------------------------------------------- backward
-int bn_bwd_partials(long M, int C) {
-  RowMap mp = row_map(C);
-  return grid_for_rows(M, mp.rpb, 1024);
-}
-
 template <bool TWO>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const __bf16* __restrict__ dz, const __bf16* __restrict__ z, const __bf16* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const __bf16* __restrict__ y2, const float* __restrict__ mean2,
-    const float* __restrict__ invstd2, bool relu, long M, int C, float* __restrict__ pg,
-    float* __restrict__ pgx, float* __restrict__ pgx2) {
+    const float* __restrict__ invstd2, bool relu, long M, int C, float* __restrict__ rep) {
   __shared__ float red[3][kT][8];
   const RowMap mp = row_map(C);
   const int t = threadIdx.x;
   const int rg = t / mp.tpr;
   const bool active = rg < mp.rpb;
+  float* rrow = rep + (long)(blockIdx.x % kStatReplicas) * C;
+  const long rstride = (long)kStatReplicas * C;
   for (int pass = 0; pass < mp.passes; ++pass) {
     const int cg = pass * mp.tpr + (t % mp.tpr);
     const int c0 = cg * 8;
@@ -270,63 +218,76 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
       red[2][t][q] = sx2[q];
     }
     __syncthreads();
-    if (active && rg == 0 && c0 < C) {
-      for (int k = 1; k < mp.rpb; ++k) {
-        int src = k * mp.tpr + (t % mp.tpr);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          sg[q] += red[0][src][q];
-          sx[q] += red[1][src][q];
-          sx2[q] += red[2][src][q];
-        }
+    // transpose through LDS so each atomic wave-instruction covers 64 consecutive channels
+    const int cpass = min(C - pass * mp.tpr * 8, mp.tpr * 8);
+    for (int c = t; c < cpass; c += kT) {
+      const int owner = c >> 3, q = c & 7;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+      for (int k = 0; k < mp.rpb; ++k) {
+        a0 += red[0][k * mp.tpr + owner][q];
+        a1 += red[1][k * mp.tpr + owner][q];
+        if (TWO) a2 += red[2][k * mp.tpr + owner][q];
       }
-      long o = (long)blockIdx.x * C + c0;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        pg[o + q] = sg[q];
-        pgx[o + q] = sx[q];
-        if (TWO) pgx2[o + q] = sx2[q];
-      }
+      const int cc = pass * mp.tpr * 8 + c;
+      atomicAdd(rrow + cc, a0);
+      atomicAdd(rrow + rstride + cc, a1);
+      if (TWO) atomicAdd(rrow + 2 * rstride + cc, a2);
     }
     __syncthreads();
   }
 }
 
-__global__ void sum_rows3_kernel(const float* a, const float* b, const float* c, int S, int C,
-                                 float* oa, float* ob, float* oc) {
-  int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= C) return;
-  float x = 0.f, y = 0.f, z = 0.f;
-  for (int s = 0; s < S; ++s) {
-    x += a[(long)s * C + col];
-    y += b[(long)s * C + col];
-    if (c) z += c[(long)s * C + col];
+// Sum the replica rows into the outputs and zero the replicas for reuse.  Optionally also
+// ACCUMULATE the parameter gradients (dβ = Σg, dγ = Σg·x̂; dβ₂ = Σg, dγ₂ = Σg·x̂₂) straight into
+// the flat gradient buffer, replacing autograd's AccumulateGrad kernels.
+__global__ void bn_bwd_collect_kernel(float* __restrict__ rep, int C, float* og, float* ogx,
+                                      float* ogx2, float* dgamma, float* dbeta, float* dgamma2,
+                                      float* dbeta2) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const long rs = (long)kStatReplicas * C;
+  float a = 0.f, b = 0.f, d = 0.f;
+  for (int r = 0; r < kStatReplicas; ++r) {
+    long o = (long)r * C + c;
+    a += rep[o];
+    b += rep[rs + o];
+    d += rep[2 * rs + o];
+    rep[o] = 0.f;
+    rep[rs + o] = 0.f;
+    rep[2 * rs + o] = 0.f;
   }
-  oa[col] = x;
-  ob[col] = y;
-  if (oc) oc[col] = z;
+  og[c] = a;
+  ogx[c] = b;
+  if (ogx2 != nullptr) ogx2[c] = d;
+  if (dgamma != nullptr) {
+    dgamma[c] += b;
+    dbeta[c] += a;
+  }
+  if (dgamma2 != nullptr) {
+    dgamma2[c] += d;
+    dbeta2[c] += a;
+  }
 }
 
 void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float* mean,
                        const float* invstd, const void* y2, const float* mean2,
                        const float* invstd2, bool relu, long M, int C, float* out_g,
-                       float* out_gx, float* out_gx2, float* work, hipStream_t st) {
+                       float* out_gx, float* out_gx2, float* rep, float* dgamma, float* dbeta,
+                       float* dgamma2, float* dbeta2, hipStream_t st) {
   RowMap mp = row_map(C);
-  int G = grid_for_rows(M, mp.rpb, 1024);
-  float* pg = work;
-  float* pgx = work + (long)G * C;
-  float* pgx2 = work + 2L * G * C;
-  float* rest = work + 3L * G * C;
+  // >= 16 row-iterations per thread, and at most ~1M atomic adds in total
+  long cap = std::max<long>(64, (1l << 20) / (3l * C));
+  int G = (int)std::max<long>(1, std::min<long>(std::min<long>(1024, cap),
+                                                (M + mp.rpb * 16 - 1) / (mp.rpb * 16)));
   const __bf16 *dzp = (const __bf16*)dz, *zp = (const __bf16*)z, *yp = (const __bf16*)y,
                *y2p = (const __bf16*)y2;
   if (y2 == nullptr)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, pg, pgx, pgx2);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, rep);
   else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, pg, pgx, pgx2);
-  const float *ra, *rb, *rc;
-  int S = stage_reduce(pg, pgx, y2 ? pgx2 : nullptr, G, C, rest, &ra, &rb, &rc, st);
-  hipLaunchKernelGGL(sum_rows3_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ra, rb,
-                     y2 ? rc : nullptr, S, C, out_g, out_gx, y2 ? out_gx2 : nullptr);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, rep);
+  hipLaunchKernelGGL(bn_bwd_collect_kernel, dim3((C + 255) / 256), dim3(256), 0, st, rep, C, out_g,
+                     out_gx, y2 ? out_gx2 : nullptr, dgamma, dbeta, y2 ? dgamma2 : nullptr,
+                     y2 ? dbeta2 : nullptr);
 }
 
 template <int MODE>  // 0: dy only, 1: dy + dres (=g), 2: dy + dy2 (second BN branch)

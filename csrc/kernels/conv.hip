@@ -18,7 +18,7 @@ __device__ __attribute__((aligned(64))) uint4 g_conv_zero[8];
 template <int BM, int BN>
 constexpr int lds_bytes_bf16() {
   constexpr int a = 2 * (BM + BN) * BK * 2;
-  constexpr int b = BM * (BN * 2 + 16);
+  constexpr int b = kStatsLdsOffset<BM, BN>() + 4 * BN * 4;
   return a > b ? a : b;
 }
 template <int BM, int BN>
@@ -49,13 +49,14 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
   b.init(w, K, e.N, K, n0, wave, lane, g_conv_zero);
   f32x4 acc[BM / 32][BN / 32];
   MainLoop<BM, BN, OpA, KCDense<BN>>::run(smem, a, b, 0, nk, acc, wave, lane);
-  epilogue_bf16<BM, BN>(smem, acc, e, m0, n0, tm * 2, wave, lane);
+  epilogue_bf16<BM, BN>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
 template <int BM, int BN, bool DENSE>
 __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const __bf16* __restrict__ dy,
                                                              const __bf16* __restrict__ w,
-                                                             ConvGeom g, FastDiv fHW, FastDiv fW,
+                                                             int Ho, int Wo, int Co, int taps,
+                                                             FastDiv fCo, DgradClass cls,
                                                              uint32_t M, uint32_t tilesN,
                                                              EpiParams e) {
   __shared__ __attribute__((aligned(16))) char smem[lds_bytes_bf16<BM, BN>()];
@@ -64,8 +65,8 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const __bf16* __rest
   const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
   const uint32_t tm = id / tilesN, tn = id % tilesN;
   const uint32_t m0 = tm * BM, n0 = tn * BN;
-  const uint32_t Co = (uint32_t)g.C, Ci = e.N, taps = (uint32_t)(g.KH * g.KW);
-  const uint32_t K = taps * Co;
+  const uint32_t Ci = e.N;
+  const uint32_t K = (uint32_t)(cls.ntaps * Co);
   const int nk = (int)((K + BK - 1) / BK);
   typedef typename std::conditional<DENSE, KCDense<BM>, KCDgrad<BM>>::type OpA;
   typedef typename std::conditional<DENSE, MCDense<BN>, MCDgradW<BN>>::type OpB;
@@ -75,8 +76,8 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const __bf16* __rest
     a.init(dy, Co, M, K, m0, wave, lane, g_conv_zero);
     b.init(w, Ci, Ci, K, n0, wave, lane, g_conv_zero);
   } else {
-    a.init(dy, g, fHW, fW, M, m0, wave, lane, g_conv_zero);
-    b.init(w, Co, taps, Ci, g.fC, n0, wave, lane, g_conv_zero);
+    a.init(dy, Ho, Wo, Co, fCo, cls, M, m0, wave, lane, g_conv_zero);
+    b.init(w, (uint32_t)Co, (uint32_t)taps, Ci, fCo, cls, n0, wave, lane, g_conv_zero);
   }
   f32x4 acc[BM / 32][BN / 32];
   MainLoop<BM, BN, OpA, OpB>::run(smem, a, b, 0, nk, acc, wave, lane);
@@ -133,8 +134,8 @@ static bool is_dense(const ConvShape& s) {
 }
 
 int conv_fwd_stat_rows(const ConvShape& s) {
-  long M = (long)s.N * s.Ho * s.Wo;
-  return (int)cdiv(M, 128) * 2;  // both tile configs use BM = 128
+  (void)s;
+  return kStatReplicas;
 }
 
 #define MIPIPE_LAUNCH(kern, grid, ...) hipLaunchKernelGGL((kern), (grid), dim3(256), 0, st, __VA_ARGS__)
@@ -145,7 +146,7 @@ void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq
   uint32_t M = (uint32_t)s.N * s.Ho * s.Wo;
   EpiParams e{};
   e.C = y; e.ldc = s.Co; e.M = M; e.N = s.Co; e.bias = nullptr; e.act = 0;
-  e.st_sum = st_sum; e.st_sq = st_sq; e.st_shift = st_shift; e.st_rows_per_block = 2;
+  e.st_sum = st_sum; e.st_sq = st_sq; e.st_shift = st_shift; e.st_R = kStatReplicas;
   const bool dense = is_dense(s);
   const __bf16* xp = (const __bf16*)x;
   const __bf16* wp = (const __bf16*)w;
@@ -161,23 +162,49 @@ void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq
 }
 
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st) {
-  // geometry seen from the dgrad GEMM: N,H,W = dx dims; C = Co (dy channels); Ho,Wo = dy dims
-  ConvGeom g = make_geom(s.N, s.H, s.W, s.Co, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad);
-  FastDiv fHW((uint32_t)(s.H * s.W)), fW((uint32_t)s.W);
-  uint32_t M = (uint32_t)s.N * s.H * s.W;
-  EpiParams e{};
-  e.C = dx; e.ldc = s.Ci; e.M = M; e.N = s.Ci;
   const bool dense = is_dense(s);
   const __bf16* dyp = (const __bf16*)dy;
   const __bf16* wp = (const __bf16*)w;
-  if (s.Ci <= 64) {
-    uint32_t tN = cdiv(s.Ci, 64), tiles = cdiv(M, 128) * tN;
-    if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 64, true>), dim3(tiles), dyp, wp, g, fHW, fW, M, tN, e);
-    else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 64, false>), dim3(tiles), dyp, wp, g, fHW, fW, M, tN, e);
-  } else {
-    uint32_t tN = cdiv(s.Ci, 128), tiles = cdiv(M, 128) * tN;
-    if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true>), dim3(tiles), dyp, wp, g, fHW, fW, M, tN, e);
-    else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, false>), dim3(tiles), dyp, wp, g, fHW, fW, M, tN, e);
+  const int S = s.stride;
+  FastDiv fCo((uint32_t)s.Co);
+  for (int ph = 0; ph < S; ++ph) {
+    for (int pw = 0; pw < S; ++pw) {
+      DgradClass c{};
+      c.ph = ph; c.pw = pw;
+      c.Hc = (s.H - ph + S - 1) / S;
+      c.Wc = (s.W - pw + S - 1) / S;
+      if (c.Hc <= 0 || c.Wc <= 0) continue;
+      // taps reaching this phase: kh = (ph + pad) mod S + S*a, kw likewise
+      c.S = S; c.KW = s.KW;
+      c.kh0 = (ph + s.pad) % S;
+      c.kw0 = (pw + s.pad) % S;
+      int nkh = c.kh0 < s.KH ? (s.KH - c.kh0 + S - 1) / S : 0;
+      int nkw = c.kw0 < s.KW ? (s.KW - c.kw0 + S - 1) / S : 0;
+      c.nkw = std::max(nkw, 1);
+      c.ntaps = nkh * nkw;
+      c.dh0 = (ph + s.pad - c.kh0) / S;
+      c.dw0 = (pw + s.pad - c.kw0) / S;
+      c.fnkw = FastDiv((uint32_t)c.nkw);
+      c.fHcWc = FastDiv((uint32_t)(c.Hc * c.Wc));
+      c.fWc = FastDiv((uint32_t)c.Wc);
+      uint32_t M = (uint32_t)s.N * c.Hc * c.Wc;
+      EpiParams e{};
+      e.C = dx; e.ldc = s.Ci; e.M = M; e.N = s.Ci;
+      if (S > 1) {
+        e.rm_s = S; e.rm_ph = ph; e.rm_pw = pw; e.rm_H = s.H; e.rm_W = s.W;
+        e.rm_Hc = c.Hc; e.rm_Wc = c.Wc; e.rm_fHcWc = c.fHcWc; e.rm_fWc = c.fWc;
+      }
+      int taps = s.KH * s.KW;
+      if (s.Ci <= 64) {
+        uint32_t tN = cdiv(s.Ci, 64), tiles = cdiv(M, 128) * tN;
+        if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 64, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
+        else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 64, false>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
+      } else {
+        uint32_t tN = cdiv(s.Ci, 128), tiles = cdiv(M, 128) * tN;
+        if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
+        else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, false>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
+      }
+    }
   }
 }
 

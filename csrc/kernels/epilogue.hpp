@@ -17,8 +17,24 @@ struct EpiParams {
   float* st_sum;
   float* st_sq;
   const float* st_shift;
-  int st_rows_per_block;  // 2 (one per wave row)
+  int st_R;  // number of replica rows in the stats slabs
+  // optional output-row remap (strided dgrad classes): m -> (img, i, j) over an Hc x Wc grid,
+  // stored at dx row (img*H + ph + s*i)*W + pw + s*j.  rm_s == 0 disables.
+  int rm_s, rm_ph, rm_pw, rm_H, rm_W, rm_Hc, rm_Wc;
+  FastDiv rm_fHcWc, rm_fWc;
 };
+
+__device__ __forceinline__ long out_row(const EpiParams& e, uint32_t m) {
+  if (e.rm_s == 0) return (long)m;
+  uint32_t img = fdiv(e.rm_fHcWc, m);
+  uint32_t rem = m - img * (uint32_t)(e.rm_Hc * e.rm_Wc);
+  uint32_t i = fdiv(e.rm_fWc, rem);
+  uint32_t j = rem - i * (uint32_t)e.rm_Wc;
+  return ((long)img * e.rm_H + e.rm_ph + e.rm_s * (long)i) * e.rm_W + e.rm_pw + e.rm_s * (long)j;
+}
+
+template <int BM, int BN>
+constexpr int kStatsLdsOffset() { return ((BM * (BN * 2 + 16)) + 255) / 256 * 256; }
 
 // bf16 output.  acc layout: lane holds C[m][n..n+3] for tile (i, j).
 template <int BM, int BN>
@@ -47,8 +63,11 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
         }
     }
   }
-  // BatchNorm partial statistics from the fp32 accumulators
+  // BatchNorm partial statistics from the fp32 accumulators, reduced over the block's BM rows
+  // and added with fp32 atomics into replica slab (blockIdx % st_R) — 256-B-contiguous
+  // wave-instructions, no per-block partial rows to reduce later.
   if (e.st_sum != nullptr) {
+    float* lst = reinterpret_cast<float*>(smem + kStatsLdsOffset<BM, BN>());  // [2][2][BN]
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       uint32_t n = n0 + nl0 + j * 16;
@@ -76,12 +95,26 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
           ss[q] += __shfl_xor(ss[q], o);
         }
       }
-      if ((lane & 15) == 0 && n < e.N) {
-        uint32_t prow = prow_base + wr;
-        *reinterpret_cast<float4*>(e.st_sum + (long)prow * e.N + n) = make_float4(s[0], s[1], s[2], s[3]);
-        *reinterpret_cast<float4*>(e.st_sq + (long)prow * e.N + n) = make_float4(ss[0], ss[1], ss[2], ss[3]);
+      if ((lane & 15) == 0) {
+        uint32_t nl = nl0 + j * 16;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          lst[(0 * 2 + wr) * BN + nl + q] = s[q];
+          lst[(1 * 2 + wr) * BN + nl + q] = ss[q];
+        }
       }
     }
+    __syncthreads();
+    for (int t = threadIdx.x; t < 2 * BN; t += kThreads) {
+      int arr = t / BN, c = t % BN;
+      uint32_t n = n0 + c;
+      if (n < e.N) {
+        float v = lst[(arr * 2 + 0) * BN + c] + lst[(arr * 2 + 1) * BN + c];
+        float* dst = (arr == 0 ? e.st_sum : e.st_sq) + (long)(blockIdx.x % e.st_R) * e.N + n;
+        atomicAdd(dst, v);
+      }
+    }
+    __syncthreads();
   }
   // stage bf16 tile in LDS: pitch BN*2 + 16 bytes
   constexpr int P = BN * 2 + 16;
@@ -101,7 +134,7 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
     uint32_t m = m0 + r, n = n0 + cc * 8;
     if (m < e.M && n < e.N) {
       uint4 v = *reinterpret_cast<const uint4*>(smem + r * P + cc * 16);
-      *reinterpret_cast<uint4*>(C + (long)m * e.ldc + n) = v;
+      *reinterpret_cast<uint4*>(C + out_row(e, m) * e.ldc + n) = v;
     }
   }
 }

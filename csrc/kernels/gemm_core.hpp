@@ -157,40 +157,55 @@ struct KCIm2col {
   }
 };
 
-// Conv data-grad A operand: gather of NHWC dy.  row m -> (img, h, w) of dx; k -> (kh, kw, co);
-// source dy[img, (h+p-kh)/s, (w+p-kw)/s, co] when divisible and in range.
+// Conv data-grad, sub-pixel ("parity class") form.  For stride s the dx pixels split into s*s
+// classes (ph, pw); class pixels (h, w) = (ph + s*i, pw + s*j) receive contributions only from the
+// taps with kh = (ph + pad) mod s (and kw likewise), each through dy[i + dh, j + dw] with a fixed
+// offset (dh, dw) = ((ph + pad - kh)/s, (pw + pad - kw)/s).  So every class is a dense GEMM over
+// its own tap list — no MFMA work is spent on the (s*s - 1)/(s*s) structurally-zero products a
+// masked implicit GEMM would do.  Stride 1 is the single class with every tap.
+struct DgradClass {
+  int Hc, Wc;          // class grid
+  int ph, pw;          // phase
+  int ntaps;           // nkh * nkw
+  int kh0, kw0;        // first tap of the class; taps kh = kh0 + s*a, kw = kw0 + s*b
+  int nkw;             // taps along kw
+  int dh0, dw0;        // dy offset of the first tap: dh = dh0 - a, dw = dw0 - b
+  int S, KW;
+  FastDiv fHcWc, fWc, fnkw;
+};
+
 template <int R>
 struct KCDgrad {
   static constexpr bool KC = true;
   static constexpr int NI = R / 32;
   const __bf16* dy;
-  int h[NI], w[NI];
+  int i_[NI], j_[NI];
   long imgbase[NI];  // img*Ho*Wo ; -1 invalid
   uint32_t kcol, K;
-  ConvGeom g;  // here C = Co (dy channels); N,H,W describe dx; Ho,Wo describe dy
+  int Ho, Wo, Co;
+  FastDiv fCo, fnkw;
+  int dh0, dw0;
   const void* zero;
-  FastDiv fHW, fW;
-  __device__ void init(const __bf16* dy_, const ConvGeom& g_, const FastDiv& fHW_, const FastDiv& fW_,
-                       uint32_t M, uint32_t origin, int wave, int lane, const void* zero_page) {
-    dy = dy_;
-    g = g_;
-    fHW = fHW_;
-    fW = fW_;
+  __device__ void init(const __bf16* dy_, int Ho_, int Wo_, int Co_, FastDiv fCo_,
+                       const DgradClass& cls, uint32_t M, uint32_t origin, int wave, int lane,
+                       const void* zero_page) {
+    dy = dy_; Ho = Ho_; Wo = Wo_; Co = Co_; fCo = fCo_; fnkw = cls.fnkw;
+    dh0 = cls.dh0; dw0 = cls.dw0;
     zero = zero_page;
-    K = (uint32_t)(g.KH * g.KW * g.C);
+    K = (uint32_t)(cls.ntaps * Co);
     kcol = KCGeom<R>::chunk(lane) * 8;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       uint32_t m = origin + KCGeom<R>::row(wave, i, lane);
       if (m < M) {
-        uint32_t img = fdiv(fHW, m);
-        uint32_t rem = m - img * (uint32_t)(g.H * g.W);
-        uint32_t hh = fdiv(fW, rem);
-        h[i] = (int)hh + g.pad;
-        w[i] = (int)(rem - hh * (uint32_t)g.W) + g.pad;
-        imgbase[i] = (long)img * g.Ho * g.Wo;
+        uint32_t img = fdiv(cls.fHcWc, m);
+        uint32_t rem = m - img * (uint32_t)(cls.Hc * cls.Wc);
+        uint32_t ii = fdiv(cls.fWc, rem);
+        i_[i] = (int)ii;
+        j_[i] = (int)(rem - ii * (uint32_t)cls.Wc);
+        imgbase[i] = (long)img * Ho * Wo;
       } else {
-        h[i] = w[i] = 0;
+        i_[i] = j_[i] = 0;
         imgbase[i] = -1;
       }
     }
@@ -198,20 +213,13 @@ struct KCDgrad {
   __device__ const void* src(int kt, int i) const {
     uint32_t k = (uint32_t)kt * BK + kcol;
     if (k >= K || imgbase[i] < 0) return zero;
-    uint32_t tap = fdiv(g.fC, k);
-    uint32_t co = k - tap * (uint32_t)g.C;
-    uint32_t kh = fdiv(g.fKW, tap);
-    uint32_t kw = tap - kh * (uint32_t)g.KW;
-    int hn = h[i] - (int)kh, wn = w[i] - (int)kw;
-    if (hn < 0 || wn < 0) return zero;
-    int ho = hn, wo = wn;
-    if (g.stride != 1) {
-      if ((hn % g.stride) | (wn % g.stride)) return zero;
-      ho = hn / g.stride;
-      wo = wn / g.stride;
-    }
-    if (ho >= g.Ho || wo >= g.Wo) return zero;
-    return dy + (imgbase[i] + (long)ho * g.Wo + wo) * g.C + co;
+    uint32_t t = fdiv(fCo, k);
+    uint32_t co = k - t * (uint32_t)Co;
+    uint32_t a = fdiv(fnkw, t);
+    uint32_t b = t - a * fnkw.d;
+    int ho = i_[i] + dh0 - (int)a, wo = j_[i] + dw0 - (int)b;
+    if ((unsigned)ho >= (unsigned)Ho || (unsigned)wo >= (unsigned)Wo) return zero;
+    return dy + (imgbase[i] + (long)ho * Wo + wo) * Co + co;
   }
 };
 
@@ -243,7 +251,7 @@ struct MCDense {
   }
 };
 
-// Conv data-grad B operand: B(k = (kh,kw,co), n = ci) = Wt[co][kh][kw][ci] (weights [Co,KH,KW,Ci]).
+// Conv data-grad B operand: B(k = (t, co), n = ci) = W[co][tap(t)][ci] (weights [Co,KH,KW,Ci]).
 template <int W>
 struct MCDgradW {
   static constexpr bool KC = false;
@@ -251,12 +259,15 @@ struct MCDgradW {
   const __bf16* colptr[NI];
   uint32_t krow[NI];
   uint32_t K, Co, taps, Ci;
-  FastDiv fCo;
+  FastDiv fCo, fnkw;
+  int kh0, kw0, S, KW;
   const void* zero;
   __device__ void init(const __bf16* w, uint32_t Co_, uint32_t taps_, uint32_t Ci_, FastDiv fCo_,
-                       uint32_t origin, int wave, int lane, const void* zero_page) {
-    Co = Co_; taps = taps_; Ci = Ci_; fCo = fCo_;
-    K = Co * taps;
+                       const DgradClass& cls, uint32_t origin, int wave, int lane,
+                       const void* zero_page) {
+    Co = Co_; taps = taps_; Ci = Ci_; fCo = fCo_; fnkw = cls.fnkw;
+    kh0 = cls.kh0; kw0 = cls.kw0; S = cls.S; KW = cls.KW;
+    K = Co * (uint32_t)cls.ntaps;
     zero = zero_page;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -268,8 +279,11 @@ struct MCDgradW {
   __device__ const void* src(int kt, int i) const {
     uint32_t k = (uint32_t)kt * BK + krow[i];
     if (colptr[i] == nullptr || k >= K) return zero;
-    uint32_t tap = fdiv(fCo, k);
-    uint32_t co = k - tap * Co;
+    uint32_t t = fdiv(fCo, k);
+    uint32_t co = k - t * Co;
+    uint32_t a = fdiv(fnkw, t);
+    uint32_t b = t - a * fnkw.d;
+    uint32_t tap = (uint32_t)(kh0 + S * (int)a) * (uint32_t)KW + (uint32_t)(kw0 + S * (int)b);
     return colptr[i] + ((long)co * taps + tap) * Ci;
   }
 };

@@ -14,12 +14,17 @@ struct ConvShape {
   int Ho, Wo;        // output
 };
 
-// Number of BN-partial rows the forward kernel writes (stats slab height).
+// BatchNorm statistics are accumulated with fp32 atomics into kStatReplicas replica rows of a
+// [R][C] slab (spreads contention); the consumer (bn_finalize / bwd finalize) reduces the R rows
+// and ZEROES the slab again, so a persistent zero-initialised slab can be reused every step.
+constexpr int kStatReplicas = 16;
 int conv_fwd_stat_rows(const ConvShape& s);
+// st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
               const float* st_shift, const ConvShape& s, hipStream_t st);
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st);
-// dw must be zero-filled by the caller (split-K accumulates with fp32 atomics)
+// dw is ACCUMULATED into with fp32 atomics (split-K): pass a zeroed buffer, or the parameter's
+// gradient buffer to fuse autograd's accumulation (gradient lands directly in the DDP bucket)
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st);
 
 // ---- dense GEMM: C[M][N] = op(A) op(B) --------------------------------------------------------
@@ -31,20 +36,22 @@ void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc
 // ---- BatchNorm ------------------------------------------------------------------------------
 // Reduce a [P][C] partial slab pair (shifted sums) and finalize: mean, invstd, scale, bias and
 // running-stat update.  work: >= 2*64*C floats scratch.
-void bn_finalize(const float* psum, const float* psq, int P, int C, long count, const float* shift,
+// psum/psq: [P][C] slabs; when zero_after the slabs are re-zeroed (replica slabs).
+void bn_finalize(float* psum, float* psq, int P, int C, long count, const float* shift,
                  const float* gamma, const float* beta, float* run_mean, float* run_var,
                  float momentum, float eps, float* mean, float* invstd, float* scale, float* bias,
-                 float* work, hipStream_t st);
+                 bool zero_after, hipStream_t st);
 // z = act(y*scale + bias [+ r | + r*rscale + rbias])   (M rows of C channels, bf16)
 void bn_act_fwd(const void* y, const float* scale, const float* bias, const void* r,
                 const float* rscale, const float* rbias, void* z, long M, int C, bool relu,
                 hipStream_t st);
-// sums: out_g[C], out_gx[C], out_gx2[C] (if y2); work >= 3*P*C floats where P = partial rows
-int bn_bwd_partials(long M, int C);
+// sums: out_g[C], out_gx[C], out_gx2[C] (if y2).  rep: zeroed [3][kStatReplicas][C] slab,
+// left zeroed on return.
 void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float* mean,
                        const float* invstd, const void* y2, const float* mean2,
                        const float* invstd2, bool relu, long M, int C, float* out_g,
-                       float* out_gx, float* out_gx2, float* work, hipStream_t st);
+                       float* out_gx, float* out_gx2, float* rep, float* dgamma, float* dbeta,
+                       float* dgamma2, float* dbeta2, hipStream_t st);
 void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float* mean,
                       const float* invstd, const float* gamma, const float* sum_g,
                       const float* sum_gx, const void* y2, const float* mean2,

@@ -87,10 +87,11 @@ class Conv2d(ShadowMixin, tnn.Module):
             self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
         return r
 
-    def forward(self, x: torch.Tensor, stats_shift: Optional[torch.Tensor] = None):
+    def forward(self, x: torch.Tensor, stats_shift: Optional[torch.Tensor] = None, slabs=None):
         """x: NHWC.  Returns y, or (y, psum, psumsq) when ``stats_shift`` is given."""
         w_c = self.compute_weight(x.dtype)
-        y, ps, pss = MF.conv2d(x, self.weight, w_c, self.stride[0], self.padding[0], stats_shift)
+        y, ps, pss = MF.conv2d(x, self.weight, w_c, self.stride[0], self.padding[0], stats_shift,
+                               slabs)
         if self.bias is not None:
             y = y + self.bias.to(y.dtype)
         return y if stats_shift is None else (y, ps, pss)
@@ -124,12 +125,20 @@ def conv_bn_act(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d, relu: bool = Tru
     same elementwise pass as the main path.
     """
     use_batch = bn.training
-    y, ps, pss = conv(x, bn.running_mean if use_batch else None) if use_batch else (conv(x), None, None)
+    if use_batch:
+        ws = MF.bn_workspace(bn, "fwd", x.device)
+        y, ps, pss = conv(x, bn.running_mean, None if ws is None else (ws[0], ws[1]))
+    else:
+        y, ps, pss = conv(x), None, None
     count = y.numel() // y.shape[-1]
     st = MF.bn_stats_from_partials(ps, pss, count, bn, use_batch)
     if branch is not None:
         xb, convb, bnb = branch
-        yb, psb, pssb = convb(xb, bnb.running_mean) if bnb.training else (convb(xb), None, None)
+        if bnb.training:
+            wsb = MF.bn_workspace(bnb, "fwd", xb.device)
+            yb, psb, pssb = convb(xb, bnb.running_mean, None if wsb is None else (wsb[0], wsb[1]))
+        else:
+            yb, psb, pssb = convb(xb), None, None
         stb = MF.bn_stats_from_partials(psb, pssb, count, bnb, bnb.training)
         return MF.batchnorm_act(y, st, bn, relu, y2=yb, st2=stb, bn2=bnb)
     return MF.batchnorm_act(y, st, bn, relu, residual=residual)

@@ -30,11 +30,26 @@ Tensor = torch.Tensor
 
 
 # ----------------------------------------------------------------------------- conv
+def _direct_grad_target(p: Tensor):
+    """If ``p.grad`` is p's view in a flat gradient buffer, return (space, grad) so a kernel can
+    accumulate straight into it (the DDP bucket), else None."""
+    from mipipe.optim.flat import flat_space_for
+    fs = flat_space_for(p)
+    g = p.grad
+    if fs is None or g is None or not g.is_cuda:
+        return None
+    if g.data_ptr() != fs.flat_grad.data_ptr() + 4 * fs.offset(p):
+        return None
+    return fs, g
+
+
 class _ConvFn(Function):
     @staticmethod
-    def forward(ctx, x, weight, w_c, stride, pad, shift):
-        y, psum, psumsq = K.conv_fwd(x, w_c, stride, pad, shift)
+    def forward(ctx, x, weight, w_c, stride, pad, shift, slabs=None):
+        y, psum, psumsq = K.conv_fwd(x, w_c, stride, pad, shift, slabs)
+        ctx.set_materialize_grads(False)  # stats outputs never get gradients: no zero fills
         ctx.save_for_backward(x, w_c)
+        ctx.weight = weight
         ctx.conf = (stride, pad, weight.shape[2], weight.shape[3], weight.shape[1])
         if psum is not None:
             ctx.mark_non_differentiable(psum, psumsq)
@@ -43,23 +58,34 @@ class _ConvFn(Function):
     @staticmethod
     def backward(ctx, dy, _g1, _g2):
         x, w_c = ctx.saved_tensors
+        if dy is None:
+            return None, None, None, None, None, None, None
         stride, pad, kh, kw, ci = ctx.conf
         dy = dy.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = K.conv_dgrad(dy, w_c, x.shape, stride, pad)
         if ctx.needs_input_grad[1]:
-            dw = K.conv_wgrad(dy, x, kh, kw, stride, pad)
-            if dw.shape[-1] != ci:  # input channels were zero-padded for the kernel
-                dw = dw[..., :ci]
-            dw = dw.permute(0, 3, 1, 2)
-        return dx, dw, None, None, None, None
+            weight = ctx.weight
+            tgt = _direct_grad_target(weight) if x.shape[-1] == ci and K.use_native(dy) else None
+            if tgt is not None:
+                # gradient accumulates straight into the flat DDP bucket: no zero-fill, no
+                # autograd AccumulateGrad add; tell the reducer the gradient is ready.
+                fs, g = tgt
+                K.conv_wgrad(dy, x, kh, kw, stride, pad, out=g.permute(0, 2, 3, 1))
+                fs.grad_ready(weight)
+            else:
+                dw = K.conv_wgrad(dy, x, kh, kw, stride, pad)
+                if dw.shape[-1] != ci:  # input channels were zero-padded for the kernel
+                    dw = dw[..., :ci]
+                dw = dw.permute(0, 3, 1, 2)
+        return dx, dw, None, None, None, None, None
 
 
 def conv2d(x: Tensor, weight: Tensor, w_c: Tensor, stride: int, pad: int,
-           stats_shift: Optional[Tensor] = None):
+           stats_shift: Optional[Tensor] = None, slabs=None):
     """NHWC conv.  Returns (y, psum, psumsq); the partials are None unless ``stats_shift``."""
-    return _ConvFn.apply(x, weight, w_c, stride, pad, stats_shift)
+    return _ConvFn.apply(x, weight, w_c, stride, pad, stats_shift, slabs)
 
 
 # ----------------------------------------------------------------------------- batchnorm
@@ -73,6 +99,31 @@ class BNStats:
     batch_stats: bool
 
 
+def bn_workspace(bn, kind: str, device) -> Optional[Tensor]:
+    """Persistent zero-initialised replica slab for BN statistics on the GPU ('fwd': [2,R,C],
+    'bwd': [3,R,C]).  Kernels that accumulate into it are always followed by the kernel that
+    reads AND re-zeroes it; a per-module 'pending' flag re-zeroes after an interrupted step."""
+    if device.type != "cuda" or not K.native_available():
+        return None
+    C = bn.num_features
+    R = K.native().STAT_REPLICAS
+    attr = "_mipipe_ws_" + kind
+    ws = bn.__dict__.get(attr)
+    rows = 2 if kind == "fwd" else 3
+    if ws is None or ws.device != device or ws.numel() != rows * R * C:
+        ws = torch.zeros(rows, R, C, device=device, dtype=torch.float32)
+        bn.__dict__[attr] = ws
+    pend = "_mipipe_pending_" + kind
+    if bn.__dict__.get(pend):
+        ws.zero_()
+    bn.__dict__[pend] = True
+    return ws
+
+
+def _ws_done(bn, kind: str) -> None:
+    bn.__dict__["_mipipe_pending_" + kind] = False
+
+
 def bn_stats_from_partials(psum, psumsq, count, bn, training: bool) -> BNStats:
     """Finalize batch statistics (training) or use running statistics (eval)."""
     if training:
@@ -81,6 +132,7 @@ def bn_stats_from_partials(psum, psumsq, count, bn, training: bool) -> BNStats:
             psum, psumsq, count, bn.running_mean, bn.weight.detach(), bn.bias.detach(),
             bn.running_mean if bn.track_running_stats else None,
             bn.running_var if bn.track_running_stats else None, mom, bn.eps)
+        _ws_done(bn, "fwd")
         if bn.track_running_stats:
             bn.num_batches_tracked.add_(1)
         return BNStats(mean, invstd, scale, bias, count, True)
@@ -93,13 +145,15 @@ def bn_stats_from_partials(psum, psumsq, count, bn, training: bool) -> BNStats:
 
 class _BNActFn(Function):
     @staticmethod
-    def forward(ctx, y, gamma, beta, residual, y2, gamma2, beta2, st, st2, relu):
+    def forward(ctx, y, gamma, beta, residual, y2, gamma2, beta2, st, st2, relu, bn=None):
         z = K.bn_act_fwd(y, st.scale, st.bias, relu,
                          residual if y2 is None else y2,
                          None if st2 is None else st2.scale, None if st2 is None else st2.bias)
         ctx.save_for_backward(y, z, y2, gamma, gamma2)
         ctx.st, ctx.st2, ctx.relu = st, st2, relu
         ctx.has_res = residual is not None
+        ctx.bn = bn
+        ctx.beta, ctx.beta2 = beta, beta2
         return z
 
     @staticmethod
@@ -107,14 +161,36 @@ class _BNActFn(Function):
         y, z, y2, gamma, gamma2 = ctx.saved_tensors
         st, st2, relu = ctx.st, ctx.st2, ctx.relu
         dz = dz.contiguous()
+        rep = bn_workspace(ctx.bn, "bwd", dz.device) if ctx.bn is not None else None
+        # BN affine grads accumulate straight into the flat gradient buffer when possible
+        direct = None
+        if rep is not None and st.batch_stats and ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
+            tg, tb = _direct_grad_target(gamma), _direct_grad_target(ctx.beta)
+            ok = tg is not None and tb is not None
+            t2g = t2b = None
+            if y2 is not None:
+                t2g, t2b = _direct_grad_target(gamma2), _direct_grad_target(ctx.beta2)
+                ok = ok and t2g is not None and t2b is not None and st2.batch_stats
+            if ok:
+                direct = (tg[1], tb[1], None if t2g is None else t2g[1],
+                          None if t2b is None else t2b[1])
         sg, sgx, sgx2 = K.bn_act_bwd_reduce(dz, z, y, st.mean, st.invstd, relu, y2,
                                             None if st2 is None else st2.mean,
-                                            None if st2 is None else st2.invstd)
-        zero = torch.zeros_like(sg)
-        a_g, a_gx = (sg, sgx) if st.batch_stats else (zero, zero)
-        a_gx2 = None
-        if st2 is not None:
-            a_gx2 = sgx2 if st2.batch_stats else zero
+                                            None if st2 is None else st2.invstd, rep, direct)
+        if ctx.bn is not None:
+            _ws_done(ctx.bn, "bwd")
+        if direct is not None:
+            fs = _direct_grad_target(gamma)[0]
+            for p in (gamma, ctx.beta) + ((gamma2, ctx.beta2) if y2 is not None else ()):
+                fs.grad_ready(p)
+        if st.batch_stats and (st2 is None or st2.batch_stats):
+            a_g, a_gx, a_gx2 = sg, sgx, sgx2
+        else:
+            zero = torch.zeros_like(sg)
+            a_g, a_gx = (sg, sgx) if st.batch_stats else (zero, zero)
+            a_gx2 = None
+            if st2 is not None:
+                a_gx2 = sgx2 if st2.batch_stats else zero
         dy, other = K.bn_act_bwd_apply(
             dz, z, y, st.mean, st.invstd, gamma.detach(), a_g, a_gx, st.count, relu,
             want_dres=ctx.has_res, y2=y2, mean2=None if st2 is None else st2.mean,
@@ -122,11 +198,13 @@ class _BNActFn(Function):
             gamma2=None if gamma2 is None else gamma2.detach(), sum_gx2=a_gx2)
         dres = other if ctx.has_res else None
         dy2 = other if y2 is not None else None
+        if direct is not None:
+            return dy, None, None, dres, dy2, None, None, None, None, None, None
         dgamma2 = sgx2 if y2 is not None else None
         dbeta2 = sg if y2 is not None else None
         return (dy, sgx.to(gamma.dtype), sg.to(gamma.dtype), dres, dy2,
                 None if dgamma2 is None else dgamma2.to(gamma2.dtype),
-                None if dbeta2 is None else dbeta2.to(gamma2.dtype), None, None, None)
+                None if dbeta2 is None else dbeta2.to(gamma2.dtype), None, None, None, None)
 
 
 def batchnorm_act(y: Tensor, st: BNStats, bn, relu: bool, residual: Optional[Tensor] = None,
@@ -134,7 +212,7 @@ def batchnorm_act(y: Tensor, st: BNStats, bn, relu: bool, residual: Optional[Ten
     """z = relu?( bn(y) [+ residual | + bn2(y2)] )."""
     return _BNActFn.apply(y, bn.weight, bn.bias, residual, y2,
                           None if bn2 is None else bn2.weight,
-                          None if bn2 is None else bn2.bias, st, st2, relu)
+                          None if bn2 is None else bn2.bias, st, st2, relu, bn)
 
 
 def channel_partials(y: Tensor, shift: Tensor) -> Tuple[Tensor, Tensor]:
@@ -195,6 +273,7 @@ class _LinearFn(Function):
             y = K.gemm(x2, w_c, False, True, bias, act, x.dtype)
             ctx.save_for_backward(x2, w_c, y if act == "relu" else None)
         ctx.act, ctx.shp, ctx.has_bias = act, shp, bias is not None
+        ctx.weight = weight
         return y.reshape(*shp[:-1], y.shape[-1])
 
     @staticmethod
@@ -210,7 +289,13 @@ class _LinearFn(Function):
             dx = K.gemm(dy2, w_c, False, False, None, "none", dy2.dtype).reshape(ctx.shp)
         gdt = torch.float64 if dy2.dtype == torch.float64 else torch.float32
         if ctx.needs_input_grad[1]:
-            dw = K.gemm(dy2, x2, True, False, None, "none", gdt)
+            tgt = _direct_grad_target(ctx.weight) if K.use_native(dy2) else None
+            if tgt is not None:
+                fs, g = tgt
+                K.gemm(dy2, x2, True, False, None, "none", torch.float32, g, 1.0)
+                fs.grad_ready(ctx.weight)
+            else:
+                dw = K.gemm(dy2, x2, True, False, None, "none", gdt)
         if ctx.has_bias and ctx.needs_input_grad[3]:
             db = dy2.to(gdt).sum(0)
         return dx, dw, None, db, None

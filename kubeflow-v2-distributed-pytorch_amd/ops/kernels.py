@@ -36,9 +36,12 @@ def use_native(t: torch.Tensor) -> bool:
         "`python setup.py build_ext --inplace`).  Set MIPIPE_ALLOW_REF_ON_GPU=1 only to debug.")
 
 
-def conv_fwd(x, w, stride, pad, stats_shift=None):
+def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None):
+    """``slabs``: persistent zeroed (sum, sumsq) replica slabs the GPU epilogue accumulates BN
+    statistics into (re-zeroed by :func:`bn_finalize`)."""
     if use_native(x):
-        return native().conv_fwd(x, w, stride, pad, stats_shift)
+        s1, s2 = slabs if slabs is not None else (None, None)
+        return native().conv_fwd(x, w, stride, pad, stats_shift, s1, s2)
     return _ref.conv_fwd(x, w, stride, pad, stats_shift)
 
 
@@ -48,10 +51,15 @@ def conv_dgrad(dy, w, x_shape, stride, pad):
     return _ref.conv_dgrad(dy, w, x_shape, stride, pad)
 
 
-def conv_wgrad(dy, x, kh, kw, stride, pad):
+def conv_wgrad(dy, x, kh, kw, stride, pad, out=None):
+    """``out``: accumulate into this fp32 [Co,KH,KW,Ci] buffer (the parameter's flat gradient)."""
     if use_native(dy):
-        return native().conv_wgrad(dy, x, kh, kw, stride, pad)
-    return _ref.conv_wgrad(dy, x, kh, kw, stride, pad)
+        return native().conv_wgrad(dy, x, kh, kw, stride, pad, out)
+    dw = _ref.conv_wgrad(dy, x, kh, kw, stride, pad)
+    if out is not None:
+        out.add_(dw)
+        return out
+    return dw
 
 
 def bn_finalize(psum, psumsq, count, shift, gamma, beta, running_mean, running_var,
@@ -69,15 +77,25 @@ def bn_act_fwd(y, scale, bias, relu, residual=None, res_scale=None, res_bias=Non
     return _ref.bn_act_fwd(y, scale, bias, relu, residual, res_scale, res_bias)
 
 
-def bn_act_bwd_reduce(dz, z, y, mean, invstd, relu, y2=None, mean2=None, invstd2=None):
+def bn_act_bwd_reduce(dz, z, y, mean, invstd, relu, y2=None, mean2=None, invstd2=None,
+                      rep=None, acc=None):
     """Returns (Σg, Σg·x̂) for y and, when ``y2`` is given (downsample branch sharing the same
-    add/ReLU), (Σg·x̂2) for y2 as a third output."""
+    add/ReLU), (Σg·x̂2) for y2 as a third output.  ``rep``: persistent zeroed replica slab."""
     if use_native(dz):
-        return native().bn_act_bwd_reduce(dz, z, y, mean, invstd, relu, y2, mean2, invstd2)
+        a = acc if acc is not None else (None, None, None, None)
+        return native().bn_act_bwd_reduce(dz, z, y, mean, invstd, relu, y2, mean2, invstd2, rep,
+                                          *a)
     sg, sgx = _ref.bn_act_bwd_reduce(dz, z, y, mean, invstd, relu)
-    if y2 is None:
-        return sg, sgx, None
-    _, sgx2 = _ref.bn_act_bwd_reduce(dz, z, y2, mean2, invstd2, relu)
+    sgx2 = None
+    if y2 is not None:
+        _, sgx2 = _ref.bn_act_bwd_reduce(dz, z, y2, mean2, invstd2, relu)
+    if acc is not None:  # same contract as the native kernel: accumulate dγ/dβ in place
+        dg, db, dg2, db2 = acc
+        dg.add_(sgx.to(dg.dtype))
+        db.add_(sg.to(db.dtype))
+        if dg2 is not None:
+            dg2.add_(sgx2.to(dg2.dtype))
+            db2.add_(sg.to(db2.dtype))
     return sg, sgx, sgx2
 
 
@@ -121,11 +139,42 @@ def avgpool_bwd(dy, x_shape):
     return _ref.avgpool_bwd(dy, x_shape)
 
 
+def _pad2(t, r, c):
+    """Zero-pad a 2-D tensor to [r, c] (no copy when already that shape)."""
+    if t.shape[0] == r and t.shape[1] == c:
+        return t
+    out = t.new_zeros(r, c)
+    out[: t.shape[0], : t.shape[1]] = t
+    return out
+
+
 def gemm(a, b, trans_a=False, trans_b=False, bias=None, act="none", out_dtype=None, c=None,
          beta=0.0):
     if use_native(a):
-        return native().gemm(a, b, trans_a, trans_b, bias, act,
-                             out_dtype if out_dtype is not None else a.dtype, c, beta)
+        odt = out_dtype if out_dtype is not None else a.dtype
+        M = a.shape[1] if trans_a else a.shape[0]
+        Kd = a.shape[0] if trans_a else a.shape[1]
+        N = b.shape[0] if trans_b else b.shape[1]
+        r8 = lambda v: (v + 7) // 8 * 8  # noqa: E731
+        if M % 8 == 0 and N % 8 == 0 and Kd % 8 == 0:
+            return native().gemm(a, b, trans_a, trans_b, bias, act, odt, c, beta)
+        # odd sizes (e.g. a 10-class head): zero-pad every operand dim to a multiple of 8 —
+        # the kernels vectorise 16-byte rows; the pad contributes exact zeros
+        Mp, Np, Kp = r8(M), r8(N), r8(Kd)
+        ap = _pad2(a, Kp, Mp) if trans_a else _pad2(a, Mp, Kp)
+        bp = _pad2(b, Np, Kp) if trans_b else _pad2(b, Kp, Np)
+        biasp = None
+        if bias is not None:
+            biasp = bias.new_zeros(Np)
+            biasp[:N] = bias
+        accumulate = c is not None and beta != 0.0
+        y = native().gemm(ap.contiguous(), bp.contiguous(), trans_a, trans_b, biasp, act,
+                          torch.float32 if accumulate else odt, None, 0.0)
+        y = y[:M, :N]
+        if accumulate:
+            c.add_(y)
+            return c
+        return y.contiguous()
     return _ref.gemm(a, b, trans_a, trans_b, bias, act, out_dtype, c, beta)
 
 

@@ -74,6 +74,17 @@ class FlatParamSpace:
         self._synced_version = -1
         self.refresh_shadow()
         self._bound_modules: List[weakref.ref] = []
+        self._ready_listeners: List = []
+
+    # ------------------------------------------------------------------ readiness
+    def add_ready_listener(self, fn) -> None:
+        """``fn(param)`` is called when a kernel wrote a parameter's gradient directly into the
+        flat buffer (bypassing autograd's AccumulateGrad and its post-accumulate hooks)."""
+        self._ready_listeners.append(fn)
+
+    def grad_ready(self, p: torch.Tensor) -> None:
+        for fn in self._ready_listeners:
+            fn(p)
 
     # ------------------------------------------------------------------ views
     def offset(self, p: torch.Tensor) -> int:

@@ -110,7 +110,9 @@ class DistributedDataParallel(tnn.Module):
                 self._bucket_of[id(p)] = b
         self._next_bucket = 0
         self._callback_queued = False
-        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(p)) for p in params]
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_ready) for p in params]
+        # kernels that accumulate weight gradients straight into the flat buffer report here
+        self.space.add_ready_listener(self._on_ready)
 
     # ------------------------------------------------------------------ construction
     def _verify_shapes(self, params) -> None:
@@ -200,17 +202,17 @@ class DistributedDataParallel(tnn.Module):
         self._callback_queued = False
         self.space.ensure_grad_views()
 
-    def _make_hook(self, p):
-        def hook(param):
-            if self.world <= 1 or not self._sync_enabled:
-                return
-            if not self._callback_queued:
-                self._callback_queued = True
-                torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
-            b = self._bucket_of[id(param)]
-            b.pending -= 1
-            self._launch_ready()
-        return hook
+    def _on_ready(self, param) -> None:
+        if self.world <= 1 or not self._sync_enabled:
+            return
+        b = self._bucket_of.get(id(param))
+        if b is None:
+            return
+        if not self._callback_queued:
+            self._callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+        b.pending -= 1
+        self._launch_ready()
 
     def _launch(self, b: Bucket) -> None:
         g = self.space.flat_grad[b.start:b.end]

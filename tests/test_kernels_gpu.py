@@ -145,8 +145,10 @@ def test_bn_pipeline(C):
     beta = torch.randn(C, device=dev)
     rm, rv = torch.randn(C, device=dev), torch.rand(C, device=dev) + 0.5
     rm2, rv2 = rm.clone(), rv.clone()
+    # reference first: the native finalize re-zeroes the (replica) slabs it consumed
+    ref = _ref.bn_finalize(psum.clone(), psq.clone(), M, shift, gamma, beta, rm2, rv2, 0.1, 1e-5)
     out = native().bn_finalize(psum, psq, M, shift, gamma, beta, rm, rv, 0.1, 1e-5)
-    ref = _ref.bn_finalize(psum, psq, M, shift, gamma, beta, rm2, rv2, 0.1, 1e-5)
+    assert float(psum.abs().max()) == 0.0 and float(psq.abs().max()) == 0.0
     for o, r in zip(out, ref):
         assert rel_err(o, r) < 1e-4
     assert rel_err(rm, rm2) < 1e-5 and rel_err(rv, rv2) < 1e-5
@@ -266,3 +268,21 @@ def test_layernorm_gelu_embedding():
     assert rel_err(e, _ref.embedding_bwd(dy.float(), idx, 50)) < 1e-3
     cs = native().colsum(dy)
     assert rel_err(cs, dy.float().sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 10, 2048), (30, 100, 512), (64, 16, 27)])
+def test_gemm_odd_sizes_padded(M, N, K):
+    """Odd sizes (10/100-class heads) go through the zero-padded path of ops.kernels.gemm."""
+    from mipipe.ops import kernels as Kx
+    x = bf(M, K)
+    w = bf(N, K)
+    bias = torch.randn(N, device=dev)
+    y = Kx.gemm(x, w, False, True, bias, "none", torch.bfloat16)
+    assert y.shape == (M, N)
+    assert rel_err(y, x.float() @ w.float().t() + bias) < 1e-2
+    dy = bf(M, N)
+    g = torch.zeros(N, K, device=dev)
+    Kx.gemm(dy, x, True, False, None, "none", torch.float32, g, 1.0)
+    assert rel_err(g, dy.float().t() @ x.float()) < 2e-3
+    dx = Kx.gemm(dy, w, False, False, None, "none", torch.bfloat16)
+    assert rel_err(dx, dy.float() @ w.float()) < 1e-2
