@@ -41,7 +41,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU batch (weak scaling); default 256 images / 32 sequences")
+    ap.add_argument("--seq", type=int, default=128, help="BERT sequence length")
     ap.add_argument("--res", type=int, default=224)
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--bucket-cap-mb", type=float, default=32.0)
@@ -62,6 +64,111 @@ def main() -> int:
         dist.init_process_group("nccl", device_id=dev)
     torch.manual_seed(0)
 
+    is_bert = a.model.startswith("bert")
+    if a.batch is None:
+        a.batch = 32 if is_bert else 256
+    if is_bert:
+        step, model, batches = build_bert(a, world, local, dev, rank)
+    else:
+        step, model, batches = build_cnn(a, world, local, dev, rank)
+
+    model.train()
+    for i in range(a.warmup):
+        loss = step(*batches[i % 2])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(*batches[i % 2])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    value = a.batch * world * a.steps / dt
+    if is_bert:
+        key = f"{a.model}_{a.seq}"
+        opt_s = "AdamW(lr=1e-4,wd=0.01)"
+    else:
+        key = a.model if a.res == 224 else f"{a.model}_{a.res}"
+        opt_s = "SGD(lr=0.1,momentum=0.9,wd=1e-4)"
+    base = STOCK_1GPU.get(key)
+    loss_v = float(loss.detach().float().item())
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / (base * world), 4) if base else None,
+            "dtype": "bf16", "data": "synthetic (on-device, random-init weights)",
+            "config": {"model": a.model, "global_batch": a.batch * world,
+                       "seq_len": a.seq if is_bert else None,
+                       "image_size": None if is_bert else a.res, "batch_per_gpu": a.batch,
+                       "parallelism": f"dp{world}", "impl": a.impl, "optimizer": opt_s},
+            "final_loss": loss_v}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def build_bert(a, world, local, dev, rank):
+    """BERT-base MLM: B sequences of S tokens, 15 % masked (max_predictions 20 @128 / 80 @512
+    as in the NVIDIA/Google pretraining recipe), AdamW, dropout 0.1 on."""
+    V = 30522
+    S = a.seq
+    P = max(1, round(0.15 * S)) if S != 128 else 20
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    batches = []
+    for _ in range(2):
+        ids = torch.randint(0, V, (a.batch, S), device=dev, generator=g)
+        am = torch.ones(a.batch, S, device=dev, dtype=torch.int64)
+        pos = torch.stack([torch.randperm(S, device=dev, generator=g)[:P] for _ in range(a.batch)])
+        labels = torch.randint(0, V, (a.batch, P), device=dev, generator=g)
+        batches.append((ids, am, pos, labels))
+    if a.impl == "mipipe":
+        from mipipe.models import create_model
+        from mipipe.optim import AdamW
+        from mipipe.parallel import DistributedDataParallel
+        model = create_model(a.model).to(dev)
+        model.compute_dtype = torch.bfloat16
+        if world > 1:
+            model = DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=a.bucket_cap_mb)
+        opt = AdamW(model.parameters(), lr=1e-4, weight_decay=0.01)
+
+        def step(ids, am, pos, labels):
+            opt.zero_grad()
+            loss = model(ids, am, masked_positions=pos, labels=labels)
+            loss.backward()
+            opt.step()
+            return loss
+    else:
+        from mipipe.models.reference import ref_bert
+        model = ref_bert(a.model).to(dev)
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local])
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01, fused=True)
+        inner = model.module if world > 1 else model
+
+        def step(ids, am, pos, labels):
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                logits = model(ids, am, masked_positions=pos)
+            loss = inner.loss(logits, labels)
+            loss.backward()
+            opt.step()
+            return loss
+    return step, model, batches
+
+
+def build_cnn(a, world, local, dev, rank):
     from mipipe.data.synthetic import synthetic_batch
     idx = [torch.arange(i * a.batch, (i + 1) * a.batch, device=dev) + rank * 10_000_000
            for i in range(2)]
@@ -102,45 +209,7 @@ def main() -> int:
             opt.step()
             return loss
 
-    model.train()
-    for i in range(a.warmup):
-        loss = step(*batches[i % 2])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        loss = step(*batches[i % 2])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    value = a.batch * world * a.steps / dt
-    key = a.model if a.res == 224 else f"{a.model}_{a.res}"
-    base = STOCK_1GPU.get(key)
-    loss_v = float(loss.detach().float().item())
-    if rank == 0:
-        print(json.dumps({
-            "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": round(value / (base * world), 4) if base else None,
-            "dtype": "bf16", "data": "synthetic (on-device, random-init weights)",
-            "config": {"model": a.model, "global_batch": a.batch * world, "seq_len": None,
-                       "image_size": a.res, "batch_per_gpu": a.batch,
-                       "parallelism": f"dp{world}", "impl": a.impl,
-                       "optimizer": "SGD(lr=0.1,momentum=0.9,wd=1e-4)"},
-            "final_loss": loss_v}), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    return 0
+    return step, model, batches
 
 
 if __name__ == "__main__":

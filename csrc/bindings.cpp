@@ -547,6 +547,65 @@ Tensor colsum(Tensor x) {
   return out;
 }
 
+void check_attn(const Tensor& qkv, int64_t B, int64_t S, int64_t H) {
+  check_bf16(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B * S && qkv.size(1) == 3 * H * 64,
+              "qkv must be [B*S, 3*H*64] (head_dim 64), got ", qkv.sizes());
+  TORCH_CHECK(S >= 1 && S <= 2048, "attention supports 1 <= S <= 2048, got ", S);
+  TORCH_CHECK(B * S * H * 64 < (1ll << 31), "attention problem too large");
+}
+
+const float* mask_ptr(const optional<Tensor>& mask, int64_t B, int64_t S) {
+  if (!mask.has_value()) return nullptr;
+  check_f32(*mask, "mask");
+  TORCH_CHECK(mask->numel() == B * S, "mask must be [B, S]");
+  return mask->data_ptr<float>();
+}
+
+std::tuple<Tensor, Tensor> attention_fwd(Tensor qkv, int64_t B, int64_t S, int64_t H,
+                                         optional<Tensor> mask, double scale, double p_drop,
+                                         int64_t seed) {
+  check_attn(qkv, B, S, H);
+  c10::DeviceGuard g(qkv.device());
+  TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "dropout p must be in [0, 1)");
+  auto o = torch::empty({B * S, H * 64}, qkv.options());
+  auto lse = torch::empty({B, H, S}, qkv.options().dtype(at::kFloat));
+  mipipe::attention_fwd(qkv.data_ptr(), mask_ptr(mask, B, S), o.data_ptr(), lse.data_ptr<float>(),
+                        (int)B, (int)S, (int)H, (float)scale, (float)p_drop, (uint32_t)seed,
+                        stream());
+  return {o, lse};
+}
+
+Tensor attention_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, int64_t B, int64_t S,
+                     int64_t H, optional<Tensor> mask, double scale, double p_drop, int64_t seed) {
+  check_attn(qkv, B, S, H);
+  check_bf16(dout, "dout");
+  check_bf16(o, "o");
+  check_f32(lse, "lse");
+  c10::DeviceGuard g(qkv.device());
+  TORCH_CHECK(dout.numel() == B * S * H * 64 && o.numel() == B * S * H * 64, "dout/o shape");
+  TORCH_CHECK(lse.numel() == B * H * S, "lse shape");
+  auto dqkv = torch::empty_like(qkv);
+  auto f = qkv.options().dtype(at::kFloat);
+  auto delta = torch::empty({B, H, S}, f);
+  auto dq_acc = torch::empty({B * S, H * 64}, f);
+  mipipe::attention_bwd(dout.data_ptr(), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                        mask_ptr(mask, B, S), dqkv.data_ptr(), delta.data_ptr<float>(),
+                        dq_acc.data_ptr<float>(), (int)B, (int)S, (int)H, (float)scale,
+                        (float)p_drop, (uint32_t)seed, stream());
+  return dqkv;
+}
+
+Tensor dropout_fwd(Tensor x, double p, int64_t seed) {
+  check_bf16(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
+  TORCH_CHECK(x.numel() % 8 == 0, "dropout needs numel % 8 == 0");
+  auto y = torch::empty_like(x);
+  mipipe::dropout_fwd(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (uint32_t)seed, stream());
+  return y;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -584,4 +643,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("colsum", &colsum);
+  m.def("attention_fwd", &attention_fwd, py::arg("qkv"), py::arg("B"), py::arg("S"), py::arg("H"),
+        py::arg("mask") = py::none(), py::arg("scale") = 0.125, py::arg("p_drop") = 0.0,
+        py::arg("seed") = 0);
+  m.def("attention_bwd", &attention_bwd, py::arg("dout"), py::arg("qkv"), py::arg("o"),
+        py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("mask") = py::none(),
+        py::arg("scale") = 0.125, py::arg("p_drop") = 0.0, py::arg("seed") = 0);
+  m.def("dropout_fwd", &dropout_fwd);
 }

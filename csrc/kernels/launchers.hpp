@@ -91,12 +91,18 @@ void layernorm_bwd(const void* dy, const void* x, const float* mean, const float
                    long rows, int H, hipStream_t st);
 void gelu_fwd(const void* x, void* y, long n, hipStream_t st);
 void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st);
-void attention_fwd(const void* q, const void* k, const void* v, const float* mask_bias, void* o,
-                   float* lse, int B, int H, int S, int D, float scale, hipStream_t st);
-void attention_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
-                   const float* lse, const float* mask_bias, void* dq, void* dk, void* dv,
-                   float* delta, float* dq_acc, int B, int H, int S, int D, float scale,
-                   hipStream_t st);
+// Fused self-attention, head_dim 64, on the packed projection layout (attention.hip):
+//   qkv [B*S][3*H*64] bf16, o [B*S][H*64] bf16, lse [B][H][S] fp32, mask [B][S] additive or null.
+// p_drop > 0 applies attention-probability dropout keyed by (seed, b, h, q, k).
+void attention_fwd(const void* qkv, const float* mask, void* o, float* lse, int B, int S, int H,
+                   float scale, float p_drop, uint32_t seed, hipStream_t st);
+// dqkv [B*S][3*H*64]; delta [B][H][S] and dq_acc [B*S][H*64] fp32 are scratch.
+void attention_bwd(const void* dout, const void* qkv, const void* o, const float* lse,
+                   const float* mask, void* dqkv, float* delta, float* dq_acc, int B, int S,
+                   int H, float scale, float p_drop, uint32_t seed, hipStream_t st);
+// Elementwise dropout keyed by (seed, element index): y = x * keep / (1 - p); the backward
+// recomputes the same keep mask from the seed (no mask tensor).
+void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStream_t st);
 void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, hipStream_t st);
 void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
                 hipStream_t st);

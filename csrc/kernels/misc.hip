@@ -545,4 +545,35 @@ void layernorm_bwd(const void* dy, const void* x, const float* mean, const float
   colsum_f32(pb, false, dbeta, G, H, scratch + 64L * H, st);
 }
 
+// ------------------------------------------------------------------------------ dropout
+__device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
+  x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
+  return x;
+}
+
+__global__ __launch_bounds__(256) void dropout_kernel(const __bf16* __restrict__ x,
+                                                      __bf16* __restrict__ y, long n8, float scale,
+                                                      uint32_t thr, uint32_t seed) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], f);
+    const uint32_t base = drop_mix(seed * 0x9e3779b1u + 0x7f4a7c15u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t hsh = drop_mix(base ^ (uint32_t)(i * 8 + e) * 0x85ebca77u);
+      f[e] = hsh >= thr ? f[e] * scale : 0.f;
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(f);
+  }
+}
+
+void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStream_t st) {
+  const long n8 = n / 8;
+  double t = (double)p * 4294967296.0;
+  uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid1d(n8)), dim3(256), 0, st, (const __bf16*)x,
+                     (__bf16*)y, n8, 1.f / (1.f - p), thr, seed);
+}
+
 }  // namespace mipipe

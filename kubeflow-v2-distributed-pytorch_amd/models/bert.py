@@ -1,0 +1,282 @@
+"""BERT-base masked-LM on mipipe's fused kernels (BASELINE config 4).
+
+The reference trains torchvision CNNs only (task.py:50-52, 165-171); BASELINE.json adds a
+"BERT-base MLM DDP" config whose kernel list SURVEY.md §2.5 gives: QKV / output / FFN GEMMs with
+bias and GELU epilogues, LayerNorm fwd/bwd, flash-style attention, embedding gather +
+scatter-add backward, the MLM head GEMM + cross-entropy over 30522 classes, dropout and fused
+AdamW.  Every one of those runs on a mipipe HIP kernel here:
+
+* one fused QKV projection GEMM per layer; its [tokens, 3*768] output is consumed in place by
+  the attention kernel (attention.hip) and the attention output feeds the output projection
+  without any head transpose;
+* post-LN residual adds are fused into the LayerNorm kernel (``LN(x + residual)``);
+* dropout masks are hashed from (seed, element) and regenerated in the backward;
+* the MLM head runs only on the masked positions (``masked_positions``, NVIDIA/Megatron
+  style) — the loss and gradients equal the dense head's, which spends ~85 % of its FLOPs on
+  ignored (-100) tokens.
+
+``state_dict`` keys follow HuggingFace ``BertForMaskedLM`` (``bert.embeddings.*``,
+``bert.encoder.layer.N.attention.self.{query,key,value}.*`` ...): the fused QKV parameter is
+split / merged by state-dict hooks, so checkpoints interchange with the stock model in
+:mod:`mipipe.models.reference`.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as tnn
+
+from mipipe import nn as mnn
+from mipipe.ops import functional as MF
+
+from . import register_model
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden_size: int = 768
+    num_hidden_layers: int = 12
+    num_attention_heads: int = 12
+    intermediate_size: int = 3072
+    max_position_embeddings: int = 512
+    type_vocab_size: int = 2
+    layer_norm_eps: float = 1e-12
+    hidden_dropout_prob: float = 0.1
+    attention_probs_dropout_prob: float = 0.1
+    initializer_range: float = 0.02
+
+
+def _seed(base: int, step: int, site: int) -> int:
+    return (base * 0x9E3779B1 + step * 0x85EBCA77 + site * 0xC2B2AE35 + 0x165667B1) & 0xFFFFFFFF
+
+
+class _Embeddings(tnn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.word_embeddings = mnn.Embedding(c.vocab_size, c.hidden_size)
+        self.position_embeddings = mnn.Embedding(c.max_position_embeddings, c.hidden_size)
+        self.token_type_embeddings = mnn.Embedding(c.type_vocab_size, c.hidden_size)
+        self.LayerNorm = mnn.LayerNorm(c.hidden_size, eps=c.layer_norm_eps)
+
+
+class _SelfAttention(tnn.Module):
+    """Holds the fused ``qkv`` projection; exposes HF's query/key/value keys via hooks."""
+
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.qkv = mnn.Linear(c.hidden_size, 3 * c.hidden_size)
+
+
+class _Dense(tnn.Module):
+    def __init__(self, cin: int, cout: int, eps: Optional[float] = None):
+        super().__init__()
+        self.dense = mnn.Linear(cin, cout)
+        if eps is not None:
+            self.LayerNorm = mnn.LayerNorm(cout, eps=eps)
+
+
+class _Attention(tnn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.self = _SelfAttention(c)
+        self.output = _Dense(c.hidden_size, c.hidden_size, c.layer_norm_eps)
+
+
+class BertLayer(tnn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.attention = _Attention(c)
+        self.intermediate = _Dense(c.hidden_size, c.intermediate_size)
+        self.output = _Dense(c.intermediate_size, c.hidden_size, c.layer_norm_eps)
+        self.heads = c.num_attention_heads
+        self.p_hidden = c.hidden_dropout_prob
+        self.p_attn = c.attention_probs_dropout_prob
+
+    def forward(self, h: torch.Tensor, B: int, S: int, mask: Optional[torch.Tensor],
+                seeds) -> torch.Tensor:
+        train = self.training
+        qkv = self.attention.self.qkv(h)
+        ctx = MF.attention(qkv, B, S, self.heads, mask, p_drop=self.p_attn if train else 0.0,
+                           seed=seeds[0])
+        a = self.attention.output.dense(ctx)
+        a = MF.dropout(a, self.p_hidden, seeds[1], train)
+        h1 = self.attention.output.LayerNorm(a, residual=h)
+        f = self.intermediate.dense(h1, act="gelu")
+        f2 = self.output.dense(f)
+        f2 = MF.dropout(f2, self.p_hidden, seeds[2], train)
+        return self.output.LayerNorm(f2, residual=h1)
+
+
+class _Encoder(tnn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.layer = tnn.ModuleList([BertLayer(c) for _ in range(c.num_hidden_layers)])
+
+
+class _BertModel(tnn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.embeddings = _Embeddings(c)
+        self.encoder = _Encoder(c)
+
+
+class _Transform(tnn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.dense = mnn.Linear(c.hidden_size, c.hidden_size)
+        self.LayerNorm = mnn.LayerNorm(c.hidden_size, eps=c.layer_norm_eps)
+
+
+class _Predictions(tnn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.transform = _Transform(c)
+        self.bias = tnn.Parameter(torch.zeros(c.vocab_size))
+
+
+class _Cls(tnn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.predictions = _Predictions(c)
+
+
+class BertForMaskedLM(tnn.Module):
+    """``forward(input_ids, attention_mask=None, token_type_ids=None, masked_positions=None)``
+    -> MLM logits ``[B*P, V]`` for the masked positions (or ``[B*S, V]`` for all tokens).
+    ``loss(logits, labels)`` = mean cross-entropy (labels -100 ignored)."""
+
+    def __init__(self, config: Optional[BertConfig] = None, compute_dtype=None, seed: int = 0,
+                 **kw):
+        super().__init__()
+        c = config or BertConfig(**{k: v for k, v in kw.items() if hasattr(BertConfig, k)})
+        self.config = c
+        self.compute_dtype = compute_dtype
+        self.bert = _BertModel(c)
+        self.cls = _Cls(c)
+        self.seed = seed
+        self._step = 0
+        self._vpad = (-c.vocab_size) % 64  # decoder N padded to the GEMM's 64-wide tiles
+        self._init_weights()
+        self._register_state_dict_hook(_split_qkv_hook)
+        self._register_load_state_dict_pre_hook(_merge_qkv_hook, with_module=True)
+
+    # HF BertPreTrainedModel._init_weights
+    def _init_weights(self):
+        std = self.config.initializer_range
+        for m in self.modules():
+            if isinstance(m, tnn.Linear):
+                tnn.init.normal_(m.weight, 0.0, std)
+                if m.bias is not None:
+                    tnn.init.zeros_(m.bias)
+            elif isinstance(m, tnn.Embedding):
+                tnn.init.normal_(m.weight, 0.0, std)
+            elif isinstance(m, tnn.LayerNorm):
+                tnn.init.ones_(m.weight)
+                tnn.init.zeros_(m.bias)
+
+    def activation_dtype(self, ref: torch.Tensor) -> torch.dtype:
+        if self.compute_dtype is not None:
+            return self.compute_dtype
+        return torch.bfloat16 if ref.is_cuda else torch.float32
+
+    def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
+                token_type_ids: Optional[torch.Tensor] = None,
+                masked_positions: Optional[torch.Tensor] = None,
+                labels: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Returns the MLM loss when ``labels`` is given (cross-entropy straight on the
+        tile-padded logits: the pad columns carry -30000 and never win), else the logits."""
+        c = self.config
+        B, S = input_ids.shape
+        dt = self.activation_dtype(input_ids)
+        emb = self.bert.embeddings
+        if self.training:
+            self._step += 1
+        rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+        base = (self.seed + 7919 * rank) & 0xFFFFFFFF
+        ids = input_ids.reshape(-1)
+        pos = torch.arange(S, device=ids.device).repeat(B)
+        tt = torch.zeros_like(ids) if token_type_ids is None else token_type_ids.reshape(-1)
+        w = emb.word_embeddings(ids, dt)
+        pt = emb.position_embeddings(pos, dt) + emb.token_type_embeddings(tt, dt)
+        h = emb.LayerNorm(w, residual=pt)
+        h = MF.dropout(h, c.hidden_dropout_prob, _seed(base, self._step, 0), self.training)
+        mask = None
+        if attention_mask is not None:
+            mask = (1.0 - attention_mask.float()) * -10000.0  # HF extended attention mask
+        for i, layer in enumerate(self.bert.encoder.layer):
+            seeds = [_seed(base, self._step, 3 * i + j + 1) for j in range(3)]
+            h = layer(h, B, S, mask, seeds)
+        if masked_positions is not None:
+            P = masked_positions.shape[1]
+            rows = (masked_positions + torch.arange(B, device=h.device)[:, None] * S).reshape(-1)
+            h = h.index_select(0, rows)
+        pr = self.cls.predictions
+        t = pr.transform.dense(h, act="gelu")
+        t = pr.transform.LayerNorm(t)
+        wd = emb.word_embeddings.compute_weight(dt)  # tied decoder
+        bias = pr.bias
+        if self._vpad:
+            # pad the vocabulary to the GEMM tile width with -inf-like logits (exact softmax)
+            wd = torch.cat([wd, wd.new_zeros(self._vpad, wd.shape[1])], 0)
+            bias = torch.cat([bias, bias.new_full((self._vpad,), -30000.0)])
+        logits = MF.linear(t, emb.word_embeddings.weight, wd, bias, "none")
+        if labels is not None:
+            return MF.cross_entropy(logits, labels.reshape(-1), ignore_index=-100)
+        return logits[:, : c.vocab_size] if self._vpad else logits
+
+    def loss(self, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        return MF.cross_entropy(logits.contiguous(), labels.reshape(-1), ignore_index=-100)
+
+
+def _split_qkv_hook(module, state_dict, prefix, local_metadata):
+    for k in list(state_dict.keys()):
+        if k.endswith("attention.self.qkv.weight") or k.endswith("attention.self.qkv.bias"):
+            kind = k.rsplit(".", 1)[1]
+            base = k[: -len(f"qkv.{kind}")]
+            t = state_dict.pop(k)
+            for name, part in zip(("query", "key", "value"), t.chunk(3, 0)):
+                state_dict[f"{base}{name}.{kind}"] = part
+        if k.endswith("cls.predictions.bias"):
+            state_dict[k[: -len("bias")] + "decoder.bias"] = state_dict[k]
+    if prefix + "bert.embeddings.word_embeddings.weight" in state_dict:
+        state_dict[prefix + "cls.predictions.decoder.weight"] = \
+            state_dict[prefix + "bert.embeddings.word_embeddings.weight"]
+    for k in list(state_dict.keys()):
+        if k.endswith("position_ids"):
+            state_dict.pop(k)
+    return state_dict
+
+
+def _merge_qkv_hook(module, state_dict, prefix, local_metadata, strict, missing_keys,
+                    unexpected_keys, error_msgs):
+    for k in list(state_dict.keys()):
+        for kind in ("weight", "bias"):
+            if k.startswith(prefix) and k.endswith(f"attention.self.query.{kind}"):
+                base = k[: -len(f"query.{kind}")]
+                parts = [state_dict.pop(f"{base}{n}.{kind}") for n in ("query", "key", "value")]
+                state_dict[f"{base}qkv.{kind}"] = torch.cat(parts, 0)
+    for extra in ("cls.predictions.decoder.weight", "cls.predictions.decoder.bias",
+                  "bert.embeddings.position_ids"):
+        state_dict.pop(prefix + extra, None)
+
+
+def bert_base(**kw) -> BertForMaskedLM:
+    return BertForMaskedLM(**kw)
+
+
+def bert_tiny(**kw) -> BertForMaskedLM:
+    """2-layer, hidden 128 variant for tests."""
+    cfg = BertConfig(hidden_size=128, num_hidden_layers=2, num_attention_heads=2,
+                     intermediate_size=512, **{k: v for k, v in kw.items()
+                                                if k in BertConfig.__dataclass_fields__})
+    rest = {k: v for k, v in kw.items() if k not in BertConfig.__dataclass_fields__}
+    return BertForMaskedLM(cfg, **rest)
+
+
+register_model("bert_base", bert_base)
+register_model("bert", bert_base)
+register_model("bert_tiny", bert_tiny)

@@ -152,3 +152,105 @@ class RefMnistCNN(nn.Module):
         x = torch.relu(self.bn3(self.conv3(x)))
         x = x.mean(dim=(2, 3))
         return self.fc2(torch.relu(self.fc1(x)))
+
+
+# ----------------------------------------------------------------------------- BERT (stock)
+class _RefBertLayer(nn.Module):
+    def __init__(self, H: int, heads: int, inter: int, eps: float, p: float, pa: float):
+        super().__init__()
+        self.heads, self.pa = heads, pa
+        self.attention = nn.Module()
+        self.attention.self = nn.Module()
+        self.attention.self.query = nn.Linear(H, H)
+        self.attention.self.key = nn.Linear(H, H)
+        self.attention.self.value = nn.Linear(H, H)
+        self.attention.output = nn.Module()
+        self.attention.output.dense = nn.Linear(H, H)
+        self.attention.output.LayerNorm = nn.LayerNorm(H, eps=eps)
+        self.intermediate = nn.Module()
+        self.intermediate.dense = nn.Linear(H, inter)
+        self.output = nn.Module()
+        self.output.dense = nn.Linear(inter, H)
+        self.output.LayerNorm = nn.LayerNorm(H, eps=eps)
+        self.drop = nn.Dropout(p)
+
+    def forward(self, h, mask):
+        B, S, H = h.shape
+        sa = self.attention.self
+
+        def split(t):
+            return t.view(B, S, self.heads, H // self.heads).transpose(1, 2)
+
+        q, k, v = split(sa.query(h)), split(sa.key(h)), split(sa.value(h))
+        ctx = torch.nn.functional.scaled_dot_product_attention(
+            q, k, v, attn_mask=mask, dropout_p=self.pa if self.training else 0.0)
+        ctx = ctx.transpose(1, 2).reshape(B, S, H)
+        a = self.drop(self.attention.output.dense(ctx))
+        h1 = self.attention.output.LayerNorm(a + h)
+        f = torch.nn.functional.gelu(self.intermediate.dense(h1))
+        f2 = self.drop(self.output.dense(f))
+        return self.output.LayerNorm(f2 + h1)
+
+
+class RefBertForMaskedLM(nn.Module):
+    """HuggingFace-``BertForMaskedLM``-keyed stock PyTorch BERT (torch.nn + SDPA): oracle for
+    :class:`mipipe.models.bert.BertForMaskedLM` and the BERT stock comparator."""
+
+    def __init__(self, vocab_size=30522, hidden_size=768, num_hidden_layers=12,
+                 num_attention_heads=12, intermediate_size=3072, max_position_embeddings=512,
+                 type_vocab_size=2, layer_norm_eps=1e-12, hidden_dropout_prob=0.1,
+                 attention_probs_dropout_prob=0.1):
+        super().__init__()
+        H = hidden_size
+        self.bert = nn.Module()
+        e = self.bert.embeddings = nn.Module()
+        e.word_embeddings = nn.Embedding(vocab_size, H)
+        e.position_embeddings = nn.Embedding(max_position_embeddings, H)
+        e.token_type_embeddings = nn.Embedding(type_vocab_size, H)
+        e.LayerNorm = nn.LayerNorm(H, eps=layer_norm_eps)
+        self.bert.encoder = nn.Module()
+        self.bert.encoder.layer = nn.ModuleList(
+            [_RefBertLayer(H, num_attention_heads, intermediate_size, layer_norm_eps,
+                           hidden_dropout_prob, attention_probs_dropout_prob)
+             for _ in range(num_hidden_layers)])
+        self.cls = nn.Module()
+        pr = self.cls.predictions = nn.Module()
+        pr.transform = nn.Module()
+        pr.transform.dense = nn.Linear(H, H)
+        pr.transform.LayerNorm = nn.LayerNorm(H, eps=layer_norm_eps)
+        pr.bias = nn.Parameter(torch.zeros(vocab_size))
+        pr.decoder = nn.Linear(H, vocab_size)
+        pr.decoder.weight = e.word_embeddings.weight
+        pr.decoder.bias = pr.bias
+        self.drop = nn.Dropout(hidden_dropout_prob)
+
+    def forward(self, input_ids, attention_mask=None, token_type_ids=None, masked_positions=None):
+        B, S = input_ids.shape
+        e = self.bert.embeddings
+        pos = torch.arange(S, device=input_ids.device)[None, :]
+        tt = torch.zeros_like(input_ids) if token_type_ids is None else token_type_ids
+        h = e.word_embeddings(input_ids) + e.position_embeddings(pos) + e.token_type_embeddings(tt)
+        h = self.drop(e.LayerNorm(h))
+        mask = None
+        if attention_mask is not None:
+            mask = ((1.0 - attention_mask.to(h.dtype)) * -10000.0)[:, None, None, :]
+        for layer in self.bert.encoder.layer:
+            h = layer(h, mask)
+        h = h.reshape(B * S, -1)
+        if masked_positions is not None:
+            rows = (masked_positions + torch.arange(B, device=h.device)[:, None] * S).reshape(-1)
+            h = h.index_select(0, rows)
+        pr = self.cls.predictions
+        t = pr.transform.LayerNorm(torch.nn.functional.gelu(pr.transform.dense(h)))
+        return pr.decoder(t)
+
+    def loss(self, logits, labels):
+        lf = logits if logits.dtype == torch.float64 else logits.float()
+        return torch.nn.functional.cross_entropy(lf, labels.reshape(-1), ignore_index=-100)
+
+
+def ref_bert(arch: str = "bert_base", **kw) -> RefBertForMaskedLM:
+    if arch == "bert_tiny":
+        kw = {**dict(hidden_size=128, num_hidden_layers=2, num_attention_heads=2,
+                     intermediate_size=512), **kw}
+    return RefBertForMaskedLM(**kw)

@@ -253,39 +253,102 @@ def layernorm_bwd(dy: Tensor, x: Tensor, mean: Tensor, rstd: Tensor,
     return dx.reshape(x.shape).to(dy.dtype), dgamma, dbeta
 
 
-def attention_fwd(q: Tensor, k: Tensor, v: Tensor, mask_bias: Optional[Tensor],
-                  scale: float) -> Tuple[Tensor, Tensor]:
-    """q,k,v: [B, H, S, D].  mask_bias: [B, S] additive key bias or None.
-    Returns (o, lse[B,H,S])."""
-    s = torch.einsum("bhqd,bhkd->bhqk", _f(q), _f(k)) * scale
-    if mask_bias is not None:
-        s = s + _f(mask_bias)[:, None, None, :]
+_M32 = 0xFFFFFFFF
+
+
+def _mix32(x: Tensor) -> Tensor:
+    """murmur3 finaliser on uint32 values held in int64 (bit-exact with the HIP kernels)."""
+    x = x & _M32
+    x = x ^ (x >> 16)
+    x = (x * 0x85EBCA6B) & _M32
+    x = x ^ (x >> 13)
+    x = (x * 0xC2B2AE35) & _M32
+    return x ^ (x >> 16)
+
+
+def _drop_threshold(p: float) -> int:
+    return min(int(p * 4294967296.0), _M32)
+
+
+def attention_keep(B: int, S: int, H: int, p: float, seed: int, device) -> Tensor:
+    """[B,H,S(q),S(k)] keep mask of the attention-probability dropout (attention.hip keep_elem)."""
+    q = torch.arange(S, device=device, dtype=torch.int64)
+    bh = torch.arange(B * H, device=device, dtype=torch.int64)
+    row_id = (bh[:, None] * S + q[None, :]) & _M32                      # [BH, S]
+    a = _mix32(torch.full_like(row_id, seed & _M32) ^ ((row_id * 0x9E3779B1) & _M32))
+    k = torch.arange(S, device=device, dtype=torch.int64)
+    kk = (k * 0x85EBCA77 + 0x27D4EB2F) & _M32
+    h = _mix32(a[:, :, None] ^ kk[None, None, :])
+    return (h >= _drop_threshold(p)).reshape(B, H, S, S)
+
+
+def dropout_keep(n: int, p: float, seed: int, device) -> Tensor:
+    """flat keep mask of misc.hip dropout_kernel."""
+    base = _mix32(torch.tensor(((seed & _M32) * 0x9E3779B1 + 0x7F4A7C15) & _M32, dtype=torch.int64))
+    i = torch.arange(n, device=device, dtype=torch.int64)
+    h = _mix32(base.to(device) ^ (((i & _M32) * 0x85EBCA77) & _M32))
+    return h >= _drop_threshold(p)
+
+
+def dropout_fwd(x: Tensor, p: float, seed: int) -> Tensor:
+    if p <= 0.0:
+        return x.clone()
+    keep = dropout_keep(x.numel(), p, seed, x.device).reshape(x.shape)
+    return (_f(x) * keep / (1.0 - p)).to(x.dtype)
+
+
+def _split_qkv(qkv: Tensor, B: int, S: int, H: int):
+    x = _f(qkv).reshape(B, S, 3, H, -1)
+    return (x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2))
+
+
+def attention_fwd(qkv: Tensor, B: int, S: int, H: int, mask: Optional[Tensor], scale: float,
+                  p_drop: float = 0.0, seed: int = 0) -> Tuple[Tensor, Tensor]:
+    """Packed layout of attention.hip: qkv [B*S, 3*H*D] -> (o [B*S, H*D], lse [B,H,S])."""
+    q, k, v = _split_qkv(qkv, B, S, H)
+    s = torch.einsum("bhqd,bhkd->bhqk", q, k) * scale
+    if mask is not None:
+        s = s + _f(mask).reshape(B, 1, 1, S)
     lse = torch.logsumexp(s, dim=-1)
     p = torch.exp(s - lse[..., None])
-    o = torch.einsum("bhqk,bhkd->bhqd", p, _f(v))
-    return o.to(q.dtype), lse
+    if p_drop > 0.0:
+        p = p * attention_keep(B, S, H, p_drop, seed, qkv.device) / (1.0 - p_drop)
+    o = torch.einsum("bhqk,bhkd->bhqd", p, v)
+    return o.transpose(1, 2).reshape(B * S, -1).to(qkv.dtype), lse
 
 
-def attention_bwd(do: Tensor, q: Tensor, k: Tensor, v: Tensor, o: Tensor, lse: Tensor,
-                  mask_bias: Optional[Tensor], scale: float) -> Tuple[Tensor, Tensor, Tensor]:
-    s = torch.einsum("bhqd,bhkd->bhqk", _f(q), _f(k)) * scale
-    if mask_bias is not None:
-        s = s + _f(mask_bias)[:, None, None, :]
+def attention_bwd(do: Tensor, qkv: Tensor, o: Tensor, lse: Tensor, B: int, S: int, H: int,
+                  mask: Optional[Tensor], scale: float, p_drop: float = 0.0,
+                  seed: int = 0) -> Tensor:
+    q, k, v = _split_qkv(qkv, B, S, H)
+    D = q.shape[-1]
+    s = torch.einsum("bhqd,bhkd->bhqk", q, k) * scale
+    if mask is not None:
+        s = s + _f(mask).reshape(B, 1, 1, S)
     p = torch.exp(s - lse[..., None])
-    dof = _f(do)
-    dv = torch.einsum("bhqk,bhqd->bhkd", p, dof)
-    dp = torch.einsum("bhqd,bhkd->bhqk", dof, _f(v))
-    delta = (dof * _f(o)).sum(-1, keepdim=True)
+    dof = _f(do).reshape(B, S, H, D).transpose(1, 2)
+    of = _f(o).reshape(B, S, H, D).transpose(1, 2)
+    keep = None
+    if p_drop > 0.0:
+        keep = attention_keep(B, S, H, p_drop, seed, qkv.device) / (1.0 - p_drop)
+    pd = p if keep is None else p * keep
+    dv = torch.einsum("bhqk,bhqd->bhkd", pd, dof)
+    dp = torch.einsum("bhqd,bhkd->bhqk", dof, v)
+    if keep is not None:
+        dp = dp * keep
+    delta = (dof * of).sum(-1, keepdim=True)
     ds = p * (dp - delta) * scale
-    dq = torch.einsum("bhqk,bhkd->bhqd", ds, _f(k))
-    dk = torch.einsum("bhqk,bhqd->bhkd", ds, _f(q))
-    return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
+    dq = torch.einsum("bhqk,bhkd->bhqd", ds, k)
+    dk = torch.einsum("bhqk,bhqd->bhkd", ds, q)
+    out = torch.stack([t.transpose(1, 2) for t in (dq, dk, dv)], dim=2)  # [B,S,3,H,D]
+    return out.reshape(B * S, 3 * H * D).to(qkv.dtype)
 
 
 def embedding_bwd(dy: Tensor, idx: Tensor, num_rows: int) -> Tensor:
     H = dy.shape[-1]
-    out = torch.zeros(num_rows, H, dtype=torch.float32, device=dy.device)
-    out.index_add_(0, idx.reshape(-1).long(), _f(dy.reshape(-1, H)))
+    src = _f(dy.reshape(-1, H))
+    out = torch.zeros(num_rows, H, dtype=src.dtype, device=dy.device)
+    out.index_add_(0, idx.reshape(-1).long(), src)
     return out
 
 
@@ -298,13 +361,6 @@ def gelu_bwd(dy: Tensor, x: Tensor) -> Tensor:
     cdf = 0.5 * (1.0 + torch.erf(xf / math.sqrt(2.0)))
     pdf = torch.exp(-0.5 * xf * xf) / math.sqrt(2.0 * math.pi)
     return (_f(dy) * (cdf + xf * pdf)).to(dy.dtype)
-
-
-def dropout_fwd(x: Tensor, p: float, seed: int, offset: int) -> Tuple[Tensor, Tensor]:
-    g = torch.Generator(device=x.device)
-    g.manual_seed(int(seed) * 1000003 + int(offset))
-    keep = (torch.rand(x.shape, generator=g, device=x.device) >= p)
-    return (_f(x) * keep / (1 - p)).to(x.dtype), keep
 
 
 def synthetic_images(indices: Tensor, num_classes: int, shape, seed: int,

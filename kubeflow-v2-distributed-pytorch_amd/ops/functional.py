@@ -289,13 +289,16 @@ class _LinearFn(Function):
             dx = K.gemm(dy2, w_c, False, False, None, "none", dy2.dtype).reshape(ctx.shp)
         gdt = torch.float64 if dy2.dtype == torch.float64 else torch.float32
         if ctx.needs_input_grad[1]:
-            tgt = _direct_grad_target(ctx.weight) if K.use_native(dy2) else None
+            padded = w_c.shape[0] != ctx.weight.shape[0]  # e.g. vocab padded to the tile width
+            tgt = _direct_grad_target(ctx.weight) if K.use_native(dy2) and not padded else None
             if tgt is not None:
                 fs, g = tgt
                 K.gemm(dy2, x2, True, False, None, "none", torch.float32, g, 1.0)
                 fs.grad_ready(ctx.weight)
             else:
                 dw = K.gemm(dy2, x2, True, False, None, "none", gdt)
+                if padded:
+                    dw = dw[: ctx.weight.shape[0]]
         if ctx.has_bias and ctx.needs_input_grad[3]:
             db = dy2.to(gdt).sum(0)
         return dx, dw, None, db, None
@@ -366,25 +369,54 @@ def gelu(x: Tensor) -> Tensor:
 
 class _AttentionFn(Function):
     @staticmethod
-    def forward(ctx, q, k, v, mask_bias, scale):
-        o, lse = K.attention_fwd(q, k, v, mask_bias, scale)
-        ctx.save_for_backward(q, k, v, o, lse, mask_bias)
-        ctx.scale = scale
+    def forward(ctx, qkv, B, S, H, mask, scale, p_drop, seed):
+        o, lse = K.attention_fwd(qkv, B, S, H, mask, scale, p_drop, seed)
+        ctx.save_for_backward(qkv, o, lse, mask)
+        ctx.cfg = (B, S, H, scale, p_drop, seed)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse, mask_bias = ctx.saved_tensors
-        dq, dk, dv = K.attention_bwd(do.contiguous(), q, k, v, o, lse, mask_bias, ctx.scale)
-        return dq, dk, dv, None, None
+        qkv, o, lse, mask = ctx.saved_tensors
+        B, S, H, scale, p_drop, seed = ctx.cfg
+        dqkv = K.attention_bwd(do.contiguous(), qkv, o, lse, B, S, H, mask, scale, p_drop, seed)
+        return dqkv, None, None, None, None, None, None, None
 
 
-def attention(q: Tensor, k: Tensor, v: Tensor, mask_bias: Optional[Tensor] = None,
-              scale: Optional[float] = None) -> Tensor:
-    """Flash-style softmax(QKᵀ·scale + mask)·V; q,k,v [B,H,S,D]."""
+def attention(qkv: Tensor, batch: int, seq: int, heads: int, mask: Optional[Tensor] = None,
+              scale: Optional[float] = None, p_drop: float = 0.0, seed: int = 0) -> Tensor:
+    """Fused softmax(QKᵀ·scale + mask)·V over the packed QKV projection output.
+
+    qkv [B*S, 3*H*D] (q | k | v column blocks, head-major), mask [B, S] additive key bias
+    (0 / -inf style) -> o [B*S, H*D], ready for the output projection.  ``p_drop`` is the
+    attention-probability dropout (keyed by ``seed``; recomputed in the backward)."""
+    D = qkv.shape[-1] // (3 * heads)
     if scale is None:
-        scale = 1.0 / math.sqrt(q.shape[-1])
-    return _AttentionFn.apply(q, k, v, mask_bias, scale)
+        scale = 1.0 / math.sqrt(D)
+    if mask is not None:
+        mask = mask.float().contiguous()
+    return _AttentionFn.apply(qkv.contiguous(), batch, seq, heads, mask, float(scale),
+                              float(p_drop), int(seed) & 0xFFFFFFFF)
+
+
+class _DropoutFn(Function):
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        ctx.cfg = (p, seed)
+        return K.dropout_fwd(x.contiguous(), p, seed)
+
+    @staticmethod
+    def backward(ctx, dy):
+        p, seed = ctx.cfg
+        return K.dropout_fwd(dy.contiguous(), p, seed), None, None
+
+
+def dropout(x: Tensor, p: float, seed: int, training: bool = True) -> Tensor:
+    """Hash-keyed dropout: the mask is a pure function of (seed, element index), so the backward
+    regenerates it instead of storing it."""
+    if not training or p <= 0.0:
+        return x
+    return _DropoutFn.apply(x, float(p), int(seed) & 0xFFFFFFFF)
 
 
 class _EmbeddingFn(Function):

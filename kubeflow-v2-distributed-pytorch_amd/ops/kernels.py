@@ -17,7 +17,7 @@ from ._native import native, native_available
 __all__ = ["conv_fwd", "conv_dgrad", "conv_wgrad", "bn_finalize", "bn_act_fwd",
            "bn_act_bwd_reduce", "bn_act_bwd_apply", "maxpool_fwd", "maxpool_bwd",
            "avgpool_fwd", "avgpool_bwd", "gemm", "cross_entropy_fwd_bwd", "sgd_step",
-           "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd",
+           "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd", "dropout_fwd",
            "embedding_bwd", "gelu_fwd", "gelu_bwd", "nchw_to_nhwc", "use_native"]
 
 _ALLOW_REF_ON_GPU = os.environ.get("MIPIPE_ALLOW_REF_ON_GPU", "0") == "1"
@@ -214,16 +214,24 @@ def layernorm_bwd(dy, x, mean, rstd, gamma):
     return _ref.layernorm_bwd(dy, x, mean, rstd, gamma)
 
 
-def attention_fwd(q, k, v, mask_bias, scale):
-    if use_native(q):
-        return native().attention_fwd(q, k, v, mask_bias, scale)
-    return _ref.attention_fwd(q, k, v, mask_bias, scale)
+def attention_fwd(qkv, B, S, H, mask, scale, p_drop=0.0, seed=0):
+    if use_native(qkv):
+        return native().attention_fwd(qkv, B, S, H, mask, scale, p_drop, seed)
+    return _ref.attention_fwd(qkv, B, S, H, mask, scale, p_drop, seed)
 
 
-def attention_bwd(do, q, k, v, o, lse, mask_bias, scale):
+def attention_bwd(do, qkv, o, lse, B, S, H, mask, scale, p_drop=0.0, seed=0):
     if use_native(do):
-        return native().attention_bwd(do, q, k, v, o, lse, mask_bias, scale)
-    return _ref.attention_bwd(do, q, k, v, o, lse, mask_bias, scale)
+        return native().attention_bwd(do, qkv, o, lse, B, S, H, mask, scale, p_drop, seed)
+    return _ref.attention_bwd(do, qkv, o, lse, B, S, H, mask, scale, p_drop, seed)
+
+
+def dropout_fwd(x, p, seed):
+    """y = x·keep/(1-p) with keep hashed from (seed, element index); applying it to dy with the
+    same seed is the backward."""
+    if use_native(x) and x.numel() % 8 == 0:
+        return native().dropout_fwd(x, p, seed & 0xFFFFFFFF)
+    return _ref.dropout_fwd(x, p, seed)
 
 
 def embedding_bwd(dy, idx, num_rows):
