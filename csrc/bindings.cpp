@@ -504,8 +504,9 @@ std::tuple<Tensor, Tensor, Tensor, optional<Tensor>> layernorm_fwd(Tensor x, Ten
   return {y, mean, rstd, xs};
 }
 
-std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mean, Tensor rstd,
-                                                 Tensor gamma) {
+std::tuple<Tensor, optional<Tensor>, optional<Tensor>> layernorm_bwd(
+    Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, optional<Tensor> dgamma_acc,
+    optional<Tensor> dbeta_acc) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   c10::DeviceGuard g(x.device());
@@ -513,14 +514,23 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(Tensor dy, Tensor x, Tensor mea
   TORCH_CHECK(H % 8 == 0 && H <= 2048 && dy.sizes() == x.sizes(), "layernorm_bwd shape mismatch");
   check_vec(gamma, H, "gamma");
   TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "mean/rstd size mismatch");
+  TORCH_CHECK(dgamma_acc.has_value() == dbeta_acc.has_value(), "pass both accumulators or none");
   auto dx = torch::empty_like(x);
   auto o = x.options().dtype(at::kFloat);
-  auto dg = torch::empty({H}, o), db = torch::empty({H}, o);
-  int64_t G = std::max<int64_t>(1, std::min<int64_t>(256, (rows + 15) / 16));
-  auto work = torch::empty({2 * G * H + 128 * H + 64}, o);
+  optional<Tensor> dg, db;
+  float *pg, *pb;
+  if (dgamma_acc.has_value()) {
+    pg = fptr(dgamma_acc, H);
+    pb = fptr(dbeta_acc, H);
+  } else {
+    dg = torch::zeros({H}, o);
+    db = torch::zeros({H}, o);
+    pg = dg->data_ptr<float>();
+    pb = db->data_ptr<float>();
+  }
   mipipe::layernorm_bwd(dy.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                        gamma.data_ptr<float>(), dx.data_ptr(), dg.data_ptr<float>(),
-                        db.data_ptr<float>(), work.data_ptr<float>(), rows, (int)H, stream());
+                        gamma.data_ptr<float>(), dx.data_ptr(), pg, pb, nullptr, rows, (int)H,
+                        stream());
   return {dx, dg, db};
 }
 
@@ -536,15 +546,23 @@ Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows) {
   return out;
 }
 
-Tensor colsum(Tensor x) {
+// out[c] (+)= Σ_rows x[:, c]; accumulates into ``out`` when given (e.g. a flat-grad view)
+Tensor colsum(Tensor x, optional<Tensor> out) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "colsum dtype");
   int64_t cols = x.size(-1), rows = x.numel() / cols;
-  auto out = torch::empty({cols}, x.options().dtype(at::kFloat));
-  auto work = torch::empty({64 * cols}, x.options().dtype(at::kFloat));
-  mipipe::colsum_f32(x.data_ptr(), x.scalar_type() == at::kBFloat16, out.data_ptr<float>(), rows,
-                     (int)cols, work.data_ptr<float>(), stream());
-  return out;
+  TORCH_CHECK(cols % 8 == 0, "colsum needs cols % 8 == 0");
+  Tensor o;
+  if (out.has_value()) {
+    check_vec(*out, cols, "out");
+    o = *out;
+  } else {
+    o = torch::zeros({cols}, x.options().dtype(at::kFloat));
+  }
+  mipipe::colsum_f32(x.data_ptr(), x.scalar_type() == at::kBFloat16, o.data_ptr<float>(), rows,
+                     (int)cols, nullptr, stream());
+  return o;
 }
 
 void check_attn(const Tensor& qkv, int64_t B, int64_t S, int64_t H) {
@@ -640,9 +658,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("mean"),
+        py::arg("rstd"), py::arg("gamma"), py::arg("dgamma") = py::none(),
+        py::arg("dbeta") = py::none());
   m.def("embedding_bwd", &embedding_bwd);
-  m.def("colsum", &colsum);
+  m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none());
   m.def("attention_fwd", &attention_fwd, py::arg("qkv"), py::arg("B"), py::arg("S"), py::arg("H"),
         py::arg("mask") = py::none(), py::arg("scale") = 0.125, py::arg("p_drop") = 0.0,
         py::arg("seed") = 0);
@@ -650,4 +670,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("mask") = py::none(),
         py::arg("scale") = 0.125, py::arg("p_drop") = 0.0, py::arg("seed") = 0);
   m.def("dropout_fwd", &dropout_fwd);
+  m.def("set_splitk_target", [](int v) { mipipe::g_splitk_target = std::max(1, v); });
+  m.def("get_splitk_target", []() { return mipipe::g_splitk_target; });
 }

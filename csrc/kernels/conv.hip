@@ -209,7 +209,7 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
 }
 
 static int pick_splits(uint32_t tiles, int nk) {
-  int target = 1024;
+  int target = g_splitk_target;
   int splits = (int)std::max<uint32_t>(1, target / std::max<uint32_t>(1, tiles));
   int max_splits = std::max(1, nk / 4);
   return std::min(splits, max_splits);

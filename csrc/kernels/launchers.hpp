@@ -18,6 +18,9 @@ struct ConvShape {
 // [R][C] slab (spreads contention); the consumer (bn_finalize / bwd finalize) reduces the R rows
 // and ZEROES the slab again, so a persistent zero-initialised slab can be reused every step.
 constexpr int kStatReplicas = 16;
+// Split-K sizing for the atomically-accumulated weight-gradient GEMMs: splits are chosen so
+// that tiles * splits ~= this many workgroups (tunable at runtime for sweeps).
+extern int g_splitk_target;
 int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,

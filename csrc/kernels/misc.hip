@@ -328,42 +328,54 @@ void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------ column sums
-__global__ __launch_bounds__(256) void colsum_partial_kernel(const void* __restrict__ x, bool bf16,
-                                                             float* __restrict__ part, long rows,
-                                                             int cols, long chunk) {
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rp = threadIdx.x >> 6;
-  __shared__ float red[4][64];
-  long r0 = (long)blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
-  float acc = 0.f;
-  if (col < cols)
-    for (long r = r0 + rp; r < r1; r += 4)
-      acc += bf16 ? (float)reinterpret_cast<const __bf16*>(x)[r * cols + col]
-                  : reinterpret_cast<const float*>(x)[r * cols + col];
-  red[rp][threadIdx.x & 63] = acc;
-  __syncthreads();
-  if (rp == 0 && col < cols)
-    part[(long)blockIdx.y * cols + col] =
-        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+// out[c] += Σ_r x[r][c]  (bias gradients; out may be a view of the flat gradient buffer).
+// tpr threads cover a row in 16-B vectors, rpb = 256/tpr rows per block-iteration; block
+// partials are reduced through LDS and added with one fp32 atomic per column per block.
+__global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x, bool bf16,
+                                                     float* __restrict__ out, long rows, int cols,
+                                                     long rows_per_block) {
+  __shared__ float red[256 * 8 + 8];
+  const int nvec = bf16 ? cols / 8 : cols / 4;  // vectors per row
+  const int per = bf16 ? 8 : 4;
+  const int tpr = min(nvec, 256), rpb = 256 / tpr;
+  const int t = threadIdx.x, rr = t / tpr, cc = t % tpr;
+  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  for (int vb = 0; vb < nvec; vb += tpr) {
+    const int v = vb + cc;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (rr < rpb && v < nvec) {
+      for (long r = r0 + rr; r < r1; r += rpb) {
+        if (bf16) {
+          float f[8];
+          unpack8(reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(x) + r * cols)[v], f);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[q] += f[q];
+        } else {
+          float4 f = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x) + r * cols)[v];
+          acc[0] += f.x; acc[1] += f.y; acc[2] += f.z; acc[3] += f.w;
+        }
+      }
+    }
+    __syncthreads();
+    // LDS image [rpb][tpr*per] so the final pass reads/atomics consecutive columns per lane
+    if (rr < rpb)
+      for (int q = 0; q < per; ++q) red[rr * tpr * per + cc * per + q] = acc[q];
+    __syncthreads();
+    const int ncol = min(tpr, nvec - vb) * per;
+    for (int c = t; c < ncol; c += 256) {
+      float a = 0.f;
+      for (int k = 0; k < rpb; ++k) a += red[k * tpr * per + c];
+      atomicAdd(out + (long)vb * per + c, a);
+    }
+  }
 }
 
-__global__ void colsum_final_kernel(const float* __restrict__ part, int S, int cols,
-                                    float* __restrict__ out) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  float a = 0.f;
-  for (int s = 0; s < S; ++s) a += part[(long)s * cols + c];
-  out[c] = a;
-}
-
-void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
+void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* /*work*/,
                 hipStream_t st) {
-  int S = (int)std::max<long>(1, std::min<long>(64, (rows + 255) / 256));
-  long chunk = (rows + S - 1) / S;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + 63) / 64, S), dim3(256), 0, st, x, bf16,
-                     work, rows, cols, chunk);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, st, work, S, cols,
-                     out);
+  long G = std::max<long>(1, std::min<long>(512, (rows + 31) / 32));
+  long rpb = (rows + G - 1) / G;
+  G = (rows + rpb - 1) / rpb;
+  hipLaunchKernelGGL(colsum_kernel, dim3(G), dim3(256), 0, st, x, bf16, out, rows, cols, rpb);
 }
 
 // ------------------------------------------------------------------------------ embedding grad
@@ -511,38 +523,34 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
       }
     }
   }
-  // block partial of dγ/dβ: reduce the 4 waves through LDS
-  __shared__ float red[4][LN_MAXC * 64 * 8 / 8];  // reused per array
+  // block partials of dγ/dβ: the 4 waves reduce through LDS, one atomic per column per block
+  __shared__ float red[4][LN_MAXC * 64 * 8];
   for (int arr = 0; arr < 2; ++arr) {
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < LN_MAXC; ++k) {
       int c = lane + k * 64;
-      for (int q = 0; q < 8; ++q) {
-        __syncthreads();
-        if (c < nc) red[w][c] = arr == 0 ? accg[k][q] : accb[k][q];
-        __syncthreads();
-        if (w == 0 && c < nc) {
-          float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
-          (arr == 0 ? pg : pb)[(long)blockIdx.x * H + c * 8 + q] = v;
-        }
-      }
+      if (c < nc)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) red[w][c * 8 + q] = arr == 0 ? accg[k][q] : accb[k][q];
     }
+    __syncthreads();
+    float* dst = arr == 0 ? pg : pb;
+    for (int c = threadIdx.x; c < H; c += 256)
+      atomicAdd(dst + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
   }
 }
 
 void layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd,
                    const float* gamma, void* dx, float* dgamma, float* dbeta, float* work,
                    long rows, int H, hipStream_t st) {
-  int G = (int)std::max<long>(1, std::min<long>(256, (rows + 15) / 16));
+  // dgamma / dbeta are ACCUMULATED into (zeroed buffers or the flat gradient views)
+  int G = (int)std::max<long>(1, std::min<long>(512, (rows + 7) / 8));
   int rpb = (int)((rows + G - 1) / G);
   G = (int)((rows + rpb - 1) / rpb);
-  float* pg = work;
-  float* pb = work + (long)G * H;
-  float* scratch = work + 2L * G * H;
   hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(G), dim3(256), 0, st, (const __bf16*)dy,
-                     (const __bf16*)x, mean, rstd, gamma, (__bf16*)dx, pg, pb, rows, H, rpb);
-  colsum_f32(pg, false, dgamma, G, H, scratch, st);
-  colsum_f32(pb, false, dbeta, G, H, scratch + 64L * H, st);
+                     (const __bf16*)x, mean, rstd, gamma, (__bf16*)dx, dgamma, dbeta, rows, H,
+                     rpb);
 }
 
 // ------------------------------------------------------------------------------ dropout

@@ -273,7 +273,7 @@ class _LinearFn(Function):
             y = K.gemm(x2, w_c, False, True, bias, act, x.dtype)
             ctx.save_for_backward(x2, w_c, y if act == "relu" else None)
         ctx.act, ctx.shp, ctx.has_bias = act, shp, bias is not None
-        ctx.weight = weight
+        ctx.weight, ctx.bias = weight, bias
         return y.reshape(*shp[:-1], y.shape[-1])
 
     @staticmethod
@@ -300,7 +300,15 @@ class _LinearFn(Function):
                 if padded:
                     dw = dw[: ctx.weight.shape[0]]
         if ctx.has_bias and ctx.needs_input_grad[3]:
-            db = dy2.to(gdt).sum(0)
+            tb = _direct_grad_target(ctx.bias) if K.use_native(dy2) else None
+            if tb is not None and tb[1].shape == (dy2.shape[1],):
+                K.colsum(dy2, tb[1])
+                tb[0].grad_ready(ctx.bias)
+            else:
+                db = K.colsum(dy2)
+                if ctx.bias.shape[0] != db.shape[0]:
+                    db = db[: ctx.bias.shape[0]]
+                db = db.to(gdt)
         return dx, dw, None, db, None
 
 
@@ -335,13 +343,24 @@ class _LayerNormFn(Function):
     def forward(ctx, x, gamma, beta, eps, residual):
         y, mean, rstd, xs = K.layernorm_fwd(x, gamma, beta, eps, residual)
         ctx.save_for_backward(x if xs is None else xs, mean, rstd, gamma)
+        ctx.beta = beta
         ctx.has_res = residual is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mean, rstd, gamma = ctx.saved_tensors
-        dx, dgamma, dbeta = K.layernorm_bwd(dy.contiguous(), x, mean, rstd, gamma)
+        acc = None
+        if K.use_native(dy) and ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
+            tg, tb = _direct_grad_target(gamma), _direct_grad_target(ctx.beta)
+            if tg is not None and tb is not None:
+                acc = (tg[1], tb[1])
+        dx, dgamma, dbeta = K.layernorm_bwd(dy.contiguous(), x, mean, rstd, gamma, acc)
+        if acc is not None:
+            fs = _direct_grad_target(gamma)[0]
+            fs.grad_ready(gamma)
+            fs.grad_ready(ctx.beta)
+            return dx, None, None, None, (dx if ctx.has_res else None)
         return dx, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), None, (dx if ctx.has_res else None)
 
 

@@ -17,7 +17,7 @@ from ._native import native, native_available
 __all__ = ["conv_fwd", "conv_dgrad", "conv_wgrad", "bn_finalize", "bn_act_fwd",
            "bn_act_bwd_reduce", "bn_act_bwd_apply", "maxpool_fwd", "maxpool_bwd",
            "avgpool_fwd", "avgpool_bwd", "gemm", "cross_entropy_fwd_bwd", "sgd_step",
-           "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd", "dropout_fwd",
+           "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd", "dropout_fwd", "colsum",
            "embedding_bwd", "gelu_fwd", "gelu_bwd", "nchw_to_nhwc", "use_native"]
 
 _ALLOW_REF_ON_GPU = os.environ.get("MIPIPE_ALLOW_REF_ON_GPU", "0") == "1"
@@ -208,10 +208,29 @@ def layernorm_fwd(x, gamma, beta, eps, residual=None):
     return _ref.layernorm_fwd(x, gamma, beta, eps, residual)
 
 
-def layernorm_bwd(dy, x, mean, rstd, gamma):
+def layernorm_bwd(dy, x, mean, rstd, gamma, acc=None):
+    """-> (dx, dgamma, dbeta); with ``acc=(dgamma_buf, dbeta_buf)`` the parameter grads are
+    accumulated into those buffers and returned as None."""
     if use_native(dy):
-        return native().layernorm_bwd(dy, x, mean, rstd, gamma)
-    return _ref.layernorm_bwd(dy, x, mean, rstd, gamma)
+        a = acc if acc is not None else (None, None)
+        return native().layernorm_bwd(dy, x, mean, rstd, gamma, *a)
+    dx, dg, db = _ref.layernorm_bwd(dy, x, mean, rstd, gamma)
+    if acc is not None:
+        acc[0].add_(dg.to(acc[0].dtype))
+        acc[1].add_(db.to(acc[1].dtype))
+        return dx, None, None
+    return dx, dg, db
+
+
+def colsum(x, out=None):
+    """Σ over rows of a [rows, cols] tensor in fp32; accumulates into ``out`` when given."""
+    if use_native(x) and x.shape[-1] % 8 == 0 and x.dtype in (torch.bfloat16, torch.float32):
+        return native().colsum(x.contiguous(), out)
+    s = x.reshape(-1, x.shape[-1]).to(torch.float64 if x.dtype == torch.float64 else torch.float32).sum(0)
+    if out is not None:
+        out.add_(s.to(out.dtype))
+        return out
+    return s
 
 
 def attention_fwd(qkv, B, S, H, mask, scale, p_drop=0.0, seed=0):
