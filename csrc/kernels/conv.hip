@@ -208,8 +208,10 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
   }
 }
 
-static int pick_splits(uint32_t tiles, int nk) {
-  int target = g_splitk_target;
+static int pick_splits(uint32_t tiles, int nk, int Ci) {
+  // measured (tools/sweep_splitk.py): ~512 workgroups is best for most ResNet-50 wgrads; narrow
+  // inputs (Ci <= 64: the 7x7 stem and layer1 3x3) prefer ~1.5x more
+  int target = Ci <= 64 ? g_splitk_target * 3 / 2 : g_splitk_target;
   int splits = (int)std::max<uint32_t>(1, target / std::max<uint32_t>(1, tiles));
   int max_splits = std::max(1, nk / 4);
   return std::min(splits, max_splits);
@@ -227,13 +229,13 @@ void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hi
   const __bf16* xp = (const __bf16*)x;
   if (s.Co <= 64) {
     uint32_t tN = cdiv(Ntot, 128), tiles = cdiv(s.Co, 64) * tN;
-    int splits = pick_splits(tiles, nk), per = (int)cdiv(nk, splits);
+    int splits = pick_splits(tiles, nk, s.Ci), per = (int)cdiv(nk, splits);
     splits = (int)cdiv(nk, per);
     if (dense) MIPIPE_LAUNCH((conv_wgrad_kernel<64, 128, true>), dim3(tiles, splits), dyp, xp, g, tN, per, e);
     else MIPIPE_LAUNCH((conv_wgrad_kernel<64, 128, false>), dim3(tiles, splits), dyp, xp, g, tN, per, e);
   } else {
     uint32_t tN = cdiv(Ntot, 128), tiles = cdiv(s.Co, 128) * tN;
-    int splits = pick_splits(tiles, nk), per = (int)cdiv(nk, splits);
+    int splits = pick_splits(tiles, nk, s.Ci), per = (int)cdiv(nk, splits);
     splits = (int)cdiv(nk, per);
     if (dense) MIPIPE_LAUNCH((conv_wgrad_kernel<128, 128, true>), dim3(tiles, splits), dyp, xp, g, tN, per, e);
     else MIPIPE_LAUNCH((conv_wgrad_kernel<128, 128, false>), dim3(tiles, splits), dyp, xp, g, tN, per, e);

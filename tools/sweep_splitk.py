@@ -34,7 +34,7 @@ for (H, Ci, Co, k, st, p) in [(56, 64, 64, 3, 1, 1), (56, 64, 256, 1, 1, 0), (28
     Ho = (H + 2 * p - k) // st + 1
     x = torch.randn(B, H, H, Ci, device=dev).to(torch.bfloat16)
     dy = torch.randn(B, Ho, Ho, Co, device=dev).to(torch.bfloat16)
-    out = torch.zeros(Co, k * k * Ci, device=dev)
+    out = torch.zeros(Co, k, k, Ci, device=dev)
     cases.append((f"conv{H}x{Ci}->{Co}k{k}s{st}",
                   lambda x=x, dy=dy, k=k, st=st, p=p, out=out: C.conv_wgrad(dy, x, k, k, st, p, out)))
 for (T, fin, fout) in [(4096, 768, 2304), (4096, 768, 768), (4096, 768, 3072), (4096, 3072, 768)]:
@@ -51,7 +51,7 @@ for rnd in range(3):
         C.set_splitk_target(t)
         for n, fn in cases:
             res[(t, n)].append(t_us(fn))
-C.set_splitk_target(1024)
+C.set_splitk_target(512)
 for n, _ in cases:
     row = {"shape": n}
     for t in targets:
