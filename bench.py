@@ -32,7 +32,10 @@ METRIC = "samples/sec (whole node) task.py DDP at 1/2/4/8 MI355X; scaling effici
 # Measured comparator: stock PyTorch-ROCm 2.10 (MIOpen + hipBLASLt, channels_last,
 # bf16 autocast, torch SGD) on ONE MI355X, ResNet-50 b256 224x224: 6580.1 samples/s.
 # vs_baseline = value / (comparator_per_gpu * n_gpus)  (ideal linear scaling of the comparator).
-STOCK_1GPU = {"resnet50": 6580.1, "resnet18_32": 76880.3}
+# BERT-base MLM (B=32 x S=128 / B=8 x S=512 per GPU, AdamW fused, SDPA, bf16 autocast): stock
+# torch measured on the same MI355X with tools/gpu_bert.sh / gpu_prof_bert.sh.
+STOCK_1GPU = {"resnet50": 6580.1, "resnet18_32": 76880.3,
+              "bert_base_128": 2184.8, "bert_base_512": 540.8}
 
 
 def parse():

@@ -223,6 +223,13 @@ class RefBertForMaskedLM(nn.Module):
         pr.decoder.weight = e.word_embeddings.weight
         pr.decoder.bias = pr.bias
         self.drop = nn.Dropout(hidden_dropout_prob)
+        for mod in self.modules():  # HF BertPreTrainedModel._init_weights (std 0.02)
+            if isinstance(mod, nn.Linear):
+                nn.init.normal_(mod.weight, 0.0, 0.02)
+                if mod.bias is not None:
+                    nn.init.zeros_(mod.bias)
+            elif isinstance(mod, nn.Embedding):
+                nn.init.normal_(mod.weight, 0.0, 0.02)
 
     def forward(self, input_ids, attention_mask=None, token_type_ids=None, masked_positions=None):
         B, S = input_ids.shape
