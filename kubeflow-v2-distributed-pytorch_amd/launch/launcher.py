@@ -169,7 +169,34 @@ def build_envs(spec: LaunchSpec) -> List[Dict[str, str]]:
 
 
 def launch(spec: LaunchSpec) -> int:
-    """Run the job; return 0 or the first failing process' exit code."""
+    """Run the job; return 0 or the first failing process' exit code (124 on timeout).
+
+    Uses the native supervisor (csrc/runtime/supervisor.cpp) when built, else a
+    subprocess-based equivalent with the same semantics."""
+    from mipipe.runtime import runtime, runtime_available
+    if runtime_available():
+        return _launch_native(spec, runtime())
+    return _launch_python(spec)
+
+
+def _launch_native(spec: LaunchSpec, rt) -> int:
+    envs = build_envs(spec)
+    if spec.log_dir:
+        os.makedirs(spec.log_dir, exist_ok=True)
+    pg = rt.ProcessGroup(echo=spec.echo)
+    for i, e in enumerate(envs):
+        log_path = os.path.join(spec.log_dir, f"rank{i}.log") if spec.log_dir else ""
+        pg.spawn(list(spec.command), [f"{k}={v}" for k, v in e.items()], spec.cwd or "",
+                 log_path, f"[rank{i}] ")
+    try:
+        rc = pg.wait(float(spec.timeout or 0.0), float(spec.grace_period))
+    except KeyboardInterrupt:  # pragma: no cover - interactive
+        pg.interrupt()
+        rc = pg.wait(0.0, float(spec.grace_period))
+    return int(rc)
+
+
+def _launch_python(spec: LaunchSpec) -> int:
     envs = build_envs(spec)
     if spec.log_dir:
         os.makedirs(spec.log_dir, exist_ok=True)

@@ -168,39 +168,37 @@ class PipelineRunner:
         return params, arts
 
     def _run_dag(self, dag: Dict[str, Any], scope: Dict[str, Any], prefix: str) -> Dict[str, Any]:
+        """Dependency-ordered execution of one (sub-)DAG on the worker pool; the state machine
+        (ready / cancel / fail-fast) is the native DagScheduler (csrc/runtime/dag.cpp) or its
+        Python twin :class:`_PyDag`."""
         tasks = dag.get("tasks", {})
+        names = list(tasks)
+        pos = {n: i for i, n in enumerate(names)}
+        deps = [[pos[d] for d in tasks[n].get("dependentTasks", [])] for n in names]
+        always = [((tasks[n].get("triggerPolicy") or {}).get("strategy")
+                   == "ALL_UPSTREAM_TASKS_COMPLETED") for n in names]
+        from mipipe.runtime import runtime, runtime_available
+        sched = (runtime().DagScheduler(len(names), deps, always, True) if runtime_available()
+                 else _PyDag(len(names), deps, always, True))
+        code = {SUCCEEDED: 2, CACHED: 3, SKIPPED: 4, FAILED: 5}
         outputs: Dict[str, Dict[str, Any]] = {}
-        state: Dict[str, str] = {n: PENDING for n in tasks}
-        for n in tasks:
+        for n in names:
             self._record(prefix + n, state=PENDING)
         futures: Dict[cf.Future, str] = {}
         with cf.ThreadPoolExecutor(max_workers=self.max_parallel) as pool:
             while True:
-                progressed = False
-                for n, t in tasks.items():
-                    if state[n] != PENDING:
-                        continue
-                    deps = t.get("dependentTasks", [])
-                    if any(state[d] not in TERMINAL_STATES for d in deps):
-                        continue
-                    strategy = (t.get("triggerPolicy") or {}).get("strategy")
-                    dep_failed = any(state[d] in (FAILED, CANCELLED) for d in deps)
-                    if (dep_failed and strategy != "ALL_UPSTREAM_TASKS_COMPLETED") or (
-                            self._failed.is_set() and strategy != "ALL_UPSTREAM_TASKS_COMPLETED"):
-                        state[n] = CANCELLED
-                        self._record(prefix + n, state=CANCELLED)
-                        progressed = True
-                        continue
-                    state[n] = RUNNING
-                    fut = pool.submit(self._run_task, n, t, scope, outputs, prefix)
+                if self._failed.is_set():
+                    sched_fail_fast(sched)
+                for i in sched.next_ready():
+                    n = names[i]
+                    fut = pool.submit(self._run_task, n, tasks[n], scope, outputs, prefix)
                     futures[fut] = n
-                    progressed = True
+                for i in sched.take_cancelled():
+                    self._record(prefix + names[i], state=CANCELLED)
                 if not futures:
-                    if all(s in TERMINAL_STATES for s in state.values()):
+                    if sched.finished():
                         break
-                    if not progressed:
-                        raise RunFailed(f"DAG deadlock: {state}")
-                    continue
+                    raise RunFailed(f"DAG deadlock in {prefix or 'root'}: {sched.states()}")
                 done, _ = cf.wait(list(futures), return_when=cf.FIRST_COMPLETED)
                 for fut in done:
                     n = futures.pop(fut)
@@ -209,8 +207,8 @@ class PipelineRunner:
                     except Exception as e:  # orchestrator-side error
                         st, out = FAILED, {"parameters": {}, "artifacts": {}}
                         self._record(prefix + n, state=FAILED, error=repr(e))
-                    state[n] = st
                     outputs[n] = out
+                    sched.complete(pos[n], code.get(st, 5))
                     if st == FAILED:
                         self._failed.set()
         return outputs
@@ -350,3 +348,74 @@ def run_job_spec(job_spec_path: str, pipeline_root: Optional[str] = None,
     with open(job_spec_path) as f:
         spec = json.load(f)
     return PipelineRunner(spec, pipeline_root, parameter_values, **kw).run()
+
+
+def sched_fail_fast(sched) -> None:
+    """A failure elsewhere in the run (another sub-DAG) cancels this DAG's pending tasks."""
+    if isinstance(sched, _PyDag):
+        sched.any_failed = True
+    else:
+        sched.mark_external_failure()
+
+
+class _PyDag:
+    """Pure-Python twin of the native DagScheduler (same states and semantics)."""
+
+    PENDING, RUNNING, SUCCEEDED, CACHED, SKIPPED, FAILED, CANCELLED = range(7)
+
+    def __init__(self, n, deps, always_run, fail_fast=True):
+        self.n, self.deps, self.always, self.fail_fast = n, deps, always_run, fail_fast
+        self.state = [self.PENDING] * n
+        self.cancelled = []
+        self.any_failed = False
+        indeg = [len(d) for d in deps]
+        children = [[] for _ in range(n)]
+        for i, ds in enumerate(deps):
+            for d in ds:
+                children[d].append(i)
+        q = [i for i in range(n) if indeg[i] == 0]
+        for i in q:
+            for c in children[i]:
+                indeg[c] -= 1
+                if indeg[c] == 0:
+                    q.append(c)
+        if len(q) != n:
+            raise ValueError("pipeline DAG has a cycle")
+        self.topo = q
+
+    def next_ready(self):
+        out, changed = [], True
+        while changed:
+            changed = False
+            for i in self.topo:
+                if self.state[i] != self.PENDING:
+                    continue
+                ds = self.deps[i]
+                if any(self.state[d] < self.SUCCEEDED for d in ds):
+                    continue
+                up_failed = any(self.state[d] in (self.FAILED, self.CANCELLED) for d in ds)
+                if not self.always[i] and (up_failed or (self.fail_fast and self.any_failed)):
+                    self.state[i] = self.CANCELLED
+                    self.cancelled.append(i)
+                    changed = True
+                    continue
+                self.state[i] = self.RUNNING
+                out.append(i)
+        return out
+
+    def complete(self, i, st):
+        if self.state[i] != self.RUNNING:
+            raise RuntimeError("complete() on a task that is not running")
+        self.state[i] = st
+        if st == self.FAILED:
+            self.any_failed = True
+
+    def take_cancelled(self):
+        r, self.cancelled = self.cancelled, []
+        return r
+
+    def finished(self):
+        return all(s >= self.SUCCEEDED for s in self.state)
+
+    def states(self):
+        return list(self.state)

@@ -142,6 +142,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--dataset", default="cifar10", choices=sorted(DATASET_SHAPES),
                    help="synthetic dataset shape")
     p.add_argument("--image-size", type=int, default=None, help="override image H=W")
+    p.add_argument("--data-dir", default="",
+                   help="directory with CIFAR-binary record files (<dataset>_{train,test}.bin or "
+                        "cifar-10-batches-bin/); read by the native loader. Empty: synthetic "
+                        "on-device data")
     p.add_argument("--train-samples", type=int, default=None)
     p.add_argument("--test-samples", type=int, default=None)
     p.add_argument("--num_classes", type=int, default=None,
@@ -285,16 +289,42 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
         else:
             print(f"=> no checkpoint found at '{path}'")
 
-    train_n = args.train_samples or N
-    test_n = args.test_samples or min(N, 10000)
-    train_set = SyntheticImageDataset(args.dataset, train_n, seed=args.random_seed,
-                                      shape=(C, H, W), num_classes=K)
-    test_set = SyntheticImageDataset(args.dataset, test_n, seed=args.random_seed,
-                                     shape=(C, H, W), num_classes=K)
-    train_sampler = DistributedSampler(train_set, seed=args.random_seed)
-    test_sampler = DistributedSampler(test_set, shuffle=False)
-    train_loader = DeviceBatchLoader(train_set, args.batch_size, train_sampler, device)
-    test_loader = DeviceBatchLoader(test_set, 128, test_sampler, device)
+    train_files = test_files = []
+    if args.data_dir:
+        from mipipe.data import records as REC
+        train_files = REC.dataset_files(args.data_dir, args.dataset, "train")
+        test_files = REC.dataset_files(args.data_dir, args.dataset, "test")
+        if not train_files:
+            raise FileNotFoundError(f"no {args.dataset} record files in {args.data_dir}")
+    if train_files:
+        # task.py:246-267: RandomCrop(32, 4) + flip + Normalize, DistributedSampler shards,
+        # test loader batch 128 unshuffled — on the native multi-threaded loader
+        from mipipe.data import records as REC
+        mean, std = ((REC.MNIST_MEAN, REC.MNIST_STD) if args.dataset == "mnist"
+                     else (REC.CIFAR10_MEAN, REC.CIFAR10_STD))
+        pad = 4 if args.dataset == "cifar10" else 0
+        probe = REC.RecordDataLoader(train_files, (C, H, W), args.batch_size, train=True,
+                                     pad=pad, mean=mean, std=std, seed=args.random_seed,
+                                     workers=max(1, args.workers), device=device)
+        train_sampler = DistributedSampler(probe.num_samples_total, seed=args.random_seed)
+        probe.sampler = train_sampler
+        train_loader = probe
+        tfiles = test_files or train_files
+        test_loader = REC.RecordDataLoader(tfiles, (C, H, W), 128, train=False, mean=mean,
+                                           std=std, workers=max(1, args.workers), device=device)
+        test_sampler = DistributedSampler(test_loader.num_samples_total, shuffle=False)
+        test_loader.sampler = test_sampler
+    else:
+        train_n = args.train_samples or N
+        test_n = args.test_samples or min(N, 10000)
+        train_set = SyntheticImageDataset(args.dataset, train_n, seed=args.random_seed,
+                                          shape=(C, H, W), num_classes=K)
+        test_set = SyntheticImageDataset(args.dataset, test_n, seed=args.random_seed,
+                                         shape=(C, H, W), num_classes=K)
+        train_sampler = DistributedSampler(train_set, seed=args.random_seed)
+        test_sampler = DistributedSampler(test_set, shuffle=False)
+        train_loader = DeviceBatchLoader(train_set, args.batch_size, train_sampler, device)
+        test_loader = DeviceBatchLoader(test_set, 128, test_sampler, device)
 
     meter = ThroughputMeter(device, warmup_steps=args.warmup_steps)
     global_step = 0

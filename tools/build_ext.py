@@ -98,7 +98,9 @@ def build_runtime(jobs: int = 8, force: bool = False, verbose: bool = True) -> s
     if not srcs:
         return ""
     py_inc = sysconfig.get_paths()["include"]
-    flags = ["-O2", "-std=c++17", "-fPIC", f"-I{py_inc}", f"-I{CSRC}", "-Wall", "-Wno-unused-result"]
+    import pybind11
+    flags = ["-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"-I{py_inc}",
+             f"-I{pybind11.get_include()}", f"-I{CSRC}", "-Wall", "-Wno-unused-result"]
     hdr = _newest_header()
     objs = []
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
