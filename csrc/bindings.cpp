@@ -94,12 +94,14 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
   return {y, ps, pss};
 }
 
-Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride, int pad) {
+Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride, int pad,
+                  optional<Tensor> addend, optional<Tensor> bn_y, optional<Tensor> bn_mean,
+                  optional<Tensor> bn_invstd, optional<Tensor> bn_scale, optional<Tensor> bn_bias,
+                  optional<Tensor> bn_rep) {
   check_bf16(dy, "dy");
   check_bf16(w, "w");
   c10::DeviceGuard g(dy.device());
   TORCH_CHECK(x_shape.size() == 4, "x_shape must be [N,H,W,Ci]");
-  auto xmeta = torch::empty({0}, dy.options());
   mipipe::ConvShape s;
   s.N = (int)x_shape[0]; s.H = (int)x_shape[1]; s.W = (int)x_shape[2]; s.Ci = (int)x_shape[3];
   s.Co = (int)w.size(0); s.KH = (int)w.size(1); s.KW = (int)w.size(2);
@@ -112,8 +114,46 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
   TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv dgrad needs Ci, Co % 8 == 0");
   TORCH_CHECK(s.pad < s.KH, "conv dgrad expects pad < kernel size");
   auto dx = torch::empty({s.N, s.H, s.W, s.Ci}, dy.options());
-  mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream());
+  mipipe::DgradFusion fz;
+  bool any = false;
+  if (addend.has_value()) {
+    check_bf16(*addend, "addend");
+    TORCH_CHECK(addend->sizes() == dx.sizes(), "addend must match dx");
+    fz.addend = addend->data_ptr();
+    any = true;
+  }
+  if (bn_rep.has_value()) {
+    TORCH_CHECK(bn_y.has_value() && bn_mean.has_value() && bn_invstd.has_value() &&
+                bn_scale.has_value() && bn_bias.has_value(), "BN fusion needs y/mean/invstd/scale/bias");
+    check_bf16(*bn_y, "bn_y");
+    TORCH_CHECK(bn_y->sizes() == dx.sizes(), "bn_y must match dx");
+    check_vec(*bn_mean, s.Ci, "bn_mean");
+    check_vec(*bn_invstd, s.Ci, "bn_invstd");
+    check_vec(*bn_scale, s.Ci, "bn_scale");
+    check_vec(*bn_bias, s.Ci, "bn_bias");
+    check_f32(*bn_rep, "bn_rep");
+    TORCH_CHECK(bn_rep->numel() == 3ll * mipipe::kStatReplicas * s.Ci, "bn_rep must be [3,R,Ci]");
+    fz.bn_y = bn_y->data_ptr();
+    fz.bn_mean = bn_mean->data_ptr<float>(); fz.bn_invstd = bn_invstd->data_ptr<float>();
+    fz.bn_scale = bn_scale->data_ptr<float>(); fz.bn_bias = bn_bias->data_ptr<float>();
+    fz.bn_rep = bn_rep->data_ptr<float>();
+    any = true;
+  }
+  mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), any ? &fz : nullptr);
   return dx;
+}
+
+std::tuple<Tensor, Tensor> bn_bwd_collect(Tensor rep, int64_t C, optional<Tensor> dgamma,
+                                          optional<Tensor> dbeta) {
+  check_f32(rep, "rep");
+  c10::DeviceGuard g(rep.device());
+  TORCH_CHECK(rep.numel() == 3ll * mipipe::kStatReplicas * C, "rep must be [3,R,C]");
+  TORCH_CHECK(dgamma.has_value() == dbeta.has_value(), "pass both accumulators or none");
+  auto o = rep.options();
+  auto sg = torch::empty({C}, o), sgx = torch::empty({C}, o);
+  mipipe::bn_bwd_collect(rep.data_ptr<float>(), (int)C, sg.data_ptr<float>(), sgx.data_ptr<float>(),
+                         fptr(dgamma, C), fptr(dbeta, C), stream());
+  return {sg, sgx};
 }
 
 Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, optional<Tensor> out) {
@@ -632,7 +672,13 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift") = py::none(), py::arg("slab_sum") = py::none(),
         py::arg("slab_sq") = py::none());
   m.attr("STAT_REPLICAS") = mipipe::kStatReplicas;
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("x_shape"),
+        py::arg("stride"), py::arg("pad"), py::arg("addend") = py::none(),
+        py::arg("bn_y") = py::none(), py::arg("bn_mean") = py::none(),
+        py::arg("bn_invstd") = py::none(), py::arg("bn_scale") = py::none(),
+        py::arg("bn_bias") = py::none(), py::arg("bn_rep") = py::none());
+  m.def("bn_bwd_collect", &bn_bwd_collect, py::arg("rep"), py::arg("C"),
+        py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("out") = py::none());
   m.def("bn_finalize", &bn_finalize, py::arg("psum"), py::arg("psq"), py::arg("count"),

@@ -371,4 +371,10 @@ void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float*
     hipLaunchKernelGGL(bn_bwd_apply_kernel<0>, dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C);
 }
 
+void bn_bwd_collect(float* rep, int C, float* out_g, float* out_gx, float* dgamma, float* dbeta,
+                    hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_collect_kernel, dim3((C + 255) / 256), dim3(256), 0, st, rep, C, out_g,
+                     out_gx, nullptr, dgamma, dbeta, nullptr, nullptr);
+}
+
 }  // namespace mipipe

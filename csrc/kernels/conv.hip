@@ -161,7 +161,8 @@ void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq
   }
 }
 
-void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st) {
+void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
+                const DgradFusion* fz) {
   const bool dense = is_dense(s);
   const __bf16* dyp = (const __bf16*)dy;
   const __bf16* wp = (const __bf16*)w;
@@ -190,6 +191,12 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
       uint32_t M = (uint32_t)s.N * c.Hc * c.Wc;
       EpiParams e{};
       e.C = dx; e.ldc = s.Ci; e.M = M; e.N = s.Ci;
+      if (fz != nullptr) {
+        e.addend = (const __bf16*)fz->addend;
+        e.bnr_y = (const __bf16*)fz->bn_y;
+        e.bnr_mean = fz->bn_mean; e.bnr_invstd = fz->bn_invstd;
+        e.bnr_scale = fz->bn_scale; e.bnr_bias = fz->bn_bias; e.bnr_rep = fz->bn_rep;
+      }
       if (S > 1) {
         e.rm_s = S; e.rm_ph = ph; e.rm_pw = pw; e.rm_H = s.H; e.rm_W = s.W;
         e.rm_Hc = c.Hc; e.rm_Wc = c.Wc; e.rm_fHcWc = c.fHcWc; e.rm_fWc = c.fWc;

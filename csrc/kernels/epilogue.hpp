@@ -3,6 +3,7 @@
 // whole 16-B (bf16) or 256-B-contiguous (fp32 atomics) row segments.
 #pragma once
 #include "gemm_core.hpp"
+#include "launchers.hpp"
 
 namespace mipipe {
 namespace gk {
@@ -22,6 +23,14 @@ struct EpiParams {
   // stored at dx row (img*H + ph + s*i)*W + pw + s*j.  rm_s == 0 disables.
   int rm_s, rm_ph, rm_pw, rm_H, rm_W, rm_Hc, rm_Wc;
   FastDiv rm_fHcWc, rm_fWc;
+  // optional bf16 [rows][ldc] tensor added to the output (residual-gradient fusion)
+  const __bf16* addend;
+  // optional BatchNorm-backward fusion (conv dgrad whose input was relu(bn(y))): the output
+  // becomes g = dx * [y*scale + bias > 0] and Σg, Σg·(y-mean)*invstd are accumulated into
+  // replica rows (blockIdx % R) of rep[0] / rep[1] ([3][R][N] slab)
+  const __bf16* bnr_y;
+  const float *bnr_mean, *bnr_invstd, *bnr_scale, *bnr_bias;
+  float* bnr_rep;
 };
 
 __device__ __forceinline__ long out_row(const EpiParams& e, uint32_t m) {
@@ -128,13 +137,70 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
     }
   __syncthreads();
   constexpr int CPR = BN / 8;  // 16-B chunks per row
+  static_assert(kThreads % CPR == 0, "thread -> column-chunk map must be loop invariant");
   __bf16* C = reinterpret_cast<__bf16*>(e.C);
+  const bool bnr = e.bnr_rep != nullptr;
+  const uint32_t my_cc = threadIdx.x % CPR, my_n = n0 + my_cc * 8;
+  float b_sc[8], b_bi[8], b_mu[8], b_is[8], sg[8], sgx[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    sg[q] = sgx[q] = 0.f;
+    const bool ok = bnr && my_n + q < e.N;
+    b_sc[q] = ok ? e.bnr_scale[my_n + q] : 0.f;
+    b_bi[q] = ok ? e.bnr_bias[my_n + q] : 0.f;
+    b_mu[q] = ok ? e.bnr_mean[my_n + q] : 0.f;
+    b_is[q] = ok ? e.bnr_invstd[my_n + q] : 0.f;
+  }
   for (int c = threadIdx.x; c < BM * CPR; c += kThreads) {
     uint32_t r = c / CPR, cc = c % CPR;
     uint32_t m = m0 + r, n = n0 + cc * 8;
     if (m < e.M && n < e.N) {
       uint4 v = *reinterpret_cast<const uint4*>(smem + r * P + cc * 16);
-      *reinterpret_cast<uint4*>(C + out_row(e, m) * e.ldc + n) = v;
+      const long orow = out_row(e, m);
+      if (e.addend != nullptr || bnr) {
+        float f[8];
+        unpack8(v, f);
+        if (e.addend != nullptr) {
+          float a[8];
+          unpack8(*reinterpret_cast<const uint4*>(e.addend + orow * e.ldc + n), a);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] += a[q];
+        }
+        if (bnr) {
+          float yv[8];
+          unpack8(*reinterpret_cast<const uint4*>(e.bnr_y + orow * e.ldc + n), yv);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float zq = yv[q] * b_sc[q] + b_bi[q];
+            const float gq = zq > 0.f ? bf2f(f2bf(f[q])) : 0.f;  // stats of the stored bf16 g
+            f[q] = gq;
+            sg[q] += gq;
+            sgx[q] += gq * (yv[q] - b_mu[q]) * b_is[q];
+          }
+        }
+        v = pack8(f);
+      }
+      *reinterpret_cast<uint4*>(C + orow * e.ldc + n) = v;
+    }
+  }
+  if (bnr) {
+    // threads t, t+CPR, ... share a column chunk: reduce them through LDS, then one atomic
+    // per column per block into replica row blockIdx % R
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [kThreads][16]
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      red[threadIdx.x * 16 + q] = sg[q];
+      red[threadIdx.x * 16 + 8 + q] = sgx[q];
+    }
+    __syncthreads();
+    const uint32_t R = kStatReplicas;
+    for (int j = threadIdx.x; j < 2 * BN; j += kThreads) {
+      const int arr = j / BN, col = j % BN, cc = col >> 3, q = col & 7;
+      float a = 0.f;
+      for (int t = cc; t < kThreads; t += CPR) a += red[t * 16 + arr * 8 + q];
+      if (n0 + col < e.N)
+        atomicAdd(e.bnr_rep + ((long)arr * R + blockIdx.x % R) * e.N + n0 + col, a);
     }
   }
 }

@@ -25,7 +25,18 @@ int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
               const float* st_shift, const ConvShape& s, hipStream_t st);
-void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st);
+// Optional dgrad epilogue fusions:
+//  addend: bf16 [N*H*W][Ci] added to dx (the block input's other gradient, e.g. the residual);
+//  bn_*:   the conv input was relu(bn(y)) with a single consumer: dx becomes g = dx*[z > 0] and
+//          Σg, Σg·x̂ go to rep rows 0/1 ([3][kStatReplicas][Ci] zeroed slab, see bn_bwd_collect).
+struct DgradFusion {
+  const void* addend = nullptr;
+  const void* bn_y = nullptr;
+  const float *bn_mean = nullptr, *bn_invstd = nullptr, *bn_scale = nullptr, *bn_bias = nullptr;
+  float* bn_rep = nullptr;
+};
+void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
+                const DgradFusion* fz = nullptr);
 // dw is ACCUMULATED into with fp32 atomics (split-K): pass a zeroed buffer, or the parameter's
 // gradient buffer to fuse autograd's accumulation (gradient lands directly in the DDP bucket)
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st);
@@ -55,6 +66,10 @@ void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float
                        const float* invstd2, bool relu, long M, int C, float* out_g,
                        float* out_gx, float* out_gx2, float* rep, float* dgamma, float* dbeta,
                        float* dgamma2, float* dbeta2, hipStream_t st);
+// Sum the replica rows of a bwd slab (filled by a fused dgrad epilogue) into out_g / out_gx,
+// re-zero it, optionally accumulate dγ += Σg·x̂, dβ += Σg.
+void bn_bwd_collect(float* rep, int C, float* out_g, float* out_gx, float* dgamma, float* dbeta,
+                    hipStream_t st);
 void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float* mean,
                       const float* invstd, const float* gamma, const float* sum_g,
                       const float* sum_gx, const void* y2, const float* mean2,

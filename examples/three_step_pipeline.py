@@ -60,7 +60,8 @@ def train(data: Input[Dataset], arch: str, dataset: str, epochs: int, batch_size
     args = ["--dist-url=env://", f"--arch={arch}", f"--dataset={dataset}",
             f"--data-dir={data.path}", f"--num_epochs={epochs}", f"--batch_size={batch_size}",
             f"--learning_rate={learning_rate}", "--eval-every=1000", "--log-every=10",
-            "--model_filename=model.pth"] + json.loads(extra_args)
+            "--model_filename=model.pth", f"--num_classes={int(data.metadata.get('num_classes', 10))}"
+            ] + json.loads(extra_args)
     if gpus > 1:
         args.append("--multiprocessing-distributed")
     job = aiplatform.CustomTrainingJob(display_name=f"train_{arch}_{ts}",
@@ -108,11 +109,12 @@ def evaluate(data: Input[Dataset], model: Input[Model], arch: str, dataset: str,
     if path is None:
         raise FileNotFoundError(f"no model.pth under {model.path}")
     shape = (3, 32, 32) if dataset == "cifar10" else (1, 28, 28)
-    ncls = 10
+    sd = strip_module_prefix(torch.load(path, map_location="cpu", weights_only=True))
+    head = [v for k, v in sd.items() if v.dim() == 2][-1]  # classifier weight [classes, feat]
+    ncls = int(head.shape[0])
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
     net = create_model(arch, num_classes=ncls)
-    net.load_state_dict(strip_module_prefix(torch.load(path, map_location="cpu",
-                                                       weights_only=True)))
+    net.load_state_dict(sd)
     net = net.to(dev).eval()
     mean, std = ((REC.MNIST_MEAN, REC.MNIST_STD) if dataset == "mnist"
                  else (REC.CIFAR10_MEAN, REC.CIFAR10_STD))

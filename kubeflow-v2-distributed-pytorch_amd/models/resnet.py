@@ -46,11 +46,14 @@ class BasicBlock(tnn.Module):
         self.stride = stride
 
     def forward(self, x):
-        out = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        slot = MF.ResidualSlot()
+        out = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True, res_take=slot)
         if self.downsample is not None:
             ds_conv, ds_bn = self.downsample[0], self.downsample[1]
-            return mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, branch=(x, ds_conv, ds_bn))
-        return mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=x)
+            return mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, fuse_prev=True,
+                                   branch=(x, ds_conv, ds_bn), res_give=slot)
+        return mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=x, fuse_prev=True,
+                               res_give=slot)
 
 
 class Bottleneck(tnn.Module):
@@ -70,12 +73,17 @@ class Bottleneck(tnn.Module):
         self.stride = stride
 
     def forward(self, x):
-        out = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-        out = mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True)
+        # conv2 / conv3 are the only consumers of their inputs: BN1 / BN2 backward reductions
+        # run in their dgrad epilogues; conv1's dgrad adds the identity/downsample gradient
+        slot = MF.ResidualSlot()
+        out = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True, res_take=slot)
+        out = mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, fuse_prev=True)
         if self.downsample is not None:
             ds_conv, ds_bn = self.downsample[0], self.downsample[1]
-            return mnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, branch=(x, ds_conv, ds_bn))
-        return mnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=x)
+            return mnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, fuse_prev=True,
+                                   branch=(x, ds_conv, ds_bn), res_give=slot)
+        return mnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=x, fuse_prev=True,
+                               res_give=slot)
 
 
 class _StemConv(mnn.Conv2d):

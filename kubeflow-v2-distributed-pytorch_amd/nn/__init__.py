@@ -87,11 +87,12 @@ class Conv2d(ShadowMixin, tnn.Module):
             self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
         return r
 
-    def forward(self, x: torch.Tensor, stats_shift: Optional[torch.Tensor] = None, slabs=None):
+    def forward(self, x: torch.Tensor, stats_shift: Optional[torch.Tensor] = None, slabs=None,
+                prev=None, res_take=None, res_give=None):
         """x: NHWC.  Returns y, or (y, psum, psumsq) when ``stats_shift`` is given."""
         w_c = self.compute_weight(x.dtype)
         y, ps, pss = MF.conv2d(x, self.weight, w_c, self.stride[0], self.padding[0], stats_shift,
-                               slabs)
+                               slabs, prev, res_take, res_give)
         if self.bias is not None:
             y = y + self.bias.to(y.dtype)
         return y if stats_shift is None else (y, ps, pss)
@@ -118,30 +119,46 @@ class BatchNorm2d(tnn.BatchNorm2d):
 
 def conv_bn_act(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d, relu: bool = True,
                 residual: Optional[torch.Tensor] = None,
-                branch: Optional[tuple] = None) -> torch.Tensor:
+                branch: Optional[tuple] = None, fuse_prev: bool = False,
+                res_take: Optional[MF.ResidualSlot] = None,
+                res_give: Optional[MF.ResidualSlot] = None) -> torch.Tensor:
     """Fused conv -> BN -> [+residual | +BN(conv(branch_x))] -> ReLU on NHWC activations.
 
     ``branch`` = (x_b, conv_b, bn_b): the ResNet downsample path, normalised and added in the
     same elementwise pass as the main path.
+    ``fuse_prev``: the caller guarantees this conv is the ONLY consumer of ``x`` (an output of
+    a previous relu-only conv_bn_act) -> that BN's backward reductions run in this conv's
+    dgrad epilogue.  ``res_take`` / ``res_give``: residual-gradient hand-off (the conv that
+    also reads the block input adds the identity/downsample gradient in its dgrad epilogue).
     """
     use_batch = bn.training
+    prev = getattr(x, "_mipipe_bnact", None) if fuse_prev else None
     if use_batch:
         ws = MF.bn_workspace(bn, "fwd", x.device)
-        y, ps, pss = conv(x, bn.running_mean, None if ws is None else (ws[0], ws[1]))
+        y, ps, pss = conv(x, bn.running_mean, None if ws is None else (ws[0], ws[1]), prev=prev,
+                          res_take=res_take)
     else:
-        y, ps, pss = conv(x), None, None
+        y, ps, pss = conv(x, prev=prev, res_take=res_take), None, None
     count = y.numel() // y.shape[-1]
     st = MF.bn_stats_from_partials(ps, pss, count, bn, use_batch)
     if branch is not None:
         xb, convb, bnb = branch
         if bnb.training:
             wsb = MF.bn_workspace(bnb, "fwd", xb.device)
-            yb, psb, pssb = convb(xb, bnb.running_mean, None if wsb is None else (wsb[0], wsb[1]))
+            yb, psb, pssb = convb(xb, bnb.running_mean, None if wsb is None else (wsb[0], wsb[1]),
+                                  res_give=res_give)
         else:
-            yb, psb, pssb = convb(xb), None, None
+            yb, psb, pssb = convb(xb, res_give=res_give), None, None
         stb = MF.bn_stats_from_partials(psb, pssb, count, bnb, bnb.training)
         return MF.batchnorm_act(y, st, bn, relu, y2=yb, st2=stb, bn2=bnb)
-    return MF.batchnorm_act(y, st, bn, relu, residual=residual)
+    token = None
+    if relu and residual is None and use_batch:
+        token = MF.BNActToken(bn, st, y)
+    z = MF.batchnorm_act(y, st, bn, relu, residual=residual, token=token,
+                         res_give=res_give if residual is not None else None)
+    if token is not None:
+        z._mipipe_bnact = token
+    return z
 
 
 class ReLU(tnn.ReLU):

@@ -43,14 +43,52 @@ def _direct_grad_target(p: Tensor):
     return fs, g
 
 
+class ResidualSlot:
+    """Hands a block input's second gradient (identity / downsample path) to the conv that
+    also consumes that input, so its dgrad epilogue adds it (no separate elementwise add).
+
+    Order-independent: a producer that runs before the consumer stashes its gradient and
+    returns None to autograd; if the consumer already ran, the producer returns it normally."""
+
+    __slots__ = ("pending", "consumed")
+
+    def __init__(self):
+        self.pending = None
+        self.consumed = False
+
+    def produce(self, g):
+        if g is None or self.consumed:
+            return g
+        self.pending = g if self.pending is None else self.pending + g
+        return None
+
+    def take(self):
+        self.consumed = True
+        p, self.pending = self.pending, None
+        return p
+
+
+class BNActToken:
+    """Links a BN(+ReLU) output to its single consuming conv: the conv's backward computes the
+    BN-backward reductions in its dgrad epilogue and flags the BN's backward to skip them."""
+
+    __slots__ = ("bn", "st", "y", "pre_reduced")
+
+    def __init__(self, bn, st, y):
+        self.bn, self.st, self.y = bn, st, y
+        self.pre_reduced = False
+
+
 class _ConvFn(Function):
     @staticmethod
-    def forward(ctx, x, weight, w_c, stride, pad, shift, slabs=None):
+    def forward(ctx, x, weight, w_c, stride, pad, shift, slabs=None, prev=None, res_take=None,
+                res_give=None):
         y, psum, psumsq = K.conv_fwd(x, w_c, stride, pad, shift, slabs)
         ctx.set_materialize_grads(False)  # stats outputs never get gradients: no zero fills
         ctx.save_for_backward(x, w_c)
         ctx.weight = weight
         ctx.conf = (stride, pad, weight.shape[2], weight.shape[3], weight.shape[1])
+        ctx.prev, ctx.res_take, ctx.res_give = prev, res_take, res_give
         if psum is not None:
             ctx.mark_non_differentiable(psum, psumsq)
         return y, psum, psumsq
@@ -59,12 +97,24 @@ class _ConvFn(Function):
     def backward(ctx, dy, _g1, _g2):
         x, w_c = ctx.saved_tensors
         if dy is None:
-            return None, None, None, None, None, None, None
+            return (None,) * 10
         stride, pad, kh, kw, ci = ctx.conf
         dy = dy.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = K.conv_dgrad(dy, w_c, x.shape, stride, pad)
+            addend = ctx.res_take.take() if ctx.res_take is not None else None
+            bnr = None
+            tok = ctx.prev
+            if tok is not None and K.use_native(dy) and tok.st.batch_stats:
+                rep = bn_workspace(tok.bn, "bwd", dy.device)  # zeroed; pending until collect
+                if rep is not None:
+                    st = tok.st
+                    bnr = (tok.y, st.mean, st.invstd, st.scale, st.bias, rep)
+            dx = K.conv_dgrad(dy, w_c, x.shape, stride, pad, addend=addend, bnr=bnr)
+            if bnr is not None:
+                tok.pre_reduced = True
+            if ctx.res_give is not None:
+                dx = ctx.res_give.produce(dx)
         if ctx.needs_input_grad[1]:
             weight = ctx.weight
             tgt = _direct_grad_target(weight) if x.shape[-1] == ci and K.use_native(dy) else None
@@ -79,13 +129,18 @@ class _ConvFn(Function):
                 if dw.shape[-1] != ci:  # input channels were zero-padded for the kernel
                     dw = dw[..., :ci]
                 dw = dw.permute(0, 3, 1, 2)
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None, None
 
 
 def conv2d(x: Tensor, weight: Tensor, w_c: Tensor, stride: int, pad: int,
-           stats_shift: Optional[Tensor] = None, slabs=None):
-    """NHWC conv.  Returns (y, psum, psumsq); the partials are None unless ``stats_shift``."""
-    return _ConvFn.apply(x, weight, w_c, stride, pad, stats_shift, slabs)
+           stats_shift: Optional[Tensor] = None, slabs=None, prev: Optional[BNActToken] = None,
+           res_take: Optional[ResidualSlot] = None, res_give: Optional[ResidualSlot] = None):
+    """NHWC conv.  Returns (y, psum, psumsq); the partials are None unless ``stats_shift``.
+    ``prev``: token of the BN(+ReLU) that produced x (x has no other consumer) -> BN-backward
+    reductions fused into this conv's dgrad.  ``res_take`` / ``res_give``: residual-gradient
+    slot this conv's dgrad adds / hands over (see :class:`ResidualSlot`)."""
+    return _ConvFn.apply(x, weight, w_c, stride, pad, stats_shift, slabs, prev, res_take,
+                         res_give)
 
 
 # ----------------------------------------------------------------------------- batchnorm
@@ -145,7 +200,8 @@ def bn_stats_from_partials(psum, psumsq, count, bn, training: bool) -> BNStats:
 
 class _BNActFn(Function):
     @staticmethod
-    def forward(ctx, y, gamma, beta, residual, y2, gamma2, beta2, st, st2, relu, bn=None):
+    def forward(ctx, y, gamma, beta, residual, y2, gamma2, beta2, st, st2, relu, bn=None,
+                token=None, res_give=None):
         z = K.bn_act_fwd(y, st.scale, st.bias, relu,
                          residual if y2 is None else y2,
                          None if st2 is None else st2.scale, None if st2 is None else st2.bias)
@@ -154,6 +210,7 @@ class _BNActFn(Function):
         ctx.has_res = residual is not None
         ctx.bn = bn
         ctx.beta, ctx.beta2 = beta, beta2
+        ctx.token, ctx.res_give = token, res_give
         return z
 
     @staticmethod
@@ -161,6 +218,9 @@ class _BNActFn(Function):
         y, z, y2, gamma, gamma2 = ctx.saved_tensors
         st, st2, relu = ctx.st, ctx.st2, ctx.relu
         dz = dz.contiguous()
+        tok = ctx.token
+        if tok is not None and tok.pre_reduced:
+            return _BNActFn._backward_pre_reduced(ctx, dz, y, gamma)
         rep = bn_workspace(ctx.bn, "bwd", dz.device) if ctx.bn is not None else None
         # BN affine grads accumulate straight into the flat gradient buffer when possible
         direct = None
@@ -197,22 +257,55 @@ class _BNActFn(Function):
             invstd2=None if st2 is None else st2.invstd,
             gamma2=None if gamma2 is None else gamma2.detach(), sum_gx2=a_gx2)
         dres = other if ctx.has_res else None
+        if dres is not None and ctx.res_give is not None:
+            dres = ctx.res_give.produce(dres)
         dy2 = other if y2 is not None else None
         if direct is not None:
-            return dy, None, None, dres, dy2, None, None, None, None, None, None
+            return dy, None, None, dres, dy2, None, None, None, None, None, None, None, None
         dgamma2 = sgx2 if y2 is not None else None
         dbeta2 = sg if y2 is not None else None
         return (dy, sgx.to(gamma.dtype), sg.to(gamma.dtype), dres, dy2,
                 None if dgamma2 is None else dgamma2.to(gamma2.dtype),
-                None if dbeta2 is None else dbeta2.to(gamma2.dtype), None, None, None, None)
+                None if dbeta2 is None else dbeta2.to(gamma2.dtype), None, None, None, None,
+                None, None)
+
+    @staticmethod
+    def _backward_pre_reduced(ctx, g, y, gamma):
+        """The consuming conv's dgrad already produced g = dz·relu'(z) and Σg, Σg·x̂ in the
+        bwd replica slab: collect them (+ direct dγ/dβ) and apply, no reduction pass."""
+        tok = ctx.token
+        tok.pre_reduced = False
+        st, bn = ctx.st, ctx.bn
+        rep = bn.__dict__["_mipipe_ws_bwd"]
+        C = y.shape[-1]
+        direct = None
+        if ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
+            tg, tb = _direct_grad_target(gamma), _direct_grad_target(ctx.beta)
+            if tg is not None and tb is not None:
+                direct = (tg[1], tb[1])
+        sg, sgx = K.bn_bwd_collect(rep, C, direct)
+        _ws_done(bn, "bwd")
+        if direct is not None:
+            fs = _direct_grad_target(gamma)[0]
+            fs.grad_ready(gamma)
+            fs.grad_ready(ctx.beta)
+        dy, _ = K.bn_act_bwd_apply(g, g, y, st.mean, st.invstd, gamma.detach(), sg, sgx,
+                                   st.count, False)
+        if direct is not None:
+            return dy, None, None, None, None, None, None, None, None, None, None, None, None
+        return (dy, sgx.to(gamma.dtype), sg.to(gamma.dtype), None, None, None, None, None, None,
+                None, None, None, None)
 
 
 def batchnorm_act(y: Tensor, st: BNStats, bn, relu: bool, residual: Optional[Tensor] = None,
-                  y2: Optional[Tensor] = None, st2: Optional[BNStats] = None, bn2=None) -> Tensor:
-    """z = relu?( bn(y) [+ residual | + bn2(y2)] )."""
+                  y2: Optional[Tensor] = None, st2: Optional[BNStats] = None, bn2=None,
+                  token: Optional[BNActToken] = None,
+                  res_give: Optional[ResidualSlot] = None) -> Tensor:
+    """z = relu?( bn(y) [+ residual | + bn2(y2)] ).  ``token``: z's single consumer will fuse
+    this BN's backward reductions; ``res_give``: slot receiving the residual's gradient."""
     return _BNActFn.apply(y, bn.weight, bn.bias, residual, y2,
                           None if bn2 is None else bn2.weight,
-                          None if bn2 is None else bn2.bias, st, st2, relu, bn)
+                          None if bn2 is None else bn2.bias, st, st2, relu, bn, token, res_give)
 
 
 def channel_partials(y: Tensor, shift: Tensor) -> Tuple[Tensor, Tensor]:

@@ -17,7 +17,7 @@ from ._native import native, native_available
 __all__ = ["conv_fwd", "conv_dgrad", "conv_wgrad", "bn_finalize", "bn_act_fwd",
            "bn_act_bwd_reduce", "bn_act_bwd_apply", "maxpool_fwd", "maxpool_bwd",
            "avgpool_fwd", "avgpool_bwd", "gemm", "cross_entropy_fwd_bwd", "sgd_step",
-           "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd", "dropout_fwd", "colsum",
+           "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd", "dropout_fwd", "colsum", "bn_bwd_collect",
            "embedding_bwd", "gelu_fwd", "gelu_bwd", "nchw_to_nhwc", "use_native"]
 
 _ALLOW_REF_ON_GPU = os.environ.get("MIPIPE_ALLOW_REF_ON_GPU", "0") == "1"
@@ -45,10 +45,26 @@ def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None):
     return _ref.conv_fwd(x, w, stride, pad, stats_shift)
 
 
-def conv_dgrad(dy, w, x_shape, stride, pad):
+def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None):
+    """dx of an NHWC conv.  ``addend``: tensor added to dx in the epilogue (residual gradient).
+    ``bnr = (y, mean, invstd, scale, bias, rep)``: the conv input was relu(bn(y)); dx becomes
+    g = dx·[y·scale+bias > 0] and Σg, Σg·x̂ accumulate into ``rep`` rows 0/1 (native only)."""
     if use_native(dy):
-        return native().conv_dgrad(dy, w, list(x_shape), stride, pad)
-    return _ref.conv_dgrad(dy, w, x_shape, stride, pad)
+        if bnr is None:
+            return native().conv_dgrad(dy, w, list(x_shape), stride, pad, addend)
+        y, mean, invstd, scale, bias, rep = bnr
+        return native().conv_dgrad(dy, w, list(x_shape), stride, pad, addend, y, mean, invstd,
+                                   scale, bias, rep)
+    if bnr is not None:
+        raise RuntimeError("BN-reduce dgrad fusion is a native-kernel path")
+    dx = _ref.conv_dgrad(dy, w, x_shape, stride, pad)
+    return dx if addend is None else (dx + addend).to(dx.dtype)
+
+
+def bn_bwd_collect(rep, C, acc=None):
+    """(Σg, Σg·x̂) from a bwd replica slab filled by a fused dgrad; re-zeroes the slab."""
+    a = acc if acc is not None else (None, None)
+    return native().bn_bwd_collect(rep, C, *a)
 
 
 def conv_wgrad(dy, x, kh, kw, stride, pad, out=None):

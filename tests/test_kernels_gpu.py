@@ -286,3 +286,38 @@ def test_gemm_odd_sizes_padded(M, N, K):
     assert rel_err(g, dy.float().t() @ x.float()) < 2e-3
     dx = Kx.gemm(dy, w, False, False, None, "none", torch.bfloat16)
     assert rel_err(dx, dy.float() @ w.float()) < 1e-2
+
+
+@pytest.mark.parametrize("case", [(2, 16, 16, 64, 64, 3, 1, 1), (2, 16, 16, 128, 256, 1, 1, 0),
+                                  (2, 16, 16, 128, 128, 3, 2, 1), (2, 14, 14, 64, 256, 1, 2, 0)])
+def test_conv_dgrad_fused_epilogues(case):
+    """dgrad + residual addend + BN-backward reduction epilogue vs the unfused reference."""
+    N, H, W, Ci, Co, k, s, p = case
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = bf(N, Ho, Wo, Co)
+    w = bf(Co, k, k, Ci, scale=0.1)
+    add = bf(N, H, W, Ci)
+    y = bf(N, H, W, Ci)
+    mean = torch.randn(Ci, device=dev) * 0.1
+    invstd = torch.rand(Ci, device=dev) + 0.5
+    scale = torch.randn(Ci, device=dev)
+    bias = torch.randn(Ci, device=dev) * 0.3
+    R = native().STAT_REPLICAS
+    rep = torch.zeros(3, R, Ci, device=dev)
+    g = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, add, y, mean, invstd, scale, bias, rep)
+    dx = _ref.conv_dgrad(dy.float(), w.float(), (N, H, W, Ci), s, p) + add.float()
+    mask = (y.float() * scale + bias) > 0
+    g_ref = dx * mask
+    assert rel_err(g, g_ref) < 2e-2
+    xh = (y.float() - mean) * invstd
+    gb = g.float()  # stats are of the stored bf16 g
+    sg_ref = gb.reshape(-1, Ci).sum(0)
+    sgx_ref = (gb * xh).reshape(-1, Ci).sum(0)
+    dgam = torch.zeros(Ci, device=dev)
+    dbet = torch.ones(Ci, device=dev)
+    sg, sgx = native().bn_bwd_collect(rep, Ci, dgam, dbet)
+    assert rel_err(sg, sg_ref) < 1e-3 and rel_err(sgx, sgx_ref) < 1e-3
+    assert rel_err(dgam, sgx_ref) < 1e-3 and rel_err(dbet - 1, sg_ref) < 1e-3
+    assert float(rep.abs().max()) == 0.0  # collect re-zeroes the slab
+    only_add = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, add)
+    assert rel_err(only_add, dx) < 2e-2
