@@ -53,6 +53,26 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
   const int wr = wave >> 1, wc = wave & 1;
   const uint32_t ml0 = wr * (BM / 2) + (lane & 15);
   const uint32_t nl0 = wc * (BN / 2) + (lane >> 4) * 4;
+  // dgrad fusions: issue this thread's addend / y loads now so their latency overlaps the
+  // accumulator staging below (a thread always owns the same 16-B column chunk)
+  constexpr int CPR = BN / 8;  // 16-B chunks per row
+  constexpr int ITER = BM * CPR / kThreads;
+  static_assert(kThreads % CPR == 0 && (BM * CPR) % kThreads == 0, "epilogue thread map");
+  const bool bnr = e.bnr_rep != nullptr;
+  const bool has_add = e.addend != nullptr;
+  const uint32_t my_cc = threadIdx.x % CPR, my_n = n0 + my_cc * 8;
+  const uint32_t ld_n = my_n < e.N ? my_n : 0;
+  uint4 ad_raw[ITER], y_raw[ITER];
+  if (has_add || bnr) {
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const uint32_t r = (threadIdx.x + it * kThreads) / CPR;
+      const uint32_t m = min(m0 + r, e.M - 1);
+      const long orow = out_row(e, m);
+      if (has_add) ad_raw[it] = *reinterpret_cast<const uint4*>(e.addend + orow * e.ldc + ld_n);
+      if (bnr) y_raw[it] = *reinterpret_cast<const uint4*>(e.bnr_y + orow * e.ldc + ld_n);
+    }
+  }
   // bias / activation
   if (e.bias != nullptr || e.act) {
 #pragma unroll
@@ -136,11 +156,7 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
       *reinterpret_cast<uint2*>(smem + ml * P + nl * 2) = v;
     }
   __syncthreads();
-  constexpr int CPR = BN / 8;  // 16-B chunks per row
-  static_assert(kThreads % CPR == 0, "thread -> column-chunk map must be loop invariant");
   __bf16* C = reinterpret_cast<__bf16*>(e.C);
-  const bool bnr = e.bnr_rep != nullptr;
-  const uint32_t my_cc = threadIdx.x % CPR, my_n = n0 + my_cc * 8;
   float b_sc[8], b_bi[8], b_mu[8], b_is[8], sg[8], sgx[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -151,24 +167,26 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
     b_mu[q] = ok ? e.bnr_mean[my_n + q] : 0.f;
     b_is[q] = ok ? e.bnr_invstd[my_n + q] : 0.f;
   }
-  for (int c = threadIdx.x; c < BM * CPR; c += kThreads) {
-    uint32_t r = c / CPR, cc = c % CPR;
-    uint32_t m = m0 + r, n = n0 + cc * 8;
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    const int c = threadIdx.x + it * kThreads;
+    const uint32_t r = c / CPR, cc = c % CPR;
+    const uint32_t m = m0 + r, n = n0 + cc * 8;
     if (m < e.M && n < e.N) {
       uint4 v = *reinterpret_cast<const uint4*>(smem + r * P + cc * 16);
       const long orow = out_row(e, m);
-      if (e.addend != nullptr || bnr) {
+      if (has_add || bnr) {
         float f[8];
         unpack8(v, f);
-        if (e.addend != nullptr) {
+        if (has_add) {
           float a[8];
-          unpack8(*reinterpret_cast<const uint4*>(e.addend + orow * e.ldc + n), a);
+          unpack8(ad_raw[it], a);
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] += a[q];
         }
         if (bnr) {
           float yv[8];
-          unpack8(*reinterpret_cast<const uint4*>(e.bnr_y + orow * e.ldc + n), yv);
+          unpack8(y_raw[it], yv);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const float zq = yv[q] * b_sc[q] + b_bi[q];
