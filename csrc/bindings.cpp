@@ -97,7 +97,7 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
 Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride, int pad,
                   optional<Tensor> addend, optional<Tensor> bn_y, optional<Tensor> bn_mean,
                   optional<Tensor> bn_invstd, optional<Tensor> bn_scale, optional<Tensor> bn_bias,
-                  optional<Tensor> bn_rep) {
+                  optional<Tensor> bn_rep, optional<Tensor> bn_z) {
   check_bf16(dy, "dy");
   check_bf16(w, "w");
   c10::DeviceGuard g(dy.device());
@@ -137,6 +137,11 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     fz.bn_mean = bn_mean->data_ptr<float>(); fz.bn_invstd = bn_invstd->data_ptr<float>();
     fz.bn_scale = bn_scale->data_ptr<float>(); fz.bn_bias = bn_bias->data_ptr<float>();
     fz.bn_rep = bn_rep->data_ptr<float>();
+    if (bn_z.has_value()) {
+      check_bf16(*bn_z, "bn_z");
+      TORCH_CHECK(bn_z->sizes() == dx.sizes(), "bn_z must match dx");
+      fz.bn_z = bn_z->data_ptr();
+    }
     any = true;
   }
   mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), any ? &fz : nullptr);
@@ -676,7 +681,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stride"), py::arg("pad"), py::arg("addend") = py::none(),
         py::arg("bn_y") = py::none(), py::arg("bn_mean") = py::none(),
         py::arg("bn_invstd") = py::none(), py::arg("bn_scale") = py::none(),
-        py::arg("bn_bias") = py::none(), py::arg("bn_rep") = py::none());
+        py::arg("bn_bias") = py::none(), py::arg("bn_rep") = py::none(),
+        py::arg("bn_z") = py::none());
   m.def("bn_bwd_collect", &bn_bwd_collect, py::arg("rep"), py::arg("C"),
         py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),

@@ -196,6 +196,7 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
         e.bnr_y = (const __bf16*)fz->bn_y;
         e.bnr_mean = fz->bn_mean; e.bnr_invstd = fz->bn_invstd;
         e.bnr_scale = fz->bn_scale; e.bnr_bias = fz->bn_bias; e.bnr_rep = fz->bn_rep;
+        e.bnr_z = (const __bf16*)fz->bn_z;
       }
       if (S > 1) {
         e.rm_s = S; e.rm_ph = ph; e.rm_pw = pw; e.rm_H = s.H; e.rm_W = s.W;

@@ -31,6 +31,9 @@ struct EpiParams {
   const __bf16* bnr_y;
   const float *bnr_mean, *bnr_invstd, *bnr_scale, *bnr_bias;
   float* bnr_rep;
+  // when set, the ReLU mask is read from this stored post-activation tensor (z > 0) instead of
+  // recomputed from y (needed when a residual was added before the ReLU)
+  const __bf16* bnr_z;
 };
 
 __device__ __forceinline__ long out_row(const EpiParams& e, uint32_t m) {
@@ -62,7 +65,8 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
   const bool has_add = e.addend != nullptr;
   const uint32_t my_cc = threadIdx.x % CPR, my_n = n0 + my_cc * 8;
   const uint32_t ld_n = my_n < e.N ? my_n : 0;
-  uint4 ad_raw[ITER], y_raw[ITER];
+  const bool zmask = bnr && e.bnr_z != nullptr;
+  uint4 ad_raw[ITER], y_raw[ITER], z_raw[ITER];
   if (has_add || bnr) {
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
@@ -71,6 +75,7 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
       const long orow = out_row(e, m);
       if (has_add) ad_raw[it] = *reinterpret_cast<const uint4*>(e.addend + orow * e.ldc + ld_n);
       if (bnr) y_raw[it] = *reinterpret_cast<const uint4*>(e.bnr_y + orow * e.ldc + ld_n);
+      if (zmask) z_raw[it] = *reinterpret_cast<const uint4*>(e.bnr_z + orow * e.ldc + ld_n);
     }
   }
   // bias / activation
@@ -185,11 +190,12 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
           for (int q = 0; q < 8; ++q) f[q] += a[q];
         }
         if (bnr) {
-          float yv[8];
+          float yv[8], zv[8];
           unpack8(y_raw[it], yv);
+          if (zmask) unpack8(z_raw[it], zv);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const float zq = yv[q] * b_sc[q] + b_bi[q];
+            const float zq = zmask ? zv[q] : yv[q] * b_sc[q] + b_bi[q];
             const float gq = zq > 0.f ? bf2f(f2bf(f[q])) : 0.f;  // stats of the stored bf16 g
             f[q] = gq;
             sg[q] += gq;

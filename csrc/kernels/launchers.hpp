@@ -34,6 +34,7 @@ struct DgradFusion {
   const void* bn_y = nullptr;
   const float *bn_mean = nullptr, *bn_invstd = nullptr, *bn_scale = nullptr, *bn_bias = nullptr;
   float* bn_rep = nullptr;
+  const void* bn_z = nullptr;  // optional stored relu output: mask = z > 0 (residual blocks)
 };
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
                 const DgradFusion* fz = nullptr);

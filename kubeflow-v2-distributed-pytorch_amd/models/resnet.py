@@ -47,7 +47,7 @@ class BasicBlock(tnn.Module):
 
     def forward(self, x):
         slot = MF.ResidualSlot()
-        out = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True, res_take=slot)
+        out = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True, res_take=slot, fuse_prev=True)
         if self.downsample is not None:
             ds_conv, ds_bn = self.downsample[0], self.downsample[1]
             return mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, fuse_prev=True,
@@ -76,7 +76,9 @@ class Bottleneck(tnn.Module):
         # conv2 / conv3 are the only consumers of their inputs: BN1 / BN2 backward reductions
         # run in their dgrad epilogues; conv1's dgrad adds the identity/downsample gradient
         slot = MF.ResidualSlot()
-        out = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True, res_take=slot)
+        # fuse_prev on conv1: if x is the previous block's BN+residual+ReLU output, its BN
+        # backward reductions run in conv1's dgrad epilogue once the identity gradient is added
+        out = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True, res_take=slot, fuse_prev=True)
         out = mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, fuse_prev=True)
         if self.downsample is not None:
             ds_conv, ds_bn = self.downsample[0], self.downsample[1]

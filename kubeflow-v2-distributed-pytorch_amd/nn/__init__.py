@@ -152,11 +152,13 @@ def conv_bn_act(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d, relu: bool = Tru
         stb = MF.bn_stats_from_partials(psb, pssb, count, bnb, bnb.training)
         return MF.batchnorm_act(y, st, bn, relu, y2=yb, st2=stb, bn2=bnb)
     token = None
-    if relu and residual is None and use_batch:
+    if relu and use_batch:
         token = MF.BNActToken(bn, st, y)
     z = MF.batchnorm_act(y, st, bn, relu, residual=residual, token=token,
                          res_give=res_give if residual is not None else None)
     if token is not None:
+        if residual is not None:
+            token.z = z  # mask source for the (multi-consumer) block-output fusion
         z._mipipe_bnact = token
     return z
 

@@ -72,10 +72,13 @@ class BNActToken:
     """Links a BN(+ReLU) output to its single consuming conv: the conv's backward computes the
     BN-backward reductions in its dgrad epilogue and flags the BN's backward to skip them."""
 
-    __slots__ = ("bn", "st", "y", "pre_reduced")
+    __slots__ = ("bn", "st", "y", "z", "pre_reduced")
 
-    def __init__(self, bn, st, y):
-        self.bn, self.st, self.y = bn, st, y
+    def __init__(self, bn, st, y, z=None):
+        # z set: BN + residual + ReLU block output.  Its consumer conv also feeds the next
+        # block's identity path, so the fusion is valid only when that conv's dgrad also adds
+        # the identity gradient (residual slot delivered) - the mask comes from stored z.
+        self.bn, self.st, self.y, self.z = bn, st, y, z
         self.pre_reduced = False
 
 
@@ -105,11 +108,14 @@ class _ConvFn(Function):
             addend = ctx.res_take.take() if ctx.res_take is not None else None
             bnr = None
             tok = ctx.prev
-            if tok is not None and K.use_native(dy) and tok.st.batch_stats:
+            if (tok is not None and K.use_native(dy) and tok.st.batch_stats
+                    and (tok.z is None or addend is not None)):
                 rep = bn_workspace(tok.bn, "bwd", dy.device)  # zeroed; pending until collect
                 if rep is not None:
                     st = tok.st
                     bnr = (tok.y, st.mean, st.invstd, st.scale, st.bias, rep)
+                    if tok.z is not None:
+                        bnr = bnr + (tok.z,)
             dx = K.conv_dgrad(dy, w_c, x.shape, stride, pad, addend=addend, bnr=bnr)
             if bnr is not None:
                 tok.pre_reduced = True
@@ -291,9 +297,12 @@ class _BNActFn(Function):
             fs.grad_ready(ctx.beta)
         dy, _ = K.bn_act_bwd_apply(g, g, y, st.mean, st.invstd, gamma.detach(), sg, sgx,
                                    st.count, False)
+        dres = None
+        if ctx.has_res:  # gradient of the pre-ReLU sum = g itself: hand it on, no copy
+            dres = ctx.res_give.produce(g) if ctx.res_give is not None else g
         if direct is not None:
-            return dy, None, None, None, None, None, None, None, None, None, None, None, None
-        return (dy, sgx.to(gamma.dtype), sg.to(gamma.dtype), None, None, None, None, None, None,
+            return dy, None, None, dres, None, None, None, None, None, None, None, None, None
+        return (dy, sgx.to(gamma.dtype), sg.to(gamma.dtype), dres, None, None, None, None, None,
                 None, None, None, None)
 
 

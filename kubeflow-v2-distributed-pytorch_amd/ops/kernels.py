@@ -47,14 +47,16 @@ def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None):
 
 def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None):
     """dx of an NHWC conv.  ``addend``: tensor added to dx in the epilogue (residual gradient).
-    ``bnr = (y, mean, invstd, scale, bias, rep)``: the conv input was relu(bn(y)); dx becomes
-    g = dx·[y·scale+bias > 0] and Σg, Σg·x̂ accumulate into ``rep`` rows 0/1 (native only)."""
+    ``bnr = (y, mean, invstd, scale, bias, rep[, z])``: the conv input was relu(bn(y)[+res]);
+    dx becomes g = dx·[z > 0] (z recomputed from y unless given) and Σg, Σg·x̂ accumulate into
+    ``rep`` rows 0/1 (native only)."""
     if use_native(dy):
         if bnr is None:
             return native().conv_dgrad(dy, w, list(x_shape), stride, pad, addend)
-        y, mean, invstd, scale, bias, rep = bnr
+        y, mean, invstd, scale, bias, rep = bnr[:6]
+        z = bnr[6] if len(bnr) > 6 else None
         return native().conv_dgrad(dy, w, list(x_shape), stride, pad, addend, y, mean, invstd,
-                                   scale, bias, rep)
+                                   scale, bias, rep, z)
     if bnr is not None:
         raise RuntimeError("BN-reduce dgrad fusion is a native-kernel path")
     dx = _ref.conv_dgrad(dy, w, x_shape, stride, pad)
