@@ -15,9 +15,12 @@ namespace gk {
 
 __device__ __attribute__((aligned(64))) uint4 g_conv_zero[8];
 
-template <int BM, int BN>
+// NS = LDS stages.  NS = 1 is used when the whole reduction is one k-step (K <= 64, e.g. the
+// 64-channel 1x1 convs of layer1): half the LDS, so 3 blocks fit per CU instead of 2 and the
+// block-level overlap of loads with epilogues hides these memory-bound layers' latency.
+template <int BM, int BN, int NS = 2>
 constexpr int lds_bytes_bf16() {
-  constexpr int a = 2 * (BM + BN) * BK * 2;
+  constexpr int a = NS * (BM + BN) * BK * 2;
   constexpr int b = kStatsLdsOffset<BM, BN>() + 4 * BN * 4;
   return a > b ? a : b;
 }
@@ -28,12 +31,11 @@ constexpr int lds_bytes_f32() {
   return a > b ? a : b;
 }
 
-template <int BM, int BN, bool DENSE>
-__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restrict__ x,
-                                                           const __bf16* __restrict__ w,
-                                                           ConvGeom g, uint32_t M, uint32_t tilesN,
-                                                           EpiParams e) {
-  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_bf16<BM, BN>()];
+template <int BM, int BN, bool DENSE, int NS = 2>
+__global__ __launch_bounds__(256, NS == 1 ? 3 : 2) void conv_fwd_kernel(
+    const __bf16* __restrict__ x, const __bf16* __restrict__ w, ConvGeom g, uint32_t M,
+    uint32_t tilesN, EpiParams e) {
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_bf16<BM, BN, NS>()];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
@@ -52,14 +54,11 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(const __bf16* __restri
   epilogue_bf16<BM, BN>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
-template <int BM, int BN, bool DENSE>
-__global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const __bf16* __restrict__ dy,
-                                                             const __bf16* __restrict__ w,
-                                                             int Ho, int Wo, int Co, int taps,
-                                                             FastDiv fCo, DgradClass cls,
-                                                             uint32_t M, uint32_t tilesN,
-                                                             EpiParams e) {
-  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_bf16<BM, BN>()];
+template <int BM, int BN, bool DENSE, int NS = 2>
+__global__ __launch_bounds__(256, NS == 1 ? 3 : 2) void conv_dgrad_kernel(
+    const __bf16* __restrict__ dy, const __bf16* __restrict__ w, int Ho, int Wo, int Co, int taps,
+    FastDiv fCo, DgradClass cls, uint32_t M, uint32_t tilesN, EpiParams e) {
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_bf16<BM, BN, NS>()];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
@@ -81,7 +80,7 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_kernel(const __bf16* __rest
   }
   f32x4 acc[BM / 32][BN / 32];
   MainLoop<BM, BN, OpA, OpB>::run(smem, a, b, 0, nk, acc, wave, lane);
-  epilogue_bf16<BM, BN>(smem, acc, e, m0, n0, 0, wave, lane);
+  epilogue_bf16<BM, BN, true>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
 template <int BM, int BN, bool DENSE>
@@ -156,7 +155,8 @@ void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq
     else MIPIPE_LAUNCH((conv_fwd_kernel<128, 64, false>), dim3(tiles), xp, wp, g, M, tN, e);
   } else {
     uint32_t tN = cdiv(s.Co, 128), tiles = cdiv(M, 128) * tN;
-    if (dense) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, true>), dim3(tiles), xp, wp, g, M, tN, e);
+    if (dense && s.Ci <= BK) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, true, 1>), dim3(tiles), xp, wp, g, M, tN, e);
+    else if (dense) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, true>), dim3(tiles), xp, wp, g, M, tN, e);
     else MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, false>), dim3(tiles), xp, wp, g, M, tN, e);
   }
 }
@@ -209,7 +209,8 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
         else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 64, false>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
       } else {
         uint32_t tN = cdiv(s.Ci, 128), tiles = cdiv(M, 128) * tN;
-        if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
+        if (dense && s.Co <= BK) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true, 1>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
+        else if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, false>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
       }
     }

@@ -49,7 +49,9 @@ template <int BM, int BN>
 constexpr int kStatsLdsOffset() { return ((BM * (BN * 2 + 16)) + 255) / 256 * 256; }
 
 // bf16 output.  acc layout: lane holds C[m][n..n+3] for tile (i, j).
-template <int BM, int BN>
+// FUSE: compile the dgrad fusions (addend / BN-backward reduction); kernels that never use
+// them keep their register budget.
+template <int BM, int BN, bool FUSE = false>
 __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const EpiParams& e,
                               uint32_t m0, uint32_t n0, uint32_t prow_base, int wave, int lane) {
   constexpr int MT = BM / 32, NT = BN / 32;
@@ -61,22 +63,26 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
   constexpr int CPR = BN / 8;  // 16-B chunks per row
   constexpr int ITER = BM * CPR / kThreads;
   static_assert(kThreads % CPR == 0 && (BM * CPR) % kThreads == 0, "epilogue thread map");
-  const bool bnr = e.bnr_rep != nullptr;
-  const bool has_add = e.addend != nullptr;
+  const bool bnr = FUSE && e.bnr_rep != nullptr;
+  const bool has_add = FUSE && e.addend != nullptr;
+  const bool zmask = bnr && e.bnr_z != nullptr;
   const uint32_t my_cc = threadIdx.x % CPR, my_n = n0 + my_cc * 8;
   const uint32_t ld_n = my_n < e.N ? my_n : 0;
-  const bool zmask = bnr && e.bnr_z != nullptr;
-  uint4 ad_raw[ITER], y_raw[ITER], z_raw[ITER];
-  if (has_add || bnr) {
+  // software-pipelined operand ring: PF iterations in flight; the first PF are issued now so
+  // their latency overlaps the accumulator staging below
+  constexpr int PF = FUSE ? (ITER < 4 ? ITER : 4) : 1;
+  uint4 ad_raw[PF], y_raw[PF], z_raw[PF];
+  auto issue = [&](int it, int slot) {
+    const uint32_t r = (threadIdx.x + it * kThreads) / CPR;
+    const uint32_t m = min(m0 + r, e.M - 1);
+    const long orow = out_row(e, m);
+    if (has_add) ad_raw[slot] = *reinterpret_cast<const uint4*>(e.addend + orow * e.ldc + ld_n);
+    if (bnr) y_raw[slot] = *reinterpret_cast<const uint4*>(e.bnr_y + orow * e.ldc + ld_n);
+    if (zmask) z_raw[slot] = *reinterpret_cast<const uint4*>(e.bnr_z + orow * e.ldc + ld_n);
+  };
+  if (FUSE && (has_add || bnr)) {
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-      const uint32_t r = (threadIdx.x + it * kThreads) / CPR;
-      const uint32_t m = min(m0 + r, e.M - 1);
-      const long orow = out_row(e, m);
-      if (has_add) ad_raw[it] = *reinterpret_cast<const uint4*>(e.addend + orow * e.ldc + ld_n);
-      if (bnr) y_raw[it] = *reinterpret_cast<const uint4*>(e.bnr_y + orow * e.ldc + ld_n);
-      if (zmask) z_raw[it] = *reinterpret_cast<const uint4*>(e.bnr_z + orow * e.ldc + ld_n);
-    }
+    for (int it = 0; it < PF; ++it) issue(it, it);
   }
   // bias / activation
   if (e.bias != nullptr || e.act) {
@@ -180,19 +186,19 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
     if (m < e.M && n < e.N) {
       uint4 v = *reinterpret_cast<const uint4*>(smem + r * P + cc * 16);
       const long orow = out_row(e, m);
-      if (has_add || bnr) {
+      if (FUSE && (has_add || bnr)) {
         float f[8];
         unpack8(v, f);
         if (has_add) {
           float a[8];
-          unpack8(ad_raw[it], a);
+          unpack8(ad_raw[it % PF], a);
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] += a[q];
         }
         if (bnr) {
           float yv[8], zv[8];
-          unpack8(y_raw[it], yv);
-          if (zmask) unpack8(z_raw[it], zv);
+          unpack8(y_raw[it % PF], yv);
+          if (zmask) unpack8(z_raw[it % PF], zv);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const float zq = zmask ? zv[q] : yv[q] * b_sc[q] + b_bi[q];
@@ -206,8 +212,9 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
       }
       *reinterpret_cast<uint4*>(C + orow * e.ldc + n) = v;
     }
+    if (FUSE && (has_add || bnr) && it + PF < ITER) issue(it + PF, it % PF);
   }
-  if (bnr) {
+  if (FUSE && bnr) {
     // threads t, t+CPR, ... share a column chunk: reduce them through LDS, then one atomic
     // per column per block into replica row blockIdx % R
     __syncthreads();
