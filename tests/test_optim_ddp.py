@@ -64,7 +64,7 @@ def test_adamw_matches_torch():
         assert torch.allclose(p, q, atol=1e-5)
 
 
-def _ddp_worker(rank, world, port, out, check_mismatch):
+def _ddp_worker(rank, world, port, out, check_mismatch, double_report=False):
     import torch.distributed as dist
     from mipipe.parallel import DistributedDataParallel, CollectiveSequenceError
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -72,9 +72,15 @@ def _ddp_worker(rank, world, port, out, check_mismatch):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(rank)  # different init per rank: DDP must broadcast rank 0's
     m = MLP()
-    ddp = DistributedDataParallel(m, bucket_cap_mb=0.0005, first_bucket_mb=0.0001,
+    cap, first = (1.0, 1.0) if double_report else (0.0005, 0.0001)  # one multi-param bucket
+    ddp = DistributedDataParallel(m, bucket_cap_mb=cap, first_bucket_mb=first,
                                   check_collectives=True, check_every=1)
     opt = SGD(ddp.parameters(), 0.1, momentum=0.9)
+    if double_report:
+        # what a kernel writing a gradient straight into the flat buffer does (space listener)
+        # on top of autograd's post-accumulate hook: readiness must be counted once per step
+        for p in m.parameters():
+            p.register_post_accumulate_grad_hook(lambda q: ddp.space.grad_ready(q))
     g = torch.Generator().manual_seed(123)
     X = torch.randn(4 * world, 16, generator=g)
     Y = torch.randint(0, 8, (4 * world,), generator=g)
@@ -97,16 +103,17 @@ def _ddp_worker(rank, world, port, out, check_mismatch):
     dist.destroy_process_group()
 
 
-def test_ddp_gloo_matches_single_process():
+@pytest.mark.parametrize("double_report", [False, True])
+def test_ddp_gloo_matches_single_process(double_report):
     world = 2
-    port = 29000 + os.getpid() % 1000
+    port = 29000 + os.getpid() % 1000 + (500 if double_report else 0)
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_ddp_worker, args=(world, port, out, True), nprocs=world, join=True)
+    mp.spawn(_ddp_worker, args=(world, port, out, True, double_report), nprocs=world, join=True)
     f0, nb, ok0 = out[0]
     f1, _, ok1 = out[1]
     assert torch.allclose(f0, f1), "replicas diverged"
-    assert nb > 1, "expected several buckets"
+    assert nb > 1 or double_report, "expected several buckets"
     assert ok0 and ok1, "collective checker missed a mismatched sequence"
     # single process on the global batch, starting from rank 0's init
     torch.manual_seed(0)
