@@ -63,11 +63,15 @@ mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int p
 std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor w, int stride,
                                                                 int pad, optional<Tensor> shift,
                                                                 optional<Tensor> slab_sum,
-                                                                optional<Tensor> slab_sq) {
+                                                                optional<Tensor> slab_sq,
+                                                                optional<Tensor> bias, bool relu) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   c10::DeviceGuard g(x.device());
   auto s = conv_shape(x, w, stride, pad);
+  if (bias.has_value()) check_vec(*bias, s.Co, "bias");
+  TORCH_CHECK(!(shift.has_value() && (bias.has_value() || relu)),
+              "BN-statistics epilogue and bias/ReLU epilogue are exclusive");
   auto y = torch::empty({s.N, s.Ho, s.Wo, s.Co}, x.options());
   optional<Tensor> ps, pss;
   float *psp = nullptr, *pssp = nullptr;
@@ -90,7 +94,8 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
     pssp = pss->data_ptr<float>();
     sh = shift->data_ptr<float>();
   }
-  mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), psp, pssp, sh, s, stream());
+  mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), psp, pssp, sh, s, stream(),
+                   bias.has_value() ? bias->data_ptr<float>() : nullptr, relu);
   return {y, ps, pss};
 }
 
@@ -675,7 +680,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "mipipe gfx950 (MI355X) HIP kernels";
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("shift") = py::none(), py::arg("slab_sum") = py::none(),
-        py::arg("slab_sq") = py::none());
+        py::arg("slab_sq") = py::none(), py::arg("bias") = py::none(), py::arg("relu") = false);
   m.attr("STAT_REPLICAS") = mipipe::kStatReplicas;
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("x_shape"),
         py::arg("stride"), py::arg("pad"), py::arg("addend") = py::none(),

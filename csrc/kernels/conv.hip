@@ -140,11 +140,12 @@ int conv_fwd_stat_rows(const ConvShape& s) {
 #define MIPIPE_LAUNCH(kern, grid, ...) hipLaunchKernelGGL((kern), (grid), dim3(256), 0, st, __VA_ARGS__)
 
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
-              const float* st_shift, const ConvShape& s, hipStream_t st) {
+              const float* st_shift, const ConvShape& s, hipStream_t st, const float* bias,
+              bool relu) {
   ConvGeom g = make_geom(s.N, s.H, s.W, s.Ci, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad);
   uint32_t M = (uint32_t)s.N * s.Ho * s.Wo;
   EpiParams e{};
-  e.C = y; e.ldc = s.Co; e.M = M; e.N = s.Co; e.bias = nullptr; e.act = 0;
+  e.C = y; e.ldc = s.Co; e.M = M; e.N = s.Co; e.bias = bias; e.act = relu ? 1 : 0;
   e.st_sum = st_sum; e.st_sq = st_sq; e.st_shift = st_shift; e.st_R = kStatReplicas;
   const bool dense = is_dense(s);
   const __bf16* xp = (const __bf16*)x;

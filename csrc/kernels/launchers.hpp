@@ -23,8 +23,10 @@ constexpr int kStatReplicas = 16;
 extern int g_splitk_target;
 int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
+// bias / relu: optional per-channel bias and ReLU in the epilogue (convs without BN: VGG, AlexNet)
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
-              const float* st_shift, const ConvShape& s, hipStream_t st);
+              const float* st_shift, const ConvShape& s, hipStream_t st,
+              const float* bias = nullptr, bool relu = false);
 // Optional dgrad epilogue fusions:
 //  addend: bf16 [N*H*W][Ci] added to dx (the block input's other gradient, e.g. the residual);
 //  bn_*:   the conv input was relu(bn(y)) with a single consumer: dx becomes g = dx*[z > 0] and

@@ -261,3 +261,63 @@ def ref_bert(arch: str = "bert_base", **kw) -> RefBertForMaskedLM:
         kw = {**dict(hidden_size=128, num_hidden_layers=2, num_attention_heads=2,
                      intermediate_size=512), **kw}
     return RefBertForMaskedLM(**kw)
+
+
+# ----------------------------------------------------------------------------- VGG / AlexNet
+_VGG_CFGS = {
+    "vgg11": [64, "M", 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
+    "vgg13": [64, 64, "M", 128, 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
+    "vgg16": [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M",
+              512, 512, 512, "M"],
+    "vgg19": [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M",
+              512, 512, 512, 512, "M"],
+}
+
+
+class RefVGG(nn.Module):
+    """torchvision-structured VGG (plain torch.nn) — oracle / stock comparator."""
+
+    def __init__(self, arch: str = "vgg16", num_classes: int = 1000, dropout: float = 0.5):
+        super().__init__()
+        bn = arch.endswith("_bn")
+        layers: List[nn.Module] = []
+        c = 3
+        for v in _VGG_CFGS[arch.replace("_bn", "")]:
+            if v == "M":
+                layers.append(nn.MaxPool2d(2, 2))
+                continue
+            layers.append(nn.Conv2d(c, v, 3, padding=1))
+            if bn:
+                layers.append(nn.BatchNorm2d(v))
+            layers.append(nn.ReLU(inplace=True))
+            c = v
+        self.features = nn.Sequential(*layers)
+        self.avgpool = nn.AdaptiveAvgPool2d((7, 7))
+        self.classifier = nn.Sequential(
+            nn.Linear(512 * 7 * 7, 4096), nn.ReLU(True), nn.Dropout(dropout),
+            nn.Linear(4096, 4096), nn.ReLU(True), nn.Dropout(dropout),
+            nn.Linear(4096, num_classes))
+
+    def forward(self, x):
+        x = self.avgpool(self.features(x))
+        return self.classifier(torch.flatten(x, 1))
+
+
+class RefAlexNet(nn.Module):
+    def __init__(self, num_classes: int = 1000, dropout: float = 0.5):
+        super().__init__()
+        self.features = nn.Sequential(
+            nn.Conv2d(3, 64, 11, stride=4, padding=2), nn.ReLU(True), nn.MaxPool2d(3, 2),
+            nn.Conv2d(64, 192, 5, padding=2), nn.ReLU(True), nn.MaxPool2d(3, 2),
+            nn.Conv2d(192, 384, 3, padding=1), nn.ReLU(True),
+            nn.Conv2d(384, 256, 3, padding=1), nn.ReLU(True),
+            nn.Conv2d(256, 256, 3, padding=1), nn.ReLU(True), nn.MaxPool2d(3, 2))
+        self.avgpool = nn.AdaptiveAvgPool2d((6, 6))
+        self.classifier = nn.Sequential(
+            nn.Dropout(dropout), nn.Linear(256 * 6 * 6, 4096), nn.ReLU(True),
+            nn.Dropout(dropout), nn.Linear(4096, 4096), nn.ReLU(True),
+            nn.Linear(4096, num_classes))
+
+    def forward(self, x):
+        x = self.avgpool(self.features(x))
+        return self.classifier(torch.flatten(x, 1))

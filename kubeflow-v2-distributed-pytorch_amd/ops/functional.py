@@ -149,6 +149,53 @@ def conv2d(x: Tensor, weight: Tensor, w_c: Tensor, stride: int, pad: int,
                          res_give)
 
 
+class _ConvBiasActFn(Function):
+    """y = act(conv(x) + b) with bias and ReLU in the conv epilogue (VGG / AlexNet convs)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, w_c, bias, stride, pad, relu):
+        y, _, _ = K.conv_fwd(x, w_c, stride, pad, None, None, bias, relu)
+        ctx.save_for_backward(x, w_c, y if relu else None)
+        ctx.weight, ctx.bias = weight, bias
+        ctx.conf = (stride, pad, weight.shape[2], weight.shape[3], weight.shape[1], relu)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w_c, y = ctx.saved_tensors
+        stride, pad, kh, kw, ci, relu = ctx.conf
+        g = dy.contiguous()
+        if relu:
+            g = (g * (y > 0)).to(g.dtype)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = K.conv_dgrad(g, w_c, x.shape, stride, pad)
+        native = K.use_native(g)
+        if ctx.needs_input_grad[1]:
+            tgt = _direct_grad_target(ctx.weight) if x.shape[-1] == ci and native else None
+            if tgt is not None:
+                K.conv_wgrad(g, x, kh, kw, stride, pad, out=tgt[1].permute(0, 2, 3, 1))
+                tgt[0].grad_ready(ctx.weight)
+            else:
+                dw = K.conv_wgrad(g, x, kh, kw, stride, pad)
+                if dw.shape[-1] != ci:
+                    dw = dw[..., :ci]
+                dw = dw.permute(0, 3, 1, 2)
+        if ctx.bias is not None and ctx.needs_input_grad[3]:
+            tb = _direct_grad_target(ctx.bias) if native else None
+            if tb is not None:
+                K.colsum(g.reshape(-1, g.shape[-1]), tb[1])
+                tb[0].grad_ready(ctx.bias)
+            else:
+                db = K.colsum(g.reshape(-1, g.shape[-1])).to(ctx.bias.dtype)
+        return dx, dw, None, db, None, None, None
+
+
+def conv2d_bias_act(x: Tensor, weight: Tensor, w_c: Tensor, bias: Optional[Tensor], stride: int,
+                    pad: int, relu: bool) -> Tensor:
+    return _ConvBiasActFn.apply(x, weight, w_c, bias, stride, pad, relu)
+
+
 # ----------------------------------------------------------------------------- batchnorm
 @dataclass
 class BNStats:

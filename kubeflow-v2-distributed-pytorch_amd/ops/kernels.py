@@ -12,6 +12,7 @@ from typing import Optional
 import torch
 
 from . import _ref
+from ._ref import _f
 from ._native import native, native_available
 
 __all__ = ["conv_fwd", "conv_dgrad", "conv_wgrad", "bn_finalize", "bn_act_fwd",
@@ -36,13 +37,18 @@ def use_native(t: torch.Tensor) -> bool:
         "`python setup.py build_ext --inplace`).  Set MIPIPE_ALLOW_REF_ON_GPU=1 only to debug.")
 
 
-def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None):
+def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None, bias=None, relu=False):
     """``slabs``: persistent zeroed (sum, sumsq) replica slabs the GPU epilogue accumulates BN
-    statistics into (re-zeroed by :func:`bn_finalize`)."""
+    statistics into (re-zeroed by :func:`bn_finalize`).  ``bias`` / ``relu``: epilogue bias and
+    ReLU for convolutions without BatchNorm (exclusive with the statistics epilogue)."""
     if use_native(x):
         s1, s2 = slabs if slabs is not None else (None, None)
-        return native().conv_fwd(x, w, stride, pad, stats_shift, s1, s2)
-    return _ref.conv_fwd(x, w, stride, pad, stats_shift)
+        return native().conv_fwd(x, w, stride, pad, stats_shift, s1, s2, bias, relu)
+    y, a, b = _ref.conv_fwd(x, w, stride, pad, stats_shift)
+    if bias is not None or relu:
+        yf = _f(y) if bias is None else _f(y) + _f(bias)
+        y = (torch.relu(yf) if relu else yf).to(x.dtype)
+    return y, a, b
 
 
 def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None):

@@ -321,3 +321,14 @@ def test_conv_dgrad_fused_epilogues(case):
     assert float(rep.abs().max()) == 0.0  # collect re-zeroes the slab
     only_add = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, add)
     assert rel_err(only_add, dx) < 2e-2
+
+
+def test_conv_fwd_bias_relu_epilogue():
+    N, H, W, Ci, Co = 2, 12, 12, 64, 96
+    x = bf(N, H, W, Ci)
+    w = bf(Co, 3, 3, Ci, scale=0.1)
+    b = torch.randn(Co, device=dev)
+    y, _, _ = native().conv_fwd(x, w, 1, 1, None, None, None, b, True)
+    ref, _, _ = _ref.conv_fwd(x.float(), w.float(), 1, 1)
+    ref = torch.relu(ref + b)
+    assert rel_err(y, ref) < 1e-2

@@ -102,3 +102,25 @@ def test_training_reduces_loss():
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < losses[0] * 0.7, losses
+
+
+@pytest.mark.parametrize("arch,res", [("vgg11_bn", 64), ("alexnet", 96), ("vgg11", 64)])
+def test_vgg_alexnet_gpu(arch, res):
+    from mipipe.models.reference import RefAlexNet, RefVGG
+    torch.manual_seed(0)
+    m = create_model(arch, num_classes=10, dropout=0.0).cuda()
+    r = (RefAlexNet(num_classes=10, dropout=0.0) if arch == "alexnet"
+         else RefVGG(arch, num_classes=10, dropout=0.0)).cuda()
+    r.load_state_dict(m.state_dict())
+    x = torch.randn(8, 3, res, res, device="cuda")
+    assert cos(m(x), r(x)) > 0.99
+    opt = SGD(m.parameters(), 0.01, momentum=0.9, weight_decay=1e-4)
+    y = torch.randint(0, 10, (8,), device="cuda")
+    losses = []
+    for _ in range(8):
+        opt.zero_grad()
+        loss = cross_entropy(m(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0], losses
