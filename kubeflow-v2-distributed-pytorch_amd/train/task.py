@@ -40,6 +40,8 @@ import torch
 import torch.multiprocessing as mp
 
 from mipipe.models import create_model, model_names
+from mipipe.obs import trace
+from mipipe.obs.log import JsonlLogger
 from mipipe.parallel import DataParallel, DistributedDataParallel, DistributedSampler
 from mipipe.parallel import dist_utils
 from mipipe.data.synthetic import DATASET_SHAPES, DeviceBatchLoader, SyntheticImageDataset
@@ -162,6 +164,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--compat-nested-model-dir", action="store_true",
                    help="export to AIP_MODEL_DIR/model/<file> like task.py:291")
     p.add_argument("--metrics-file", default="", help="write final metrics JSON here")
+    p.add_argument("--trace", action="store_true",
+                   help="roctx ranges around step phases (for rocprofv3 --marker-trace)")
+    p.add_argument("--log-dir", default=os.environ.get("MIPIPE_LOG_DIR", ""),
+                   help="per-rank JSON-lines logs (rank<k>.jsonl)")
     p.add_argument("--cpu-procs", type=int, default=1,
                    help="processes per node when no GPU is visible (gloo)")
     return p
@@ -327,6 +333,9 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
         test_loader = DeviceBatchLoader(test_set, 128, test_sampler, device)
 
     meter = ThroughputMeter(device, warmup_steps=args.warmup_steps)
+    jlog = JsonlLogger(args.rank, args.log_dir or None)
+    if args.trace:
+        trace.enable(True)
     global_step = 0
     last_loss = float("nan")
     accuracy = None
@@ -343,20 +352,34 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
                       f"{datetime.now().strftime('%Y_%m_%d_%H_%M_%S')}")
                 print("-" * 75, flush=True)
         model.train()
-        for i, (inputs, labels) in enumerate(train_loader):
+        it = iter(train_loader)
+        i = 0
+        while True:
             if args.steps and i >= args.steps:
                 break
+            with trace.phase("data"):
+                batch = next(it, None)
+            if batch is None:
+                break
+            inputs, labels = batch
             _fault_check(args.rank, global_step)
             meter.step_begin()
-            optimizer.zero_grad()
-            outputs = model(inputs)
-            loss = criterion(outputs, labels)
-            loss.backward()
-            optimizer.step()
+            with trace.phase("zero_grad"):
+                optimizer.zero_grad()
+            with trace.phase("forward"):
+                outputs = model(inputs)
+                loss = criterion(outputs, labels)
+            with trace.phase("backward+allreduce"):
+                loss.backward()
+            with trace.phase("optimizer"):
+                optimizer.step()
             meter.step_end(inputs.shape[0])
             global_step += 1
+            i += 1
             if args.log_every and global_step % args.log_every == 0:
                 last_loss = float(loss.detach().float().item())
+                jlog.log("step", epoch=epoch, step=global_step, loss=last_loss,
+                         samples_per_sec=meter.samples_per_sec())
                 if args.rank == 0:
                     print(f"epoch {epoch} step {global_step} loss {last_loss:.4f} "
                           f"{meter.samples_per_sec() * world:.1f} samples/s (job)", flush=True)
@@ -378,6 +401,8 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
         print("MIPIPE_METRICS " + json.dumps(metrics), flush=True)
         if args.metrics_file:
             ckpt.write_json(args.metrics_file, metrics)
+    jlog.log("final", **metrics)
+    jlog.close()
     epoch_end = datetime.now().strftime("%Y_%m_%d_%H_%M_%S")
     print(f"Epoch complete: {epoch_end}", flush=True)
     dist_utils.barrier(device if use_gpu else None)
