@@ -52,6 +52,7 @@ mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int p
   s.Wo = (s.W + 2 * pad - s.KW) / stride + 1;
   TORCH_CHECK(s.Ho > 0 && s.Wo > 0, "empty conv output");
   TORCH_CHECK(s.Ci % 8 == 0, "conv kernels need Ci % 8 == 0 (pad channels), got ", s.Ci);
+  TORCH_CHECK(x.numel() < (1ll << 31), "conv input too large for 32-bit gather offsets");
   TORCH_CHECK(s.Co % 8 == 0, "conv kernels need Co % 8 == 0, got ", s.Co);
   TORCH_CHECK((int64_t)s.N * s.H * s.W * s.Ci < (1ll << 31) &&
                   (int64_t)s.N * s.Ho * s.Wo * s.Co < (1ll << 31),
@@ -117,6 +118,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo && dy.size(3) == s.Co,
               "dy shape does not match the convolution");
   TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv dgrad needs Ci, Co % 8 == 0");
+  TORCH_CHECK(dy.numel() < (1ll << 31), "conv dgrad dy too large for 32-bit gather offsets");
   TORCH_CHECK(s.pad < s.KH, "conv dgrad expects pad < kernel size");
   auto dx = torch::empty({s.N, s.H, s.W, s.Ci}, dy.options());
   mipipe::DgradFusion fz;

@@ -31,7 +31,7 @@ constexpr int lds_bytes_f32() {
   return a > b ? a : b;
 }
 
-template <int BM, int BN, bool DENSE, int NS = 2>
+template <int BM, int BN, bool DENSE, int NS = 2, bool ALIGNED = false>
 __global__ __launch_bounds__(256, NS == 1 ? 3 : 2) void conv_fwd_kernel(
     const __bf16* __restrict__ x, const __bf16* __restrict__ w, ConvGeom g, uint32_t M,
     uint32_t tilesN, EpiParams e) {
@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256, NS == 1 ? 3 : 2) void conv_fwd_kernel(
   const uint32_t m0 = tm * BM, n0 = tn * BN;
   const uint32_t K = (uint32_t)(g.KH * g.KW * g.C);
   const int nk = (int)((K + BK - 1) / BK);
-  typedef typename std::conditional<DENSE, KCDense<BM>, KCIm2col<BM>>::type OpA;
+  typedef typename std::conditional<DENSE, KCDense<BM>, KCIm2col<BM, ALIGNED>>::type OpA;
   OpA a;
   if constexpr (DENSE) a.init(x, g.C, M, K, m0, wave, lane, g_conv_zero);
   else a.init(x, g, M, m0, wave, lane, g_conv_zero);
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256, NS == 1 ? 3 : 2) void conv_fwd_kernel(
   epilogue_bf16<BM, BN>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
-template <int BM, int BN, bool DENSE, int NS = 2>
+template <int BM, int BN, bool DENSE, int NS = 2, bool ALIGNED = false>
 __global__ __launch_bounds__(256, NS == 1 ? 3 : 2) void conv_dgrad_kernel(
     const __bf16* __restrict__ dy, const __bf16* __restrict__ w, int Ho, int Wo, int Co, int taps,
     FastDiv fCo, DgradClass cls, uint32_t M, uint32_t tilesN, EpiParams e) {
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256, NS == 1 ? 3 : 2) void conv_dgrad_kernel(
   const uint32_t Ci = e.N;
   const uint32_t K = (uint32_t)(cls.ntaps * Co);
   const int nk = (int)((K + BK - 1) / BK);
-  typedef typename std::conditional<DENSE, KCDense<BM>, KCDgrad<BM>>::type OpA;
+  typedef typename std::conditional<DENSE, KCDense<BM>, KCDgrad<BM, ALIGNED>>::type OpA;
   typedef typename std::conditional<DENSE, MCDense<BN>, MCDgradW<BN>>::type OpB;
   OpA a;
   OpB b;
@@ -153,11 +153,13 @@ void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq
   if (s.Co <= 64) {
     uint32_t tN = cdiv(s.Co, 64), tiles = cdiv(M, 128) * tN;
     if (dense) MIPIPE_LAUNCH((conv_fwd_kernel<128, 64, true>), dim3(tiles), xp, wp, g, M, tN, e);
+    else if (s.Ci % BK == 0) MIPIPE_LAUNCH((conv_fwd_kernel<128, 64, false, 2, true>), dim3(tiles), xp, wp, g, M, tN, e);
     else MIPIPE_LAUNCH((conv_fwd_kernel<128, 64, false>), dim3(tiles), xp, wp, g, M, tN, e);
   } else {
     uint32_t tN = cdiv(s.Co, 128), tiles = cdiv(M, 128) * tN;
     if (dense && s.Ci <= BK) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, true, 1>), dim3(tiles), xp, wp, g, M, tN, e);
     else if (dense) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, true>), dim3(tiles), xp, wp, g, M, tN, e);
+    else if (s.Ci % BK == 0) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, false, 2, true>), dim3(tiles), xp, wp, g, M, tN, e);
     else MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, false>), dim3(tiles), xp, wp, g, M, tN, e);
   }
 }
@@ -207,11 +209,13 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
       if (s.Ci <= 64) {
         uint32_t tN = cdiv(s.Ci, 64), tiles = cdiv(M, 128) * tN;
         if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 64, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
+        else if (s.Co % BK == 0) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 64, false, 2, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 64, false>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
       } else {
         uint32_t tN = cdiv(s.Ci, 128), tiles = cdiv(M, 128) * tN;
         if (dense && s.Co <= BK) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true, 1>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
+        else if (s.Co % BK == 0) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, false, 2, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, false>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
       }
     }

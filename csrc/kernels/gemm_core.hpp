@@ -85,6 +85,7 @@ struct KCDense {
   uint32_t kcol;
   uint32_t K;
   const void* zero;
+  __device__ void prep(int) {}
   __device__ void init(const __bf16* base, long ld, uint32_t rows_total, uint32_t K_,
                        uint32_t origin, int wave, int lane, const void* zero_page) {
     K = K_;
@@ -110,16 +111,18 @@ struct ConvGeom {
   FastDiv fHoWo, fWo, fC, fKW;
 };
 
-template <int R>
+template <int R, bool ALIGNED = false>
 struct KCIm2col {
   static constexpr bool KC = true;
   static constexpr int NI = R / 32;
   const __bf16* x;
   int hi0[NI], wi0[NI];
-  long pix[NI];   // (img*H + hi0)*W + wi0 ; -1 when row invalid
+  int rowoff[NI];   // ((img*H + hi0)*W + wi0)*C  (32-bit: host checks numel < 2^31)
   uint32_t kcol, K;
   ConvGeom g;
   const void* zero;
+  int p_kh, p_kw, p_toff;  // ALIGNED: this k-step's tap (kh, kw) and (kh*W + kw)*C + ci0 + kcol
+  bool p_kok;
   __device__ void init(const __bf16* x_, const ConvGeom& g_, uint32_t M, uint32_t origin, int wave,
                        int lane, const void* zero_page) {
     x = x_;
@@ -137,23 +140,47 @@ struct KCIm2col {
         uint32_t wo = rem - ho * (uint32_t)g.Wo;
         hi0[i] = (int)ho * g.stride - g.pad;
         wi0[i] = (int)wo * g.stride - g.pad;
-        pix[i] = ((long)img * g.H + hi0[i]) * g.W + wi0[i];
+        rowoff[i] = (((int)img * g.H + hi0[i]) * g.W + wi0[i]) * g.C;
       } else {
-        hi0[i] = wi0[i] = -100000;
-        pix[i] = -1;
+        hi0[i] = wi0[i] = -100000;  // fails every bounds check
+        rowoff[i] = 0;
       }
     }
   }
+  // Branch-free, 32-bit address math.  ALIGNED (C % 64 == 0): a 64-wide k-step never
+  // straddles a filter tap, so (kh, kw, ci0) are computed once per k-step in prep() as
+  // wave-uniform scalars and a lane adds only its row offset; out-of-image taps select the
+  // zero page.
+  __device__ void prep(int kt) {
+    if constexpr (ALIGNED) {
+      const uint32_t k0 = (uint32_t)kt * BK;
+      const uint32_t tap = fdiv(g.fC, k0);
+      const uint32_t kh = fdiv(g.fKW, tap);
+      const uint32_t kw = tap - kh * (uint32_t)g.KW;
+      p_kh = (int)kh;
+      p_kw = (int)kw;
+      p_toff = ((int)kh * g.W + (int)kw) * g.C + (int)(k0 - tap * (uint32_t)g.C) + (int)kcol;
+      p_kok = k0 < K;
+    }
+  }
   __device__ const void* src(int kt, int i) const {
-    uint32_t k = (uint32_t)kt * BK + kcol;
-    if (k >= K) return zero;  // invalid rows carry hi0 = -100000 -> fail the bounds check
-    uint32_t tap = fdiv(g.fC, k);
-    uint32_t ci = k - tap * (uint32_t)g.C;
-    uint32_t kh = fdiv(g.fKW, tap);
-    uint32_t kw = tap - kh * (uint32_t)g.KW;
-    int hi = hi0[i] + (int)kh, wi = wi0[i] + (int)kw;
-    if ((unsigned)hi >= (unsigned)g.H || (unsigned)wi >= (unsigned)g.W) return zero;
-    return x + (pix[i] + (long)kh * g.W + kw) * g.C + ci;
+    int kh, kw, off;
+    bool kok;
+    if constexpr (ALIGNED) {
+      kh = p_kh; kw = p_kw; kok = p_kok;
+      off = rowoff[i] + p_toff;
+    } else {
+      const uint32_t k = (uint32_t)kt * BK + kcol;
+      const uint32_t tap = fdiv(g.fC, k);
+      const uint32_t ukh = fdiv(g.fKW, tap);
+      kh = (int)ukh;
+      kw = (int)(tap - ukh * (uint32_t)g.KW);
+      kok = k < K;
+      off = rowoff[i] + (kh * g.W + kw) * g.C + (int)(k - tap * (uint32_t)g.C);
+    }
+    const int hi = hi0[i] + kh, wi = wi0[i] + kw;
+    const bool ok = kok & ((unsigned)hi < (unsigned)g.H) & ((unsigned)wi < (unsigned)g.W);
+    return ok ? (const void*)(x + off) : zero;
   }
 };
 
@@ -174,23 +201,23 @@ struct DgradClass {
   FastDiv fHcWc, fWc, fnkw;
 };
 
-template <int R>
+template <int R, bool ALIGNED = false>
 struct KCDgrad {
   static constexpr bool KC = true;
   static constexpr int NI = R / 32;
   const __bf16* dy;
-  int i_[NI], j_[NI];
-  long imgbase[NI];  // img*Ho*Wo ; -1 invalid
+  int ib[NI], jb[NI];   // i + dh0, j + dw0 (dy row/col of the class's first tap)
+  int rowoff[NI];       // ((img*Ho + ib)*Wo + jb)*Co  (32-bit: host checks numel < 2^31)
   uint32_t kcol, K;
   int Ho, Wo, Co;
   FastDiv fCo, fnkw;
-  int dh0, dw0;
   const void* zero;
+  int p_a, p_b, p_toff;  // ALIGNED: this k-step's tap offsets and -(a*Wo + b)*Co + co0 + kcol
+  bool p_kok;
   __device__ void init(const __bf16* dy_, int Ho_, int Wo_, int Co_, FastDiv fCo_,
                        const DgradClass& cls, uint32_t M, uint32_t origin, int wave, int lane,
                        const void* zero_page) {
     dy = dy_; Ho = Ho_; Wo = Wo_; Co = Co_; fCo = fCo_; fnkw = cls.fnkw;
-    dh0 = cls.dh0; dw0 = cls.dw0;
     zero = zero_page;
     K = (uint32_t)(cls.ntaps * Co);
     kcol = KCGeom<R>::chunk(lane) * 8;
@@ -201,25 +228,45 @@ struct KCDgrad {
         uint32_t img = fdiv(cls.fHcWc, m);
         uint32_t rem = m - img * (uint32_t)(cls.Hc * cls.Wc);
         uint32_t ii = fdiv(cls.fWc, rem);
-        i_[i] = (int)ii;
-        j_[i] = (int)(rem - ii * (uint32_t)cls.Wc);
-        imgbase[i] = (long)img * Ho * Wo;
+        ib[i] = (int)ii + cls.dh0;
+        jb[i] = (int)(rem - ii * (uint32_t)cls.Wc) + cls.dw0;
+        rowoff[i] = (((int)img * Ho + ib[i]) * Wo + jb[i]) * Co;
       } else {
-        i_[i] = j_[i] = 0;
-        imgbase[i] = -1;
+        ib[i] = jb[i] = -100000;
+        rowoff[i] = 0;
       }
     }
   }
+  __device__ void prep(int kt) {
+    if constexpr (ALIGNED) {  // Co % 64 == 0: the tap index is wave-uniform per k-step
+      const uint32_t k0 = (uint32_t)kt * BK;
+      const uint32_t t = fdiv(fCo, k0);
+      const uint32_t a = fdiv(fnkw, t);
+      const uint32_t b = t - a * fnkw.d;
+      p_a = (int)a;
+      p_b = (int)b;
+      p_toff = -((int)a * Wo + (int)b) * Co + (int)(k0 - t * (uint32_t)Co) + (int)kcol;
+      p_kok = k0 < K;
+    }
+  }
   __device__ const void* src(int kt, int i) const {
-    uint32_t k = (uint32_t)kt * BK + kcol;
-    if (k >= K || imgbase[i] < 0) return zero;
-    uint32_t t = fdiv(fCo, k);
-    uint32_t co = k - t * (uint32_t)Co;
-    uint32_t a = fdiv(fnkw, t);
-    uint32_t b = t - a * fnkw.d;
-    int ho = i_[i] + dh0 - (int)a, wo = j_[i] + dw0 - (int)b;
-    if ((unsigned)ho >= (unsigned)Ho || (unsigned)wo >= (unsigned)Wo) return zero;
-    return dy + (imgbase[i] + (long)ho * Wo + wo) * Co + co;
+    int a, b, off;
+    bool kok;
+    if constexpr (ALIGNED) {
+      a = p_a; b = p_b; kok = p_kok;
+      off = rowoff[i] + p_toff;
+    } else {
+      const uint32_t k = (uint32_t)kt * BK + kcol;
+      const uint32_t t = fdiv(fCo, k);
+      const uint32_t ua = fdiv(fnkw, t);
+      a = (int)ua;
+      b = (int)(t - ua * fnkw.d);
+      kok = k < K;
+      off = rowoff[i] - (a * Wo + b) * Co + (int)(k - t * (uint32_t)Co);
+    }
+    const int ho = ib[i] - a, wo = jb[i] - b;
+    const bool ok = kok & ((unsigned)ho < (unsigned)Ho) & ((unsigned)wo < (unsigned)Wo);
+    return ok ? (const void*)(dy + off) : zero;
   }
 };
 
@@ -233,6 +280,7 @@ struct MCDense {
   long ld;
   uint32_t K;
   const void* zero;
+  __device__ void prep(int) {}
   __device__ void init(const __bf16* base, long ld_, uint32_t cols_total, uint32_t K_,
                        uint32_t origin, int wave, int lane, const void* zero_page) {
     ld = ld_;
@@ -262,6 +310,7 @@ struct MCDgradW {
   FastDiv fCo, fnkw;
   int kh0, kw0, S, KW;
   const void* zero;
+  __device__ void prep(int) {}
   __device__ void init(const __bf16* w, uint32_t Co_, uint32_t taps_, uint32_t Ci_, FastDiv fCo_,
                        const DgradClass& cls, uint32_t origin, int wave, int lane,
                        const void* zero_page) {
@@ -300,6 +349,7 @@ struct MCIm2colT {
   uint32_t K;
   ConvGeom g;
   const void* zero;
+  __device__ void prep(int) {}
   __device__ void init(const __bf16* x_, const ConvGeom& g_, uint32_t origin, int wave, int lane,
                        const void* zero_page) {
     x = x_;
@@ -374,7 +424,9 @@ struct MainLoop {
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
   static constexpr int LDS_BYTES = 2 * STAGE_BYTES;
 
-  __device__ static void stage(char* buf, const OpA& a, const OpB& b, int kt, int wave) {
+  __device__ static void stage(char* buf, OpA& a, OpB& b, int kt, int wave) {
+    a.prep(kt);  // per-k-step wave-uniform address state (filter tap ...), computed once
+    b.prep(kt);
 #pragma unroll
     for (int i = 0; i < OpA::NI; ++i)
       glds16(a.src(kt, i), buf + (wave * OpA::NI + i) * 1024);
@@ -383,7 +435,7 @@ struct MainLoop {
       glds16(b.src(kt, i), buf + A_BYTES + (wave * OpB::NI + i) * 1024);
   }
 
-  __device__ static void run(char* smem, const OpA& a, const OpB& b, int kt0, int kt1,
+  __device__ static void run(char* smem, OpA& a, OpB& b, int kt0, int kt1,
                              f32x4 (&acc)[MT][NT], int wave, int lane) {
 #pragma unroll
     for (int i = 0; i < MT; ++i)
