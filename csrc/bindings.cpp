@@ -177,6 +177,7 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
   s.Co = (int)dy.size(3); s.KH = kh; s.KW = kw; s.stride = stride; s.pad = pad;
   s.Ho = (s.H + 2 * pad - kh) / stride + 1;
   s.Wo = (s.W + 2 * pad - kw) / stride + 1;
+  TORCH_CHECK(x.numel() < (1ll << 31), "conv wgrad input too large for 32-bit gather offsets");
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo, "dy/x mismatch");
   TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv wgrad needs Ci, Co % 8 == 0");
   Tensor dw;

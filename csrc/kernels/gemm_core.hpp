@@ -369,17 +369,19 @@ struct MCIm2colT {
       kw[i] = (int)(tap - a * (uint32_t)g.KW);
     }
   }
+  // branch-free, 32-bit offsets (host checks numel < 2^31); the zero page via select
   __device__ const void* src(int kt, int i) const {
-    uint32_t k = (uint32_t)kt * BK + krow[i];
-    if (!colok[i] || k >= K) return zero;
-    uint32_t img = fdiv(g.fHoWo, k);
-    uint32_t rem = k - img * (uint32_t)(g.Ho * g.Wo);
-    uint32_t ho = fdiv(g.fWo, rem);
-    uint32_t wo = rem - ho * (uint32_t)g.Wo;
-    int hi = (int)ho * g.stride - g.pad + kh[i];
-    int wi = (int)wo * g.stride - g.pad + kw[i];
-    if ((unsigned)hi >= (unsigned)g.H || (unsigned)wi >= (unsigned)g.W) return zero;
-    return x + (((long)img * g.H + hi) * g.W + wi) * g.C + ci[i];
+    const uint32_t k = (uint32_t)kt * BK + krow[i];
+    const uint32_t img = fdiv(g.fHoWo, k);
+    const uint32_t rem = k - img * (uint32_t)(g.Ho * g.Wo);
+    const uint32_t ho = fdiv(g.fWo, rem);
+    const uint32_t wo = rem - ho * (uint32_t)g.Wo;
+    const int hi = (int)ho * g.stride - g.pad + kh[i];
+    const int wi = (int)wo * g.stride - g.pad + kw[i];
+    const bool ok = colok[i] & (k < K) & ((unsigned)hi < (unsigned)g.H) &
+                    ((unsigned)wi < (unsigned)g.W);
+    const int off = (((int)img * g.H + hi) * g.W + wi) * g.C + ci[i];
+    return ok ? (const void*)(x + off) : zero;
   }
 };
 
@@ -453,21 +455,26 @@ struct MainLoop {
       if (kt + 1 < kt1) stage(smem + (cur ^ 1) * STAGE_BYTES, a, b, kt + 1, wave);
       const char* aimg = cbuf;
       const char* bimg = cbuf + A_BYTES;
+      // both k-substeps' fragments are requested up front, so the second substep's LDS reads
+      // are in flight under the first substep's MFMAs (only a counted lgkmcnt before each)
+      bf16x8 af[2][MT], bfr[2][NT];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 af[MT], bfr[NT];
 #pragma unroll
         for (int i = 0; i < MT; ++i)
-          af[i] = FragLoader<OpA::KC, BM>::load(aimg, arow0 + i * 16, ks, lane);
+          af[ks][i] = FragLoader<OpA::KC, BM>::load(aimg, arow0 + i * 16, ks, lane);
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          bfr[j] = FragLoader<OpB::KC, BN>::load(bimg, bcol0 + j * 16, ks, lane);
+          bfr[ks][j] = FragLoader<OpB::KC, BN>::load(bimg, bcol0 + j * 16, ks, lane);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
           for (int j = 0; j < NT; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-      }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ks][j], af[ks][i], acc[i][j],
+                                                                0, 0, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       cur ^= 1;
