@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--bucket-cap-mb", type=float, default=32.0)
     ap.add_argument("--impl", default="mipipe", choices=["mipipe", "stock"],
                     help="stock = torch DDP + MIOpen comparator")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="replay the whole training step from a captured hipGraph (single GPU, "
+                         "SGD); auto = on when safe")
     return ap.parse_args()
 
 
@@ -113,7 +116,8 @@ def main() -> int:
             "config": {"model": a.model, "global_batch": a.batch * world,
                        "seq_len": a.seq if is_bert else None,
                        "image_size": None if is_bert else a.res, "batch_per_gpu": a.batch,
-                       "parallelism": f"dp{world}", "impl": a.impl, "optimizer": opt_s},
+                       "parallelism": f"dp{world}", "impl": a.impl, "optimizer": opt_s,
+                       "hip_graph": bool(getattr(a, "graph_used", False))},
             "final_loss": loss_v}), flush=True)
     if world > 1:
         dist.barrier()
@@ -194,6 +198,21 @@ def build_cnn(a, world, local, dev, rank):
             loss.backward()
             opt.step()
             return loss
+
+        from mipipe.train.graph import GraphedStep, graph_safe
+        ok, why = graph_safe(model, opt)
+        if a.graph == "on" or (a.graph == "auto" and world == 1 and ok):
+            if world > 1 or not ok:
+                raise SystemExit(f"--graph on is not possible here: {why or 'multi-GPU DDP'}")
+            model.train()
+            # one captured step per resident synthetic batch: replays issue every kernel of the
+            # step (fwd, bwd, SGD) from one launch; no batch copies
+            gs = GraphedStep(step, batches[0], warmup=max(2, a.warmup), inputs=batches)
+            a.graph_used = True
+            ids = {id(b[0]): k for k, b in enumerate(batches)}
+
+            def step(x, y):  # noqa: F811
+                return gs.replay(ids[id(x)])
     else:
         from mipipe.models.reference import ref_resnet
         model = ref_resnet(a.model, num_classes=a.classes).to(dev).to(memory_format=torch.channels_last)

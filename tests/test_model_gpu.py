@@ -124,3 +124,37 @@ def test_vgg_alexnet_gpu(arch, res):
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < losses[0], losses
+
+
+def test_graphed_step_matches_eager():
+    """A captured hipGraph step replays the same training math as eager steps."""
+    from mipipe.train.graph import GraphedStep, graph_safe
+    torch.manual_seed(0)
+    a = create_model("resnet18", num_classes=10).cuda()
+    b = copy.deepcopy(a)
+    oa = SGD(a.parameters(), 0.05, momentum=0.9, weight_decay=1e-4)
+    ob = SGD(b.parameters(), 0.05, momentum=0.9, weight_decay=1e-4)
+    assert graph_safe(b, ob)[0]
+    x = torch.randn(32, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+
+    def step_b(xx, yy):
+        ob.zero_grad()
+        loss = cross_entropy(b(xx), yy)
+        loss.backward()
+        ob.step()
+        return loss
+
+    la = []
+    for _ in range(4):
+        oa.zero_grad()
+        loss = cross_entropy(a(x), y)
+        loss.backward()
+        oa.step()
+        la.append(loss.item())
+    gs = GraphedStep(step_b, (x, y), warmup=1, inputs=[(x, y)])  # 1 eager step
+    lb = [gs.replay(0).item() for _ in range(3)]
+    torch.cuda.synchronize()
+    assert abs(la[-1] - lb[-1]) < 0.05 * abs(la[-1]) + 1e-3, (la, lb)
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        assert cos(p, q) > 0.999, n
