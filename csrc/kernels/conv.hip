@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256, NS == 1 ? 3 : 2) void conv_fwd_kernel(
   KCDense<BN> b;
   b.init(w, K, e.N, K, n0, wave, lane, g_conv_zero);
   f32x4 acc[BM / 32][BN / 32];
-  MainLoop<BM, BN, OpA, KCDense<BN>>::run(smem, a, b, 0, nk, acc, wave, lane);
+  MainLoop<BM, BN, OpA, KCDense<BN>, NS>::run(smem, a, b, 0, nk, acc, wave, lane);
   epilogue_bf16<BM, BN>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256, NS == 1 ? 3 : 2) void conv_dgrad_kernel(
     b.init(w, (uint32_t)Co, (uint32_t)taps, Ci, fCo, cls, n0, wave, lane, g_conv_zero);
   }
   f32x4 acc[BM / 32][BN / 32];
-  MainLoop<BM, BN, OpA, OpB>::run(smem, a, b, 0, nk, acc, wave, lane);
+  MainLoop<BM, BN, OpA, OpB, NS>::run(smem, a, b, 0, nk, acc, wave, lane);
   epilogue_bf16<BM, BN, true>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
@@ -157,7 +157,7 @@ void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq
     else MIPIPE_LAUNCH((conv_fwd_kernel<128, 64, false>), dim3(tiles), xp, wp, g, M, tN, e);
   } else {
     uint32_t tN = cdiv(s.Co, 128), tiles = cdiv(M, 128) * tN;
-    if (dense && s.Ci <= BK) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, true, 1>), dim3(tiles), xp, wp, g, M, tN, e);
+    if (dense && s.Ci <= g_ns1_max_k) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, true, 1>), dim3(tiles), xp, wp, g, M, tN, e);
     else if (dense) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, true>), dim3(tiles), xp, wp, g, M, tN, e);
     else if (s.Ci % BK == 0) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, false, 2, true>), dim3(tiles), xp, wp, g, M, tN, e);
     else MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, false>), dim3(tiles), xp, wp, g, M, tN, e);
@@ -213,7 +213,7 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
         else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 64, false>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
       } else {
         uint32_t tN = cdiv(s.Ci, 128), tiles = cdiv(M, 128) * tN;
-        if (dense && s.Co <= BK) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true, 1>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
+        if (dense && s.Co <= g_ns1_max_k) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true, 1>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else if (s.Co % BK == 0) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, false, 2, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, false>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);

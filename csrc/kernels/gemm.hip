@@ -6,6 +6,7 @@
 
 namespace mipipe {
 int g_splitk_target = 512;
+int g_ns1_max_k = 512;  // measured: tools/sweep_ns1.py (profiles/r1_ns1_sweep.jsonl)
 namespace gk {
 
 __device__ __attribute__((aligned(64))) uint4 g_gemm_zero[8];

@@ -417,7 +417,10 @@ struct FragLoader<false, W> {  // MC image: 2 x ds_read_b64_tr_b16
 
 // ---------------------------------------------------------------------------------------------
 // Main loop.  Returns accumulators acc[MT][NT] (swapped orientation: lane holds C[m][n..n+3]).
-template <int BM, int BN, class OpA, class OpB>
+// NS = LDS stages.  2: double-buffered (next k-step's glds in flight under this one's MFMAs).
+// 1: single buffer, k-steps strictly serial inside the block — half the LDS, so more blocks fit
+// per CU and the overlap comes from neighbouring blocks (short-K, memory-bound GEMMs).
+template <int BM, int BN, class OpA, class OpB, int NS = 2>
 struct MainLoop {
   static constexpr int MT = BM / 32;  // 16-row tiles per wave (wave tile BM/2)
   static constexpr int NT = BN / 32;
@@ -451,8 +454,13 @@ struct MainLoop {
     __syncthreads();
     int cur = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
+      if (NS == 1 && kt > kt0) {  // serial: refill the single buffer (all waves done with it)
+        stage(smem, a, b, kt, wave);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
       char* cbuf = smem + cur * STAGE_BYTES;
-      if (kt + 1 < kt1) stage(smem + (cur ^ 1) * STAGE_BYTES, a, b, kt + 1, wave);
+      if (NS == 2 && kt + 1 < kt1) stage(smem + (cur ^ 1) * STAGE_BYTES, a, b, kt + 1, wave);
       const char* aimg = cbuf;
       const char* bimg = cbuf + A_BYTES;
       // both k-substeps' fragments are requested up front, so the second substep's LDS reads
@@ -475,9 +483,13 @@ struct MainLoop {
           for (int j = 0; j < NT; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ks][j], af[ks][i], acc[i][j],
                                                                 0, 0, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      cur ^= 1;
+      if (NS == 2) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        cur ^= 1;
+      } else if (kt + 1 < kt1) {
+        __syncthreads();
+      }
     }
   }
 };

@@ -21,6 +21,8 @@ constexpr int kStatReplicas = 16;
 // Split-K sizing for the atomically-accumulated weight-gradient GEMMs: splits are chosen so
 // that tiles * splits ~= this many workgroups (tunable at runtime for sweeps).
 extern int g_splitk_target;
+// Dense (1x1) conv fwd/dgrad with reduction K <= this use the single-LDS-stage kernels.
+extern int g_ns1_max_k;
 int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 // bias / relu: optional per-channel bias and ReLU in the epilogue (convs without BN: VGG, AlexNet)
