@@ -159,6 +159,7 @@ void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq
     uint32_t tN = cdiv(s.Co, 128), tiles = cdiv(M, 128) * tN;
     if (dense && s.Ci <= g_ns1_max_k) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, true, 1>), dim3(tiles), xp, wp, g, M, tN, e);
     else if (dense) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, true>), dim3(tiles), xp, wp, g, M, tN, e);
+    else if (s.Ci % BK == 0 && (long)s.KH * s.KW * s.Ci <= g_ns1_max_k_gather) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, false, 1, true>), dim3(tiles), xp, wp, g, M, tN, e);
     else if (s.Ci % BK == 0) MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, false, 2, true>), dim3(tiles), xp, wp, g, M, tN, e);
     else MIPIPE_LAUNCH((conv_fwd_kernel<128, 128, false>), dim3(tiles), xp, wp, g, M, tN, e);
   }
@@ -215,6 +216,7 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
         uint32_t tN = cdiv(s.Ci, 128), tiles = cdiv(M, 128) * tN;
         if (dense && s.Co <= g_ns1_max_k) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true, 1>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else if (dense) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
+        else if (s.Co % BK == 0 && (long)c.ntaps * s.Co <= g_ns1_max_k_gather) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, false, 1, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else if (s.Co % BK == 0) MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, false, 2, true>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else MIPIPE_LAUNCH((conv_dgrad_kernel<128, 128, false>), dim3(tiles), dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
       }

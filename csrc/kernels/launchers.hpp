@@ -23,6 +23,7 @@ constexpr int kStatReplicas = 16;
 extern int g_splitk_target;
 // Dense (1x1) conv fwd/dgrad with reduction K <= this use the single-LDS-stage kernels.
 extern int g_ns1_max_k;
+extern int g_ns1_max_k_gather;  // same for the gathered (im2col / strided dgrad) convs
 int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 // bias / relu: optional per-channel bias and ReLU in the epilogue (convs without BN: VGG, AlexNet)
