@@ -127,34 +127,33 @@ def test_vgg_alexnet_gpu(arch, res):
 
 
 def test_graphed_step_matches_eager():
-    """A captured hipGraph step replays the same training math as eager steps."""
+    """A captured hipGraph step replays the same training math as eager steps (compared with
+    the run-to-run noise of two eager runs: fp32 atomics make bf16 training nondeterministic)."""
     from mipipe.train.graph import GraphedStep, graph_safe
     torch.manual_seed(0)
     a = create_model("resnet18", num_classes=10).cuda()
     b = copy.deepcopy(a)
-    oa = SGD(a.parameters(), 0.05, momentum=0.9, weight_decay=1e-4)
-    ob = SGD(b.parameters(), 0.05, momentum=0.9, weight_decay=1e-4)
-    assert graph_safe(b, ob)[0]
+    c = copy.deepcopy(a)
+    opts = [SGD(m.parameters(), 0.05, momentum=0.9, weight_decay=1e-4) for m in (a, b, c)]
+    assert graph_safe(b, opts[1])[0]
     x = torch.randn(32, 3, 32, 32, device="cuda")
     y = torch.randint(0, 10, (32,), device="cuda")
 
-    def step_b(xx, yy):
-        ob.zero_grad()
-        loss = cross_entropy(b(xx), yy)
-        loss.backward()
-        ob.step()
-        return loss
+    def make_step(m, o):
+        def step(xx, yy):
+            o.zero_grad()
+            loss = cross_entropy(m(xx), yy)
+            loss.backward()
+            o.step()
+            return loss
+        return step
 
-    la = []
-    for _ in range(4):
-        oa.zero_grad()
-        loss = cross_entropy(a(x), y)
-        loss.backward()
-        oa.step()
-        la.append(loss.item())
-    gs = GraphedStep(step_b, (x, y), warmup=1, inputs=[(x, y)])  # 1 eager step
+    la = [make_step(a, opts[0])(x, y).item() for _ in range(4)]
+    lc = [make_step(c, opts[2])(x, y).item() for _ in range(4)]
+    gs = GraphedStep(make_step(b, opts[1]), (x, y), warmup=1, inputs=[(x, y)])  # 1 eager step
     lb = [gs.replay(0).item() for _ in range(3)]
     torch.cuda.synchronize()
-    assert abs(la[-1] - lb[-1]) < 0.05 * abs(la[-1]) + 1e-3, (la, lb)
-    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
-        assert cos(p, q) > (0.999 if p.dim() > 1 else 0.99), n  # bf16 + fp32-atomic noise
+    assert abs(la[-1] - lb[-1]) < 0.05 * abs(la[-1]) + 1e-3, (la, lb, lc)
+    for (n, p), (_, q), (_, r) in zip(a.named_parameters(), b.named_parameters(),
+                                      c.named_parameters()):
+        assert cos(p, q) > min(0.999, cos(p, r) - 0.01), (n, cos(p, q), cos(p, r))
