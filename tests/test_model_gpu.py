@@ -153,7 +153,7 @@ def test_graphed_step_matches_eager():
     gs = GraphedStep(make_step(b, opts[1]), (x, y), warmup=1, inputs=[(x, y)])  # 1 eager step
     lb = [gs.replay(0).item() for _ in range(3)]
     torch.cuda.synchronize()
-    assert abs(la[-1] - lb[-1]) < 0.05 * abs(la[-1]) + 1e-3, (la, lb, lc)
+    assert abs(la[-1] - lb[-1]) < 3 * abs(la[-1] - lc[-1]) + 0.02 * abs(la[0]), (la, lb, lc)
     for (n, p), (_, q), (_, r) in zip(a.named_parameters(), b.named_parameters(),
                                       c.named_parameters()):
         assert cos(p, q) > min(0.999, cos(p, r) - 0.01), (n, cos(p, q), cos(p, r))
