@@ -40,7 +40,8 @@ float* fptr(const optional<Tensor>& t, int64_t n) {
   return t->data_ptr<float>();
 }
 
-mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int pad) {
+mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int pad,
+                             int stride_w = 0) {
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv expects NHWC x and [Co,KH,KW,Ci] w");
   mipipe::ConvShape s;
   s.N = (int)x.size(0); s.H = (int)x.size(1); s.W = (int)x.size(2); s.Ci = (int)x.size(3);
@@ -48,8 +49,10 @@ mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int p
   TORCH_CHECK(w.size(3) == s.Ci, "weight Ci ", w.size(3), " != input channels ", s.Ci);
   TORCH_CHECK(stride >= 1 && pad >= 0, "bad stride/pad");
   s.stride = stride; s.pad = pad;
+  s.stride_w = stride_w > 0 ? stride_w : 0;
+  const int sw = stride_w > 0 ? stride_w : stride;
   s.Ho = (s.H + 2 * pad - s.KH) / stride + 1;
-  s.Wo = (s.W + 2 * pad - s.KW) / stride + 1;
+  s.Wo = (s.W + 2 * pad - s.KW) / sw + 1;
   TORCH_CHECK(s.Ho > 0 && s.Wo > 0, "empty conv output");
   TORCH_CHECK(s.Ci % 8 == 0, "conv kernels need Ci % 8 == 0 (pad channels), got ", s.Ci);
   TORCH_CHECK(x.numel() < (1ll << 31), "conv input too large for 32-bit gather offsets");
@@ -65,11 +68,12 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
                                                                 int pad, optional<Tensor> shift,
                                                                 optional<Tensor> slab_sum,
                                                                 optional<Tensor> slab_sq,
-                                                                optional<Tensor> bias, bool relu) {
+                                                                optional<Tensor> bias, bool relu,
+                                                                int stride_w) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   c10::DeviceGuard g(x.device());
-  auto s = conv_shape(x, w, stride, pad);
+  auto s = conv_shape(x, w, stride, pad, stride_w);
   if (bias.has_value()) check_vec(*bias, s.Co, "bias");
   TORCH_CHECK(!(shift.has_value() && (bias.has_value() || relu)),
               "BN-statistics epilogue and bias/ReLU epilogue are exclusive");
@@ -168,15 +172,17 @@ std::tuple<Tensor, Tensor> bn_bwd_collect(Tensor rep, int64_t C, optional<Tensor
   return {sg, sgx};
 }
 
-Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, optional<Tensor> out) {
+Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, optional<Tensor> out,
+                  int stride_w) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   c10::DeviceGuard g(dy.device());
   mipipe::ConvShape s;
   s.N = (int)x.size(0); s.H = (int)x.size(1); s.W = (int)x.size(2); s.Ci = (int)x.size(3);
   s.Co = (int)dy.size(3); s.KH = kh; s.KW = kw; s.stride = stride; s.pad = pad;
+  s.stride_w = stride_w > 0 ? stride_w : 0;
   s.Ho = (s.H + 2 * pad - kh) / stride + 1;
-  s.Wo = (s.W + 2 * pad - kw) / stride + 1;
+  s.Wo = (s.W + 2 * pad - kw) / (stride_w > 0 ? stride_w : stride) + 1;
   TORCH_CHECK(x.numel() < (1ll << 31), "conv wgrad input too large for 32-bit gather offsets");
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo, "dy/x mismatch");
   TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv wgrad needs Ci, Co % 8 == 0");
@@ -618,6 +624,18 @@ Tensor colsum(Tensor x, optional<Tensor> out) {
   return o;
 }
 
+Tensor stem_pack(Tensor x, int64_t pad, int64_t Hp, int64_t Wsp) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.dim() == 4 && x.size(1) <= 4, "stem_pack expects NCHW with C <= 4");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x dtype");
+  auto y = torch::empty({x.size(0), Hp, Wsp, 8}, x.options().dtype(at::kBFloat16));
+  mipipe::stem_pack(x.data_ptr(), x.scalar_type() == at::kBFloat16, y.data_ptr(), (int)x.size(0),
+                    (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)pad, (int)Hp, (int)Wsp,
+                    stream());
+  return y;
+}
+
 void check_attn(const Tensor& qkv, int64_t B, int64_t S, int64_t H) {
   check_bf16(qkv, "qkv");
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B * S && qkv.size(1) == 3 * H * 64,
@@ -683,7 +701,8 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "mipipe gfx950 (MI355X) HIP kernels";
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("shift") = py::none(), py::arg("slab_sum") = py::none(),
-        py::arg("slab_sq") = py::none(), py::arg("bias") = py::none(), py::arg("relu") = false);
+        py::arg("slab_sq") = py::none(), py::arg("bias") = py::none(), py::arg("relu") = false,
+        py::arg("stride_w") = 0);
   m.attr("STAT_REPLICAS") = mipipe::kStatReplicas;
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("x_shape"),
         py::arg("stride"), py::arg("pad"), py::arg("addend") = py::none(),
@@ -694,7 +713,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_collect", &bn_bwd_collect, py::arg("rep"), py::arg("C"),
         py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
-        py::arg("stride"), py::arg("pad"), py::arg("out") = py::none());
+        py::arg("stride"), py::arg("pad"), py::arg("out") = py::none(), py::arg("stride_w") = 0);
   m.def("bn_finalize", &bn_finalize, py::arg("psum"), py::arg("psq"), py::arg("count"),
         py::arg("shift"), py::arg("gamma"), py::arg("beta"), py::arg("rm"), py::arg("rv"),
         py::arg("momentum"), py::arg("eps"), py::arg("zero_after") = true);
@@ -730,6 +749,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("mask") = py::none(),
         py::arg("scale") = 0.125, py::arg("p_drop") = 0.0, py::arg("seed") = 0);
   m.def("dropout_fwd", &dropout_fwd);
+  m.def("stem_pack", &stem_pack);
   m.def("set_splitk_target", [](int v) { mipipe::g_splitk_target = std::max(1, v); });
   m.def("get_splitk_target", []() { return mipipe::g_splitk_target; });
   m.def("set_ns1_max_k", [](int v) { mipipe::g_ns1_max_k = v; });

@@ -115,8 +115,9 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const __bf16* __rest
 using namespace gk;
 
 static ConvGeom make_geom(int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int stride,
-                          int pad) {
+                          int pad, int stride_w = 0) {
   ConvGeom g;
+  g.stride_w = stride_w > 0 ? stride_w : stride;
   g.N = N; g.H = H; g.W = W; g.C = C; g.Ho = Ho; g.Wo = Wo;
   g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
   g.fHoWo = FastDiv((uint32_t)(Ho * Wo));
@@ -129,7 +130,8 @@ static ConvGeom make_geom(int N, int H, int W, int C, int Ho, int Wo, int KH, in
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 static bool is_dense(const ConvShape& s) {
-  return s.KH == 1 && s.KW == 1 && s.stride == 1 && s.pad == 0;
+  return s.KH == 1 && s.KW == 1 && s.stride == 1 && s.pad == 0 &&
+         (s.stride_w == 0 || s.stride_w == 1);
 }
 
 int conv_fwd_stat_rows(const ConvShape& s) {
@@ -142,7 +144,7 @@ int conv_fwd_stat_rows(const ConvShape& s) {
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
               const float* st_shift, const ConvShape& s, hipStream_t st, const float* bias,
               bool relu) {
-  ConvGeom g = make_geom(s.N, s.H, s.W, s.Ci, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad);
+  ConvGeom g = make_geom(s.N, s.H, s.W, s.Ci, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad, s.stride_w);
   uint32_t M = (uint32_t)s.N * s.Ho * s.Wo;
   EpiParams e{};
   e.C = y; e.ldc = s.Co; e.M = M; e.N = s.Co; e.bias = bias; e.act = relu ? 1 : 0;
@@ -234,7 +236,7 @@ static int pick_splits(uint32_t tiles, int nk, int Ci) {
 }
 
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st) {
-  ConvGeom g = make_geom(s.N, s.H, s.W, s.Ci, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad);
+  ConvGeom g = make_geom(s.N, s.H, s.W, s.Ci, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad, s.stride_w);
   uint32_t Ntot = (uint32_t)(s.KH * s.KW * s.Ci);
   EpiParams e{};
   e.C = dw; e.ldc = Ntot; e.M = s.Co; e.N = Ntot;

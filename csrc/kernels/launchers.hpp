@@ -12,6 +12,7 @@ struct ConvShape {
   int N, H, W, Ci;   // input
   int Co, KH, KW, stride, pad;
   int Ho, Wo;        // output
+  int stride_w = 0;  // horizontal stride when != stride (0: same); fwd / wgrad only
 };
 
 // BatchNorm statistics are accumulated with fp32 atomics into kStatReplicas replica rows of a
@@ -103,6 +104,12 @@ void adamw_step(float* p, const float* g, float* m, float* v, void* shadow, long
                 hipStream_t st);
 void nchw_to_nhwc(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int Cp,
                   hipStream_t st);
+// Stem "super-pixel" packing (C <= 4): y[n][h'][j][p*4 + c] = x[n][c][h'-pad][2j+p-pad] (zero
+// outside), h' < Hp, j < Wsp.  A KxK stride-2 conv on x becomes a K x ceil(K/2) conv with
+// vertical stride 2 and horizontal stride 1 on 8-channel super-pixels: 16-byte operand rows with
+// 3 of 8 lanes padding instead of 5 of 8 (the reduction shrinks from K*K*8 to K*ceil(K/2)*8).
+void stem_pack(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int pad,
+               int Hp, int Wsp, hipStream_t st);
 void synthetic_batch(const int64_t* idx, int n, int C, int H, int W, int classes, int seed,
                      void* x, bool bf16_out, int64_t* labels, hipStream_t st);
 

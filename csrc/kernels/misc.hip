@@ -584,4 +584,49 @@ void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStre
                      (__bf16*)y, n8, 1.f / (1.f - p), thr, seed);
 }
 
+// ------------------------------------------------------------------------------ stem packing
+// One thread per output 16-byte super-pixel: 2 horizontally adjacent padded pixels x 4 channels.
+template <bool IN_BF16>
+__global__ __launch_bounds__(256) void stem_pack_kernel(const void* __restrict__ xin,
+                                                        __bf16* __restrict__ y, int N, int C,
+                                                        int H, int W, int pad, int Hp, int Wsp) {
+  const long total = (long)N * Hp * Wsp;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(t % Wsp);
+    const long r = t / Wsp;
+    const int hp = (int)(r % Hp);
+    const int n = (int)(r / Hp);
+    const int h = hp - pad;
+    float v[8];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int w = 2 * j + p - pad;
+      const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float x = 0.f;
+        if (in && c < C) {
+          const long idx = (((long)n * C + c) * H + h) * W + w;
+          x = IN_BF16 ? (float)reinterpret_cast<const __bf16*>(xin)[idx]
+                      : reinterpret_cast<const float*>(xin)[idx];
+        }
+        v[p * 4 + c] = x;
+      }
+    }
+    reinterpret_cast<uint4*>(y)[t] = pack8(v);
+  }
+}
+
+void stem_pack(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int pad,
+               int Hp, int Wsp, hipStream_t st) {
+  const long total = (long)N * Hp * Wsp;
+  if (x_is_bf16)
+    hipLaunchKernelGGL(stem_pack_kernel<true>, dim3(grid1d(total)), dim3(256), 0, st, x,
+                       (__bf16*)y, N, C, H, W, pad, Hp, Wsp);
+  else
+    hipLaunchKernelGGL(stem_pack_kernel<false>, dim3(grid1d(total)), dim3(256), 0, st, x,
+                       (__bf16*)y, N, C, H, W, pad, Hp, Wsp);
+}
+
 }  // namespace mipipe

@@ -89,9 +89,63 @@ class Bottleneck(tnn.Module):
 
 
 class _StemConv(mnn.Conv2d):
-    """7x7/2 stem: input channels zero-padded 3 -> 8 so every 16-byte operand load is one tap."""
+    """7x7/2, pad 3 stem on 3-channel images, run as a "super-pixel" convolution: the image is
+    packed (``stem_pack``) into 8-channel super-pixels of 2 horizontally adjacent padded pixels x
+    4 channels, and the filter into [Co, 7, 4, 8]; the conv then has vertical stride 2,
+    horizontal stride 1 and no padding, with K = 7*4*8 = 224 instead of the 7*7*8 = 392 a
+    channel-padded NHWC stem needs (1.75x fewer MFMA operations, every 16-byte load one tap).
+    Parameter layout/state stay torchvision's [64, 3, 7, 7]."""
 
     CIN_PAD = 8
+
+    def packed_geometry(self, H: int, W: int):
+        k, s, p = self.kernel_size[0], self.stride[0], self.padding[0]
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        return Ho, Wo, s * (Ho - 1) + k, Wo + (k + 1) // 2 - 1
+
+    def packable(self) -> bool:
+        return (self.in_channels <= 4 and self.kernel_size[0] == self.kernel_size[1]
+                and self.stride[0] == 2 and self.stride[1] == 2)
+
+    def pack_input(self, x: torch.Tensor, dtype) -> torch.Tensor:
+        _, _, Hp, Wsp = self.packed_geometry(x.shape[2], x.shape[3])
+        return K.stem_pack(x, dtype, self.padding[0], Hp, Wsp)
+
+    def compute_weight(self, dtype):
+        w = self.weight.detach()
+        Co, C, k, _ = w.shape
+        kw2 = (k + 1) // 2
+        wp = w.new_zeros(Co, k, 2 * kw2, 4)            # [co, kh, kw(padded), c(padded)]
+        wp[:, :, :k, :C] = w.permute(0, 2, 3, 1)
+        # super-tap j holds kw = 2j + p at channels p*4 + c
+        return wp.reshape(Co, k, kw2, 8).to(dtype).contiguous()
+
+    def forward(self, x, stats_shift=None, slabs=None, prev=None, res_take=None, res_give=None):
+        """x: packed super-pixels from :meth:`pack_input`."""
+        w_c = self.compute_weight(x.dtype)
+        if getattr(self.weight, "_mipipe_wgrad_map", None) is None:
+            k, C = self.kernel_size[0], self.in_channels
+
+            def unpack(dw, k=k, C=C):  # [Co, k, k2, 8] (kernel layout) -> [Co, C, k, k]
+                Co = dw.shape[0]
+                d = dw.reshape(Co, k, -1, 4)[:, :, :k, :C]
+                return d.permute(0, 3, 1, 2).contiguous()
+            self.weight._mipipe_wgrad_map = unpack
+        y, ps, pss = MF.conv2d(x, self.weight, w_c, (self.stride[0], 1), 0, stats_shift, slabs,
+                               prev, res_take, res_give)
+        return y if stats_shift is None else (y, ps, pss)
+
+
+class _PaddedStemConv(mnn.Conv2d):
+    """Generic stem for > 4 input channels: channels zero-padded to a multiple of 8."""
+
+    CIN_PAD = 8
+
+    def packable(self) -> bool:
+        return False
+
+    def pack_input(self, x: torch.Tensor, dtype) -> torch.Tensor:
+        return K.nchw_to_nhwc(x, dtype, self.CIN_PAD)
 
     def compute_weight(self, dtype):
         w = self.weight.detach().permute(0, 2, 3, 1)
@@ -111,7 +165,8 @@ class ResNet(tnn.Module):
         self.base_width = width_per_group
         self.in_chans = in_chans
         self.compute_dtype = compute_dtype
-        self.conv1 = _StemConv(in_chans, 64, 7, stride=2, padding=3, bias=False)
+        stem_cls = _StemConv if in_chans <= 4 else _PaddedStemConv
+        self.conv1 = stem_cls(in_chans, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = mnn.BatchNorm2d(64)
         self.relu = mnn.ReLU(inplace=True)
         self.maxpool = mnn.MaxPool2d(kernel_size=3, stride=2, padding=1)
@@ -152,7 +207,7 @@ class ResNet(tnn.Module):
 
     def forward_features(self, x: torch.Tensor) -> torch.Tensor:
         """NCHW float input -> NHWC features of layer4."""
-        x = K.nchw_to_nhwc(x, self.activation_dtype(x), _StemConv.CIN_PAD)
+        x = self.conv1.pack_input(x, self.activation_dtype(x))
         x = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
         x = self.maxpool(x)
         x = self.layer1(x)

@@ -90,7 +90,9 @@ class _ConvFn(Function):
         ctx.set_materialize_grads(False)  # stats outputs never get gradients: no zero fills
         ctx.save_for_backward(x, w_c)
         ctx.weight = weight
-        ctx.conf = (stride, pad, weight.shape[2], weight.shape[3], weight.shape[1])
+        # kernel-layout weight dims (the packed stem differs from the parameter's)
+        ctx.conf = (stride, pad, w_c.shape[1], w_c.shape[2], weight.shape[1])
+        ctx.wmap = getattr(weight, "_mipipe_wgrad_map", None)
         ctx.prev, ctx.res_take, ctx.res_give = prev, res_take, res_give
         if psum is not None:
             ctx.mark_non_differentiable(psum, psumsq)
@@ -105,6 +107,8 @@ class _ConvFn(Function):
         dy = dy.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[0]:
+            if not isinstance(stride, int):
+                raise NotImplementedError("dgrad of a non-square-stride conv")
             addend = ctx.res_take.take() if ctx.res_take is not None else None
             bnr = None
             tok = ctx.prev
@@ -123,7 +127,8 @@ class _ConvFn(Function):
                 dx = ctx.res_give.produce(dx)
         if ctx.needs_input_grad[1]:
             weight = ctx.weight
-            tgt = _direct_grad_target(weight) if x.shape[-1] == ci and K.use_native(dy) else None
+            tgt = (_direct_grad_target(weight)
+                   if x.shape[-1] == ci and ctx.wmap is None and K.use_native(dy) else None)
             if tgt is not None:
                 # gradient accumulates straight into the flat DDP bucket: no zero-fill, no
                 # autograd AccumulateGrad add; tell the reducer the gradient is ready.
@@ -132,9 +137,12 @@ class _ConvFn(Function):
                 fs.grad_ready(weight)
             else:
                 dw = K.conv_wgrad(dy, x, kh, kw, stride, pad)
-                if dw.shape[-1] != ci:  # input channels were zero-padded for the kernel
-                    dw = dw[..., :ci]
-                dw = dw.permute(0, 3, 1, 2)
+                if ctx.wmap is not None:  # kernel layout -> parameter layout (packed stem)
+                    dw = ctx.wmap(dw)
+                else:
+                    if dw.shape[-1] != ci:  # input channels were zero-padded for the kernel
+                        dw = dw[..., :ci]
+                    dw = dw.permute(0, 3, 1, 2)
         return dx, dw, None, None, None, None, None, None, None, None
 
 

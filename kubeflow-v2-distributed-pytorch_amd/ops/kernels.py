@@ -18,7 +18,7 @@ from ._native import native, native_available
 __all__ = ["conv_fwd", "conv_dgrad", "conv_wgrad", "bn_finalize", "bn_act_fwd",
            "bn_act_bwd_reduce", "bn_act_bwd_apply", "maxpool_fwd", "maxpool_bwd",
            "avgpool_fwd", "avgpool_bwd", "gemm", "cross_entropy_fwd_bwd", "sgd_step",
-           "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd", "dropout_fwd", "colsum", "bn_bwd_collect",
+           "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd", "dropout_fwd", "colsum", "bn_bwd_collect", "stem_pack",
            "embedding_bwd", "gelu_fwd", "gelu_bwd", "nchw_to_nhwc", "use_native"]
 
 _ALLOW_REF_ON_GPU = os.environ.get("MIPIPE_ALLOW_REF_ON_GPU", "0") == "1"
@@ -41,10 +41,12 @@ def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None, bias=None, relu=Fa
     """``slabs``: persistent zeroed (sum, sumsq) replica slabs the GPU epilogue accumulates BN
     statistics into (re-zeroed by :func:`bn_finalize`).  ``bias`` / ``relu``: epilogue bias and
     ReLU for convolutions without BatchNorm (exclusive with the statistics epilogue)."""
+    sh, sw = (stride, 0) if isinstance(stride, int) else (stride[0], stride[1])
     if use_native(x):
         s1, s2 = slabs if slabs is not None else (None, None)
-        return native().conv_fwd(x, w, stride, pad, stats_shift, s1, s2, bias, relu)
-    y, a, b = _ref.conv_fwd(x, w, stride, pad, stats_shift)
+        return native().conv_fwd(x, w, sh, pad, stats_shift, s1, s2, bias, relu, sw)
+    y, a, b = _ref.conv_fwd(x, w, stride if isinstance(stride, int) else tuple(stride), pad,
+                            stats_shift)
     if bias is not None or relu:
         yf = _f(y) if bias is None else _f(y) + _f(bias)
         y = (torch.relu(yf) if relu else yf).to(x.dtype)
@@ -76,10 +78,12 @@ def bn_bwd_collect(rep, C, acc=None):
 
 
 def conv_wgrad(dy, x, kh, kw, stride, pad, out=None):
-    """``out``: accumulate into this fp32 [Co,KH,KW,Ci] buffer (the parameter's flat gradient)."""
+    """``out``: accumulate into this fp32 [Co,KH,KW,Ci] buffer (the parameter's flat gradient).
+    ``stride``: int or (vertical, horizontal)."""
+    sh, sw = (stride, 0) if isinstance(stride, int) else (stride[0], stride[1])
     if use_native(dy):
-        return native().conv_wgrad(dy, x, kh, kw, stride, pad, out)
-    dw = _ref.conv_wgrad(dy, x, kh, kw, stride, pad)
+        return native().conv_wgrad(dy, x, kh, kw, sh, pad, out, sw)
+    dw = _ref.conv_wgrad(dy, x, kh, kw, stride if isinstance(stride, int) else tuple(stride), pad)
     if out is not None:
         out.add_(dw)
         return out
@@ -293,6 +297,19 @@ def gelu_bwd(dy, x):
     if use_native(dy):
         return native().gelu_bwd(dy, x)
     return _ref.gelu_bwd(dy, x)
+
+
+def stem_pack(x, dtype, pad: int, Hp: int, Wsp: int):
+    """NCHW image (C <= 4) -> bf16/``dtype`` super-pixels [N, Hp, Wsp, 8]: channel p*4 + c of
+    super-pixel (h', j) is x[c, h'-pad, 2j+p-pad] (zero outside the image)."""
+    if use_native(x) and dtype == torch.bfloat16:
+        return native().stem_pack(x.contiguous(), pad, Hp, Wsp)
+    N, C, H, W = x.shape
+    P = x.new_zeros(N, 4, Hp, 2 * Wsp, dtype=torch.float64 if x.dtype == torch.float64 else torch.float32)
+    hh, ww = min(H, Hp - pad), min(W, 2 * Wsp - pad)
+    P[:, :C, pad:pad + hh, pad:pad + ww] = x[:, :, :hh, :ww].to(P.dtype)
+    y = P.reshape(N, 4, Hp, Wsp, 2).permute(0, 2, 3, 4, 1).reshape(N, Hp, Wsp, 8)
+    return y.contiguous().to(dtype)
 
 
 def nchw_to_nhwc(x, dtype, pad_channels_to: int = 0):

@@ -332,3 +332,33 @@ def test_conv_fwd_bias_relu_epilogue():
     ref, _, _ = _ref.conv_fwd(x.float(), w.float(), 1, 1)
     ref = torch.relu(ref + b)
     assert rel_err(y, ref) < 1e-2
+
+
+def test_stem_superpixel_conv_matches_direct():
+    """Packed stem (super-pixels, stride (2,1)) == 7x7/2 pad-3 conv on the image, fwd + wgrad."""
+    from mipipe.ops import kernels as Kx
+    from mipipe.models.resnet import _StemConv
+    N, H, W = 2, 38, 30
+    conv = _StemConv(3, 64, 7, stride=2, padding=3, bias=False).cuda()
+    x = torch.randn(N, 3, H, W, device=dev)
+    xp = conv.pack_input(x, torch.bfloat16)
+    Ho, Wo, Hp, Wsp = conv.packed_geometry(H, W)
+    assert xp.shape == (N, Hp, Wsp, 8)
+    xr = Kx.stem_pack(x.cpu(), torch.float32, 3, Hp, Wsp)
+    assert torch.equal(xp.float().cpu(), xr.to(torch.bfloat16).float())
+    wk = conv.compute_weight(torch.bfloat16)
+    y, _, _ = native().conv_fwd(xp, wk, 2, 0, None, None, None, None, False, 1)
+    ref = torch.nn.functional.conv2d(x.to(torch.bfloat16).float(),
+                                     conv.weight.detach().to(torch.bfloat16).float(), stride=2,
+                                     padding=3).permute(0, 2, 3, 1)
+    assert y.shape == (N, Ho, Wo, 64)
+    assert rel_err(y, ref) < 1e-2
+    dy = bf(N, Ho, Wo, 64)
+    dwk = native().conv_wgrad(dy, xp, 7, 4, 2, 0, None, 1)
+    dw = conv.weight._mipipe_wgrad_map(dwk) if hasattr(conv.weight, "_mipipe_wgrad_map") else None
+    if dw is None:  # map is installed on first forward
+        conv(xp)
+        dw = conv.weight._mipipe_wgrad_map(dwk)
+    dw_ref = torch.nn.grad.conv2d_weight(x.to(torch.bfloat16).float(), (64, 3, 7, 7),
+                                         dy.permute(0, 3, 1, 2).float(), stride=2, padding=3)
+    assert rel_err(dw, dw_ref) < 1e-2
