@@ -16,7 +16,7 @@ timeout -k 10 300 python bench.py --model bert_base --steps 10 --warmup 3 > gpur
 tail -1 gpurun_out/bench_bert.txt
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 > $R/gpurun_out/prof_bench.txt 2>&1 || exit $?
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 --graph off > $R/gpurun_out/prof_bench.txt 2>&1 || exit $?
   echo "prof ok"
   cd $R
 fi

@@ -15,5 +15,5 @@ if [ "${MICRO:-1}" = "1" ]; then
   tail -1 gpurun_out/microbench.jsonl
 fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 > $R/gpurun_out/prof_bench.txt 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 5 --warmup 2 --graph off > $R/gpurun_out/prof_bench.txt 2>&1 || exit $?
 echo "prof ok"
