@@ -204,7 +204,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(Tensor psum, Tensor psq, 
                                                        Tensor shift, Tensor gamma, Tensor beta,
                                                        optional<Tensor> rm, optional<Tensor> rv,
                                                        double momentum, double eps,
-                                                       bool zero_after) {
+                                                       bool zero_after, optional<Tensor> nbt) {
   check_f32(psum, "psum");
   check_f32(psq, "psumsq");
   c10::DeviceGuard g(psum.device());
@@ -217,15 +217,21 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(Tensor psum, Tensor psq, 
     check_vec(*rm, C, "running_mean");
     check_vec(*rv, C, "running_var");
   }
-  auto o = psum.options();
-  auto mean = torch::empty({C}, o), invstd = torch::empty({C}, o), scale = torch::empty({C}, o),
-       bias = torch::empty({C}, o);
+  long long* nbt_p = nullptr;
+  if (nbt.has_value()) {
+    TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->numel() == 1 && nbt->is_cuda(),
+                "num_batches_tracked: int64 scalar on the GPU");
+    nbt_p = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
+  }
+  auto st4 = torch::empty({4, C}, psum.options());  // one allocation: mean/invstd/scale/bias
+  auto mean = st4[0], invstd = st4[1], scale = st4[2], bias = st4[3];
   mipipe::bn_finalize(psum.data_ptr<float>(), psq.data_ptr<float>(), (int)P, (int)C, count,
                       shift.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
                       rm.has_value() ? rm->data_ptr<float>() : nullptr,
                       rv.has_value() ? rv->data_ptr<float>() : nullptr, (float)momentum,
                       (float)eps, mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                      scale.data_ptr<float>(), bias.data_ptr<float>(), zero_after, stream());
+                      scale.data_ptr<float>(), bias.data_ptr<float>(), zero_after, nbt_p,
+                      stream());
   return {mean, invstd, scale, bias};
 }
 
@@ -716,7 +722,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stride"), py::arg("pad"), py::arg("out") = py::none(), py::arg("stride_w") = 0);
   m.def("bn_finalize", &bn_finalize, py::arg("psum"), py::arg("psq"), py::arg("count"),
         py::arg("shift"), py::arg("gamma"), py::arg("beta"), py::arg("rm"), py::arg("rv"),
-        py::arg("momentum"), py::arg("eps"), py::arg("zero_after") = true);
+        py::arg("momentum"), py::arg("eps"), py::arg("zero_after") = true,
+        py::arg("nbt") = py::none());
   m.def("bn_act_fwd", &bn_act_fwd);
   m.def("bn_act_bwd_reduce", &bn_act_bwd_reduce, py::arg("dz"), py::arg("z"), py::arg("y"),
         py::arg("mean"), py::arg("invstd"), py::arg("relu"), py::arg("y2") = py::none(),

@@ -48,21 +48,48 @@ inline int grid_for_rows(long M, int rpb, int cap = 2048) {
 
 // Per-channel final reduction of a [P][C] slab pair (P = replica rows) + BN statistics.
 // With zero_after the slab is cleared for reuse (replica slabs are persistent and zeroed).
-__global__ void bn_finalize_kernel(float* __restrict__ s1, float* __restrict__ s2, int P, int C,
+// All P loads are issued before any store (one memory latency, not P), and the
+// num_batches_tracked increment rides along (no separate launch).
+template <int P>
+__global__ void bn_finalize_kernel(float* __restrict__ s1, float* __restrict__ s2, int Pdyn, int C,
                                    float inv_count, float unbias, const float* shift,
                                    const float* gamma, const float* beta, float* run_mean,
                                    float* run_var, float momentum, float eps, float* mean,
-                                   float* invstd, float* scale, float* bias, bool zero_after) {
+                                   float* invstd, float* scale, float* bias, bool zero_after,
+                                   long long* nbt) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nbt != nullptr && c == 0) *nbt += 1;
   if (c >= C) return;
   float a = 0.f, b = 0.f;
-  for (int p = 0; p < P; ++p) {
-    a += s1[(long)p * C + c];
-    b += s2[(long)p * C + c];
-    if (zero_after) {
-      s1[(long)p * C + c] = 0.f;
-      s2[(long)p * C + c] = 0.f;
+  if (P > 0) {
+    float va[P > 0 ? P : 1], vb[P > 0 ? P : 1];
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      va[p] = s1[(long)p * C + c];
+      vb[p] = s2[(long)p * C + c];
     }
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      a += va[p];
+      b += vb[p];
+    }
+    if (zero_after) {
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        s1[(long)p * C + c] = 0.f;
+        s2[(long)p * C + c] = 0.f;
+      }
+    }
+  } else {
+    for (int p = 0; p < Pdyn; ++p) {
+      a += s1[(long)p * C + c];
+      b += s2[(long)p * C + c];
+    }
+    if (zero_after)
+      for (int p = 0; p < Pdyn; ++p) {
+        s1[(long)p * C + c] = 0.f;
+        s2[(long)p * C + c] = 0.f;
+      }
   }
   float ms = a * inv_count;
   float var = fmaxf(b * inv_count - ms * ms, 0.f);
@@ -82,11 +109,17 @@ __global__ void bn_finalize_kernel(float* __restrict__ s1, float* __restrict__ s
 void bn_finalize(float* psum, float* psq, int P, int C, long count, const float* shift,
                  const float* gamma, const float* beta, float* run_mean, float* run_var,
                  float momentum, float eps, float* mean, float* invstd, float* scale, float* bias,
-                 bool zero_after, hipStream_t st) {
+                 bool zero_after, long long* nbt, hipStream_t st) {
   float unbias = count > 1 ? (float)count / (float)(count - 1) : 1.f;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, psum, psq, P, C,
-                     1.f / (float)count, unbias, shift, gamma, beta, run_mean, run_var, momentum,
-                     eps, mean, invstd, scale, bias, zero_after);
+  dim3 grid((C + 255) / 256);
+  if (P == kStatReplicas)
+    hipLaunchKernelGGL(bn_finalize_kernel<kStatReplicas>, grid, dim3(256), 0, st, psum, psq, P, C,
+                       1.f / (float)count, unbias, shift, gamma, beta, run_mean, run_var, momentum,
+                       eps, mean, invstd, scale, bias, zero_after, nbt);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel<0>, grid, dim3(256), 0, st, psum, psq, P, C,
+                       1.f / (float)count, unbias, shift, gamma, beta, run_mean, run_var, momentum,
+                       eps, mean, invstd, scale, bias, zero_after, nbt);
 }
 
 // ----------------------------------------------------------------------------- forward apply
@@ -246,12 +279,21 @@ __global__ void bn_bwd_collect_kernel(float* __restrict__ rep, int C, float* og,
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const long rs = (long)kStatReplicas * C;
+  float va[kStatReplicas], vb[kStatReplicas], vd[kStatReplicas];
+#pragma unroll
+  for (int r = 0; r < kStatReplicas; ++r) {  // all loads first: one memory latency
+    long o = (long)r * C + c;
+    va[r] = rep[o];
+    vb[r] = rep[rs + o];
+    vd[r] = rep[2 * rs + o];
+  }
   float a = 0.f, b = 0.f, d = 0.f;
+#pragma unroll
   for (int r = 0; r < kStatReplicas; ++r) {
     long o = (long)r * C + c;
-    a += rep[o];
-    b += rep[rs + o];
-    d += rep[2 * rs + o];
+    a += va[r];
+    b += vb[r];
+    d += vd[r];
     rep[o] = 0.f;
     rep[rs + o] = 0.f;
     rep[2 * rs + o] = 0.f;

@@ -61,7 +61,7 @@ void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc
 void bn_finalize(float* psum, float* psq, int P, int C, long count, const float* shift,
                  const float* gamma, const float* beta, float* run_mean, float* run_var,
                  float momentum, float eps, float* mean, float* invstd, float* scale, float* bias,
-                 bool zero_after, hipStream_t st);
+                 bool zero_after, long long* nbt, hipStream_t st);
 // z = act(y*scale + bias [+ r | + r*rscale + rbias])   (M rows of C channels, bf16)
 void bn_act_fwd(const void* y, const float* scale, const float* bias, const void* r,
                 const float* rscale, const float* rbias, void* z, long M, int C, bool relu,

@@ -247,10 +247,9 @@ def bn_stats_from_partials(psum, psumsq, count, bn, training: bool) -> BNStats:
         mean, invstd, scale, bias = K.bn_finalize(
             psum, psumsq, count, bn.running_mean, bn.weight.detach(), bn.bias.detach(),
             bn.running_mean if bn.track_running_stats else None,
-            bn.running_var if bn.track_running_stats else None, mom, bn.eps)
+            bn.running_var if bn.track_running_stats else None, mom, bn.eps,
+            bn.num_batches_tracked if bn.track_running_stats else None)
         _ws_done(bn, "fwd")
-        if bn.track_running_stats:
-            bn.num_batches_tracked.add_(1)
         return BNStats(mean, invstd, scale, bias, count, True)
     up = (lambda t: t) if bn.running_var.dtype == torch.float64 else (lambda t: t.float())
     invstd = torch.rsqrt(up(bn.running_var) + bn.eps)

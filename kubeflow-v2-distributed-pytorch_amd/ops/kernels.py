@@ -91,10 +91,17 @@ def conv_wgrad(dy, x, kh, kw, stride, pad, out=None):
 
 
 def bn_finalize(psum, psumsq, count, shift, gamma, beta, running_mean, running_var,
-                momentum, eps):
+                momentum, eps, num_batches_tracked=None):
+    """``num_batches_tracked`` (int64 scalar) is incremented by the same kernel."""
     if use_native(psum):
+        nbt = num_batches_tracked
+        if nbt is not None and (nbt.dtype != torch.int64 or not nbt.is_cuda):
+            nbt.add_(1)
+            nbt = None
         return native().bn_finalize(psum, psumsq, count, shift, gamma, beta, running_mean,
-                                    running_var, momentum, eps)
+                                    running_var, momentum, eps, True, nbt)
+    if num_batches_tracked is not None:
+        num_batches_tracked.add_(1)
     return _ref.bn_finalize(psum, psumsq, count, shift, gamma, beta, running_mean,
                             running_var, momentum, eps)
 

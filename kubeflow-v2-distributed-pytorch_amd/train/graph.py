@@ -54,7 +54,7 @@ class GraphedStep:
         with torch.cuda.stream(s):  # warm up on a side stream (allocator + lazy init)
             for i in range(max(1, warmup)):
                 x, y = self.static[i % len(self.static)]
-                self.fn(x, y)
+                self.fn(x, y).detach()
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
         self.graphs: List[torch.cuda.CUDAGraph] = []
@@ -63,7 +63,7 @@ class GraphedStep:
         for x, y in self.static:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
-                loss = self.fn(x, y)
+                loss = self.fn(x, y).detach()  # drop the autograd graph: no stale grad nodes
             pool = g.pool()
             self.graphs.append(g)
             self.losses.append(loss)

@@ -134,10 +134,9 @@ def test_gemm_identity_asymmetric():
     assert torch.equal(out, b.float().t())
 
 
-@pytest.mark.parametrize("C", [64, 256, 2048])
-def test_bn_pipeline(C):
+@pytest.mark.parametrize("C,P", [(64, 37), (256, 16), (2048, 16)])
+def test_bn_pipeline(C, P):
     M = 5000
-    P = 37
     psum = torch.randn(P, C, device=dev) * 10
     psq = torch.rand(P, C, device=dev) * 100 + 400
     shift = torch.randn(C, device=dev)
@@ -147,7 +146,9 @@ def test_bn_pipeline(C):
     rm2, rv2 = rm.clone(), rv.clone()
     # reference first: the native finalize re-zeroes the (replica) slabs it consumed
     ref = _ref.bn_finalize(psum.clone(), psq.clone(), M, shift, gamma, beta, rm2, rv2, 0.1, 1e-5)
-    out = native().bn_finalize(psum, psq, M, shift, gamma, beta, rm, rv, 0.1, 1e-5)
+    nbt = torch.tensor(7, dtype=torch.int64, device=dev)
+    out = native().bn_finalize(psum, psq, M, shift, gamma, beta, rm, rv, 0.1, 1e-5, True, nbt)
+    assert int(nbt) == 8
     assert float(psum.abs().max()) == 0.0 and float(psq.abs().max()) == 0.0
     for o, r in zip(out, ref):
         assert rel_err(o, r) < 1e-4
