@@ -336,12 +336,22 @@ std::tuple<Tensor, optional<Tensor>> bn_act_bwd_apply(
 }
 
 // ------------------------------------------------------------------------------- pooling
-std::tuple<Tensor, Tensor> maxpool_fwd(Tensor x, int k, int s, int p) {
+// torch's pooling output size (ceil_mode: the last window must start inside input or left pad)
+int pool_out(int L, int k, int s, int p, bool ceil_mode) {
+  int num = L + 2 * p - k;
+  int o = (ceil_mode ? (num + s - 1) / s : num / s) + 1;
+  if (ceil_mode && (o - 1) * s >= L + p) --o;
+  return o;
+}
+
+std::tuple<Tensor, Tensor> maxpool_fwd(Tensor x, int k, int s, int p, bool ceil_mode) {
   check_bf16(x, "x");
   c10::DeviceGuard g(x.device());
   int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   TORCH_CHECK(C % 8 == 0 && k <= 15, "maxpool needs C % 8 == 0 and k <= 15");
-  int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
+  TORCH_CHECK(k >= 1 && s >= 1 && p >= 0 && 2 * p <= k, "bad maxpool geometry");
+  int Ho = pool_out(H, k, s, p, ceil_mode), Wo = pool_out(W, k, s, p, ceil_mode);
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty maxpool output");
   auto y = torch::empty({N, Ho, Wo, C}, x.options());
   auto idx = torch::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
   mipipe::maxpool_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, k, s,
@@ -701,6 +711,231 @@ Tensor dropout_fwd(Tensor x, double p, int64_t seed) {
   return y;
 }
 
+// ------------------------------------------------------------------------------- vision.hip
+mipipe::GConvShape gconv_shape(int64_t N, int64_t H, int64_t W, int64_t Ci, int64_t Co, int64_t KH,
+                               int64_t KW, int64_t Cig, const std::vector<int64_t>& stride,
+                               const std::vector<int64_t>& pad, int64_t groups) {
+  TORCH_CHECK(stride.size() == 2 && pad.size() == 2, "stride / pad must be (h, w)");
+  TORCH_CHECK(groups >= 1 && Ci % groups == 0 && Co % groups == 0,
+              "channels must divide into groups");
+  TORCH_CHECK(Cig * groups == Ci, "weight Ci/groups ", Cig, " x ", groups, " != input channels ", Ci);
+  mipipe::GConvShape s;
+  s.N = (int)N; s.H = (int)H; s.W = (int)W; s.Ci = (int)Ci;
+  s.Co = (int)Co; s.KH = (int)KH; s.KW = (int)KW;
+  s.sh = (int)stride[0]; s.sw = (int)stride[1]; s.ph = (int)pad[0]; s.pw = (int)pad[1];
+  s.groups = (int)groups;
+  TORCH_CHECK(s.KH >= 1 && s.KW >= 1 && s.sh >= 1 && s.sw >= 1 && s.ph >= 0 && s.pw >= 0,
+              "bad kernel / stride / padding");
+  s.Ho = (s.H + 2 * s.ph - s.KH) / s.sh + 1;
+  s.Wo = (s.W + 2 * s.pw - s.KW) / s.sw + 1;
+  TORCH_CHECK(s.Ho > 0 && s.Wo > 0, "empty conv output");
+  return s;
+}
+
+// the 8-channel vector depthwise kernels: groups == Ci == Co, C % 8 == 0, C/8 <= 256 threads
+bool dw_vec8(const mipipe::GConvShape& s) {
+  return s.groups == s.Ci && s.Ci == s.Co && s.Ci % 8 == 0 && s.Ci <= 2048;
+}
+
+// depthwise weights [C, KH, KW, 1] -> taps-major [KH*KW, C] (one 16-byte vector per tap)
+Tensor dw_taps_major(const Tensor& w) {
+  return w.reshape({w.size(0), w.size(1) * w.size(2)}).t().contiguous();
+}
+
+const void* act_mask_src(const optional<Tensor>& z, int64_t act, const Tensor& like) {
+  if (act == 0 || !z.has_value()) return nullptr;
+  check_bf16(*z, "z");
+  TORCH_CHECK(z->sizes() == like.sizes(), "z must match the conv output");
+  return z->data_ptr();
+}
+
+Tensor gconv_fwd(Tensor x, Tensor w, std::vector<int64_t> stride, std::vector<int64_t> pad,
+                 int64_t groups, optional<Tensor> bias, int64_t act) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "gconv expects NHWC x and [Co,KH,KW,Ci/groups] w");
+  auto s = gconv_shape(x.size(0), x.size(1), x.size(2), x.size(3), w.size(0), w.size(1),
+                       w.size(2), w.size(3), stride, pad, groups);
+  if (bias.has_value()) check_vec(*bias, s.Co, "bias");
+  TORCH_CHECK(act >= 0 && act <= 2, "act must be 0 (none), 1 (relu) or 2 (relu6)");
+  auto y = torch::empty({s.N, s.Ho, s.Wo, s.Co}, x.options());
+  const float* bp = bias.has_value() ? bias->data_ptr<float>() : nullptr;
+  if (dw_vec8(s)) {
+    auto wt = dw_taps_major(w);
+    mipipe::dwconv_fwd(x.data_ptr(), wt.data_ptr(), bp, y.data_ptr(), s, (int)act, stream());
+  } else {
+    mipipe::gconv_fwd(x.data_ptr(), w.data_ptr(), bp, y.data_ptr(), s, (int)act, stream());
+  }
+  return y;
+}
+
+Tensor gconv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, std::vector<int64_t> stride,
+                   std::vector<int64_t> pad, int64_t groups, optional<Tensor> z, int64_t act) {
+  check_bf16(dy, "dy");
+  check_bf16(w, "w");
+  c10::DeviceGuard g(dy.device());
+  TORCH_CHECK(x_shape.size() == 4 && w.dim() == 4, "x_shape must be [N,H,W,Ci]");
+  auto s = gconv_shape(x_shape[0], x_shape[1], x_shape[2], x_shape[3], w.size(0), w.size(1),
+                       w.size(2), w.size(3), stride, pad, groups);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo &&
+                  dy.size(3) == s.Co, "dy shape does not match the convolution");
+  TORCH_CHECK(act >= 0 && act <= 2, "bad act");
+  const void* zp = act_mask_src(z, act, dy);
+  auto dx = torch::empty({s.N, s.H, s.W, s.Ci}, dy.options());
+  if (dw_vec8(s)) {
+    auto wt = dw_taps_major(w);
+    mipipe::dwconv_dgrad(dy.data_ptr(), wt.data_ptr(), zp, dx.data_ptr(), s, (int)act, stream());
+  } else {
+    mipipe::gconv_dgrad(dy.data_ptr(), w.data_ptr(), zp, dx.data_ptr(), s, (int)act, stream());
+  }
+  return dx;
+}
+
+std::tuple<Tensor, optional<Tensor>> gconv_wgrad(Tensor dy, Tensor x, int64_t kh, int64_t kw,
+                                                 std::vector<int64_t> stride,
+                                                 std::vector<int64_t> pad, int64_t groups,
+                                                 optional<Tensor> z, int64_t act,
+                                                 optional<Tensor> out, optional<Tensor> dbias,
+                                                 bool want_bias) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  c10::DeviceGuard g(dy.device());
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4, "NHWC tensors expected");
+  const int64_t Co = dy.size(3), Ci = x.size(3);
+  TORCH_CHECK(groups >= 1 && Ci % groups == 0, "bad groups");
+  auto s = gconv_shape(x.size(0), x.size(1), x.size(2), Ci, Co, kh, kw, Ci / groups, stride, pad,
+                       groups);
+  TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo, "dy/x mismatch");
+  TORCH_CHECK(act >= 0 && act <= 2, "bad act");
+  const void* zp = act_mask_src(z, act, dy);
+  Tensor dw;
+  if (out.has_value()) {  // accumulate into the parameter's flat-gradient view
+    check_f32(*out, "out");
+    TORCH_CHECK(out->dim() == 4 && out->size(0) == Co && out->size(1) == kh &&
+                    out->size(2) == kw && out->size(3) == Ci / groups,
+                "wgrad out must be [Co,KH,KW,Ci/groups]");
+    dw = *out;
+  } else {
+    dw = torch::zeros({Co, kh, kw, Ci / groups}, x.options().dtype(at::kFloat));
+  }
+  optional<Tensor> db;
+  if (dbias.has_value()) {
+    check_vec(*dbias, Co, "dbias");
+    db = *dbias;
+  } else if (want_bias) {
+    db = torch::zeros({Co}, x.options().dtype(at::kFloat));
+  }
+  float* dbp = db.has_value() ? db->data_ptr<float>() : nullptr;
+  if (dw_vec8(s))
+    mipipe::dwconv_wgrad(dy.data_ptr(), x.data_ptr(), zp, dw.data_ptr<float>(), dbp, s, (int)act,
+                         stream());
+  else
+    mipipe::gconv_wgrad(dy.data_ptr(), x.data_ptr(), zp, dw.data_ptr<float>(), dbp, s, (int)act,
+                        stream());
+  return {dw, db};
+}
+
+// shifted per-channel sums (one zeroed [2, C] allocation; rows returned as [1, C] views)
+std::tuple<Tensor, Tensor> chan_stats(Tensor y, Tensor shift) {
+  check_bf16(y, "y");
+  c10::DeviceGuard g(y.device());
+  int64_t C = y.size(-1), M = y.numel() / C;
+  check_vec(shift, C, "shift");
+  auto st = torch::zeros({2, C}, y.options().dtype(at::kFloat));
+  auto ps = st.narrow(0, 0, 1), pq = st.narrow(0, 1, 1);
+  mipipe::chan_stats(y.data_ptr(), shift.data_ptr<float>(), M, (int)C, ps.data_ptr<float>(),
+                     pq.data_ptr<float>(), stream());
+  return {ps, pq};
+}
+
+Tensor affine_act(Tensor y, Tensor scale, Tensor bias, int64_t act) {
+  check_bf16(y, "y");
+  c10::DeviceGuard g(y.device());
+  int64_t C = y.size(-1), M = y.numel() / C;
+  check_vec(scale, C, "scale");
+  check_vec(bias, C, "bias");
+  TORCH_CHECK(act >= 0 && act <= 2, "bad act");
+  auto z = torch::empty_like(y);
+  mipipe::affine_act(y.data_ptr(), scale.data_ptr<float>(), bias.data_ptr<float>(), z.data_ptr(),
+                     M, (int)C, (int)act, stream());
+  return z;
+}
+
+std::tuple<Tensor, Tensor> bn_generic_bwd_reduce(Tensor dz, optional<Tensor> z, Tensor y,
+                                                 Tensor mean, Tensor invstd, int64_t act) {
+  check_bf16(dz, "dz");
+  check_bf16(y, "y");
+  c10::DeviceGuard g(y.device());
+  int64_t C = y.size(-1), M = y.numel() / C;
+  TORCH_CHECK(dz.sizes() == y.sizes(), "dz / y shape mismatch");
+  check_vec(mean, C, "mean");
+  check_vec(invstd, C, "invstd");
+  TORCH_CHECK(act >= 0 && act <= 2 && (act == 0 || z.has_value()), "activation backward needs z");
+  const void* zp = act_mask_src(z, act, y);
+  auto st = torch::zeros({2, C}, y.options().dtype(at::kFloat));
+  auto sg = st[0], sgx = st[1];
+  mipipe::bn_generic_bwd_reduce(dz.data_ptr(), zp, y.data_ptr(), mean.data_ptr<float>(),
+                                invstd.data_ptr<float>(), M, (int)C, (int)act,
+                                sg.data_ptr<float>(), sgx.data_ptr<float>(), stream());
+  return {sg, sgx};
+}
+
+Tensor bn_generic_bwd_apply(Tensor dz, optional<Tensor> z, Tensor y, Tensor mean, Tensor invstd,
+                            Tensor gamma, optional<Tensor> sum_g, optional<Tensor> sum_gx,
+                            int64_t count, int64_t act) {
+  check_bf16(dz, "dz");
+  check_bf16(y, "y");
+  c10::DeviceGuard g(y.device());
+  int64_t C = y.size(-1), M = y.numel() / C;
+  TORCH_CHECK(dz.sizes() == y.sizes(), "dz / y shape mismatch");
+  for (auto* t : {&mean, &invstd, &gamma}) check_vec(*t, C, "bn vector");
+  TORCH_CHECK(sum_g.has_value() == sum_gx.has_value(), "pass both sums or none");
+  if (sum_g.has_value()) {
+    check_vec(*sum_g, C, "sum_g");
+    check_vec(*sum_gx, C, "sum_gx");
+  }
+  TORCH_CHECK(act >= 0 && act <= 2 && (act == 0 || z.has_value()), "activation backward needs z");
+  TORCH_CHECK(count > 0, "count must be positive");
+  const void* zp = act_mask_src(z, act, y);
+  auto dy = torch::empty_like(y);
+  mipipe::bn_generic_bwd_apply(dz.data_ptr(), zp, y.data_ptr(), mean.data_ptr<float>(),
+                               invstd.data_ptr<float>(), gamma.data_ptr<float>(),
+                               sum_g.has_value() ? sum_g->data_ptr<float>() : nullptr,
+                               sum_gx.has_value() ? sum_gx->data_ptr<float>() : nullptr, count, M,
+                               (int)C, (int)act, dy.data_ptr(), stream());
+  return dy;
+}
+
+Tensor avgpool2d_fwd(Tensor x, int64_t k, int64_t s, int64_t p) {
+  check_bf16(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.dim() == 4, "x must be NHWC");
+  TORCH_CHECK(k >= 1 && s >= 1 && p >= 0 && 2 * p <= k, "bad avgpool geometry");
+  int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  int Ho = pool_out(H, k, s, p, false), Wo = pool_out(W, k, s, p, false);
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty avgpool output");
+  auto y = torch::empty({N, Ho, Wo, C}, x.options());
+  mipipe::avgpool2d_fwd(x.data_ptr(), y.data_ptr(), N, H, W, C, Ho, Wo, (int)k, (int)s, (int)p,
+                        stream());
+  return y;
+}
+
+Tensor avgpool2d_bwd(Tensor dy, std::vector<int64_t> xs, int64_t k, int64_t s, int64_t p) {
+  check_bf16(dy, "dy");
+  c10::DeviceGuard g(dy.device());
+  TORCH_CHECK(xs.size() == 4 && dy.dim() == 4, "NHWC shapes expected");
+  TORCH_CHECK(k >= 1 && s >= 1 && p >= 0 && 2 * p <= k, "bad avgpool geometry");
+  int N = xs[0], H = xs[1], W = xs[2], C = xs[3];
+  int Ho = pool_out(H, k, s, p, false), Wo = pool_out(W, k, s, p, false);
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == Ho && dy.size(2) == Wo && dy.size(3) == C,
+              "avgpool2d_bwd shape mismatch");
+  auto dx = torch::empty({N, H, W, C}, dy.options());
+  mipipe::avgpool2d_bwd(dy.data_ptr(), dx.data_ptr(), N, H, W, C, Ho, Wo, (int)k, (int)s, (int)p,
+                        stream());
+  return dx;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -731,7 +966,23 @@ PYBIND11_MODULE(_C, m) {
         py::arg("rep") = py::none(), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none(),
         py::arg("dgamma2") = py::none(), py::arg("dbeta2") = py::none());
   m.def("bn_act_bwd_apply", &bn_act_bwd_apply);
-  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("s"), py::arg("p"),
+        py::arg("ceil_mode") = false);
+  m.def("gconv_fwd", &gconv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
+        py::arg("groups"), py::arg("bias") = py::none(), py::arg("act") = 0);
+  m.def("gconv_dgrad", &gconv_dgrad, py::arg("dy"), py::arg("w"), py::arg("x_shape"),
+        py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("z") = py::none(),
+        py::arg("act") = 0);
+  m.def("gconv_wgrad", &gconv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
+        py::arg("stride"), py::arg("pad"), py::arg("groups"), py::arg("z") = py::none(),
+        py::arg("act") = 0, py::arg("out") = py::none(), py::arg("dbias") = py::none(),
+        py::arg("want_bias") = false);
+  m.def("chan_stats", &chan_stats);
+  m.def("affine_act", &affine_act);
+  m.def("bn_generic_bwd_reduce", &bn_generic_bwd_reduce);
+  m.def("bn_generic_bwd_apply", &bn_generic_bwd_apply);
+  m.def("avgpool2d_fwd", &avgpool2d_fwd);
+  m.def("avgpool2d_bwd", &avgpool2d_bwd);
   m.def("maxpool_bwd_impl", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);

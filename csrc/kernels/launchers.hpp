@@ -48,6 +48,45 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
 // gradient buffer to fuse autograd's accumulation (gradient lands directly in the DDP bucket)
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st);
 
+// ---- direct convolution, BatchNorm for any C, k x k average pool (vision.hip) ----------------
+struct GConvShape {
+  int N, H, W, Ci, Co, KH, KW, sh, sw, ph, pw, groups, Ho, Wo;
+};
+// act: 0 none, 1 relu, 2 relu6.  Weights [Co][KH][KW][Ci/groups].
+void gconv_fwd(const void* x, const void* w, const float* bias, void* y, const GConvShape& s,
+               int act, hipStream_t st);
+// z (optional): the forward OUTPUT of a fused activation; dy is masked by act'(z)
+void gconv_dgrad(const void* dy, const void* w, const void* z, void* dx, const GConvShape& s,
+                 int act, hipStream_t st);
+// dw [Co][KH][KW][Ci/groups] and dbias [Co] (optional) are ACCUMULATED into (fp32 atomics)
+void gconv_wgrad(const void* dy, const void* x, const void* z, float* dw, float* dbias,
+                 const GConvShape& s, int act, hipStream_t st);
+// depthwise (groups == Ci == Co, C % 8 == 0, C <= 2048): taps-major weights wt [KH*KW][C];
+// dw stays in the parameter layout [C][KH][KW]
+void dwconv_fwd(const void* x, const void* wt, const float* bias, void* y, const GConvShape& s,
+                int act, hipStream_t st);
+void dwconv_dgrad(const void* dy, const void* wt, const void* z, void* dx, const GConvShape& s,
+                  int act, hipStream_t st);
+void dwconv_wgrad(const void* dy, const void* x, const void* z, float* dw, float* dbias,
+                  const GConvShape& s, int act, hipStream_t st);
+// psum/psq: zeroed [C] accumulators of Σ(y - shift), Σ(y - shift)²
+void chan_stats(const void* y, const float* shift, long M, int C, float* psum, float* psq,
+                hipStream_t st);
+void affine_act(const void* y, const float* scale, const float* bias, void* z, long M, int C,
+                int act, hipStream_t st);
+// out_g / out_gx: zeroed [C] accumulators
+void bn_generic_bwd_reduce(const void* dz, const void* z, const void* y, const float* mean,
+                           const float* invstd, long M, int C, int act, float* out_g,
+                           float* out_gx, hipStream_t st);
+void bn_generic_bwd_apply(const void* dz, const void* z, const void* y, const float* mean,
+                          const float* invstd, const float* gamma, const float* sum_g,
+                          const float* sum_gx, long count, long M, int C, int act, void* dy,
+                          hipStream_t st);
+void avgpool2d_fwd(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo, int k,
+                   int stride, int pad, hipStream_t st);
+void avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho, int Wo, int k,
+                   int stride, int pad, hipStream_t st);
+
 // ---- dense GEMM: C[M][N] = op(A) op(B) --------------------------------------------------------
 //  a_kc: A stored [M][K] (else [K][M]);  b_kc: B stored [N][K] (else [K][N]).
 //  out: 0 = bf16 store (bias/act), 1 = fp32 store (bias), 2 = fp32 atomic accumulate (split-K).

@@ -8,13 +8,15 @@ from __future__ import annotations
 from typing import Callable, Dict, List
 
 from .resnet import (resnet18, resnet34, resnet50, resnet101, resnet152,  # noqa: F401
-                     wide_resnet50_2, wide_resnet101_2, ResNet)
+                     wide_resnet50_2, wide_resnet101_2, resnext50_32x4d, resnext101_32x8d,
+                     ResNet)
 from .cnn import mnist_cnn, MnistCNN  # noqa: F401
 
 _REGISTRY: Dict[str, Callable] = {
     "resnet18": resnet18, "resnet34": resnet34, "resnet50": resnet50,
     "resnet101": resnet101, "resnet152": resnet152,
     "wide_resnet50_2": wide_resnet50_2, "wide_resnet101_2": wide_resnet101_2,
+    "resnext50_32x4d": resnext50_32x4d, "resnext101_32x8d": resnext101_32x8d,
     "mnist_cnn": mnist_cnn,
 }
 
@@ -23,15 +25,15 @@ def register_model(name: str, fn: Callable) -> None:
     _REGISTRY[name] = fn
 
 
+_ZOO_MODULES = ("vgg", "mobilenet", "shufflenet", "squeezenet", "densenet", "inception", "bert")
+
+
 def _lazy_register():
-    try:
-        from . import vgg  # noqa: F401
-    except ImportError:
-        pass
-    try:
-        from . import bert  # noqa: F401
-    except ImportError:
-        pass
+    """Import the remaining families (torchvision's registry: VGG/AlexNet, MobileNetV2, MNASNet,
+    ShuffleNetV2, SqueezeNet, DenseNet, GoogLeNet, Inception-v3; plus BERT)."""
+    import importlib
+    for name in _ZOO_MODULES:
+        importlib.import_module(f"{__name__}.{name}")
 
 
 def model_names() -> List[str]:

@@ -33,7 +33,7 @@ class RefBasicBlock(nn.Module):
     expansion = 1
 
     def __init__(self, inplanes: int, planes: int, stride: int = 1,
-                 downsample: Optional[nn.Module] = None):
+                 downsample: Optional[nn.Module] = None, groups: int = 1, base_width: int = 64):
         super().__init__()
         self.conv1 = conv3x3(inplanes, planes, stride)
         self.bn1 = nn.BatchNorm2d(planes)
@@ -56,13 +56,15 @@ class RefBottleneck(nn.Module):
     expansion = 4
 
     def __init__(self, inplanes: int, planes: int, stride: int = 1,
-                 downsample: Optional[nn.Module] = None):
+                 downsample: Optional[nn.Module] = None, groups: int = 1, base_width: int = 64):
         super().__init__()
-        self.conv1 = conv1x1(inplanes, planes)
-        self.bn1 = nn.BatchNorm2d(planes)
-        self.conv2 = conv3x3(planes, planes, stride)
-        self.bn2 = nn.BatchNorm2d(planes)
-        self.conv3 = conv1x1(planes, planes * 4)
+        width = int(planes * (base_width / 64.0)) * groups  # ResNeXt / wide-ResNet width
+        self.conv1 = conv1x1(inplanes, width)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, groups=groups,
+                               bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = conv1x1(width, planes * 4)
         self.bn3 = nn.BatchNorm2d(planes * 4)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
@@ -80,9 +82,11 @@ class RefBottleneck(nn.Module):
 
 class RefResNet(nn.Module):
     def __init__(self, block: Type[Union[RefBasicBlock, RefBottleneck]], layers: List[int],
-                 num_classes: int = 1000, in_chans: int = 3):
+                 num_classes: int = 1000, in_chans: int = 3, groups: int = 1,
+                 width_per_group: int = 64):
         super().__init__()
         self.inplanes = 64
+        self.groups, self.base_width = groups, width_per_group
         self.conv1 = nn.Conv2d(in_chans, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = nn.BatchNorm2d(64)
         self.relu = nn.ReLU(inplace=True)
@@ -105,10 +109,11 @@ class RefResNet(nn.Module):
         if stride != 1 or self.inplanes != planes * block.expansion:
             downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
                                        nn.BatchNorm2d(planes * block.expansion))
-        layers = [block(self.inplanes, planes, stride, downsample)]
+        layers = [block(self.inplanes, planes, stride, downsample, self.groups, self.base_width)]
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):
-            layers.append(block(self.inplanes, planes))
+            layers.append(block(self.inplanes, planes, groups=self.groups,
+                                base_width=self.base_width))
         return nn.Sequential(*layers)
 
     def forward(self, x):
@@ -118,18 +123,23 @@ class RefResNet(nn.Module):
         return self.fc(x)
 
 
-_RESNET_CFG = {
-    "resnet18": (RefBasicBlock, [2, 2, 2, 2]),
-    "resnet34": (RefBasicBlock, [3, 4, 6, 3]),
-    "resnet50": (RefBottleneck, [3, 4, 6, 3]),
-    "resnet101": (RefBottleneck, [3, 4, 23, 3]),
-    "resnet152": (RefBottleneck, [3, 8, 36, 3]),
+_RESNET_CFG = {  # arch: (block, layers, groups, width_per_group)
+    "resnet18": (RefBasicBlock, [2, 2, 2, 2], 1, 64),
+    "resnet34": (RefBasicBlock, [3, 4, 6, 3], 1, 64),
+    "resnet50": (RefBottleneck, [3, 4, 6, 3], 1, 64),
+    "resnet101": (RefBottleneck, [3, 4, 23, 3], 1, 64),
+    "resnet152": (RefBottleneck, [3, 8, 36, 3], 1, 64),
+    "wide_resnet50_2": (RefBottleneck, [3, 4, 6, 3], 1, 128),
+    "wide_resnet101_2": (RefBottleneck, [3, 4, 23, 3], 1, 128),
+    "resnext50_32x4d": (RefBottleneck, [3, 4, 6, 3], 32, 4),
+    "resnext101_32x8d": (RefBottleneck, [3, 4, 23, 3], 32, 8),
 }
 
 
 def ref_resnet(arch: str, num_classes: int = 1000, in_chans: int = 3) -> RefResNet:
-    block, layers = _RESNET_CFG[arch]
-    return RefResNet(block, layers, num_classes=num_classes, in_chans=in_chans)
+    block, layers, groups, width = _RESNET_CFG[arch]
+    return RefResNet(block, layers, num_classes=num_classes, in_chans=in_chans, groups=groups,
+                     width_per_group=width)
 
 
 class RefMnistCNN(nn.Module):

@@ -21,7 +21,8 @@ from mipipe.ops import kernels as K
 from mipipe.ops import functional as MF
 
 __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50",
-           "resnet101", "resnet152", "wide_resnet50_2", "wide_resnet101_2"]
+           "resnet101", "resnet152", "wide_resnet50_2", "wide_resnet101_2", "resnext50_32x4d",
+           "resnext101_32x8d"]
 
 
 def _conv3x3(cin, cout, stride=1):
@@ -35,8 +36,10 @@ def _conv1x1(cin, cout, stride=1):
 class BasicBlock(tnn.Module):
     expansion = 1
 
-    def __init__(self, inplanes, planes, stride=1, downsample=None, base_width=64):
+    def __init__(self, inplanes, planes, stride=1, downsample=None, base_width=64, groups=1):
         super().__init__()
+        if groups != 1 or base_width != 64:
+            raise ValueError("BasicBlock only supports groups=1 and base_width=64")
         self.conv1 = _conv3x3(inplanes, planes, stride)
         self.bn1 = mnn.BatchNorm2d(planes)
         self.relu = mnn.ReLU(inplace=True)
@@ -59,12 +62,15 @@ class BasicBlock(tnn.Module):
 class Bottleneck(tnn.Module):
     expansion = 4
 
-    def __init__(self, inplanes, planes, stride=1, downsample=None, base_width=64):
+    def __init__(self, inplanes, planes, stride=1, downsample=None, base_width=64, groups=1):
         super().__init__()
-        width = int(planes * (base_width / 64.0))
+        width = int(planes * (base_width / 64.0)) * groups
         self.conv1 = _conv1x1(inplanes, width)
         self.bn1 = mnn.BatchNorm2d(width)
-        self.conv2 = _conv3x3(width, width, stride)
+        # ResNeXt: the grouped 3x3 runs on the direct grouped-conv kernel (vision.hip)
+        self.conv2 = (_conv3x3(width, width, stride) if groups == 1 else
+                      mnn.XConv2d(width, width, 3, stride=stride, padding=1, groups=groups,
+                                  bias=False))
         self.bn2 = mnn.BatchNorm2d(width)
         self.conv3 = _conv1x1(width, planes * self.expansion)
         self.bn3 = mnn.BatchNorm2d(planes * self.expansion)
@@ -79,7 +85,10 @@ class Bottleneck(tnn.Module):
         # fuse_prev on conv1: if x is the previous block's BN+residual+ReLU output, its BN
         # backward reductions run in conv1's dgrad epilogue once the identity gradient is added
         out = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True, res_take=slot, fuse_prev=True)
-        out = mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, fuse_prev=True)
+        if isinstance(self.conv2, mnn.XConv2d):  # grouped: direct kernel + any-C BN/ReLU pass
+            out = MF.bn_act(self.conv2.run(out), self.bn2, "relu")
+        else:
+            out = mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, fuse_prev=True)
         if self.downsample is not None:
             ds_conv, ds_bn = self.downsample[0], self.downsample[1]
             return mnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, fuse_prev=True,
@@ -159,9 +168,10 @@ class ResNet(tnn.Module):
     def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: List[int],
                  num_classes: int = 1000, zero_init_residual: bool = False,
                  width_per_group: int = 64, in_chans: int = 3,
-                 compute_dtype: Optional[torch.dtype] = None):
+                 compute_dtype: Optional[torch.dtype] = None, groups: int = 1):
         super().__init__()
         self.inplanes = 64
+        self.groups = groups
         self.base_width = width_per_group
         self.in_chans = in_chans
         self.compute_dtype = compute_dtype
@@ -177,7 +187,7 @@ class ResNet(tnn.Module):
         self.avgpool = mnn.AdaptiveAvgPool2d((1, 1))
         self.fc = mnn.Linear(512 * block.expansion, num_classes)
         for m in self.modules():
-            if isinstance(m, mnn.Conv2d):
+            if isinstance(m, (mnn.Conv2d, mnn.XConv2d)):
                 tnn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
             elif isinstance(m, tnn.BatchNorm2d):
                 tnn.init.ones_(m.weight)
@@ -194,10 +204,11 @@ class ResNet(tnn.Module):
         if stride != 1 or self.inplanes != planes * block.expansion:
             downsample = tnn.Sequential(_conv1x1(self.inplanes, planes * block.expansion, stride),
                                         mnn.BatchNorm2d(planes * block.expansion))
-        layers = [block(self.inplanes, planes, stride, downsample, self.base_width)]
+        layers = [block(self.inplanes, planes, stride, downsample, self.base_width, self.groups)]
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):
-            layers.append(block(self.inplanes, planes, base_width=self.base_width))
+            layers.append(block(self.inplanes, planes, base_width=self.base_width,
+                                groups=self.groups))
         return tnn.Sequential(*layers)
 
     def activation_dtype(self, x: torch.Tensor) -> torch.dtype:
@@ -252,3 +263,11 @@ def wide_resnet50_2(**kw) -> ResNet:
 
 def wide_resnet101_2(**kw) -> ResNet:
     return _resnet(Bottleneck, [3, 4, 23, 3], width_per_group=128, **kw)
+
+
+def resnext50_32x4d(**kw) -> ResNet:
+    return _resnet(Bottleneck, [3, 4, 6, 3], groups=32, width_per_group=4, **kw)
+
+
+def resnext101_32x8d(**kw) -> ResNet:
+    return _resnet(Bottleneck, [3, 4, 23, 3], groups=32, width_per_group=8, **kw)

@@ -22,7 +22,7 @@ from mipipe.ops import functional as MF
 from mipipe.ops import kernels as K
 
 __all__ = ["Conv2d", "BatchNorm2d", "Linear", "ReLU", "MaxPool2d", "AdaptiveAvgPool2d",
-           "Embedding", "LayerNorm", "Dropout", "ShadowMixin", "conv_bn_act"]
+           "Embedding", "LayerNorm", "Dropout", "ShadowMixin", "conv_bn_act", "XConv2d"]
 
 
 class ShadowMixin:
@@ -100,6 +100,59 @@ class Conv2d(ShadowMixin, tnn.Module):
     def extra_repr(self) -> str:
         return (f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, "
                 f"stride={self.stride}, padding={self.padding}, bias={self.bias is not None}")
+
+
+class XConv2d(ShadowMixin, tnn.Conv2d):
+    """``torch.nn.Conv2d`` with any groups / kernel / stride / padding (identical state).
+
+    ``forward`` stays torch's own NCHW convolution — the numerics oracle the model zoo's
+    ``reference_forward`` runs.  :meth:`run` executes on NHWC activations through mipipe's
+    kernels: the MFMA implicit-GEMM conv when the conv is dense (groups 1, square kernel /
+    stride / padding, channel counts % 8), the direct grouped / depthwise kernels otherwise.
+    The weight is kept ``channels_last`` so its operand view ``[Co, KH, KW, Ci/groups]`` is
+    contiguous (the layout both kernel families read)."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
+
+    def operand_view(self, w):
+        return w.permute(0, 2, 3, 1)
+
+    def _apply(self, fn, *args, **kwargs):
+        r = super()._apply(fn, *args, **kwargs)
+        if not self.weight.is_contiguous(memory_format=torch.channels_last):
+            self.weight.data = self.weight.data.contiguous(memory_format=torch.channels_last)
+        return r
+
+    def dense(self, cin: int) -> bool:
+        """Runs on the MFMA implicit-GEMM kernels for an NHWC input with ``cin`` channels."""
+        kh, kw = self.kernel_size
+        return (self.groups == 1 and kh == kw and self.dilation == (1, 1)
+                and self.padding_mode == "zeros" and not isinstance(self.padding, str)
+                and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
+                and self.padding[0] < kh and cin % 8 == 0 and self.out_channels % 8 == 0)
+
+    def kernel_weight(self, dtype: torch.dtype, cin: int) -> torch.Tensor:
+        """Operand weight; input channels zero-padded to ``cin`` (padded NHWC stem input)."""
+        w = self.compute_weight(dtype)
+        if self.groups == 1 and w.shape[-1] < cin:
+            w = torch.nn.functional.pad(w, (0, cin - w.shape[-1])).contiguous()
+        return w
+
+    def run(self, x: torch.Tensor, act: str = "none") -> torch.Tensor:
+        """act(conv(x) + bias) on NHWC ``x``; act in {none, relu, relu6}."""
+        if self.dilation != (1, 1) or self.padding_mode != "zeros" or isinstance(self.padding, str):
+            raise NotImplementedError("XConv2d.run: dilation / padding modes other than zeros")
+        cin = x.shape[-1]
+        w_c = self.kernel_weight(x.dtype, cin)
+        if self.dense(cin) and act in ("none", "relu"):
+            if self.bias is not None or act == "relu":
+                return MF.conv2d_bias_act(x, self.weight, w_c, self.bias, self.stride[0],
+                                          self.padding[0], act == "relu")
+            return MF.conv2d(x, self.weight, w_c, self.stride[0], self.padding[0])[0]
+        return MF.gconv2d(x, self.weight, w_c, self.bias, self.stride, self.padding,
+                          self.groups, act)
 
 
 class BatchNorm2d(tnn.BatchNorm2d):

@@ -133,8 +133,10 @@ def relu_mask_grad(dz: Tensor, z: Tensor) -> Tensor:
     return (_f(dz) * (z > 0)).to(dz.dtype)
 
 
-def maxpool_fwd(x: Tensor, k: int, stride: int, pad: int) -> Tuple[Tensor, Tensor]:
-    yf, idx = F.max_pool2d(_f(_nchw(x)), k, stride, pad, return_indices=True)
+def maxpool_fwd(x: Tensor, k: int, stride: int, pad: int,
+                ceil_mode: bool = False) -> Tuple[Tensor, Tensor]:
+    yf, idx = F.max_pool2d(_f(_nchw(x)), k, stride, pad, ceil_mode=ceil_mode,
+                           return_indices=True)
     return _nhwc(yf).to(x.dtype), _nhwc(idx.to(torch.int32))
 
 
@@ -361,6 +363,106 @@ def gelu_bwd(dy: Tensor, x: Tensor) -> Tensor:
     cdf = 0.5 * (1.0 + torch.erf(xf / math.sqrt(2.0)))
     pdf = torch.exp(-0.5 * xf * xf) / math.sqrt(2.0 * math.pi)
     return (_f(dy) * (cdf + xf * pdf)).to(dy.dtype)
+
+
+# ----------------------------------------------------------------------------- vision.hip
+def act_fn(t: Tensor, act: str) -> Tensor:
+    if act == "relu":
+        return torch.relu(t)
+    if act == "relu6":
+        return t.clamp(0.0, 6.0)
+    return t
+
+
+def act_keep(z: Tensor, act: str) -> Optional[Tensor]:
+    """Where the activation passes gradient, judged from its OUTPUT z like the kernels do
+    (relu: z > 0; relu6: 0 < z < 6)."""
+    if act == "relu":
+        return z > 0
+    if act == "relu6":
+        return (z > 0) & (z < 6)
+    return None
+
+
+def _masked(dy: Tensor, z: Optional[Tensor], act: str) -> Tensor:
+    g = _f(dy)
+    keep = None if z is None else act_keep(_f(z), act)
+    return g if keep is None else g * keep
+
+
+def gconv_fwd(x: Tensor, w: Tensor, stride, pad, groups: int, bias: Optional[Tensor] = None,
+              act: str = "none") -> Tensor:
+    """y = act(conv(x, w, groups) + bias); x NHWC, w [Co, KH, KW, Ci/groups]; stride/pad (h, w)."""
+    y = F.conv2d(_f(_nchw(x)), _f(_w_oihw(w)), None if bias is None else _f(bias),
+                 stride=tuple(stride), padding=tuple(pad), groups=groups)
+    return act_fn(_nhwc(y), act).to(x.dtype)
+
+
+def gconv_dgrad(dy: Tensor, w: Tensor, x_shape, stride, pad, groups: int,
+                z: Optional[Tensor] = None, act: str = "none") -> Tensor:
+    N, H, W, Ci = x_shape
+    g = _masked(dy, z, act)
+    dx = torch.nn.grad.conv2d_input((N, Ci, H, W), _f(_w_oihw(w)), _nchw(g), stride=tuple(stride),
+                                    padding=tuple(pad), groups=groups)
+    return _nhwc(dx).to(dy.dtype)
+
+
+def gconv_wgrad(dy: Tensor, x: Tensor, kh: int, kw: int, stride, pad, groups: int,
+                z: Optional[Tensor] = None, act: str = "none") -> Tuple[Tensor, Tensor]:
+    """(dw [Co, KH, KW, Ci/groups], db [Co]) in fp32 (fp64 inputs stay fp64)."""
+    g = _masked(dy, z, act)
+    Co, Ci = dy.shape[-1], x.shape[-1]
+    dw = torch.nn.grad.conv2d_weight(_f(_nchw(x)), (Co, Ci // groups, kh, kw), _nchw(g),
+                                     stride=tuple(stride), padding=tuple(pad), groups=groups)
+    return dw.permute(0, 2, 3, 1).contiguous(), g.reshape(-1, Co).sum(0)
+
+
+def chan_stats(y: Tensor, shift: Tensor) -> Tuple[Tensor, Tensor]:
+    """Shifted per-channel sums Σ(y - shift), Σ(y - shift)² ([1, C] each)."""
+    C = y.shape[-1]
+    d = _f(y).reshape(-1, C) - _f(shift)[None, :]
+    return d.sum(0, keepdim=True), (d * d).sum(0, keepdim=True)
+
+
+def affine_act(y: Tensor, scale: Tensor, bias: Tensor, act: str = "none") -> Tensor:
+    return act_fn(_f(y) * scale + bias, act).to(y.dtype)
+
+
+def bn_generic_bwd_reduce(dz: Tensor, z: Optional[Tensor], y: Tensor, mean: Tensor,
+                          invstd: Tensor, act: str = "none") -> Tuple[Tensor, Tensor]:
+    """Σg and Σg·x̂ per channel, g = dz·act'(z), x̂ = (y - mean)·invstd."""
+    C = y.shape[-1]
+    g = _masked(dz, z, act).reshape(-1, C)
+    xhat = (_f(y).reshape(-1, C) - mean) * invstd
+    return g.sum(0), (g * xhat).sum(0)
+
+
+def bn_generic_bwd_apply(dz: Tensor, z: Optional[Tensor], y: Tensor, mean: Tensor,
+                         invstd: Tensor, gamma: Tensor, sum_g: Optional[Tensor],
+                         sum_gx: Optional[Tensor], count: int, act: str = "none") -> Tensor:
+    """dy = γ·invstd·(g − Σg/n − x̂·Σgx̂/n); without sums (eval-mode BN) dy = γ·invstd·g."""
+    shp = y.shape
+    C = shp[-1]
+    g = _masked(dz, z, act).reshape(-1, C)
+    if sum_g is None:
+        dy = (_f(gamma) * invstd) * g
+    else:
+        xhat = (_f(y).reshape(-1, C) - mean) * invstd
+        dy = (_f(gamma) * invstd) * (g - sum_g / count - xhat * (sum_gx / count))
+    return dy.reshape(shp).to(dz.dtype)
+
+
+def avgpool2d_fwd(x: Tensor, k: int, stride: int, pad: int) -> Tensor:
+    return _nhwc(F.avg_pool2d(_f(_nchw(x)), k, stride, pad)).to(x.dtype)
+
+
+def avgpool2d_bwd(dy: Tensor, x_shape, k: int, stride: int, pad: int) -> Tensor:
+    N, H, W, C = x_shape
+    with torch.enable_grad():
+        xz = torch.zeros(N, C, H, W, dtype=_f(dy).dtype, device=dy.device, requires_grad=True)
+        yz = F.avg_pool2d(xz, k, stride, pad)
+        (g,) = torch.autograd.grad(yz, xz, _f(_nchw(dy)).contiguous())
+    return _nhwc(g).to(dy.dtype)
 
 
 def synthetic_images(indices: Tensor, num_classes: int, shape, seed: int,

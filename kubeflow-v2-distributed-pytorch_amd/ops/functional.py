@@ -204,6 +204,59 @@ def conv2d_bias_act(x: Tensor, weight: Tensor, w_c: Tensor, bias: Optional[Tenso
     return _ConvBiasActFn.apply(x, weight, w_c, bias, stride, pad, relu)
 
 
+class _GConvFn(Function):
+    """Grouped / depthwise / non-square / odd-channel convolution (+bias, +activation) on the
+    direct NHWC kernels of vision.hip.  The activation's mask is recomputed from the saved
+    output in the backward kernels; weight (and bias) gradients accumulate straight into the
+    flat DDP gradient buffer when the parameter lives there."""
+
+    @staticmethod
+    def forward(ctx, x, weight, w_c, bias, stride, pad, groups, act):
+        y = K.gconv_fwd(x, w_c, stride, pad, groups, None if bias is None else bias.detach(), act)
+        ctx.save_for_backward(x, w_c, y if act != "none" else None)
+        ctx.weight, ctx.bias = weight, bias
+        ctx.conf = (stride, pad, groups, act)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w_c, z = ctx.saved_tensors
+        stride, pad, groups, act = ctx.conf
+        weight, bias = ctx.weight, ctx.bias
+        dy = dy.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = K.gconv_dgrad(dy, w_c, x.shape, stride, pad, groups, z, act)
+        need_w = ctx.needs_input_grad[1]
+        need_b = bias is not None and ctx.needs_input_grad[3]
+        if need_w or need_b:
+            native = K.use_native(dy)
+            ci = weight.shape[1]
+            padded = w_c.shape[-1] != ci  # input channels zero-padded for the kernel (stem)
+            tw = _direct_grad_target(weight) if native and need_w and not padded else None
+            tb = _direct_grad_target(bias) if native and need_b else None
+            g_w, g_b = K.gconv_wgrad(dy, x, w_c.shape[1], w_c.shape[2], stride, pad, groups, z,
+                                     act, out=None if tw is None else tw[1].permute(0, 2, 3, 1),
+                                     dbias=None if tb is None else tb[1], want_bias=need_b)
+            if tw is not None:
+                tw[0].grad_ready(weight)
+            elif need_w:
+                dw = (g_w[..., :ci] if padded else g_w).permute(0, 3, 1, 2).to(weight.dtype)
+            if tb is not None:
+                tb[0].grad_ready(bias)
+            elif need_b:
+                db = g_b.to(bias.dtype)
+        return dx, dw, None, db, None, None, None, None
+
+
+def gconv2d(x: Tensor, weight: Tensor, w_c: Tensor, bias: Optional[Tensor], stride, pad,
+            groups: int, act: str = "none") -> Tensor:
+    """NHWC convolution with ``groups`` and (h, w) stride / padding on the direct kernels;
+    ``act`` in {none, relu, relu6} is applied in the same pass."""
+    return _GConvFn.apply(x, weight, w_c, bias, tuple(int(v) for v in stride),
+                          tuple(int(v) for v in pad), int(groups), act)
+
+
 # ----------------------------------------------------------------------------- batchnorm
 @dataclass
 class BNStats:
@@ -378,11 +431,53 @@ def channel_partials(y: Tensor, shift: Tensor) -> Tuple[Tensor, Tensor]:
     return d.sum(0, keepdim=True), (d * d).sum(0, keepdim=True)
 
 
+class _BNGenericFn(Function):
+    """BatchNorm (+ReLU / ReLU6) over NHWC activations with any channel count (vision.hip):
+    statistics kernel -> bn_finalize (running stats, num_batches_tracked) -> one affine +
+    activation pass; backward = one reduction pass + one apply pass."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, bn, act):
+        C = y.shape[-1]
+        count = y.numel() // C
+        if bn.training:
+            ps, pss = K.chan_stats(y, bn.running_mean)
+            st = bn_stats_from_partials(ps, pss, count, bn, True)
+        else:
+            st = bn_stats_from_partials(None, None, count, bn, False)
+        z = K.affine_act(y, st.scale, st.bias, act)
+        ctx.save_for_backward(y, z if act != "none" else None, gamma)
+        ctx.st, ctx.act = st, act
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        y, z, gamma = ctx.saved_tensors
+        st, act = ctx.st, ctx.act
+        dz = dz.contiguous()
+        sg, sgx = K.bn_generic_bwd_reduce(dz, z, y, st.mean, st.invstd, act)
+        gd = gamma.detach()
+        if st.batch_stats:
+            dy = K.bn_generic_bwd_apply(dz, z, y, st.mean, st.invstd, gd, sg, sgx, st.count, act)
+        else:
+            dy = K.bn_generic_bwd_apply(dz, z, y, st.mean, st.invstd, gd, None, None, st.count,
+                                        act)
+        return dy, sgx.to(gamma.dtype), sg.to(gamma.dtype), None, None
+
+
+def bn_act(y: Tensor, bn, act: str = "none") -> Tensor:
+    """act(BatchNorm(y)) for NHWC ``y`` with any channel count (torch BatchNorm2d semantics:
+    batch statistics + running-stat update in training, running statistics in eval)."""
+    if bn.running_mean is None:
+        raise NotImplementedError("BatchNorm without running statistics")
+    return _BNGenericFn.apply(y, bn.weight, bn.bias, bn, act)
+
+
 # ----------------------------------------------------------------------------- pooling
 class _MaxPoolFn(Function):
     @staticmethod
-    def forward(ctx, x, k, stride, pad):
-        y, idx = K.maxpool_fwd(x, k, stride, pad)
+    def forward(ctx, x, k, stride, pad, ceil_mode=False):
+        y, idx = K.maxpool_fwd(x, k, stride, pad, ceil_mode)
         ctx.save_for_backward(idx)
         ctx.xshape = tuple(x.shape)
         ctx.conf = (k, stride, pad)
@@ -392,11 +487,28 @@ class _MaxPoolFn(Function):
     @staticmethod
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
-        return K.maxpool_bwd(dy.contiguous(), idx, ctx.xshape, *ctx.conf), None, None, None
+        return K.maxpool_bwd(dy.contiguous(), idx, ctx.xshape, *ctx.conf), None, None, None, None
 
 
-def max_pool2d(x: Tensor, k: int, stride: int, pad: int) -> Tensor:
-    return _MaxPoolFn.apply(x, k, stride, pad)
+def max_pool2d(x: Tensor, k: int, stride: int, pad: int, ceil_mode: bool = False) -> Tensor:
+    return _MaxPoolFn.apply(x, k, stride, pad, bool(ceil_mode))
+
+
+class _AvgPool2dFn(Function):
+    @staticmethod
+    def forward(ctx, x, k, stride, pad):
+        ctx.conf = (tuple(x.shape), k, stride, pad)
+        return K.avgpool2d_fwd(x, k, stride, pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, k, s, p = ctx.conf
+        return K.avgpool2d_bwd(dy.contiguous(), xs, k, s, p), None, None, None
+
+
+def avg_pool2d(x: Tensor, k: int, stride: Optional[int] = None, pad: int = 0) -> Tensor:
+    """NHWC k x k average pool (count_include_pad=True, floor mode: torch's defaults)."""
+    return _AvgPool2dFn.apply(x, int(k), int(stride or k), int(pad))
 
 
 class _AvgPoolFn(Function):

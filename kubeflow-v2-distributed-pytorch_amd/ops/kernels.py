@@ -19,7 +19,9 @@ __all__ = ["conv_fwd", "conv_dgrad", "conv_wgrad", "bn_finalize", "bn_act_fwd",
            "bn_act_bwd_reduce", "bn_act_bwd_apply", "maxpool_fwd", "maxpool_bwd",
            "avgpool_fwd", "avgpool_bwd", "gemm", "cross_entropy_fwd_bwd", "sgd_step",
            "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd", "dropout_fwd", "colsum", "bn_bwd_collect", "stem_pack",
-           "embedding_bwd", "gelu_fwd", "gelu_bwd", "nchw_to_nhwc", "use_native"]
+           "embedding_bwd", "gelu_fwd", "gelu_bwd", "nchw_to_nhwc", "use_native",
+           "gconv_fwd", "gconv_dgrad", "gconv_wgrad", "chan_stats", "affine_act",
+           "bn_generic_bwd_reduce", "bn_generic_bwd_apply", "avgpool2d_fwd", "avgpool2d_bwd"]
 
 _ALLOW_REF_ON_GPU = os.environ.get("MIPIPE_ALLOW_REF_ON_GPU", "0") == "1"
 
@@ -150,10 +152,10 @@ def bn_act_bwd_apply(dz, z, y, mean, invstd, gamma, sum_g, sum_gx, count, relu,
     return dy, dres
 
 
-def maxpool_fwd(x, k, stride, pad):
+def maxpool_fwd(x, k, stride, pad, ceil_mode=False):
     if use_native(x):
-        return native().maxpool_fwd(x, k, stride, pad)
-    return _ref.maxpool_fwd(x, k, stride, pad)
+        return native().maxpool_fwd(x, k, stride, pad, bool(ceil_mode))
+    return _ref.maxpool_fwd(x, k, stride, pad, ceil_mode)
 
 
 def maxpool_bwd(dy, idx, x_shape, k, stride, pad):
@@ -317,6 +319,82 @@ def stem_pack(x, dtype, pad: int, Hp: int, Wsp: int):
     P[:, :C, pad:pad + hh, pad:pad + ww] = x[:, :, :hh, :ww].to(P.dtype)
     y = P.reshape(N, 4, Hp, Wsp, 2).permute(0, 2, 3, 4, 1).reshape(N, Hp, Wsp, 8)
     return y.contiguous().to(dtype)
+
+
+# ----------------------------------------------------------------------------- vision.hip
+_ACT = {"none": 0, "relu": 1, "relu6": 2}
+
+
+def gconv_fwd(x, w, stride, pad, groups, bias=None, act="none"):
+    """Direct NHWC convolution for grouped / depthwise / non-square / odd-channel convs:
+    y = act(conv(x, w) + bias), w [Co, KH, KW, Ci/groups]; ``stride`` / ``pad`` are (h, w)."""
+    if use_native(x):
+        return native().gconv_fwd(x, w, list(stride), list(pad), int(groups), bias, _ACT[act])
+    return _ref.gconv_fwd(x, w, stride, pad, groups, bias, act)
+
+
+def gconv_dgrad(dy, w, x_shape, stride, pad, groups, z=None, act="none"):
+    """dx.  ``z``: the forward output when an activation was fused (dy masked by act'(z))."""
+    if use_native(dy):
+        return native().gconv_dgrad(dy, w, list(x_shape), list(stride), list(pad), int(groups),
+                                    z, _ACT[act])
+    return _ref.gconv_dgrad(dy, w, x_shape, stride, pad, groups, z, act)
+
+
+def gconv_wgrad(dy, x, kh, kw, stride, pad, groups, z=None, act="none", out=None, dbias=None,
+                want_bias=False):
+    """(dw [Co, KH, KW, Ci/groups] fp32, db [Co] fp32 | None).  ``out`` / ``dbias``: accumulate
+    into these (flat-gradient views) instead of fresh buffers."""
+    if use_native(dy):
+        return native().gconv_wgrad(dy, x, kh, kw, list(stride), list(pad), int(groups), z,
+                                    _ACT[act], out, dbias, bool(want_bias))
+    dw, db = _ref.gconv_wgrad(dy, x, kh, kw, stride, pad, groups, z, act)
+    if out is not None:
+        out.add_(dw)
+        dw = out
+    if dbias is not None:
+        dbias.add_(db)
+        db = dbias
+    return dw, (db if (want_bias or dbias is not None) else None)
+
+
+def chan_stats(y, shift):
+    """Shifted per-channel Σ(y - shift), Σ(y - shift)² of an NHWC tensor ([1, C] fp32 each)."""
+    if use_native(y):
+        return native().chan_stats(y, shift)
+    return _ref.chan_stats(y, shift)
+
+
+def affine_act(y, scale, bias, act="none"):
+    """act(y * scale + bias) per channel (BatchNorm apply for any channel count)."""
+    if use_native(y):
+        return native().affine_act(y, scale, bias, _ACT[act])
+    return _ref.affine_act(y, scale, bias, act)
+
+
+def bn_generic_bwd_reduce(dz, z, y, mean, invstd, act="none"):
+    if use_native(dz):
+        return native().bn_generic_bwd_reduce(dz, z, y, mean, invstd, _ACT[act])
+    return _ref.bn_generic_bwd_reduce(dz, z, y, mean, invstd, act)
+
+
+def bn_generic_bwd_apply(dz, z, y, mean, invstd, gamma, sum_g, sum_gx, count, act="none"):
+    if use_native(dz):
+        return native().bn_generic_bwd_apply(dz, z, y, mean, invstd, gamma, sum_g, sum_gx,
+                                             int(count), _ACT[act])
+    return _ref.bn_generic_bwd_apply(dz, z, y, mean, invstd, gamma, sum_g, sum_gx, count, act)
+
+
+def avgpool2d_fwd(x, k, stride, pad):
+    if use_native(x):
+        return native().avgpool2d_fwd(x, k, stride, pad)
+    return _ref.avgpool2d_fwd(x, k, stride, pad)
+
+
+def avgpool2d_bwd(dy, x_shape, k, stride, pad):
+    if use_native(dy):
+        return native().avgpool2d_bwd(dy, list(x_shape), k, stride, pad)
+    return _ref.avgpool2d_bwd(dy, x_shape, k, stride, pad)
 
 
 def nchw_to_nhwc(x, dtype, pad_channels_to: int = 0):

@@ -70,8 +70,22 @@ class CrossEntropyLoss(torch.nn.Module):
         self.label_smoothing = label_smoothing
         self.ignore_index = ignore_index
 
-    def forward(self, logits, labels):
+    def _ce(self, logits, labels):
         return MF.cross_entropy(logits, labels, self.label_smoothing, self.ignore_index)
+
+    def forward(self, logits, labels):
+        if isinstance(logits, tuple) and hasattr(logits, "_fields"):
+            # GoogLeNet / Inception-v3 in training mode return torchvision's named tuples
+            # (main logits + auxiliary classifiers).  The reference hands them to
+            # nn.CrossEntropyLoss (task.py:310) and crashes; here the auxiliary losses are added
+            # with the papers' weights: 0.3 per GoogLeNet head, 0.4 for Inception-v3's.
+            w = 0.4 if len(logits) == 2 else 0.3
+            loss = self._ce(logits[0], labels)
+            for aux in logits[1:]:
+                if aux is not None:
+                    loss = loss + w * self._ce(aux, labels)
+            return loss
+        return self._ce(logits, labels)
 
 
 def _unwrap(model):
@@ -263,7 +277,7 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
     if args.arch == "mnist_cnn":
         kw.setdefault("num_classes", K)
         kw["in_chans"] = C
-    elif args.arch.startswith(("resnet", "wide_resnet")):
+    elif args.arch.startswith(("resnet", "wide_resnet", "resnext")):
         kw["in_chans"] = C
     model = create_model(args.arch, **kw)
     compute_dtype = torch.bfloat16 if (use_gpu and args.dtype == "bf16") else torch.float32
