@@ -41,7 +41,7 @@ float* fptr(const optional<Tensor>& t, int64_t n) {
 }
 
 mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int pad,
-                             int stride_w = 0) {
+                             int stride_w = 0, int pad_w = -1) {
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv expects NHWC x and [Co,KH,KW,Ci] w");
   mipipe::ConvShape s;
   s.N = (int)x.size(0); s.H = (int)x.size(1); s.W = (int)x.size(2); s.Ci = (int)x.size(3);
@@ -50,9 +50,11 @@ mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int p
   TORCH_CHECK(stride >= 1 && pad >= 0, "bad stride/pad");
   s.stride = stride; s.pad = pad;
   s.stride_w = stride_w > 0 ? stride_w : 0;
+  s.pad_w = pad_w >= 0 ? pad_w : -1;
   const int sw = stride_w > 0 ? stride_w : stride;
+  const int pw = pad_w >= 0 ? pad_w : pad;
   s.Ho = (s.H + 2 * pad - s.KH) / stride + 1;
-  s.Wo = (s.W + 2 * pad - s.KW) / sw + 1;
+  s.Wo = (s.W + 2 * pw - s.KW) / sw + 1;
   TORCH_CHECK(s.Ho > 0 && s.Wo > 0, "empty conv output");
   TORCH_CHECK(s.Ci % 8 == 0, "conv kernels need Ci % 8 == 0 (pad channels), got ", s.Ci);
   TORCH_CHECK(x.numel() < (1ll << 31), "conv input too large for 32-bit gather offsets");
@@ -69,11 +71,11 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
                                                                 optional<Tensor> slab_sum,
                                                                 optional<Tensor> slab_sq,
                                                                 optional<Tensor> bias, bool relu,
-                                                                int stride_w) {
+                                                                int stride_w, int pad_w) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   c10::DeviceGuard g(x.device());
-  auto s = conv_shape(x, w, stride, pad, stride_w);
+  auto s = conv_shape(x, w, stride, pad, stride_w, pad_w);
   if (bias.has_value()) check_vec(*bias, s.Co, "bias");
   TORCH_CHECK(!(shift.has_value() && (bias.has_value() || relu)),
               "BN-statistics epilogue and bias/ReLU epilogue are exclusive");
@@ -107,7 +109,7 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
 Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride, int pad,
                   optional<Tensor> addend, optional<Tensor> bn_y, optional<Tensor> bn_mean,
                   optional<Tensor> bn_invstd, optional<Tensor> bn_scale, optional<Tensor> bn_bias,
-                  optional<Tensor> bn_rep, optional<Tensor> bn_z) {
+                  optional<Tensor> bn_rep, optional<Tensor> bn_z, int pad_w) {
   check_bf16(dy, "dy");
   check_bf16(w, "w");
   c10::DeviceGuard g(dy.device());
@@ -116,14 +118,15 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
   s.N = (int)x_shape[0]; s.H = (int)x_shape[1]; s.W = (int)x_shape[2]; s.Ci = (int)x_shape[3];
   s.Co = (int)w.size(0); s.KH = (int)w.size(1); s.KW = (int)w.size(2);
   TORCH_CHECK(w.size(3) == s.Ci, "weight/input channel mismatch");
-  s.stride = stride; s.pad = pad;
+  s.stride = stride; s.pad = pad; s.pad_w = pad_w >= 0 ? pad_w : -1;
+  const int pw = pad_w >= 0 ? pad_w : pad;
   s.Ho = (s.H + 2 * pad - s.KH) / stride + 1;
-  s.Wo = (s.W + 2 * pad - s.KW) / stride + 1;
+  s.Wo = (s.W + 2 * pw - s.KW) / stride + 1;
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo && dy.size(3) == s.Co,
               "dy shape does not match the convolution");
   TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv dgrad needs Ci, Co % 8 == 0");
   TORCH_CHECK(dy.numel() < (1ll << 31), "conv dgrad dy too large for 32-bit gather offsets");
-  TORCH_CHECK(s.pad < s.KH, "conv dgrad expects pad < kernel size");
+  TORCH_CHECK(s.pad < s.KH && pw < s.KW, "conv dgrad expects padding < kernel size");
   auto dx = torch::empty({s.N, s.H, s.W, s.Ci}, dy.options());
   mipipe::DgradFusion fz;
   bool any = false;
@@ -173,7 +176,7 @@ std::tuple<Tensor, Tensor> bn_bwd_collect(Tensor rep, int64_t C, optional<Tensor
 }
 
 Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, optional<Tensor> out,
-                  int stride_w) {
+                  int stride_w, int pad_w) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   c10::DeviceGuard g(dy.device());
@@ -181,8 +184,9 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
   s.N = (int)x.size(0); s.H = (int)x.size(1); s.W = (int)x.size(2); s.Ci = (int)x.size(3);
   s.Co = (int)dy.size(3); s.KH = kh; s.KW = kw; s.stride = stride; s.pad = pad;
   s.stride_w = stride_w > 0 ? stride_w : 0;
+  s.pad_w = pad_w >= 0 ? pad_w : -1;
   s.Ho = (s.H + 2 * pad - kh) / stride + 1;
-  s.Wo = (s.W + 2 * pad - kw) / (stride_w > 0 ? stride_w : stride) + 1;
+  s.Wo = (s.W + 2 * (pad_w >= 0 ? pad_w : pad) - kw) / (stride_w > 0 ? stride_w : stride) + 1;
   TORCH_CHECK(x.numel() < (1ll << 31), "conv wgrad input too large for 32-bit gather offsets");
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo, "dy/x mismatch");
   TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv wgrad needs Ci, Co % 8 == 0");
@@ -943,18 +947,19 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("shift") = py::none(), py::arg("slab_sum") = py::none(),
         py::arg("slab_sq") = py::none(), py::arg("bias") = py::none(), py::arg("relu") = false,
-        py::arg("stride_w") = 0);
+        py::arg("stride_w") = 0, py::arg("pad_w") = -1);
   m.attr("STAT_REPLICAS") = mipipe::kStatReplicas;
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("x_shape"),
         py::arg("stride"), py::arg("pad"), py::arg("addend") = py::none(),
         py::arg("bn_y") = py::none(), py::arg("bn_mean") = py::none(),
         py::arg("bn_invstd") = py::none(), py::arg("bn_scale") = py::none(),
         py::arg("bn_bias") = py::none(), py::arg("bn_rep") = py::none(),
-        py::arg("bn_z") = py::none());
+        py::arg("bn_z") = py::none(), py::arg("pad_w") = -1);
   m.def("bn_bwd_collect", &bn_bwd_collect, py::arg("rep"), py::arg("C"),
         py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
-        py::arg("stride"), py::arg("pad"), py::arg("out") = py::none(), py::arg("stride_w") = 0);
+        py::arg("stride"), py::arg("pad"), py::arg("out") = py::none(), py::arg("stride_w") = 0,
+        py::arg("pad_w") = -1);
   m.def("bn_finalize", &bn_finalize, py::arg("psum"), py::arg("psq"), py::arg("count"),
         py::arg("shift"), py::arg("gamma"), py::arg("beta"), py::arg("rm"), py::arg("rv"),
         py::arg("momentum"), py::arg("eps"), py::arg("zero_after") = true,

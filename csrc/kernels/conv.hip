@@ -115,9 +115,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const __bf16* __rest
 using namespace gk;
 
 static ConvGeom make_geom(int N, int H, int W, int C, int Ho, int Wo, int KH, int KW, int stride,
-                          int pad, int stride_w = 0) {
+                          int pad, int stride_w = 0, int pad_w = -1) {
   ConvGeom g;
   g.stride_w = stride_w > 0 ? stride_w : stride;
+  g.pad_w = pad_w >= 0 ? pad_w : pad;
   g.N = N; g.H = H; g.W = W; g.C = C; g.Ho = Ho; g.Wo = Wo;
   g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
   g.fHoWo = FastDiv((uint32_t)(Ho * Wo));
@@ -130,7 +131,7 @@ static ConvGeom make_geom(int N, int H, int W, int C, int Ho, int Wo, int KH, in
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 static bool is_dense(const ConvShape& s) {
-  return s.KH == 1 && s.KW == 1 && s.stride == 1 && s.pad == 0 &&
+  return s.KH == 1 && s.KW == 1 && s.stride == 1 && s.pad == 0 && s.pad_w <= 0 &&
          (s.stride_w == 0 || s.stride_w == 1);
 }
 
@@ -144,7 +145,7 @@ int conv_fwd_stat_rows(const ConvShape& s) {
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
               const float* st_shift, const ConvShape& s, hipStream_t st, const float* bias,
               bool relu) {
-  ConvGeom g = make_geom(s.N, s.H, s.W, s.Ci, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad, s.stride_w);
+  ConvGeom g = make_geom(s.N, s.H, s.W, s.Ci, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad, s.stride_w, s.pad_w);
   uint32_t M = (uint32_t)s.N * s.Ho * s.Wo;
   EpiParams e{};
   e.C = y; e.ldc = s.Co; e.M = M; e.N = s.Co; e.bias = bias; e.act = relu ? 1 : 0;
@@ -173,6 +174,7 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
   const __bf16* dyp = (const __bf16*)dy;
   const __bf16* wp = (const __bf16*)w;
   const int S = s.stride;
+  const int PW = s.pad_w >= 0 ? s.pad_w : s.pad;  // horizontal padding
   FastDiv fCo((uint32_t)s.Co);
   for (int ph = 0; ph < S; ++ph) {
     for (int pw = 0; pw < S; ++pw) {
@@ -184,13 +186,13 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
       // taps reaching this phase: kh = (ph + pad) mod S + S*a, kw likewise
       c.S = S; c.KW = s.KW;
       c.kh0 = (ph + s.pad) % S;
-      c.kw0 = (pw + s.pad) % S;
+      c.kw0 = (pw + PW) % S;
       int nkh = c.kh0 < s.KH ? (s.KH - c.kh0 + S - 1) / S : 0;
       int nkw = c.kw0 < s.KW ? (s.KW - c.kw0 + S - 1) / S : 0;
       c.nkw = std::max(nkw, 1);
       c.ntaps = nkh * nkw;
       c.dh0 = (ph + s.pad - c.kh0) / S;
-      c.dw0 = (pw + s.pad - c.kw0) / S;
+      c.dw0 = (pw + PW - c.kw0) / S;
       c.fnkw = FastDiv((uint32_t)c.nkw);
       c.fHcWc = FastDiv((uint32_t)(c.Hc * c.Wc));
       c.fWc = FastDiv((uint32_t)c.Wc);
@@ -236,7 +238,7 @@ static int pick_splits(uint32_t tiles, int nk, int Ci) {
 }
 
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st) {
-  ConvGeom g = make_geom(s.N, s.H, s.W, s.Ci, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad, s.stride_w);
+  ConvGeom g = make_geom(s.N, s.H, s.W, s.Ci, s.Ho, s.Wo, s.KH, s.KW, s.stride, s.pad, s.stride_w, s.pad_w);
   uint32_t Ntot = (uint32_t)(s.KH * s.KW * s.Ci);
   EpiParams e{};
   e.C = dw; e.ldc = Ntot; e.M = s.Co; e.N = Ntot;

@@ -110,6 +110,7 @@ struct ConvGeom {
   int KH, KW, stride, pad;
   FastDiv fHoWo, fWo, fC, fKW;
   int stride_w;          // horizontal stride (== stride for square strides)
+  int pad_w;             // horizontal padding (== pad for square padding)
 };
 
 template <int R, bool ALIGNED = false>
@@ -140,7 +141,7 @@ struct KCIm2col {
         uint32_t ho = fdiv(g.fWo, rem);
         uint32_t wo = rem - ho * (uint32_t)g.Wo;
         hi0[i] = (int)ho * g.stride - g.pad;
-        wi0[i] = (int)wo * g.stride_w - g.pad;
+        wi0[i] = (int)wo * g.stride_w - g.pad_w;
         rowoff[i] = (((int)img * g.H + hi0[i]) * g.W + wi0[i]) * g.C;
       } else {
         hi0[i] = wi0[i] = -100000;  // fails every bounds check
@@ -378,7 +379,7 @@ struct MCIm2colT {
     const uint32_t ho = fdiv(g.fWo, rem);
     const uint32_t wo = rem - ho * (uint32_t)g.Wo;
     const int hi = (int)ho * g.stride - g.pad + kh[i];
-    const int wi = (int)wo * g.stride_w - g.pad + kw[i];
+    const int wi = (int)wo * g.stride_w - g.pad_w + kw[i];
     const bool ok = colok[i] & (k < K) & ((unsigned)hi < (unsigned)g.H) &
                     ((unsigned)wi < (unsigned)g.W);
     const int off = (((int)img * g.H + hi) * g.W + wi) * g.C + ci[i];

@@ -13,6 +13,7 @@ struct ConvShape {
   int Co, KH, KW, stride, pad;
   int Ho, Wo;        // output
   int stride_w = 0;  // horizontal stride when != stride (0: same); fwd / wgrad only
+  int pad_w = -1;    // horizontal padding when >= 0 (else pad): Inception 1x7 / 7x1 convs
 };
 
 // BatchNorm statistics are accumulated with fp32 atomics into kStatReplicas replica rows of a

@@ -466,6 +466,152 @@ __global__ __launch_bounds__(256) void bn_generic_bwd_apply_kernel(
   }
 }
 
+// ---- 16-byte vector variants (C % 8 == 0, C <= 2048): a thread owns one 8-channel group and
+// strides over rows (tpr = C/8 threads per row, rpb = 256/tpr rows per block pass), so the
+// per-channel coefficients stay in registers; reductions go through LDS (stride 9: conflict-free
+// column reads), then one atomic per channel per block.
+__device__ __forceinline__ void lds_reduce_atomic8(float* sh, const float* v, int tpr, int rpb,
+                                                   float* out) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sh[t * 9 + k] = v[k];
+  __syncthreads();
+  if (t < tpr) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < rpb; ++g)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += sh[(g * tpr + t) * 9 + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(out + t * 8 + k, s[k]);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void chan_stats_v8_kernel(const __bf16* __restrict__ y,
+                                                            const float* __restrict__ shift,
+                                                            long M, int C,
+                                                            float* __restrict__ psum,
+                                                            float* __restrict__ psq) {
+  __shared__ float sh[256 * 9];
+  const int tpr = C / 8, rpb = 256 / tpr;
+  const int t = threadIdx.x, cg = t % tpr, rg = t / tpr;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rg < rpb) {
+    float sf[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sf[k] = shift[cg * 8 + k];
+    for (long r = (long)blockIdx.x * rpb + rg; r < M; r += (long)gridDim.x * rpb) {
+      float v[8];
+      load8(y + r * C + cg * 8, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = v[k] - sf[k];
+        s[k] += d;
+        q[k] += d * d;
+      }
+    }
+  }
+  lds_reduce_atomic8(sh, s, tpr, rpb, psum);
+  lds_reduce_atomic8(sh, q, tpr, rpb, psq);
+}
+
+__global__ __launch_bounds__(256) void affine_act_v8_kernel(const __bf16* __restrict__ y,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ bias,
+                                                            __bf16* __restrict__ z, long M, int C,
+                                                            int act) {
+  const int tpr = C / 8, rpb = 256 / tpr;
+  const int t = threadIdx.x, cg = t % tpr, rg = t / tpr;
+  if (rg >= rpb) return;
+  float sc[8], bi[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = scale[cg * 8 + k];
+    bi[k] = bias[cg * 8 + k];
+  }
+  for (long r = (long)blockIdx.x * rpb + rg; r < M; r += (long)gridDim.x * rpb) {
+    const long off = r * C + cg * 8;
+    float v[8];
+    load8(y + off, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = act_apply(v[k] * sc[k] + bi[k], act);
+    *reinterpret_cast<uint4*>(z + off) = pack8(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_generic_bwd_reduce_v8_kernel(
+    const __bf16* __restrict__ dz, const __bf16* __restrict__ z, const __bf16* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd, long M, int C, int act,
+    float* __restrict__ out_g, float* __restrict__ out_gx) {
+  __shared__ float sh[256 * 9];
+  const int tpr = C / 8, rpb = 256 / tpr;
+  const int t = threadIdx.x, cg = t % tpr, rg = t / tpr;
+  float sg[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float sx[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rg < rpb) {
+    float mu[8], is[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      mu[k] = mean[cg * 8 + k];
+      is[k] = invstd[cg * 8 + k];
+    }
+    for (long r = (long)blockIdx.x * rpb + rg; r < M; r += (long)gridDim.x * rpb) {
+      const long off = r * C + cg * 8;
+      float g[8], v[8];
+      load8(dz + off, g);
+      if (act != 0) mask8(z + off, act, g);
+      load8(y + off, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        sg[k] += g[k];
+        sx[k] += g[k] * (v[k] - mu[k]) * is[k];
+      }
+    }
+  }
+  lds_reduce_atomic8(sh, sg, tpr, rpb, out_g);
+  lds_reduce_atomic8(sh, sx, tpr, rpb, out_gx);
+}
+
+// dy = A·g + B + Cc·(y - mean) with A = γ·invstd, B = -A·Σg/n, Cc = -A·invstd·Σg·x̂/n
+__global__ __launch_bounds__(256) void bn_generic_bwd_apply_v8_kernel(
+    const __bf16* __restrict__ dz, const __bf16* __restrict__ z, const __bf16* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ gamma, const float* __restrict__ sum_g,
+    const float* __restrict__ sum_gx, float inv_count, long M, int C, int act,
+    __bf16* __restrict__ dy) {
+  const int tpr = C / 8, rpb = 256 / tpr;
+  const int t = threadIdx.x, cg = t % tpr, rg = t / tpr;
+  if (rg >= rpb) return;
+  float A[8], B[8], Cc[8], mu[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = cg * 8 + k;
+    A[k] = gamma[c] * invstd[c];
+    B[k] = sum_g ? -A[k] * sum_g[c] * inv_count : 0.f;
+    Cc[k] = sum_g ? -A[k] * invstd[c] * sum_gx[c] * inv_count : 0.f;
+    mu[k] = mean[c];
+  }
+  for (long r = (long)blockIdx.x * rpb + rg; r < M; r += (long)gridDim.x * rpb) {
+    const long off = r * C + cg * 8;
+    float g[8], v[8];
+    load8(dz + off, g);
+    if (act != 0) mask8(z + off, act, g);
+    load8(y + off, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = A[k] * g[k] + B[k] + Cc[k] * (v[k] - mu[k]);
+    *reinterpret_cast<uint4*>(dy + off) = pack8(g);
+  }
+}
+
+static bool bn_v8(int C) { return C % 8 == 0 && C <= 2048; }
+
+static int v8_grid(long M, int C, int cap) {
+  const int rpb = 256 / (C / 8);
+  long g = (M + rpb - 1) / rpb;
+  return (int)std::max<long>(1, std::min<long>(g, cap));
+}
+
 static dim3 chan_grid(long M, int C) {
   const int bx = (C + 63) / 64;
   long by = std::max<long>(1, std::min<long>((M + 63) / 64, std::max(1, 2048 / bx)));
@@ -474,12 +620,22 @@ static dim3 chan_grid(long M, int C) {
 
 void chan_stats(const void* y, const float* shift, long M, int C, float* psum, float* psq,
                 hipStream_t st) {
+  if (bn_v8(C)) {
+    hipLaunchKernelGGL(chan_stats_v8_kernel, dim3(v8_grid(M, C, 512)), dim3(256), 0, st,
+                       (const __bf16*)y, shift, M, C, psum, psq);
+    return;
+  }
   hipLaunchKernelGGL(chan_stats_kernel, chan_grid(M, C), dim3(64, 4), 0, st, (const __bf16*)y,
                      shift, M, C, psum, psq);
 }
 
 void affine_act(const void* y, const float* scale, const float* bias, void* z, long M, int C,
                 int act, hipStream_t st) {
+  if (bn_v8(C)) {
+    hipLaunchKernelGGL(affine_act_v8_kernel, dim3(v8_grid(M, C, 4096)), dim3(256), 0, st,
+                       (const __bf16*)y, scale, bias, (__bf16*)z, M, C, act);
+    return;
+  }
   long n = M * C;
   hipLaunchKernelGGL(affine_act_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const __bf16*)y,
                      scale, bias, (__bf16*)z, n, C, act);
@@ -488,6 +644,12 @@ void affine_act(const void* y, const float* scale, const float* bias, void* z, l
 void bn_generic_bwd_reduce(const void* dz, const void* z, const void* y, const float* mean,
                            const float* invstd, long M, int C, int act, float* out_g,
                            float* out_gx, hipStream_t st) {
+  if (bn_v8(C)) {
+    hipLaunchKernelGGL(bn_generic_bwd_reduce_v8_kernel, dim3(v8_grid(M, C, 512)), dim3(256), 0,
+                       st, (const __bf16*)dz, (const __bf16*)z, (const __bf16*)y, mean, invstd, M,
+                       C, act, out_g, out_gx);
+    return;
+  }
   hipLaunchKernelGGL(bn_generic_bwd_reduce_kernel, chan_grid(M, C), dim3(64, 4), 0, st,
                      (const __bf16*)dz, (const __bf16*)z, (const __bf16*)y, mean, invstd, M, C,
                      act, out_g, out_gx);
@@ -497,6 +659,12 @@ void bn_generic_bwd_apply(const void* dz, const void* z, const void* y, const fl
                           const float* invstd, const float* gamma, const float* sum_g,
                           const float* sum_gx, long count, long M, int C, int act, void* dy,
                           hipStream_t st) {
+  if (bn_v8(C)) {
+    hipLaunchKernelGGL(bn_generic_bwd_apply_v8_kernel, dim3(v8_grid(M, C, 4096)), dim3(256), 0,
+                       st, (const __bf16*)dz, (const __bf16*)z, (const __bf16*)y, mean, invstd,
+                       gamma, sum_g, sum_gx, 1.f / (float)count, M, C, act, (__bf16*)dy);
+    return;
+  }
   long n = M * C;
   hipLaunchKernelGGL(bn_generic_bwd_apply_kernel, dim3(grid_for(n)), dim3(256), 0, st,
                      (const __bf16*)dz, (const __bf16*)z, (const __bf16*)y, mean, invstd, gamma,

@@ -54,7 +54,7 @@ def conv_bn(x: torch.Tensor, conv: mnn.XConv2d, bn: tnn.BatchNorm2d, act: str = 
     cin = x.shape[-1]
     if conv.dense(cin) and conv.bias is None and act in ("none", "relu"):
         w_c = conv.kernel_weight(x.dtype, cin)
-        s, p = conv.stride[0], conv.padding[0]
+        s, p = conv.stride[0], conv.mfma_pad()
         if bn.training:
             ws = MF.bn_workspace(bn, "fwd", x.device)
             y, ps, pss = MF.conv2d(x, conv.weight, w_c, s, p, bn.running_mean,

@@ -128,10 +128,15 @@ class XConv2d(ShadowMixin, tnn.Conv2d):
     def dense(self, cin: int) -> bool:
         """Runs on the MFMA implicit-GEMM kernels for an NHWC input with ``cin`` channels."""
         kh, kw = self.kernel_size
-        return (self.groups == 1 and kh == kw and self.dilation == (1, 1)
-                and self.padding_mode == "zeros" and not isinstance(self.padding, str)
-                and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
-                and self.padding[0] < kh and cin % 8 == 0 and self.out_channels % 8 == 0)
+        return (self.groups == 1 and self.dilation == (1, 1) and self.padding_mode == "zeros"
+                and not isinstance(self.padding, str) and self.stride[0] == self.stride[1]
+                and self.padding[0] < kh and self.padding[1] < kw
+                and cin % 8 == 0 and self.out_channels % 8 == 0)
+
+    def mfma_pad(self):
+        """Padding argument of the MFMA kernels: an int, or (h, w) for 1xn / nx1 convs."""
+        ph, pw = self.padding
+        return ph if ph == pw else (ph, pw)
 
     def kernel_weight(self, dtype: torch.dtype, cin: int) -> torch.Tensor:
         """Operand weight; input channels zero-padded to ``cin`` (padded NHWC stem input)."""
@@ -149,8 +154,8 @@ class XConv2d(ShadowMixin, tnn.Conv2d):
         if self.dense(cin) and act in ("none", "relu"):
             if self.bias is not None or act == "relu":
                 return MF.conv2d_bias_act(x, self.weight, w_c, self.bias, self.stride[0],
-                                          self.padding[0], act == "relu")
-            return MF.conv2d(x, self.weight, w_c, self.stride[0], self.padding[0])[0]
+                                          self.mfma_pad(), act == "relu")
+            return MF.conv2d(x, self.weight, w_c, self.stride[0], self.mfma_pad())[0]
         return MF.gconv2d(x, self.weight, w_c, self.bias, self.stride, self.padding,
                           self.groups, act)
 

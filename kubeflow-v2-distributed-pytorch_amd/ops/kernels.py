@@ -39,16 +39,22 @@ def use_native(t: torch.Tensor) -> bool:
         "`python setup.py build_ext --inplace`).  Set MIPIPE_ALLOW_REF_ON_GPU=1 only to debug.")
 
 
+def _pads(pad):
+    """(vertical, horizontal) padding for the kernels; -1 = same as vertical."""
+    return (pad, -1) if isinstance(pad, int) else (int(pad[0]), int(pad[1]))
+
+
 def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None, bias=None, relu=False):
     """``slabs``: persistent zeroed (sum, sumsq) replica slabs the GPU epilogue accumulates BN
     statistics into (re-zeroed by :func:`bn_finalize`).  ``bias`` / ``relu``: epilogue bias and
     ReLU for convolutions without BatchNorm (exclusive with the statistics epilogue)."""
     sh, sw = (stride, 0) if isinstance(stride, int) else (stride[0], stride[1])
+    ph, pw = _pads(pad)
     if use_native(x):
         s1, s2 = slabs if slabs is not None else (None, None)
-        return native().conv_fwd(x, w, sh, pad, stats_shift, s1, s2, bias, relu, sw)
-    y, a, b = _ref.conv_fwd(x, w, stride if isinstance(stride, int) else tuple(stride), pad,
-                            stats_shift)
+        return native().conv_fwd(x, w, sh, ph, stats_shift, s1, s2, bias, relu, sw, pw)
+    y, a, b = _ref.conv_fwd(x, w, stride if isinstance(stride, int) else tuple(stride),
+                            pad if isinstance(pad, int) else tuple(pad), stats_shift)
     if bias is not None or relu:
         yf = _f(y) if bias is None else _f(y) + _f(bias)
         y = (torch.relu(yf) if relu else yf).to(x.dtype)
@@ -61,15 +67,16 @@ def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None):
     dx becomes g = dx·[z > 0] (z recomputed from y unless given) and Σg, Σg·x̂ accumulate into
     ``rep`` rows 0/1 (native only)."""
     if use_native(dy):
+        ph, pw = _pads(pad)
         if bnr is None:
-            return native().conv_dgrad(dy, w, list(x_shape), stride, pad, addend)
+            return native().conv_dgrad(dy, w, list(x_shape), stride, ph, addend, pad_w=pw)
         y, mean, invstd, scale, bias, rep = bnr[:6]
         z = bnr[6] if len(bnr) > 6 else None
-        return native().conv_dgrad(dy, w, list(x_shape), stride, pad, addend, y, mean, invstd,
-                                   scale, bias, rep, z)
+        return native().conv_dgrad(dy, w, list(x_shape), stride, ph, addend, y, mean, invstd,
+                                   scale, bias, rep, z, pw)
     if bnr is not None:
         raise RuntimeError("BN-reduce dgrad fusion is a native-kernel path")
-    dx = _ref.conv_dgrad(dy, w, x_shape, stride, pad)
+    dx = _ref.conv_dgrad(dy, w, x_shape, stride, pad if isinstance(pad, int) else tuple(pad))
     return dx if addend is None else (dx + addend).to(dx.dtype)
 
 
@@ -84,8 +91,10 @@ def conv_wgrad(dy, x, kh, kw, stride, pad, out=None):
     ``stride``: int or (vertical, horizontal)."""
     sh, sw = (stride, 0) if isinstance(stride, int) else (stride[0], stride[1])
     if use_native(dy):
-        return native().conv_wgrad(dy, x, kh, kw, sh, pad, out, sw)
-    dw = _ref.conv_wgrad(dy, x, kh, kw, stride if isinstance(stride, int) else tuple(stride), pad)
+        ph, pw = _pads(pad)
+        return native().conv_wgrad(dy, x, kh, kw, sh, ph, out, sw, pw)
+    dw = _ref.conv_wgrad(dy, x, kh, kw, stride if isinstance(stride, int) else tuple(stride),
+                         pad if isinstance(pad, int) else tuple(pad))
     if out is not None:
         out.add_(dw)
         return out

@@ -134,6 +134,7 @@ def test_graphed_step_matches_eager():
     a = create_model("resnet18", num_classes=10).cuda()
     b = copy.deepcopy(a)
     c = copy.deepcopy(a)
+    init = [p.detach().clone() for p in a.parameters()]
     opts = [SGD(m.parameters(), 0.05, momentum=0.9, weight_decay=1e-4) for m in (a, b, c)]
     assert graph_safe(b, opts[1])[0]
     x = torch.randn(32, 3, 32, 32, device="cuda")
@@ -154,6 +155,17 @@ def test_graphed_step_matches_eager():
     lb = [gs.replay(0).item() for _ in range(3)]
     torch.cuda.synchronize()
     assert abs(la[-1] - lb[-1]) < 3 * abs(la[-1] - lc[-1]) + 0.02 * abs(la[0]), (la, lb, lc)
-    for (n, p), (_, q), (_, r) in zip(a.named_parameters(), b.named_parameters(),
-                                      c.named_parameters()):
+    # weights per tensor; BN affine / bias vectors start at 0 or 1 and move by a few noisy
+    # updates, so per-vector cosines are dominated by atomic-order noise: their UPDATES
+    # (parameter - initial value) are compared in aggregate
+    vp, vq, vr = [], [], []
+    for (n, p), (_, q), (_, r), p0 in zip(a.named_parameters(), b.named_parameters(),
+                                          c.named_parameters(), init):
+        if p.dim() == 1:
+            vp.append((p.detach() - p0).flatten())
+            vq.append((q.detach() - p0).flatten())
+            vr.append((r.detach() - p0).flatten())
+            continue
         assert cos(p, q) > min(0.999, cos(p, r) - 0.01), (n, cos(p, q), cos(p, r))
+    va, vb, vc = torch.cat(vp), torch.cat(vq), torch.cat(vr)
+    assert cos(va, vb) > min(0.99, cos(va, vc) - 0.02), (cos(va, vb), cos(va, vc))
