@@ -58,6 +58,19 @@ def parse():
     return ap.parse_args()
 
 
+def _heartbeat(every_s: float = 30.0) -> None:
+    """Progress line on stderr while a long step runs (first-call kernel compilation of stock
+    MIOpen convs can take minutes)."""
+    import threading
+
+    def beat():
+        t0 = time.time()
+        while True:
+            time.sleep(every_s)
+            print(f"bench alive {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main() -> int:
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -69,6 +82,8 @@ def main() -> int:
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     torch.manual_seed(0)
+    if rank == 0:
+        _heartbeat()
 
     is_bert = a.model.startswith("bert")
     if a.batch is None:
@@ -81,6 +96,8 @@ def main() -> int:
     model.train()
     for i in range(a.warmup):
         loss = step(*batches[i % 2])
+        if rank == 0:  # progress for long first steps (kernel autotuning, graph capture)
+            print(f"warmup step {i + 1}/{a.warmup}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -185,7 +202,8 @@ def build_cnn(a, world, local, dev, rank):
         from mipipe.models import create_model
         from mipipe.optim import SGD
         from mipipe.parallel import DistributedDataParallel
-        from mipipe.ops.functional import cross_entropy
+        from mipipe.train.task import CrossEntropyLoss
+        cross_entropy = CrossEntropyLoss()  # also sums GoogLeNet / Inception-v3 aux losses
         model = create_model(a.model, num_classes=a.classes).to(dev)
         model.compute_dtype = torch.bfloat16
         if world > 1:
@@ -214,19 +232,44 @@ def build_cnn(a, world, local, dev, rank):
             def step(x, y):  # noqa: F811
                 return gs.replay(ids[id(x)])
     else:
-        from mipipe.models.reference import ref_resnet
-        model = ref_resnet(a.model, num_classes=a.classes).to(dev).to(memory_format=torch.channels_last)
+        from mipipe.models.reference import _RESNET_CFG, ref_resnet
+        if a.model in _RESNET_CFG:
+            model = ref_resnet(a.model, num_classes=a.classes)
+            call = model
+        else:
+            # torchvision-structured zoo model: its plain-torch module tree (MIOpen convs/BN,
+            # ATen elementwise) is exactly stock PyTorch-ROCm running that architecture
+            from mipipe.models import create_model
+            if world > 1:
+                raise SystemExit("--impl stock: zoo models are benchmarked on one GPU")
+            model = create_model(a.model, num_classes=a.classes)
+            call = model.reference_forward
+        # channels_last for the ResNets (MIOpen's fastest layout there, as measured for
+        # BASELINE.md); default NCHW for the zoo (MIOpen's NHWC depthwise / grouped convs are
+        # several times slower than its NCHW ones)
+        cl = a.model in _RESNET_CFG
+        model = model.to(dev).to(memory_format=torch.channels_last if cl else torch.contiguous_format)
         if world > 1:
             model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local])
+            call = model
         opt = torch.optim.SGD(model.parameters(), 0.1, momentum=0.9, weight_decay=1e-4)
-        crit = torch.nn.CrossEntropyLoss()
-        torch.backends.cudnn.benchmark = True
-        batches = [(x.contiguous(memory_format=torch.channels_last), y) for x, y in batches]
+        # MIOpen benchmark-mode search for ResNets (as measured for BASELINE.md); the zoo's many
+        # depthwise / grouped shapes use MIOpen's immediate mode (the search takes minutes)
+        torch.backends.cudnn.benchmark = a.model in _RESNET_CFG
+        if cl:
+            batches = [(x.contiguous(memory_format=torch.channels_last), y) for x, y in batches]
+
+        def crit(out, y):
+            f = torch.nn.functional.cross_entropy
+            if isinstance(out, tuple):  # aux heads, weighted like mipipe's CrossEntropyLoss
+                w = 0.4 if len(out) == 2 else 0.3
+                return f(out[0], y) + sum(w * f(o, y) for o in out[1:] if o is not None)
+            return f(out, y)
 
         def step(x, y):
             opt.zero_grad(set_to_none=True)
             with torch.autocast("cuda", dtype=torch.bfloat16):
-                loss = crit(model(x), y)
+                loss = crit(call(x), y)
             loss.backward()
             opt.step()
             return loss

@@ -156,6 +156,14 @@ class XConv2d(ShadowMixin, tnn.Conv2d):
                 return MF.conv2d_bias_act(x, self.weight, w_c, self.bias, self.stride[0],
                                           self.mfma_pad(), act == "relu")
             return MF.conv2d(x, self.weight, w_c, self.stride[0], self.mfma_pad())[0]
+        kh, kw = self.kernel_size
+        gb = MF.grouped_conv_mfma_blocks(self.groups, w_c.shape[-1],
+                                         self.out_channels // self.groups)
+        if (gb and act == "none" and self.bias is None and self.stride[0] == self.stride[1]
+                and self.padding[0] < kh and self.padding[1] < kw):
+            # ResNeXt-style groups (4..64 channels): block-diagonal dense convs on the MFMA
+            return MF.block_group_conv2d(x, self.weight, w_c, self.stride[0], self.mfma_pad(),
+                                         self.groups, gb)
         return MF.gconv2d(x, self.weight, w_c, self.bias, self.stride, self.padding,
                           self.groups, act)
 

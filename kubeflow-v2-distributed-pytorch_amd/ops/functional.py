@@ -249,6 +249,75 @@ class _GConvFn(Function):
         return dx, dw, None, db, None, None, None, None
 
 
+class _BlockGroupConvFn(Function):
+    """Grouped convolution on the MFMA implicit-GEMM kernels: ``gb`` groups at a time form one
+    dense conv with a block-diagonal weight (channel blocks of gb*Cig inputs / gb*Cog outputs,
+    64 wide), so ResNeXt's 4..32-channel groups run on matrix cores instead of a scalar direct
+    kernel.  The off-diagonal zeros cost gb x the grouped FLOPs at MFMA rate; wgrad keeps only
+    the diagonal blocks of the dense weight gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight, w_c, stride, pad, groups, gb):
+        Co, kh, kw, cig = w_c.shape
+        cog = Co // groups
+        nb = groups // gb
+        eye = torch.eye(gb, dtype=w_c.dtype, device=w_c.device)
+        wbd = (w_c.view(nb, gb, cog, kh, kw, 1, cig) * eye.view(1, gb, 1, 1, 1, gb, 1))
+        wbd = wbd.reshape(nb, gb * cog, kh, kw, gb * cig)
+        bi, bo = gb * cig, gb * cog
+        ys = []
+        for b in range(nb):
+            xb = x if nb == 1 else x[..., b * bi:(b + 1) * bi].contiguous()
+            ys.append(K.conv_fwd(xb, wbd[b].contiguous(), stride, pad)[0])
+        ctx.save_for_backward(x, wbd)
+        ctx.weight = weight
+        ctx.conf = (stride, pad, groups, gb, kh, kw, cig, cog)
+        return ys[0] if nb == 1 else torch.cat(ys, dim=-1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wbd = ctx.saved_tensors
+        stride, pad, groups, gb, kh, kw, cig, cog = ctx.conf
+        nb = groups // gb
+        bi, bo = gb * cig, gb * cog
+        dy = dy.contiguous()
+        dxs, dws = [], []
+        for b in range(nb):
+            xb = x if nb == 1 else x[..., b * bi:(b + 1) * bi].contiguous()
+            dyb = dy if nb == 1 else dy[..., b * bo:(b + 1) * bo].contiguous()
+            if ctx.needs_input_grad[0]:
+                dxs.append(K.conv_dgrad(dyb, wbd[b].contiguous(), xb.shape, stride, pad))
+            if ctx.needs_input_grad[1]:
+                dwb = K.conv_wgrad(dyb, xb, kh, kw, stride, pad)  # [bo, kh, kw, bi]
+                d = torch.diagonal(dwb.view(gb, cog, kh, kw, gb, cig), dim1=0, dim2=4)
+                dws.append(d.permute(4, 0, 1, 2, 3))  # [gb, cog, kh, kw, cig]
+        dx = None if not dxs else (dxs[0] if nb == 1 else torch.cat(dxs, dim=-1))
+        dw = None
+        if dws:
+            dw = torch.cat(dws, 0).reshape(groups * cog, kh, kw, cig).permute(0, 3, 1, 2)
+            dw = dw.to(ctx.weight.dtype)
+        return dx, dw, None, None, None, None, None
+
+
+def grouped_conv_mfma_blocks(groups: int, cig: int, cog: int, width: int = 64) -> int:
+    """Groups per block for the block-diagonal MFMA path (0: not applicable).  Depthwise convs
+    (1 channel per group) stay on the vector direct kernels: a 64x waste is not worth it."""
+    if groups == 1 or cig != cog or cig < 4 or cig % 4:
+        return 0
+    if cig >= width:
+        return 1 if cig % 8 == 0 else 0
+    gb = width // cig
+    if width % cig or groups % gb or (gb * cig) % 8:
+        return 0
+    return gb
+
+
+def block_group_conv2d(x: Tensor, weight: Tensor, w_c: Tensor, stride: int, pad, groups: int,
+                       gb: int) -> Tensor:
+    """Grouped NHWC convolution as block-diagonal dense convs on the MFMA kernels."""
+    return _BlockGroupConvFn.apply(x, weight, w_c, stride, pad, int(groups), int(gb))
+
+
 def gconv2d(x: Tensor, weight: Tensor, w_c: Tensor, bias: Optional[Tensor], stride, pad,
             groups: int, act: str = "none") -> Tensor:
     """NHWC convolution with ``groups`` and (h, w) stride / padding on the direct kernels;

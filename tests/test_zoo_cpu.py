@@ -97,7 +97,7 @@ PARITY = [
     ("densenet121", {}, 32),
     ("googlenet", dict(dropout=0.0, dropout_aux=0.0), 64),
     ("inception_v3", dict(dropout=0.0), 299),
-    ("resnext50_32x4d", {}, 32),
+    ("resnext50_32x4d", {}, 64),
 ]
 
 

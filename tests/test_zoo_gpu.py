@@ -94,6 +94,31 @@ def test_mfma_conv_nonsquare_padding(k, p):
     assert rel_err(dw, _ref.conv_wgrad(dy.float(), x.float(), k[0], k[1], 1, p)) < 1e-2
 
 
+@pytest.mark.parametrize("Ci,groups,stride", [(128, 32, 1), (256, 32, 2), (512, 32, 1),
+                                              (2048, 32, 1)])
+def test_block_group_conv_mfma(Ci, groups, stride):
+    """ResNeXt grouped 3x3 convs as block-diagonal dense convs on the MFMA kernels, vs torch's
+    fp32 grouped conv (forward, input and weight gradients through autograd)."""
+    from mipipe.ops import functional as MF
+    N, H = 2, 9
+    cig = Ci // groups
+    gb = MF.grouped_conv_mfma_blocks(groups, cig, cig)
+    assert gb > 0
+    x = bf(N, H, H, Ci).requires_grad_()
+    wp = (torch.randn(Ci, cig, 3, 3, device=dev) / math.sqrt(cig * 9)).requires_grad_()
+    w_c = wp.detach().permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    y = MF.block_group_conv2d(x, wp, w_c, stride, 1, groups, gb)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    wr = w_c.float().permute(0, 3, 1, 2).detach().requires_grad_()
+    yr = torch.nn.functional.conv2d(xr, wr, stride=stride, padding=1, groups=groups)
+    assert rel_err(y, yr.permute(0, 2, 3, 1)) < 1e-2
+    dy = bf(*y.shape)
+    y.backward(dy)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    assert rel_err(x.grad, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    assert rel_err(wp.grad, wr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("C", [58, 96, 24, 200])
 @pytest.mark.parametrize("act", ["none", "relu", "relu6"])
 def test_bn_generic(C, act):
