@@ -97,14 +97,18 @@ def main(argv=None):
         ["--arch=mnist_cnn", "--dataset=mnist", "--batch_size=64", "--train-samples=512",
          "--test-samples=256", "--eval-every=1"]))
     ap.add_argument("--spec", default="dag.json")
+    ap.add_argument("--env-file", default=".env", help="PROJECT_ID / BUCKET (notebook nb:73-86)")
     a = ap.parse_args(argv)
     from mipipe.kfp.v2 import compiler
     from mipipe.kfp.v2.google.client import AIPlatformClient
+    from mipipe.utils import load_dotenv, pipeline_config
+    load_dotenv(a.env_file)  # the notebook's `%load_ext dotenv` + `%dotenv`
+    cfg = pipeline_config()
     stage_task_script()
     compiler.Compiler().compile(pipeline_func=pipeline, package_path=a.spec)
-    client = AIPlatformClient(project_id="local", region="local")
+    client = AIPlatformClient(project_id=cfg.project_id, region=cfg.region)
     resp = client.create_run_from_job_spec(
-        a.spec, pipeline_root="gs://test-pkl/pipeline_root",
+        a.spec, pipeline_root=cfg.pipeline_root,
         parameter_values={"baseline_accuracy": 80.0, "replica_count": a.replicas,
                           "accelerator_count": a.gpus_per_replica, "num_epochs": a.epochs,
                           "extra_args": a.extra_args}, sync=True)

@@ -75,3 +75,22 @@ def test_timeout(tmp_path):
     rc = launch(LaunchSpec(command=[sys.executable, str(script)], echo=False, timeout=1.0,
                            grace_period=1.0))
     assert rc == 124
+
+
+def test_dotenv_and_pipeline_config(tmp_path):
+    """Notebook driver config (nb:73-86): .env parsing + PIPELINE_ROOT derivation."""
+    from mipipe.utils import load_dotenv, parse_dotenv, pipeline_config
+    p = tmp_path / ".env"
+    p.write_text('# comment\nPROJECT_ID=my-proj\nexport BUCKET="my-bucket"  \n'
+                 "ROOT=gs://${BUCKET}/x # trailing comment\nRAW='${BUCKET}'\nEMPTY=\n")
+    env = {"BUCKET": "preset"}
+    vals = load_dotenv(str(p), environ=env)
+    assert vals["ROOT"] == "gs://my-bucket/x" and vals["RAW"] == "${BUCKET}" and vals["EMPTY"] == ""
+    assert env["BUCKET"] == "preset" and env["PROJECT_ID"] == "my-proj"  # existing vars win
+    load_dotenv(str(p), override=True, environ=env)
+    assert env["BUCKET"] == "my-bucket"
+    cfg = pipeline_config(env)
+    assert (cfg.project_id, cfg.bucket, cfg.region) == ("my-proj", "my-bucket", "us-central1")
+    assert cfg.pipeline_root == "gs://my-bucket/pipeline_root"
+    assert load_dotenv(str(tmp_path / "missing.env"), environ={}) == {}
+    assert parse_dotenv('A="x\\ny"', {})["A"] == "x\ny"
