@@ -128,3 +128,21 @@ def test_ddp_gloo_matches_single_process(double_report):
         opt.step()
     ref = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
     assert torch.allclose(f0, ref, atol=1e-5)
+
+
+def test_ddp_check_tool_cpu():
+    """tools/ddp_gpu_check.py on the CPU path (2 gloo ranks): bucket all-reduces intercepted --
+    no gradient lands after its bucket launched, reduced == sum of local gradients -- and the
+    ranks stay bit-identical."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    port = str(29100 + os.getpid() % 800)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", port,
+                        os.path.join(root, "tools", "ddp_gpu_check.py"), "--device", "cpu",
+                        "--arch", "resnet18"], capture_output=True, text=True, timeout=600,
+                       env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "step0 bucket check OK" in r.stdout and "DDP gpu check OK" in r.stdout
