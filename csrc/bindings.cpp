@@ -1015,6 +1015,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("stem_pack", &stem_pack);
   m.def("set_splitk_target", [](int v) { mipipe::g_splitk_target = std::max(1, v); });
   m.def("get_splitk_target", []() { return mipipe::g_splitk_target; });
+  m.def("set_stat_rows", [](int v) {
+    TORCH_CHECK(v >= 1 && v <= mipipe::kStatReplicas, "stat rows must be in [1, ", mipipe::kStatReplicas, "]");
+    mipipe::g_stat_rows = v;
+  });
   m.def("set_ns1_max_k", [](int v) { mipipe::g_ns1_max_k = v; });
   m.def("set_ns1_max_k_gather", [](int v) { mipipe::g_ns1_max_k_gather = v; });
 }

@@ -149,7 +149,7 @@ void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq
   uint32_t M = (uint32_t)s.N * s.Ho * s.Wo;
   EpiParams e{};
   e.C = y; e.ldc = s.Co; e.M = M; e.N = s.Co; e.bias = bias; e.act = relu ? 1 : 0;
-  e.st_sum = st_sum; e.st_sq = st_sq; e.st_shift = st_shift; e.st_R = kStatReplicas;
+  e.st_sum = st_sum; e.st_sq = st_sq; e.st_shift = st_shift; e.st_R = g_stat_rows;
   const bool dense = is_dense(s);
   const __bf16* xp = (const __bf16*)x;
   const __bf16* wp = (const __bf16*)w;
@@ -203,7 +203,7 @@ void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hip
         e.addend = (const __bf16*)fz->addend;
         e.bnr_y = (const __bf16*)fz->bn_y;
         e.bnr_mean = fz->bn_mean; e.bnr_invstd = fz->bn_invstd;
-        e.bnr_scale = fz->bn_scale; e.bnr_bias = fz->bn_bias; e.bnr_rep = fz->bn_rep;
+        e.bnr_scale = fz->bn_scale; e.bnr_bias = fz->bn_bias; e.bnr_rep = fz->bn_rep; e.st_R = g_stat_rows;
         e.bnr_z = (const __bf16*)fz->bn_z;
       }
       if (S > 1) {

@@ -36,6 +36,13 @@ struct EpiParams {
   const __bf16* bnr_z;
 };
 
+// Workgroup barrier that orders LDS only.  __syncthreads() also drains every outstanding global
+// load / store / atomic (s_waitcnt vmcnt(0)), which here would expose the latency of the
+// epilogue's prefetched operands and of the statistics atomics at every barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ long out_row(const EpiParams& e, uint32_t m) {
   if (e.rm_s == 0) return (long)m;
   uint32_t img = fdiv(e.rm_fHcWc, m);
@@ -144,18 +151,10 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
         }
       }
     }
-    __syncthreads();
-    for (int t = threadIdx.x; t < 2 * BN; t += kThreads) {
-      int arr = t / BN, c = t % BN;
-      uint32_t n = n0 + c;
-      if (n < e.N) {
-        float v = lst[(arr * 2 + 0) * BN + c] + lst[(arr * 2 + 1) * BN + c];
-        float* dst = (arr == 0 ? e.st_sum : e.st_sq) + (long)(blockIdx.x % e.st_R) * e.N + n;
-        atomicAdd(dst, v);
-      }
-    }
-    __syncthreads();
   }
+  // every wave is past the main loop (whose LDS the staging tile overwrites) and the
+  // statistics partials are in LDS
+  lds_barrier();
   // stage bf16 tile in LDS: pitch BN*2 + 16 bytes
   constexpr int P = BN * 2 + 16;
 #pragma unroll
@@ -166,7 +165,21 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
       uint2 v = make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
       *reinterpret_cast<uint2*>(smem + ml * P + nl * 2) = v;
     }
-  __syncthreads();
+  lds_barrier();
+  if (e.st_sum != nullptr) {
+    // one fp32 atomic per column per block into replica row blockIdx % st_R (fire and forget:
+    // no barrier below waits for them)
+    const float* lst = reinterpret_cast<const float*>(smem + kStatsLdsOffset<BM, BN>());
+    for (int t = threadIdx.x; t < 2 * BN; t += kThreads) {
+      int arr = t / BN, c = t % BN;
+      uint32_t n = n0 + c;
+      if (n < e.N) {
+        float v = lst[(arr * 2 + 0) * BN + c] + lst[(arr * 2 + 1) * BN + c];
+        float* dst = (arr == 0 ? e.st_sum : e.st_sq) + (long)(blockIdx.x % e.st_R) * e.N + n;
+        atomicAdd(dst, v);
+      }
+    }
+  }
   __bf16* C = reinterpret_cast<__bf16*>(e.C);
   float b_sc[8], b_bi[8], b_mu[8], b_is[8], sg[8], sgx[8];
 #pragma unroll
@@ -217,21 +230,21 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
   if (FUSE && bnr) {
     // threads t, t+CPR, ... share a column chunk: reduce them through LDS, then one atomic
     // per column per block into replica row blockIdx % R
-    __syncthreads();
+    lds_barrier();  // all staging-tile reads done (red overlaps it)
     float* red = reinterpret_cast<float*>(smem);  // [kThreads][16]
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       red[threadIdx.x * 16 + q] = sg[q];
       red[threadIdx.x * 16 + 8 + q] = sgx[q];
     }
-    __syncthreads();
-    const uint32_t R = kStatReplicas;
+    lds_barrier();
+    const uint32_t R = kStatReplicas, Rw = (uint32_t)e.st_R;  // layout rows / rows written
     for (int j = threadIdx.x; j < 2 * BN; j += kThreads) {
       const int arr = j / BN, col = j % BN, cc = col >> 3, q = col & 7;
       float a = 0.f;
       for (int t = cc; t < kThreads; t += CPR) a += red[t * 16 + arr * 8 + q];
       if (n0 + col < e.N)
-        atomicAdd(e.bnr_rep + ((long)arr * R + blockIdx.x % R) * e.N + n0 + col, a);
+        atomicAdd(e.bnr_rep + ((long)arr * R + blockIdx.x % Rw) * e.N + n0 + col, a);
     }
   }
 }

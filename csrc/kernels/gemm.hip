@@ -7,6 +7,7 @@
 namespace mipipe {
 int g_splitk_target = 512;
 int g_ns1_max_k_gather = 1152;  // measured: tools/sweep_ns1_gather.py (profiles/r1_ns1_gather_sweep.jsonl)
+int g_stat_rows = kStatReplicas;
 int g_ns1_max_k = 512;  // measured: tools/sweep_ns1.py (profiles/r1_ns1_sweep.jsonl)
 namespace gk {
 

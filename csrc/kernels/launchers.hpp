@@ -19,7 +19,13 @@ struct ConvShape {
 // BatchNorm statistics are accumulated with fp32 atomics into kStatReplicas replica rows of a
 // [R][C] slab (spreads contention); the consumer (bn_finalize / bwd finalize) reduces the R rows
 // and ZEROES the slab again, so a persistent zero-initialised slab can be reused every step.
+// The slab LAYOUT always has kStatReplicas rows; kernels write rows blockIdx % g_stat_rows
+// (<= kStatReplicas; the rest stay zero), so the spread is tunable at runtime for sweeps.
+// Measured (profiles/r1_stat_rows_probe.jsonl): 64 rows save <= 8 % on the widest statistics
+// epilogues but make the per-channel finalize / collect kernels (one thread per channel summing
+// every row) 10-35x slower — a net ResNet-50 loss of 30 % — so the layout stays at 16.
 constexpr int kStatReplicas = 16;
+extern int g_stat_rows;
 // Split-K sizing for the atomically-accumulated weight-gradient GEMMs: splits are chosen so
 // that tiles * splits ~= this many workgroups (tunable at runtime for sweeps).
 extern int g_splitk_target;
