@@ -146,3 +146,17 @@ def test_ddp_check_tool_cpu():
                        env=env, cwd=root)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert "step0 bucket check OK" in r.stdout and "DDP gpu check OK" in r.stdout
+
+
+def test_data_parallel_passthrough_and_unwrap():
+    """DataParallel (reference task.py:201-208 path (d)) with <= 1 device is a pass-through, and
+    task.py's unwrap returns the inner module (so evaluation and export see torchvision keys)."""
+    from mipipe.parallel import DataParallel
+    from mipipe.train.task import _unwrap
+    torch.manual_seed(0)
+    inner = torch.nn.Sequential(torch.nn.Linear(8, 4), torch.nn.ReLU(), torch.nn.Linear(4, 3))
+    dp = DataParallel(inner)
+    x = torch.randn(5, 8)
+    torch.testing.assert_close(dp(x), inner(x))
+    assert _unwrap(dp) is inner
+    assert set(inner.state_dict()) == set(_unwrap(dp).state_dict())
