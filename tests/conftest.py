@@ -8,6 +8,13 @@ if REPO not in sys.path:
     sys.path.insert(0, REPO)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
+# Under pytest-xdist every worker would otherwise start one intra-op thread per CPU; the
+# oversubscribed OpenMP pools turn a 1.4 s fp64 parity test into minutes.  Split the CPUs.
+_nworkers = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "1") or 1)
+if _nworkers > 1:
+    import torch
+    torch.set_num_threads(max(1, (os.cpu_count() or 1) // _nworkers))
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")
