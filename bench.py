@@ -14,6 +14,15 @@ sides; the reported time is the MAX over ranks.
 Single GPU:   python bench.py --gpus 1 --steps 20 --warmup 5
 Multi GPU:    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
                   --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+          or  python bench.py --gpus N ...   (no WORLD_SIZE in the env: this process spawns the
+              N rank processes itself before anything touches HIP — task.py:117-124's mp.spawn —
+              and every rank checks that the process group really has N members)
+
+The training step is replayed from a captured hipGraph on 1 GPU AND under DDP: the bucket
+all-reduces (RCCL) and the per-forward buffer broadcast are captured into the same graph on
+the process group's stream, so their overlap with backward survives replay.
+``--force-reduce`` runs the whole DDP/RCCL path at world size 1 (profiling the collectives
+on a one-GPU box); ``--device cpu`` runs the same harness on gloo (CPU tests).
 """
 from __future__ import annotations
 
@@ -34,7 +43,7 @@ METRIC = "samples/sec (whole node) task.py DDP at 1/2/4/8 MI355X; scaling effici
 # vs_baseline = value / (comparator_per_gpu * n_gpus)  (ideal linear scaling of the comparator).
 # BERT-base MLM (B=32 x S=128 / B=8 x S=512 per GPU, AdamW fused, SDPA, bf16 autocast): stock
 # torch measured on the same MI355X with tools/gpu_bert.sh / gpu_prof_bert.sh.
-STOCK_1GPU = {"resnet50": 6580.1, "resnet18_32": 76880.3,
+STOCK_1GPU = {"resnet50": 6580.1, "resnet18_32": 76880.3, "resnet18_32_fp32": 75965.3,
               "bert_base_128": 2184.8, "bert_base_512": 540.8}
 
 
@@ -53,8 +62,14 @@ def parse():
     ap.add_argument("--impl", default="mipipe", choices=["mipipe", "stock"],
                     help="stock = torch DDP + MIOpen comparator")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                    help="replay the whole training step from a captured hipGraph (single GPU, "
-                         "SGD); auto = on when safe")
+                    help="replay the whole training step (incl. DDP collectives) from a captured "
+                         "hipGraph; auto = on when safe (SGD, no dropout)")
+    ap.add_argument("--force-reduce", action="store_true",
+                    help="wrap in DDP and issue every collective even at world size 1")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = gloo backend, fp32 (harness tests without a GPU)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="compute dtype of the mipipe kernels (fp32 = the reference's precision)")
     return ap.parse_args()
 
 
@@ -71,16 +86,44 @@ def _heartbeat(every_s: float = 30.0) -> None:
     threading.Thread(target=beat, daemon=True).start()
 
 
+def _sync(dev) -> None:
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def main() -> int:
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        # launched as `python bench.py --gpus N`: become the launcher (no HIP call so far)
+        from mipipe.launch.local import spawn_local_ranks
+        return spawn_local_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                 a.gpus)
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks",
+              file=sys.stderr)
+        return 2
+    cpu = a.device == "cpu"
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    distributed = world > 1 or a.force_reduce
+    if distributed:
+        if cpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != a.gpus:
+            print(f"bench.py rank {rank}: process group has {dist.get_world_size()} ranks, "
+                  f"expected {a.gpus}", file=sys.stderr)
+            return 3
+    a.distributed = distributed
     torch.manual_seed(0)
     if rank == 0:
         _heartbeat()
@@ -98,19 +141,19 @@ def main() -> int:
         loss = step(*batches[i % 2])
         if rank == 0:  # progress for long first steps (kernel autotuning, graph capture)
             print(f"warmup step {i + 1}/{a.warmup}", file=sys.stderr, flush=True)
-    torch.cuda.synchronize()
-    if world > 1:
+    _sync(dev)
+    if distributed:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(*batches[i % 2])
-    torch.cuda.synchronize()
-    if world > 1:
+    _sync(dev)
+    if distributed:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     dt = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -120,6 +163,8 @@ def main() -> int:
         opt_s = "AdamW(lr=1e-4,wd=0.01)"
     else:
         key = a.model if a.res == 224 else f"{a.model}_{a.res}"
+        if a.dtype == "fp32":
+            key += "_fp32"
         opt_s = "SGD(lr=0.1,momentum=0.9,wd=1e-4)"
     base = STOCK_1GPU.get(key)
     loss_v = float(loss.detach().float().item())
@@ -129,14 +174,16 @@ def main() -> int:
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / (base * world), 4) if base else None,
-            "dtype": "bf16", "data": "synthetic (on-device, random-init weights)",
+            "dtype": "fp32" if (cpu or a.dtype == "fp32") else "bf16",
+            "data": "synthetic (on-device, random-init weights)",
             "config": {"model": a.model, "global_batch": a.batch * world,
                        "seq_len": a.seq if is_bert else None,
                        "image_size": None if is_bert else a.res, "batch_per_gpu": a.batch,
                        "parallelism": f"dp{world}", "impl": a.impl, "optimizer": opt_s,
-                       "hip_graph": bool(getattr(a, "graph_used", False))},
+                       "hip_graph": bool(getattr(a, "graph_used", False)),
+                       "force_reduce": bool(a.force_reduce)},
             "final_loss": loss_v}), flush=True)
-    if world > 1:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
     return 0
@@ -162,9 +209,10 @@ def build_bert(a, world, local, dev, rank):
         from mipipe.optim import AdamW
         from mipipe.parallel import DistributedDataParallel
         model = create_model(a.model).to(dev)
-        model.compute_dtype = torch.bfloat16
-        if world > 1:
-            model = DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=a.bucket_cap_mb)
+        model.compute_dtype = _compute_dtype(a)
+        if a.distributed:
+            model = DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=a.bucket_cap_mb,
+                                            force_reduce=a.force_reduce)
         opt = AdamW(model.parameters(), lr=1e-4, weight_decay=0.01)
 
         def step(ids, am, pos, labels):
@@ -192,11 +240,16 @@ def build_bert(a, world, local, dev, rank):
     return step, model, batches
 
 
+def _compute_dtype(a):
+    return torch.float32 if (a.device == "cpu" or a.dtype == "fp32") else torch.bfloat16
+
+
 def build_cnn(a, world, local, dev, rank):
     from mipipe.data.synthetic import synthetic_batch
     idx = [torch.arange(i * a.batch, (i + 1) * a.batch, device=dev) + rank * 10_000_000
            for i in range(2)]
-    batches = [synthetic_batch(t, (3, a.res, a.res), a.classes, seed=0) for t in idx]
+    in_ch = 1 if a.model == "mnist_cnn" else 3
+    batches = [synthetic_batch(t, (in_ch, a.res, a.res), a.classes, seed=0) for t in idx]
 
     if a.impl == "mipipe":
         from mipipe.models import create_model
@@ -205,9 +258,10 @@ def build_cnn(a, world, local, dev, rank):
         from mipipe.train.task import CrossEntropyLoss
         cross_entropy = CrossEntropyLoss()  # also sums GoogLeNet / Inception-v3 aux losses
         model = create_model(a.model, num_classes=a.classes).to(dev)
-        model.compute_dtype = torch.bfloat16
-        if world > 1:
-            model = DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=a.bucket_cap_mb)
+        model.compute_dtype = _compute_dtype(a)
+        if a.distributed:
+            model = DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=a.bucket_cap_mb,
+                                            force_reduce=a.force_reduce)
         opt = SGD(model.parameters(), 0.1, momentum=0.9, weight_decay=1e-4)
 
         def step(x, y):
@@ -219,9 +273,11 @@ def build_cnn(a, world, local, dev, rank):
 
         from mipipe.train.graph import GraphedStep, graph_safe
         ok, why = graph_safe(model, opt)
-        if a.graph == "on" or (a.graph == "auto" and world == 1 and ok):
-            if world > 1 or not ok:
-                raise SystemExit(f"--graph on is not possible here: {why or 'multi-GPU DDP'}")
+        if dev.type == "cpu":
+            ok, why = False, "no hipGraph on the CPU"
+        if a.graph == "on" or (a.graph == "auto" and ok):
+            if not ok:
+                raise SystemExit(f"--graph on is not possible here: {why}")
             model.train()
             # one captured step per resident synthetic batch: replays issue every kernel of the
             # step (fwd, bwd, SGD) from one launch; no batch copies
@@ -266,9 +322,11 @@ def build_cnn(a, world, local, dev, rank):
                 return f(out[0], y) + sum(w * f(o, y) for o in out[1:] if o is not None)
             return f(out, y)
 
+        amp = a.dtype == "bf16" and dev.type == "cuda"
+
         def step(x, y):
             opt.zero_grad(set_to_none=True)
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
                 loss = crit(call(x), y)
             loss.backward()
             opt.step()

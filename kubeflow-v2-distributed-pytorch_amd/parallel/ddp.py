@@ -81,7 +81,8 @@ class DistributedDataParallel(tnn.Module):
                  process_group=None, bucket_cap_mb: float = 32.0, first_bucket_mb: float = 1.0,
                  comm_dtype: Optional[torch.dtype] = None, find_unused_parameters: bool = False,
                  check_collectives: Optional[bool] = None, check_every: int = 50,
-                 gradient_as_bucket_view: bool = True, static_graph: bool = False):
+                 gradient_as_bucket_view: bool = True, static_graph: bool = False,
+                 force_reduce: Optional[bool] = None):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -97,13 +98,20 @@ class DistributedDataParallel(tnn.Module):
         self._clog = _CollectiveLog()
         self._steps = 0
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        # force_reduce (or MIPIPE_DDP_FORCE_REDUCE=1): issue every collective even at world
+        # size 1, so the RCCL path (buffer broadcast, bucket all-reduces, their overlap with
+        # backward and their capture into a hipGraph) runs and can be profiled on one GPU.
+        if force_reduce is None:
+            force_reduce = os.environ.get("MIPIPE_DDP_FORCE_REDUCE", "0") == "1"
+        self.force_reduce = bool(force_reduce) and dist.is_initialized()
+        self._comm = self.world > 1 or self.force_reduce
         params = [p for p in module.parameters() if p.requires_grad]
         dev = params[0].device
         shadow = torch.bfloat16 if dev.type == "cuda" else None
         self.space: FlatParamSpace = get_flat_space(params, shadow, module)
         backend = dist.get_backend(process_group) if dist.is_initialized() else "none"
         self._avg_supported = backend == "nccl"
-        if self.world > 1:
+        if self._comm:
             self._verify_shapes(params)
             self._sync_module_states()
         self.buckets = self._build_buckets(bucket_cap_mb * 2 ** 20, first_bucket_mb * 2 ** 20)
@@ -184,7 +192,7 @@ class DistributedDataParallel(tnn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
-        if self.world > 1 and torch.is_grad_enabled() and self.broadcast_buffers \
+        if self._comm and torch.is_grad_enabled() and self.broadcast_buffers \
                 and self.require_forward_param_sync:
             self._broadcast_buffers_now()
         if torch.is_grad_enabled() and self.module.training:
@@ -216,7 +224,7 @@ class DistributedDataParallel(tnn.Module):
         self.space.ensure_grad_views()
 
     def _on_ready(self, param) -> None:
-        if self.world <= 1 or not self._sync_enabled:
+        if not self._comm or not self._sync_enabled:
             return
         b = self._bucket_of.get(id(param))
         if b is None:

@@ -1,0 +1,85 @@
+"""bench.py's driver contract on the CPU: `python bench.py --gpus N` spawns its own N ranks
+(task.py:117-124's one-process-per-GPU), every rank checks the process-group size, rank 0
+prints exactly one JSON line with n_gpus = N.  gloo stands in for RCCL here."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+CPU_ARGS = ["--device", "cpu", "--model", "mnist_cnn", "--res", "28", "--classes", "10",
+            "--batch", "8", "--steps", "2", "--warmup", "1"]
+
+
+def _env(**kw):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e["OMP_NUM_THREADS"] = "2"
+    e.update(kw)
+    return e
+
+
+def _json_lines(out: str):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_bench_self_spawn_gloo(n):
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(n)] + CPU_ARGS, env=_env(),
+                       capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout  # only rank 0 prints to stdout
+    j = lines[0]
+    assert j["n_gpus"] == n and j["config"]["parallelism"] == f"dp{n}"
+    assert j["config"]["global_batch"] == 8 * n
+    assert j["steps"] == 2 and j["warmup"] == 1 and j["value"] > 0
+
+
+def test_bench_force_reduce_world1_gloo():
+    """--force-reduce wraps in DDP and issues the collectives at world size 1."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--force-reduce"] + CPU_ARGS,
+                       env=_env(MASTER_ADDR="127.0.0.1", MASTER_PORT="0", WORLD_SIZE="1",
+                                RANK="0", LOCAL_RANK="0"),
+                       capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _json_lines(r.stdout)[0]
+    assert j["config"]["force_reduce"] is True and j["n_gpus"] == 1
+
+
+def test_bench_rejects_world_mismatch():
+    """A launcher that started fewer ranks than --gpus must not yield a silent 1-rank number."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "4"] + CPU_ARGS,
+                       env=_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"),
+                       capture_output=True, text=True, timeout=120, cwd="/tmp")
+    assert r.returncode != 0
+    assert _json_lines(r.stdout) == []
+
+
+def test_spawn_local_ranks_fail_fast(tmp_path):
+    from mipipe.launch.local import spawn_local_ranks
+    script = tmp_path / "s.py"
+    script.write_text(
+        "import os, sys, time\n"
+        "r = int(os.environ['RANK'])\n"
+        "assert os.environ['WORLD_SIZE'] == '3' and os.environ['LOCAL_RANK'] == str(r)\n"
+        "if r == 1: sys.exit(7)\n"
+        "time.sleep(60)\n")
+    import time
+    t0 = time.time()
+    rc = spawn_local_ranks([sys.executable, str(script)], 3, grace=2.0)
+    assert rc == 7
+    assert time.time() - t0 < 30  # the sleeping ranks were terminated
+
+
+def test_spawn_local_ranks_env_contract():
+    from mipipe.launch.local import rank_envs
+    envs = rank_envs(4, port=12345)
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert all(e["WORLD_SIZE"] == "4" and e["MASTER_ADDR"] == "127.0.0.1"
+               and e["MASTER_PORT"] == "12345" and e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+               for e in envs)
