@@ -25,6 +25,18 @@ void check_bf16(const Tensor& t, const char* name) {
   check_cuda(t, name);
   TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16, got ", t.scalar_type());
 }
+// activation tensors: bf16 (mixed precision) or fp32 (the reference's precision)
+void check_act(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, name,
+              " must be bfloat16 or float32, got ", t.scalar_type());
+}
+void check_same(const Tensor& t, const Tensor& ref, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == ref.scalar_type(), name, " must be ", ref.scalar_type(),
+              " like the other operands, got ", t.scalar_type());
+}
+bool is_f32(const Tensor& t) { return t.scalar_type() == at::kFloat; }
 void check_f32(const Tensor& t, const char* name) {
   check_cuda(t, name);
   TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32, got ", t.scalar_type());
@@ -72,10 +84,11 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
                                                                 optional<Tensor> slab_sq,
                                                                 optional<Tensor> bias, bool relu,
                                                                 int stride_w, int pad_w) {
-  check_bf16(x, "x");
-  check_bf16(w, "w");
+  check_act(x, "x");
+  check_same(w, x, "w");
   c10::DeviceGuard g(x.device());
   auto s = conv_shape(x, w, stride, pad, stride_w, pad_w);
+  s.f32 = is_f32(x);
   if (bias.has_value()) check_vec(*bias, s.Co, "bias");
   TORCH_CHECK(!(shift.has_value() && (bias.has_value() || relu)),
               "BN-statistics epilogue and bias/ReLU epilogue are exclusive");
@@ -110,11 +123,12 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
                   optional<Tensor> addend, optional<Tensor> bn_y, optional<Tensor> bn_mean,
                   optional<Tensor> bn_invstd, optional<Tensor> bn_scale, optional<Tensor> bn_bias,
                   optional<Tensor> bn_rep, optional<Tensor> bn_z, int pad_w) {
-  check_bf16(dy, "dy");
-  check_bf16(w, "w");
+  check_act(dy, "dy");
+  check_same(w, dy, "w");
   c10::DeviceGuard g(dy.device());
   TORCH_CHECK(x_shape.size() == 4, "x_shape must be [N,H,W,Ci]");
   mipipe::ConvShape s;
+  s.f32 = is_f32(dy);
   s.N = (int)x_shape[0]; s.H = (int)x_shape[1]; s.W = (int)x_shape[2]; s.Ci = (int)x_shape[3];
   s.Co = (int)w.size(0); s.KH = (int)w.size(1); s.KW = (int)w.size(2);
   TORCH_CHECK(w.size(3) == s.Ci, "weight/input channel mismatch");
@@ -131,7 +145,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
   mipipe::DgradFusion fz;
   bool any = false;
   if (addend.has_value()) {
-    check_bf16(*addend, "addend");
+    check_same(*addend, dy, "addend");
     TORCH_CHECK(addend->sizes() == dx.sizes(), "addend must match dx");
     fz.addend = addend->data_ptr();
     any = true;
@@ -139,7 +153,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
   if (bn_rep.has_value()) {
     TORCH_CHECK(bn_y.has_value() && bn_mean.has_value() && bn_invstd.has_value() &&
                 bn_scale.has_value() && bn_bias.has_value(), "BN fusion needs y/mean/invstd/scale/bias");
-    check_bf16(*bn_y, "bn_y");
+    check_same(*bn_y, dy, "bn_y");
     TORCH_CHECK(bn_y->sizes() == dx.sizes(), "bn_y must match dx");
     check_vec(*bn_mean, s.Ci, "bn_mean");
     check_vec(*bn_invstd, s.Ci, "bn_invstd");
@@ -152,7 +166,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     fz.bn_scale = bn_scale->data_ptr<float>(); fz.bn_bias = bn_bias->data_ptr<float>();
     fz.bn_rep = bn_rep->data_ptr<float>();
     if (bn_z.has_value()) {
-      check_bf16(*bn_z, "bn_z");
+      check_same(*bn_z, dy, "bn_z");
       TORCH_CHECK(bn_z->sizes() == dx.sizes(), "bn_z must match dx");
       fz.bn_z = bn_z->data_ptr();
     }
@@ -177,10 +191,11 @@ std::tuple<Tensor, Tensor> bn_bwd_collect(Tensor rep, int64_t C, optional<Tensor
 
 Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, optional<Tensor> out,
                   int stride_w, int pad_w) {
-  check_bf16(dy, "dy");
-  check_bf16(x, "x");
+  check_act(dy, "dy");
+  check_same(x, dy, "x");
   c10::DeviceGuard g(dy.device());
   mipipe::ConvShape s;
+  s.f32 = is_f32(dy);
   s.N = (int)x.size(0); s.H = (int)x.size(1); s.W = (int)x.size(2); s.Ci = (int)x.size(3);
   s.Co = (int)dy.size(3); s.KH = kh; s.KW = kw; s.stride = stride; s.pad = pad;
   s.stride_w = stride_w > 0 ? stride_w : 0;
@@ -241,14 +256,14 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(Tensor psum, Tensor psq, 
 
 Tensor bn_act_fwd(Tensor y, Tensor scale, Tensor bias, bool relu, optional<Tensor> r,
                   optional<Tensor> rscale, optional<Tensor> rbias) {
-  check_bf16(y, "y");
+  check_act(y, "y");
   c10::DeviceGuard g(y.device());
   int64_t C = y.size(-1), M = y.numel() / C;
   TORCH_CHECK(C % 8 == 0, "bn_act_fwd needs C % 8 == 0");
   check_vec(scale, C, "scale");
   check_vec(bias, C, "bias");
   if (r.has_value()) {
-    check_bf16(*r, "residual");
+    check_same(*r, y, "residual");
     TORCH_CHECK(r->sizes() == y.sizes(), "residual shape mismatch");
   }
   if (rscale.has_value()) {
@@ -259,7 +274,7 @@ Tensor bn_act_fwd(Tensor y, Tensor scale, Tensor bias, bool relu, optional<Tenso
   mipipe::bn_act_fwd(y.data_ptr(), scale.data_ptr<float>(), bias.data_ptr<float>(), ptr_or_null(r),
                      rscale.has_value() ? rscale->data_ptr<float>() : nullptr,
                      rbias.has_value() ? rbias->data_ptr<float>() : nullptr, z.data_ptr(), M,
-                     (int)C, relu, stream());
+                     (int)C, relu, stream(), is_f32(y));
   return z;
 }
 
@@ -268,16 +283,16 @@ std::tuple<Tensor, Tensor, optional<Tensor>> bn_act_bwd_reduce(
     optional<Tensor> mean2, optional<Tensor> invstd2, optional<Tensor> rep,
     optional<Tensor> dgamma, optional<Tensor> dbeta, optional<Tensor> dgamma2,
     optional<Tensor> dbeta2) {
-  check_bf16(dz, "dz");
-  check_bf16(z, "z");
-  check_bf16(y, "y");
+  check_act(y, "y");
+  check_same(dz, y, "dz");
+  check_same(z, y, "z");
   c10::DeviceGuard g(dz.device());
   int64_t C = y.size(-1), M = y.numel() / C;
   TORCH_CHECK(C % 8 == 0 && dz.sizes() == y.sizes() && z.sizes() == y.sizes(), "shape mismatch");
   check_vec(mean, C, "mean");
   check_vec(invstd, C, "invstd");
   if (y2.has_value()) {
-    check_bf16(*y2, "y2");
+    check_same(*y2, y, "y2");
     TORCH_CHECK(y2->sizes() == y.sizes(), "y2 shape mismatch");
     check_vec(*mean2, C, "mean2");
     check_vec(*invstd2, C, "invstd2");
@@ -301,7 +316,7 @@ std::tuple<Tensor, Tensor, optional<Tensor>> bn_act_bwd_reduce(
                             (int)C, sg.data_ptr<float>(), sgx.data_ptr<float>(),
                             sgx2.has_value() ? sgx2->data_ptr<float>() : nullptr,
                             work.data_ptr<float>(), fptr(dgamma, C), fptr(dbeta, C),
-                            fptr(dgamma2, C), fptr(dbeta2, C), stream());
+                            fptr(dgamma2, C), fptr(dbeta2, C), stream(), is_f32(y));
   return {sg, sgx, sgx2};
 }
 
@@ -310,15 +325,15 @@ std::tuple<Tensor, optional<Tensor>> bn_act_bwd_apply(
     Tensor sum_gx, int64_t count, bool relu, bool want_dres, optional<Tensor> y2,
     optional<Tensor> mean2, optional<Tensor> invstd2, optional<Tensor> gamma2,
     optional<Tensor> sum_gx2) {
-  check_bf16(dz, "dz");
-  check_bf16(z, "z");
-  check_bf16(y, "y");
+  check_act(y, "y");
+  check_same(dz, y, "dz");
+  check_same(z, y, "z");
   c10::DeviceGuard g(dz.device());
   int64_t C = y.size(-1), M = y.numel() / C;
   TORCH_CHECK(C % 8 == 0 && dz.sizes() == y.sizes() && z.sizes() == y.sizes(), "shape mismatch");
   for (auto* t : {&mean, &invstd, &gamma, &sum_g, &sum_gx}) check_vec(*t, C, "bn vector");
   if (y2.has_value()) {
-    check_bf16(*y2, "y2");
+    check_same(*y2, y, "y2");
     TORCH_CHECK(y2->sizes() == y.sizes(), "y2 shape mismatch");
     check_vec(*mean2, C, "mean2");
     check_vec(*invstd2, C, "invstd2");
@@ -335,7 +350,8 @@ std::tuple<Tensor, optional<Tensor>> bn_act_bwd_apply(
       invstd2.has_value() ? invstd2->data_ptr<float>() : nullptr,
       gamma2.has_value() ? gamma2->data_ptr<float>() : nullptr,
       sum_gx2.has_value() ? sum_gx2->data_ptr<float>() : nullptr, count, relu, want_dres,
-      dy.data_ptr(), other.has_value() ? other->data_ptr() : nullptr, M, (int)C, stream());
+      dy.data_ptr(), other.has_value() ? other->data_ptr() : nullptr, M, (int)C, stream(),
+      is_f32(y));
   return {dy, other};
 }
 
@@ -349,7 +365,7 @@ int pool_out(int L, int k, int s, int p, bool ceil_mode) {
 }
 
 std::tuple<Tensor, Tensor> maxpool_fwd(Tensor x, int k, int s, int p, bool ceil_mode) {
-  check_bf16(x, "x");
+  check_act(x, "x");
   c10::DeviceGuard g(x.device());
   int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   TORCH_CHECK(C % 8 == 0 && k <= 15, "maxpool needs C % 8 == 0 and k <= 15");
@@ -359,12 +375,12 @@ std::tuple<Tensor, Tensor> maxpool_fwd(Tensor x, int k, int s, int p, bool ceil_
   auto y = torch::empty({N, Ho, Wo, C}, x.options());
   auto idx = torch::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
   mipipe::maxpool_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, k, s,
-                      p, stream());
+                      p, stream(), is_f32(x));
   return {y, idx};
 }
 
 Tensor maxpool_bwd(Tensor dy, Tensor idx, std::vector<int64_t> xs, int k, int s, int p) {
-  check_bf16(dy, "dy");
+  check_act(dy, "dy");
   check_cuda(idx, "idx");
   c10::DeviceGuard g(dy.device());
   int N = xs[0], H = xs[1], W = xs[2], C = xs[3];
@@ -372,35 +388,35 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, std::vector<int64_t> xs, int k, int s,
   TORCH_CHECK(idx.sizes() == dy.sizes() && dy.size(3) == C, "maxpool_bwd shape mismatch");
   auto dx = torch::empty({N, H, W, C}, dy.options());
   mipipe::maxpool_bwd(dy.data_ptr(), idx.data_ptr<uint8_t>(), dx.data_ptr(), N, H, W, C, Ho, Wo, k,
-                      s, p, stream());
+                      s, p, stream(), is_f32(dy));
   return dx;
 }
 
 Tensor avgpool_fwd(Tensor x) {
-  check_bf16(x, "x");
+  check_act(x, "x");
   c10::DeviceGuard g(x.device());
   int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
   TORCH_CHECK(C % 8 == 0, "avgpool needs C % 8 == 0");
   auto y = torch::empty({N, C}, x.options());
-  mipipe::avgpool_fwd(x.data_ptr(), y.data_ptr(), N, HW, C, stream());
+  mipipe::avgpool_fwd(x.data_ptr(), y.data_ptr(), N, HW, C, stream(), is_f32(x));
   return y;
 }
 
 Tensor avgpool_bwd(Tensor dy, std::vector<int64_t> xs) {
-  check_bf16(dy, "dy");
+  check_act(dy, "dy");
   c10::DeviceGuard g(dy.device());
   int N = xs[0], H = xs[1], W = xs[2], C = xs[3];
   TORCH_CHECK(dy.size(0) == N && dy.size(1) == C, "avgpool_bwd shape mismatch");
   auto dx = torch::empty({N, H, W, C}, dy.options());
-  mipipe::avgpool_bwd(dy.data_ptr(), dx.data_ptr(), N, H * W, C, stream());
+  mipipe::avgpool_bwd(dy.data_ptr(), dx.data_ptr(), N, H * W, C, stream(), is_f32(dy));
   return dx;
 }
 
 // ------------------------------------------------------------------------------- GEMM
 Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bias,
             std::string act, at::ScalarType out_dtype, optional<Tensor> c, double beta) {
-  check_bf16(a, "A");
-  check_bf16(b, "B");
+  check_act(a, "A");
+  check_same(b, a, "B");
   c10::DeviceGuard g(a.device());
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm expects 2-D operands");
   int64_t M = trans_a ? a.size(1) : a.size(0);
@@ -428,24 +444,25 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
     TORCH_CHECK(bias_p == nullptr && act_i == 0, "accumulating gemm has no epilogue");
     out = *c;
     mode = 2;
-  } else if (out_dtype == at::kFloat) {
+  } else if (out_dtype == a.scalar_type()) {  // activation dtype: bias / ReLU epilogue
+    out = torch::empty({M, N}, a.options());
+    mode = 0;
+  } else {
+    TORCH_CHECK(out_dtype == at::kFloat, "gemm out dtype must be the operand dtype or fp32");
     out = torch::empty({M, N}, a.options().dtype(at::kFloat));
     mode = 1;
     TORCH_CHECK(act_i == 0, "fp32 gemm output has no activation epilogue");
-  } else {
-    TORCH_CHECK(out_dtype == at::kBFloat16, "gemm out dtype must be bf16 or fp32");
-    out = torch::empty({M, N}, a.options());
-    mode = 0;
   }
   mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b,
-               out.data_ptr(), N, (int)M, (int)N, (int)K, bias_p, act_i, mode, stream());
+               out.data_ptr(), N, (int)M, (int)N, (int)K, bias_p, act_i, mode, stream(),
+               is_f32(a));
   return out;
 }
 
 // ------------------------------------------------------------------------------- loss / optim
 std::tuple<Tensor, Tensor> cross_entropy_fwd_bwd(Tensor logits, Tensor labels, double smoothing,
                                                  int64_t ignore_index) {
-  check_bf16(logits, "logits");
+  check_act(logits, "logits");
   check_cuda(labels, "labels");
   c10::DeviceGuard g(logits.device());
   TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
@@ -456,8 +473,29 @@ std::tuple<Tensor, Tensor> cross_entropy_fwd_bwd(Tensor logits, Tensor labels, d
   auto work = torch::empty({4}, logits.options().dtype(at::kInt));
   mipipe::cross_entropy_fwd_bwd(logits.data_ptr(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
                                 grad.data_ptr(), R, V, (float)smoothing, ignore_index,
-                                work.data_ptr<int>(), stream());
+                                work.data_ptr<int>(), stream(), is_f32(logits));
   return {loss, grad};
+}
+
+// number of rows whose argmax equals the label, accumulated into an int32 device counter
+Tensor top1_correct(Tensor logits, Tensor labels, optional<Tensor> out) {
+  check_act(logits, "logits");
+  check_cuda(labels, "labels");
+  c10::DeviceGuard g(logits.device());
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  TORCH_CHECK(logits.dim() == 2 && labels.numel() == logits.size(0), "top1 shape mismatch");
+  Tensor o;
+  if (out.has_value()) {
+    check_cuda(*out, "out");
+    TORCH_CHECK(out->scalar_type() == at::kInt && out->numel() == 1, "out must be one int32");
+    o = *out;
+  } else {
+    o = torch::zeros({1}, logits.options().dtype(at::kInt));
+  }
+  if (logits.size(0) > 0)
+    mipipe::top1_correct(logits.data_ptr(), labels.data_ptr<int64_t>(), (int)logits.size(0),
+                         (int)logits.size(1), o.data_ptr<int>(), stream(), is_f32(logits));
+  return o;
 }
 
 void check_flat(const Tensor& t, int64_t n, const char* name) {
@@ -508,16 +546,16 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, optional<Tensor> shadow,
 Tensor nchw_to_nhwc(Tensor x, at::ScalarType dtype, int64_t pad_to) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
-  TORCH_CHECK(dtype == at::kBFloat16, "nchw_to_nhwc produces bf16");
+  TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "nchw_to_nhwc produces bf16 / fp32");
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x must be fp32/bf16");
   TORCH_CHECK(x.dim() == 4, "x must be NCHW");
   int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   int Cp = C;
   if (pad_to > 0 && C % pad_to) Cp = (int)((C + pad_to - 1) / pad_to * pad_to);
   Cp = (Cp + 7) / 8 * 8;
-  auto y = torch::empty({N, H, W, Cp}, x.options().dtype(at::kBFloat16));
+  auto y = torch::empty({N, H, W, Cp}, x.options().dtype(dtype));
   mipipe::nchw_to_nhwc(x.data_ptr(), x.scalar_type() == at::kBFloat16, y.data_ptr(), N, C, H, W, Cp,
-                       stream());
+                       stream(), dtype == at::kFloat);
   return y;
 }
 
@@ -644,15 +682,16 @@ Tensor colsum(Tensor x, optional<Tensor> out) {
   return o;
 }
 
-Tensor stem_pack(Tensor x, int64_t pad, int64_t Hp, int64_t Wsp) {
+Tensor stem_pack(Tensor x, int64_t pad, int64_t Hp, int64_t Wsp, at::ScalarType dtype) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
   TORCH_CHECK(x.dim() == 4 && x.size(1) <= 4, "stem_pack expects NCHW with C <= 4");
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x dtype");
-  auto y = torch::empty({x.size(0), Hp, Wsp, 8}, x.options().dtype(at::kBFloat16));
+  TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "stem_pack produces bf16 / fp32");
+  auto y = torch::empty({x.size(0), Hp, Wsp, 8}, x.options().dtype(dtype));
   mipipe::stem_pack(x.data_ptr(), x.scalar_type() == at::kBFloat16, y.data_ptr(), (int)x.size(0),
                     (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)pad, (int)Hp, (int)Wsp,
-                    stream());
+                    stream(), dtype == at::kFloat);
   return y;
 }
 
@@ -1012,7 +1051,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("mask") = py::none(),
         py::arg("scale") = 0.125, py::arg("p_drop") = 0.0, py::arg("seed") = 0);
   m.def("dropout_fwd", &dropout_fwd);
-  m.def("stem_pack", &stem_pack);
+  m.def("stem_pack", &stem_pack, py::arg("x"), py::arg("pad"), py::arg("Hp"), py::arg("Wsp"),
+        py::arg("dtype") = at::kBFloat16);
+  m.def("top1_correct", &top1_correct, py::arg("logits"), py::arg("labels"),
+        py::arg("out") = py::none());
   m.def("set_splitk_target", [](int v) { mipipe::g_splitk_target = std::max(1, v); });
   m.def("get_splitk_target", []() { return mipipe::g_splitk_target; });
   m.def("set_stat_rows", [](int v) {

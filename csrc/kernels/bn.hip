@@ -1,4 +1,4 @@
-// BatchNorm (training) kernels on NHWC bf16, fused with ReLU and the ResNet residual add.
+// BatchNorm (training) kernels on NHWC bf16 / fp32 (element type T), fused with ReLU and the ResNet residual add.
 //
 // Forward: statistics come from the conv epilogue as a [P][C] slab of shifted partial sums;
 //   bn_finalize reduces it (two deterministic stages, no atomics) into mean / invstd / scale /
@@ -123,14 +123,14 @@ void bn_finalize(float* psum, float* psq, int P, int C, long count, const float*
 }
 
 // ----------------------------------------------------------------------------- forward apply
-template <int RES>  // 0 none, 1 raw residual, 2 BN'd residual
-__global__ __launch_bounds__(256) void bn_act_fwd_kernel(const __bf16* __restrict__ y,
+template <int RES, class T>  // RES: 0 none, 1 raw residual, 2 BN'd residual
+__global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ bias,
-                                                         const __bf16* __restrict__ r,
+                                                         const T* __restrict__ r,
                                                          const float* __restrict__ rscale,
                                                          const float* __restrict__ rbias,
-                                                         __bf16* __restrict__ z, long M, int C,
+                                                         T* __restrict__ z, long M, int C,
                                                          bool relu) {
   const RowMap mp = row_map(C);
   const int t = threadIdx.x;
@@ -152,15 +152,13 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const __bf16* __restric
     }
     for (long row = (long)blockIdx.x * mp.rpb + rg; row < M; row += (long)gridDim.x * mp.rpb) {
       long off = row * C + c0;
-      uint4 yv = *reinterpret_cast<const uint4*>(y + off);
       float v[8];
-      unpack8(yv, v);
+      load8(y + off, v);
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = v[q] * sc[q] + bi[q];
       if (RES != 0) {
-        uint4 rv = *reinterpret_cast<const uint4*>(r + off);
         float w[8];
-        unpack8(rv, w);
+        load8(r + off, w);
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] += (RES == 2) ? (w[q] * rs[q] + rb[q]) : w[q];
       }
@@ -168,33 +166,41 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const __bf16* __restric
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
       }
-      *reinterpret_cast<uint4*>(z + off) = pack8(v);
+      store8(z + off, v);
     }
   }
 }
 
-void bn_act_fwd(const void* y, const float* scale, const float* bias, const void* r,
-                const float* rscale, const float* rbias, void* z, long M, int C, bool relu,
-                hipStream_t st) {
+template <class T>
+static void bn_act_fwd_t(const void* y, const float* scale, const float* bias, const void* r,
+                         const float* rscale, const float* rbias, void* z, long M, int C,
+                         bool relu, hipStream_t st) {
   RowMap mp = row_map(C);
   int grid = grid_for_rows(M, mp.rpb);
-  const __bf16* yp = (const __bf16*)y;
-  const __bf16* rp = (const __bf16*)r;
-  __bf16* zp = (__bf16*)z;
+  const T* yp = (const T*)y;
+  const T* rp = (const T*)r;
+  T* zp = (T*)z;
   if (r == nullptr)
-    hipLaunchKernelGGL(bn_act_fwd_kernel<0>, dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<0, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu);
   else if (rscale == nullptr)
-    hipLaunchKernelGGL(bn_act_fwd_kernel<1>, dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<1, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu);
   else
-    hipLaunchKernelGGL(bn_act_fwd_kernel<2>, dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<2, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu);
+}
+
+void bn_act_fwd(const void* y, const float* scale, const float* bias, const void* r,
+                const float* rscale, const float* rbias, void* z, long M, int C, bool relu,
+                hipStream_t st, bool f32) {
+  if (f32) bn_act_fwd_t<float>(y, scale, bias, r, rscale, rbias, z, M, C, relu, st);
+  else bn_act_fwd_t<__bf16>(y, scale, bias, r, rscale, rbias, z, M, C, relu, st);
 }
 
 // ----------------------------------------------------------------------------- backward
-template <bool TWO>
+template <bool TWO, class T>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
-    const __bf16* __restrict__ dz, const __bf16* __restrict__ z, const __bf16* __restrict__ y,
+    const T* __restrict__ dz, const T* __restrict__ z, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
-    const __bf16* __restrict__ y2, const float* __restrict__ mean2,
+    const T* __restrict__ y2, const float* __restrict__ mean2,
     const float* __restrict__ invstd2, bool relu, long M, int C, float* __restrict__ rep) {
   __shared__ float red[3][kT][8];
   const RowMap mp = row_map(C);
@@ -223,14 +229,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
       for (long row = (long)blockIdx.x * mp.rpb + rg; row < M; row += (long)gridDim.x * mp.rpb) {
         long off = row * C + c0;
         float g[8], yv[8];
-        unpack8(*reinterpret_cast<const uint4*>(dz + off), g);
+        load8(dz + off, g);
         if (relu) {
           float zv[8];
-          unpack8(*reinterpret_cast<const uint4*>(z + off), zv);
+          load8(z + off, zv);
 #pragma unroll
           for (int q = 0; q < 8; ++q) g[q] = zv[q] > 0.f ? g[q] : 0.f;
         }
-        unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
+        load8(y + off, yv);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           sg[q] += g[q];
@@ -238,7 +244,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         }
         if (TWO) {
           float y2v[8];
-          unpack8(*reinterpret_cast<const uint4*>(y2 + off), y2v);
+          load8(y2 + off, y2v);
 #pragma unroll
           for (int q = 0; q < 8; ++q) sx2[q] += g[q] * (y2v[q] - mu2[q]) * is2[q];
         }
@@ -315,32 +321,36 @@ void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float
                        const float* invstd, const void* y2, const float* mean2,
                        const float* invstd2, bool relu, long M, int C, float* out_g,
                        float* out_gx, float* out_gx2, float* rep, float* dgamma, float* dbeta,
-                       float* dgamma2, float* dbeta2, hipStream_t st) {
+                       float* dgamma2, float* dbeta2, hipStream_t st, bool f32) {
   RowMap mp = row_map(C);
   // >= 16 row-iterations per thread, and at most ~1M atomic adds in total
   long cap = std::max<long>(64, (1l << 20) / (3l * C));
   int G = (int)std::max<long>(1, std::min<long>(std::min<long>(1024, cap),
                                                 (M + mp.rpb * 16 - 1) / (mp.rpb * 16)));
-  const __bf16 *dzp = (const __bf16*)dz, *zp = (const __bf16*)z, *yp = (const __bf16*)y,
-               *y2p = (const __bf16*)y2;
-  if (y2 == nullptr)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, rep);
-  else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, rep);
+  auto launch = [&](auto tag) {
+    typedef decltype(tag) T;
+    const T *dzp = (const T*)dz, *zp = (const T*)z, *yp = (const T*)y, *y2p = (const T*)y2;
+    if (y2 == nullptr)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, T>), dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, rep);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, T>), dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, rep);
+  };
+  if (f32) launch(float{});
+  else launch(__bf16{});
   hipLaunchKernelGGL(bn_bwd_collect_kernel, dim3((C + 255) / 256), dim3(256), 0, st, rep, C, out_g,
                      out_gx, y2 ? out_gx2 : nullptr, dgamma, dbeta, y2 ? dgamma2 : nullptr,
                      y2 ? dbeta2 : nullptr);
 }
 
-template <int MODE>  // 0: dy only, 1: dy + dres (=g), 2: dy + dy2 (second BN branch)
+template <int MODE, class T>  // MODE 0: dy only, 1: dy + dres (=g), 2: dy + dy2 (second branch)
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
-    const __bf16* __restrict__ dz, const __bf16* __restrict__ z, const __bf16* __restrict__ y,
+    const T* __restrict__ dz, const T* __restrict__ z, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, const float* __restrict__ sum_g,
-    const float* __restrict__ sum_gx, const __bf16* __restrict__ y2,
+    const float* __restrict__ sum_gx, const T* __restrict__ y2,
     const float* __restrict__ mean2, const float* __restrict__ invstd2,
     const float* __restrict__ gamma2, const float* __restrict__ sum_gx2, float inv_n, bool relu,
-    __bf16* __restrict__ dy, __bf16* __restrict__ dother, long M, int C) {
+    T* __restrict__ dy, T* __restrict__ dother, long M, int C) {
   const RowMap mp = row_map(C);
   const int t = threadIdx.x;
   const int rg = t / mp.tpr;
@@ -369,25 +379,25 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     for (long row = (long)blockIdx.x * mp.rpb + rg; row < M; row += (long)gridDim.x * mp.rpb) {
       long off = row * C + c0;
       float g[8], yv[8], o[8];
-      unpack8(*reinterpret_cast<const uint4*>(dz + off), g);
+      load8(dz + off, g);
       if (relu) {
         float zv[8];
-        unpack8(*reinterpret_cast<const uint4*>(z + off), zv);
+        load8(z + off, zv);
 #pragma unroll
         for (int q = 0; q < 8; ++q) g[q] = zv[q] > 0.f ? g[q] : 0.f;
       }
-      unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
+      load8(y + off, yv);
 #pragma unroll
       for (int q = 0; q < 8; ++q) o[q] = A[q] * g[q] + Bc[q] * yv[q] + Cc[q];
-      *reinterpret_cast<uint4*>(dy + off) = pack8(o);
+      store8(dy + off, o);
       if (MODE == 1) {
-        *reinterpret_cast<uint4*>(dother + off) = pack8(g);
+        store8(dother + off, g);
       } else if (MODE == 2) {
         float y2v[8];
-        unpack8(*reinterpret_cast<const uint4*>(y2 + off), y2v);
+        load8(y2 + off, y2v);
 #pragma unroll
         for (int q = 0; q < 8; ++q) o[q] = A2[q] * g[q] + B2[q] * y2v[q] + C2[q];
-        *reinterpret_cast<uint4*>(dother + off) = pack8(o);
+        store8(dother + off, o);
       }
     }
   }
@@ -398,19 +408,23 @@ void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float*
                       const float* sum_gx, const void* y2, const float* mean2,
                       const float* invstd2, const float* gamma2, const float* sum_gx2, long count,
                       bool relu, bool want_dres, void* dy, void* dother, long M, int C,
-                      hipStream_t st) {
+                      hipStream_t st, bool f32) {
   RowMap mp = row_map(C);
   int grid = grid_for_rows(M, mp.rpb);
   float inv_n = 1.f / (float)count;
-  const __bf16 *dzp = (const __bf16*)dz, *zp = (const __bf16*)z, *yp = (const __bf16*)y,
-               *y2p = (const __bf16*)y2;
-  __bf16 *dyp = (__bf16*)dy, *dop = (__bf16*)dother;
-  if (y2 != nullptr)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<2>, dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C);
-  else if (want_dres)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<0>, dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C);
+  auto launch = [&](auto tag) {
+    typedef decltype(tag) T;
+    const T *dzp = (const T*)dz, *zp = (const T*)z, *yp = (const T*)y, *y2p = (const T*)y2;
+    T *dyp = (T*)dy, *dop = (T*)dother;
+    if (y2 != nullptr)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<2, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C);
+    else if (want_dres)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<0, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C);
+  };
+  if (f32) launch(float{});
+  else launch(__bf16{});
 }
 
 void bn_bwd_collect(float* rep, int C, float* out_g, float* out_gx, float* dgamma, float* dbeta,

@@ -41,6 +41,63 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
+// 8-channel vector I/O for both activation dtypes: bf16 = one 16-B access, fp32 = two.  Kernels
+// templated on the element type T (bf16 mixed precision / fp32 reference precision) use these.
+__device__ __forceinline__ void load8(const __bf16* p, float* f) {
+  unpack8(*reinterpret_cast<const uint4*>(p), f);
+}
+__device__ __forceinline__ void load8(const float* p, float* f) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0];
+  const float4 b = reinterpret_cast<const float4*>(p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+  f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+__device__ __forceinline__ void store8(__bf16* p, const float* f) {
+  *reinterpret_cast<uint4*>(p) = pack8(f);
+}
+__device__ __forceinline__ void store8(float* p, const float* f) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+// 8 raw elements of T held in registers (prefetched before they are needed).
+template <class T>
+struct Raw8 {
+  uint4 v[sizeof(T) / 2];
+};
+template <class T>
+__device__ __forceinline__ Raw8<T> ld_raw8(const T* p) {
+  Raw8<T> r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 2); ++i) r.v[i] = reinterpret_cast<const uint4*>(p)[i];
+  return r;
+}
+__device__ __forceinline__ void unpack_raw(const Raw8<__bf16>& r, float* f) { unpack8(r.v[0], f); }
+__device__ __forceinline__ void unpack_raw(const Raw8<float>& r, float* f) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    f[4 * i + 0] = __uint_as_float(r.v[i].x);
+    f[4 * i + 1] = __uint_as_float(r.v[i].y);
+    f[4 * i + 2] = __uint_as_float(r.v[i].z);
+    f[4 * i + 3] = __uint_as_float(r.v[i].w);
+  }
+}
+
+// Value as the tensor stores it (rounds to bf16 for bf16 tensors): statistics fused into a
+// producing kernel must see the stored value, not the fp32 accumulator.
+template <class T>
+__device__ __forceinline__ float as_stored(float v) {
+  if constexpr (std::is_same<T, float>::value) return v;
+  else return bf2f(f2bf(v));
+}
+
+// Split an fp32 value into bf16 hi + bf16 lo (hi = rn(v), lo = rn(v - hi)): hi*b_hi + hi*b_lo +
+// lo*b_hi reproduces an fp32 product to ~2^-16 relative (the lo*lo term is below fp32 rounding
+// of the accumulation) — the "split-bf16" scheme the fp32 GEMM main loop runs on bf16 MFMA.
+__device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
+  hi = f2bf(v);
+  lo = f2bf(v - bf2f(hi));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

@@ -23,17 +23,17 @@ struct EpiParams {
   // stored at dx row (img*H + ph + s*i)*W + pw + s*j.  rm_s == 0 disables.
   int rm_s, rm_ph, rm_pw, rm_H, rm_W, rm_Hc, rm_Wc;
   FastDiv rm_fHcWc, rm_fWc;
-  // optional bf16 [rows][ldc] tensor added to the output (residual-gradient fusion)
-  const __bf16* addend;
+  // optional [rows][ldc] tensor (output dtype) added to the output (residual-gradient fusion)
+  const void* addend;
   // optional BatchNorm-backward fusion (conv dgrad whose input was relu(bn(y))): the output
   // becomes g = dx * [y*scale + bias > 0] and Σg, Σg·(y-mean)*invstd are accumulated into
   // replica rows (blockIdx % R) of rep[0] / rep[1] ([3][R][N] slab)
-  const __bf16* bnr_y;
+  const void* bnr_y;  // output dtype
   const float *bnr_mean, *bnr_invstd, *bnr_scale, *bnr_bias;
   float* bnr_rep;
   // when set, the ReLU mask is read from this stored post-activation tensor (z > 0) instead of
   // recomputed from y (needed when a residual was added before the ReLU)
-  const __bf16* bnr_z;
+  const void* bnr_z;  // output dtype
 };
 
 // Workgroup barrier that orders LDS only.  __syncthreads() also drains every outstanding global
@@ -52,22 +52,29 @@ __device__ __forceinline__ long out_row(const EpiParams& e, uint32_t m) {
   return ((long)img * e.rm_H + e.rm_ph + e.rm_s * (long)i) * e.rm_W + e.rm_pw + e.rm_s * (long)j;
 }
 
-template <int BM, int BN>
-constexpr int kStatsLdsOffset() { return ((BM * (BN * 2 + 16)) + 255) / 256 * 256; }
+// LDS pitch of the staged output tile (T elements + 16 B pad) and where the statistics
+// partials live behind it.
+template <int BN, class T = __bf16>
+constexpr int kEpiPitch() { return BN * (int)sizeof(T) + 16; }
+template <int BM, int BN, class T = __bf16>
+constexpr int kStatsLdsOffset() { return ((BM * kEpiPitch<BN, T>()) + 255) / 256 * 256; }
+template <int BM, int BN, class T = __bf16>
+constexpr int kEpiLdsBytes() { return kStatsLdsOffset<BM, BN, T>() + 4 * BN * 4; }
 
-// bf16 output.  acc layout: lane holds C[m][n..n+3] for tile (i, j).
+// Output in the activation dtype T (bf16, or fp32 on the reference-precision path).
+// acc layout: lane holds C[m][n..n+3] for tile (i, j).
 // FUSE: compile the dgrad fusions (addend / BN-backward reduction); kernels that never use
 // them keep their register budget.
-template <int BM, int BN, bool FUSE = false>
-__device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const EpiParams& e,
-                              uint32_t m0, uint32_t n0, uint32_t prow_base, int wave, int lane) {
+template <int BM, int BN, bool FUSE = false, class T = __bf16>
+__device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const EpiParams& e,
+                             uint32_t m0, uint32_t n0, uint32_t prow_base, int wave, int lane) {
   constexpr int MT = BM / 32, NT = BN / 32;
   const int wr = wave >> 1, wc = wave & 1;
   const uint32_t ml0 = wr * (BM / 2) + (lane & 15);
   const uint32_t nl0 = wc * (BN / 2) + (lane >> 4) * 4;
   // dgrad fusions: issue this thread's addend / y loads now so their latency overlaps the
-  // accumulator staging below (a thread always owns the same 16-B column chunk)
-  constexpr int CPR = BN / 8;  // 16-B chunks per row
+  // accumulator staging below (a thread always owns the same 8-column chunk)
+  constexpr int CPR = BN / 8;  // 8-element chunks per row
   constexpr int ITER = BM * CPR / kThreads;
   static_assert(kThreads % CPR == 0 && (BM * CPR) % kThreads == 0, "epilogue thread map");
   const bool bnr = FUSE && e.bnr_rep != nullptr;
@@ -78,14 +85,17 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
   // software-pipelined operand ring: PF iterations in flight; the first PF are issued now so
   // their latency overlaps the accumulator staging below
   constexpr int PF = FUSE ? (ITER < 4 ? ITER : 4) : 1;
-  uint4 ad_raw[PF], y_raw[PF], z_raw[PF];
+  Raw8<T> ad_raw[PF], y_raw[PF], z_raw[PF];
+  const T* addend = reinterpret_cast<const T*>(e.addend);
+  const T* bnr_y = reinterpret_cast<const T*>(e.bnr_y);
+  const T* bnr_z = reinterpret_cast<const T*>(e.bnr_z);
   auto issue = [&](int it, int slot) {
     const uint32_t r = (threadIdx.x + it * kThreads) / CPR;
     const uint32_t m = min(m0 + r, e.M - 1);
     const long orow = out_row(e, m);
-    if (has_add) ad_raw[slot] = *reinterpret_cast<const uint4*>(e.addend + orow * e.ldc + ld_n);
-    if (bnr) y_raw[slot] = *reinterpret_cast<const uint4*>(e.bnr_y + orow * e.ldc + ld_n);
-    if (zmask) z_raw[slot] = *reinterpret_cast<const uint4*>(e.bnr_z + orow * e.ldc + ld_n);
+    if (has_add) ad_raw[slot] = ld_raw8(addend + orow * e.ldc + ld_n);
+    if (bnr) y_raw[slot] = ld_raw8(bnr_y + orow * e.ldc + ld_n);
+    if (zmask) z_raw[slot] = ld_raw8(bnr_z + orow * e.ldc + ld_n);
   };
   if (FUSE && (has_add || bnr)) {
 #pragma unroll
@@ -114,7 +124,7 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
   // and added with fp32 atomics into replica slab (blockIdx % st_R) — 256-B-contiguous
   // wave-instructions, no per-block partial rows to reduce later.
   if (e.st_sum != nullptr) {
-    float* lst = reinterpret_cast<float*>(smem + kStatsLdsOffset<BM, BN>());  // [2][2][BN]
+    float* lst = reinterpret_cast<float*>(smem + kStatsLdsOffset<BM, BN, T>());  // [2][2][BN]
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       uint32_t n = n0 + nl0 + j * 16;
@@ -128,7 +138,7 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
         if (m < e.M) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            float d = acc[i][j][q] - sh[q];
+            float d = as_stored<T>(acc[i][j][q]) - sh[q];
             s[q] += d;
             ss[q] += d * d;
           }
@@ -155,21 +165,27 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
   // every wave is past the main loop (whose LDS the staging tile overwrites) and the
   // statistics partials are in LDS
   lds_barrier();
-  // stage bf16 tile in LDS: pitch BN*2 + 16 bytes
-  constexpr int P = BN * 2 + 16;
+  // stage the output tile in LDS: pitch BN*sizeof(T) + 16 bytes
+  constexpr int P = kEpiPitch<BN, T>();
+  constexpr bool F32 = std::is_same<T, float>::value;
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       uint32_t ml = ml0 + i * 16, nl = nl0 + j * 16;
-      uint2 v = make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
-      *reinterpret_cast<uint2*>(smem + ml * P + nl * 2) = v;
+      if constexpr (F32) {
+        *reinterpret_cast<float4*>(smem + ml * P + nl * 4) =
+            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      } else {
+        uint2 v = make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+        *reinterpret_cast<uint2*>(smem + ml * P + nl * 2) = v;
+      }
     }
   lds_barrier();
   if (e.st_sum != nullptr) {
     // one fp32 atomic per column per block into replica row blockIdx % st_R (fire and forget:
     // no barrier below waits for them)
-    const float* lst = reinterpret_cast<const float*>(smem + kStatsLdsOffset<BM, BN>());
+    const float* lst = reinterpret_cast<const float*>(smem + kStatsLdsOffset<BM, BN, T>());
     for (int t = threadIdx.x; t < 2 * BN; t += kThreads) {
       int arr = t / BN, c = t % BN;
       uint32_t n = n0 + c;
@@ -180,7 +196,7 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
       }
     }
   }
-  __bf16* C = reinterpret_cast<__bf16*>(e.C);
+  T* C = reinterpret_cast<T*>(e.C);
   float b_sc[8], b_bi[8], b_mu[8], b_is[8], sg[8], sgx[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -197,33 +213,39 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
     const uint32_t r = c / CPR, cc = c % CPR;
     const uint32_t m = m0 + r, n = n0 + cc * 8;
     if (m < e.M && n < e.N) {
-      uint4 v = *reinterpret_cast<const uint4*>(smem + r * P + cc * 16);
+      Raw8<T> v;
+#pragma unroll
+      for (int h = 0; h < (int)(sizeof(T) / 2); ++h)
+        v.v[h] = *reinterpret_cast<const uint4*>(smem + r * P + cc * 8 * sizeof(T) + 16 * h);
       const long orow = out_row(e, m);
       if (FUSE && (has_add || bnr)) {
         float f[8];
-        unpack8(v, f);
+        unpack_raw(v, f);
         if (has_add) {
           float a[8];
-          unpack8(ad_raw[it % PF], a);
+          unpack_raw(ad_raw[it % PF], a);
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] += a[q];
         }
         if (bnr) {
           float yv[8], zv[8];
-          unpack8(y_raw[it % PF], yv);
-          if (zmask) unpack8(z_raw[it % PF], zv);
+          unpack_raw(y_raw[it % PF], yv);
+          if (zmask) unpack_raw(z_raw[it % PF], zv);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const float zq = zmask ? zv[q] : yv[q] * b_sc[q] + b_bi[q];
-            const float gq = zq > 0.f ? bf2f(f2bf(f[q])) : 0.f;  // stats of the stored bf16 g
+            const float gq = zq > 0.f ? as_stored<T>(f[q]) : 0.f;  // stats of the stored g
             f[q] = gq;
             sg[q] += gq;
             sgx[q] += gq * (yv[q] - b_mu[q]) * b_is[q];
           }
         }
-        v = pack8(f);
+        store8(C + orow * e.ldc + n, f);
+      } else {
+#pragma unroll
+        for (int h = 0; h < (int)(sizeof(T) / 2); ++h)
+          reinterpret_cast<uint4*>(C + orow * e.ldc + n)[h] = v.v[h];
       }
-      *reinterpret_cast<uint4*>(C + orow * e.ldc + n) = v;
     }
     if (FUSE && (has_add || bnr) && it + PF < ITER) issue(it + PF, it % PF);
   }
@@ -247,6 +269,12 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
         atomicAdd(e.bnr_rep + ((long)arr * R + blockIdx.x % Rw) * e.N + n0 + col, a);
     }
   }
+}
+
+template <int BM, int BN, bool FUSE = false>
+__device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const EpiParams& e,
+                              uint32_t m0, uint32_t n0, uint32_t prow_base, int wave, int lane) {
+  epilogue_out<BM, BN, FUSE, __bf16>(smem, acc, e, m0, n0, prow_base, wave, lane);
 }
 
 // fp32 output; ATOMIC accumulates into C (split-K), otherwise plain store (beta = 0).

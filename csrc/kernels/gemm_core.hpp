@@ -77,16 +77,16 @@ struct MCGeom {
 };
 
 // Dense K-contiguous rows: element (r, k) at base[r*ld + k].
-template <int R>
+template <int R, class T = __bf16>
 struct KCDense {
   static constexpr bool KC = true;
   static constexpr int NI = R / 32;
-  const __bf16* ptr[NI];
+  const T* ptr[NI];
   uint32_t kcol;
   uint32_t K;
   const void* zero;
   __device__ void prep(int) {}
-  __device__ void init(const __bf16* base, long ld, uint32_t rows_total, uint32_t K_,
+  __device__ void init(const T* base, long ld, uint32_t rows_total, uint32_t K_,
                        uint32_t origin, int wave, int lane, const void* zero_page) {
     K = K_;
     zero = zero_page;
@@ -113,11 +113,11 @@ struct ConvGeom {
   int pad_w;             // horizontal padding (== pad for square padding)
 };
 
-template <int R, bool ALIGNED = false>
+template <int R, bool ALIGNED = false, class T = __bf16>
 struct KCIm2col {
   static constexpr bool KC = true;
   static constexpr int NI = R / 32;
-  const __bf16* x;
+  const T* x;
   int hi0[NI], wi0[NI];
   int rowoff[NI];   // ((img*H + hi0)*W + wi0)*C  (32-bit: host checks numel < 2^31)
   uint32_t kcol, K;
@@ -125,7 +125,7 @@ struct KCIm2col {
   const void* zero;
   int p_kh, p_kw, p_toff;  // ALIGNED: this k-step's tap (kh, kw) and (kh*W + kw)*C + ci0 + kcol
   bool p_kok;
-  __device__ void init(const __bf16* x_, const ConvGeom& g_, uint32_t M, uint32_t origin, int wave,
+  __device__ void init(const T* x_, const ConvGeom& g_, uint32_t M, uint32_t origin, int wave,
                        int lane, const void* zero_page) {
     x = x_;
     g = g_;
@@ -203,11 +203,11 @@ struct DgradClass {
   FastDiv fHcWc, fWc, fnkw;
 };
 
-template <int R, bool ALIGNED = false>
+template <int R, bool ALIGNED = false, class T = __bf16>
 struct KCDgrad {
   static constexpr bool KC = true;
   static constexpr int NI = R / 32;
-  const __bf16* dy;
+  const T* dy;
   int ib[NI], jb[NI];   // i + dh0, j + dw0 (dy row/col of the class's first tap)
   int rowoff[NI];       // ((img*Ho + ib)*Wo + jb)*Co  (32-bit: host checks numel < 2^31)
   uint32_t kcol, K;
@@ -216,7 +216,7 @@ struct KCDgrad {
   const void* zero;
   int p_a, p_b, p_toff;  // ALIGNED: this k-step's tap offsets and -(a*Wo + b)*Co + co0 + kcol
   bool p_kok;
-  __device__ void init(const __bf16* dy_, int Ho_, int Wo_, int Co_, FastDiv fCo_,
+  __device__ void init(const T* dy_, int Ho_, int Wo_, int Co_, FastDiv fCo_,
                        const DgradClass& cls, uint32_t M, uint32_t origin, int wave, int lane,
                        const void* zero_page) {
     dy = dy_; Ho = Ho_; Wo = Wo_; Co = Co_; fCo = fCo_; fnkw = cls.fnkw;
@@ -273,17 +273,17 @@ struct KCDgrad {
 };
 
 // Dense MN-contiguous operand: element (k, col) at base[k*ld + col]; W columns per tile.
-template <int W>
+template <int W, class T = __bf16>
 struct MCDense {
   static constexpr bool KC = false;
   static constexpr int NI = W / 32;
-  const __bf16* colptr[NI];
+  const T* colptr[NI];
   uint32_t krow[NI];
   long ld;
   uint32_t K;
   const void* zero;
   __device__ void prep(int) {}
-  __device__ void init(const __bf16* base, long ld_, uint32_t cols_total, uint32_t K_,
+  __device__ void init(const T* base, long ld_, uint32_t cols_total, uint32_t K_,
                        uint32_t origin, int wave, int lane, const void* zero_page) {
     ld = ld_;
     K = K_;
@@ -302,18 +302,18 @@ struct MCDense {
 };
 
 // Conv data-grad B operand: B(k = (t, co), n = ci) = W[co][tap(t)][ci] (weights [Co,KH,KW,Ci]).
-template <int W>
+template <int W, class T = __bf16>
 struct MCDgradW {
   static constexpr bool KC = false;
   static constexpr int NI = W / 32;
-  const __bf16* colptr[NI];
+  const T* colptr[NI];
   uint32_t krow[NI];
   uint32_t K, Co, taps, Ci;
   FastDiv fCo, fnkw;
   int kh0, kw0, S, KW;
   const void* zero;
   __device__ void prep(int) {}
-  __device__ void init(const __bf16* w, uint32_t Co_, uint32_t taps_, uint32_t Ci_, FastDiv fCo_,
+  __device__ void init(const T* w, uint32_t Co_, uint32_t taps_, uint32_t Ci_, FastDiv fCo_,
                        const DgradClass& cls, uint32_t origin, int wave, int lane,
                        const void* zero_page) {
     Co = Co_; taps = taps_; Ci = Ci_; fCo = fCo_; fnkw = cls.fnkw;
@@ -340,11 +340,11 @@ struct MCDgradW {
 };
 
 // Conv weight-grad B operand: B(k = output pixel, n = (kh,kw,ci)) = x[img, ho*s-p+kh, wo*s-p+kw, ci].
-template <int W>
+template <int W, class T = __bf16>
 struct MCIm2colT {
   static constexpr bool KC = false;
   static constexpr int NI = W / 32;
-  const __bf16* x;
+  const T* x;
   uint32_t krow[NI];
   int kh[NI], kw[NI], ci[NI];
   bool colok[NI];
@@ -352,7 +352,7 @@ struct MCIm2colT {
   ConvGeom g;
   const void* zero;
   __device__ void prep(int) {}
-  __device__ void init(const __bf16* x_, const ConvGeom& g_, uint32_t origin, int wave, int lane,
+  __device__ void init(const T* x_, const ConvGeom& g_, uint32_t origin, int wave, int lane,
                        const void* zero_page) {
     x = x_;
     g = g_;
@@ -494,6 +494,135 @@ struct MainLoop {
       }
     }
   }
+};
+
+// fp32-operand main loop ("split-bf16", the reference-precision path).  Operands are fp32 in
+// memory; each lane's 8-element chunk (the same chunk the bf16 policies hand to glds) is read
+// into registers one k-step ahead, split into hi = rn(v) and lo = rn(v - hi) and written as TWO
+// bf16 LDS images in exactly the bf16 layouts, so the fragment loaders are unchanged.  Each
+// 16x16x32 tile then takes 3 MFMAs: hi*hi + hi*lo + lo*hi (the lo*lo term is < 2^-16 relative),
+// i.e. fp32-class products at 3x the bf16 MFMA cost — still ~5x the v_mfma_f32_16x16x4_f32 rate.
+// One LDS stage: the register prefetch of step k+1 is what overlaps global latency with step k's
+// MFMAs, and the halved LDS keeps 2 blocks per CU for the 128x128 tile.
+template <int BM, int BN, class OpA, class OpB>
+struct MainLoopF32 {
+  static constexpr int MT = BM / 32;
+  static constexpr int NT = BN / 32;
+  static constexpr int A_BYTES = BM * BK * 2;
+  static constexpr int B_BYTES = BN * BK * 2;
+  static constexpr int IMG_BYTES = A_BYTES + B_BYTES;  // one precision image (A | B)
+  static constexpr int LDS_BYTES = 2 * IMG_BYTES;      // hi image | lo image
+  struct Regs {
+    float4 a[OpA::NI][2];
+    float4 b[OpB::NI][2];
+  };
+
+  __device__ static void load(Regs& r, OpA& a, OpB& b, int kt) {
+    a.prep(kt);
+    b.prep(kt);
+#pragma unroll
+    for (int i = 0; i < OpA::NI; ++i) {
+      const float4* p = reinterpret_cast<const float4*>(a.src(kt, i));
+      r.a[i][0] = p[0];
+      r.a[i][1] = p[1];
+    }
+#pragma unroll
+    for (int i = 0; i < OpB::NI; ++i) {
+      const float4* p = reinterpret_cast<const float4*>(b.src(kt, i));
+      r.b[i][0] = p[0];
+      r.b[i][1] = p[1];
+    }
+  }
+
+  __device__ static void split_store(char* hi_dst, char* lo_dst, const float4 (&v)[2]) {
+    const float f[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    bf16x8 h, l;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      __bf16 hq, lq;
+      split_bf16(f[q], hq, lq);
+      h[q] = hq;
+      l[q] = lq;
+    }
+    *reinterpret_cast<bf16x8*>(hi_dst) = h;
+    *reinterpret_cast<bf16x8*>(lo_dst) = l;
+  }
+
+  // lane-linear destinations, the same bytes a glds16 of this chunk would have written
+  __device__ static void store(char* smem, const Regs& r, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < OpA::NI; ++i) {
+      char* d = smem + (wave * OpA::NI + i) * 1024 + lane * 16;
+      split_store(d, d + IMG_BYTES, r.a[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < OpB::NI; ++i) {
+      char* d = smem + A_BYTES + (wave * OpB::NI + i) * 1024 + lane * 16;
+      split_store(d, d + IMG_BYTES, r.b[i]);
+    }
+  }
+
+  __device__ static void run(char* smem, OpA& a, OpB& b, int kt0, int kt1,
+                             f32x4 (&acc)[MT][NT], int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (kt0 >= kt1) return;
+    const int wr = wave >> 1, wc = wave & 1;
+    const uint32_t arow0 = wr * (BM / 2), bcol0 = wc * (BN / 2);
+    Regs r;
+    load(r, a, b, kt0);
+    store(smem, r, wave, lane);
+    __syncthreads();
+    const char* ahi = smem;
+    const char* bhi = smem + A_BYTES;
+    const char* alo = smem + IMG_BYTES;
+    const char* blo = smem + IMG_BYTES + A_BYTES;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) load(r, a, b, kt + 1);  // in flight under this step's MFMAs
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 ah[MT], al[MT], bh[NT], bl[NT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          ah[i] = FragLoader<OpA::KC, BM>::load(ahi, arow0 + i * 16, ks, lane);
+          al[i] = FragLoader<OpA::KC, BM>::load(alo, arow0 + i * 16, ks, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          bh[j] = FragLoader<OpB::KC, BN>::load(bhi, bcol0 + j * 16, ks, lane);
+          bl[j] = FragLoader<OpB::KC, BN>::load(blo, bcol0 + j * 16, ks, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], ah[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], al[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], ah[i], acc[i][j], 0, 0, 0);
+          }
+      }
+      if (more) {
+        __syncthreads();  // every wave is done reading this step's images
+        store(smem, r, wave, lane);
+        __syncthreads();
+      }
+    }
+  }
+};
+
+// Selects the main loop for the operand element type.
+template <class T, int BM, int BN, class OpA, class OpB, int NS = 2>
+struct MainLoopFor {
+  typedef MainLoop<BM, BN, OpA, OpB, NS> type;
+  static constexpr int LDS_BYTES = NS * (BM + BN) * BK * 2;
+};
+template <int BM, int BN, class OpA, class OpB, int NS>
+struct MainLoopFor<float, BM, BN, OpA, OpB, NS> {
+  typedef MainLoopF32<BM, BN, OpA, OpB> type;
+  static constexpr int LDS_BYTES = MainLoopF32<BM, BN, OpA, OpB>::LDS_BYTES;
 };
 
 // Row/col of acc element: lane holds C[m][n + e], e = 0..3, for tile (i, j):

@@ -14,6 +14,7 @@ struct ConvShape {
   int Ho, Wo;        // output
   int stride_w = 0;  // horizontal stride when != stride (0: same); fwd / wgrad only
   int pad_w = -1;    // horizontal padding when >= 0 (else pad): Inception 1x7 / 7x1 convs
+  bool f32 = false;  // fp32 activations/weights (split-bf16 MFMA main loop) instead of bf16
 };
 
 // BatchNorm statistics are accumulated with fp32 atomics into kStatReplicas replica rows of a
@@ -39,7 +40,7 @@ void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq
               const float* st_shift, const ConvShape& s, hipStream_t st,
               const float* bias = nullptr, bool relu = false);
 // Optional dgrad epilogue fusions:
-//  addend: bf16 [N*H*W][Ci] added to dx (the block input's other gradient, e.g. the residual);
+//  addend: [N*H*W][Ci] (activation dtype) added to dx (the block input's other gradient, e.g. the residual);
 //  bn_*:   the conv input was relu(bn(y)) with a single consumer: dx becomes g = dx*[z > 0] and
 //          Σg, Σg·x̂ go to rep rows 0/1 ([3][kStatReplicas][Ci] zeroed slab, see bn_bwd_collect).
 struct DgradFusion {
@@ -96,9 +97,12 @@ void avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho,
 
 // ---- dense GEMM: C[M][N] = op(A) op(B) --------------------------------------------------------
 //  a_kc: A stored [M][K] (else [K][M]);  b_kc: B stored [N][K] (else [K][N]).
-//  out: 0 = bf16 store (bias/act), 1 = fp32 store (bias), 2 = fp32 atomic accumulate (split-K).
+//  out: 0 = activation-dtype store (bias/act), 1 = fp32 store (bias), 2 = fp32 atomic accumulate
+//  (split-K).
+//  f32: A and B are fp32 (split-bf16 main loop); out 0 then stores fp32 (the activation dtype).
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
-          long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st);
+          long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
+          bool f32 = false);
 
 // ---- BatchNorm ------------------------------------------------------------------------------
 // Reduce a [P][C] partial slab pair (shifted sums) and finalize: mean, invstd, scale, bias and
@@ -108,17 +112,17 @@ void bn_finalize(float* psum, float* psq, int P, int C, long count, const float*
                  const float* gamma, const float* beta, float* run_mean, float* run_var,
                  float momentum, float eps, float* mean, float* invstd, float* scale, float* bias,
                  bool zero_after, long long* nbt, hipStream_t st);
-// z = act(y*scale + bias [+ r | + r*rscale + rbias])   (M rows of C channels, bf16)
+// z = act(y*scale + bias [+ r | + r*rscale + rbias])   (M rows of C channels, bf16 or f32)
 void bn_act_fwd(const void* y, const float* scale, const float* bias, const void* r,
                 const float* rscale, const float* rbias, void* z, long M, int C, bool relu,
-                hipStream_t st);
+                hipStream_t st, bool f32 = false);
 // sums: out_g[C], out_gx[C], out_gx2[C] (if y2).  rep: zeroed [3][kStatReplicas][C] slab,
 // left zeroed on return.
 void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float* mean,
                        const float* invstd, const void* y2, const float* mean2,
                        const float* invstd2, bool relu, long M, int C, float* out_g,
                        float* out_gx, float* out_gx2, float* rep, float* dgamma, float* dbeta,
-                       float* dgamma2, float* dbeta2, hipStream_t st);
+                       float* dgamma2, float* dbeta2, hipStream_t st, bool f32 = false);
 // Sum the replica rows of a bwd slab (filled by a fused dgrad epilogue) into out_g / out_gx,
 // re-zero it, optionally accumulate dγ += Σg·x̂, dβ += Σg.
 void bn_bwd_collect(float* rep, int C, float* out_g, float* out_gx, float* dgamma, float* dbeta,
@@ -128,20 +132,23 @@ void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float*
                       const float* sum_gx, const void* y2, const float* mean2,
                       const float* invstd2, const float* gamma2, const float* sum_gx2, long count,
                       bool relu, bool want_dres, void* dy, void* dother, long M, int C,
-                      hipStream_t st);
+                      hipStream_t st, bool f32 = false);
 
 // ---- pooling ----------------------------------------------------------------------------------
 void maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
-                 int k, int stride, int pad, hipStream_t st);
+                 int k, int stride, int pad, hipStream_t st, bool f32 = false);
 void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C, int Ho,
-                 int Wo, int k, int stride, int pad, hipStream_t st);
-void avgpool_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st);
-void avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
+                 int Wo, int k, int stride, int pad, hipStream_t st, bool f32 = false);
+void avgpool_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st, bool f32 = false);
+void avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st, bool f32 = false);
 
 // ---- loss / optimizer / data -----------------------------------------------------------------
 void cross_entropy_fwd_bwd(const void* logits, const int64_t* labels, float* loss, void* grad,
                            int R, int V, float smoothing, int64_t ignore_index, int* work,
-                           hipStream_t st);
+                           hipStream_t st, bool f32 = false);
+// *correct += #rows whose first maximal logit is at the label (torch.argmax tie rule)
+void top1_correct(const void* logits, const int64_t* labels, int R, int V, int* correct,
+                  hipStream_t st, bool f32 = false);
 void sgd_step(float* p, const float* g, float* m, void* shadow, long n, float lr, float momentum,
               float dampening, float wd, bool nesterov, bool first, float grad_scale,
               hipStream_t st);
@@ -149,13 +156,13 @@ void adamw_step(float* p, const float* g, float* m, float* v, void* shadow, long
                 float b1, float b2, float eps, float wd, float bc1, float bc2, float grad_scale,
                 hipStream_t st);
 void nchw_to_nhwc(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int Cp,
-                  hipStream_t st);
+                  hipStream_t st, bool y_f32 = false);
 // Stem "super-pixel" packing (C <= 4): y[n][h'][j][p*4 + c] = x[n][c][h'-pad][2j+p-pad] (zero
 // outside), h' < Hp, j < Wsp.  A KxK stride-2 conv on x becomes a K x ceil(K/2) conv with
 // vertical stride 2 and horizontal stride 1 on 8-channel super-pixels: 16-byte operand rows with
 // 3 of 8 lanes padding instead of 5 of 8 (the reduction shrinks from K*K*8 to K*ceil(K/2)*8).
 void stem_pack(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int pad,
-               int Hp, int Wsp, hipStream_t st);
+               int Hp, int Wsp, hipStream_t st, bool y_f32 = false);
 void synthetic_batch(const int64_t* idx, int n, int C, int H, int W, int classes, int seed,
                      void* x, bool bf16_out, int64_t* labels, hipStream_t st);
 

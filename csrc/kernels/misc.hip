@@ -39,16 +39,17 @@ __device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
   return r;
 }
 
-// one block per row; logits bf16 [R][V]
-__global__ __launch_bounds__(256) void ce_kernel(const __bf16* __restrict__ logits,
+// one block per row; logits T (bf16 / fp32) [R][V]
+template <class T>
+__global__ __launch_bounds__(256) void ce_kernel(const T* __restrict__ logits,
                                                  const int64_t* __restrict__ labels,
-                                                 float* __restrict__ loss, __bf16* __restrict__ grad,
+                                                 float* __restrict__ loss, T* __restrict__ grad,
                                                  int V, float eps, int64_t ignore,
                                                  const int* __restrict__ nvalid) {
   __shared__ float sh[8];
   const long row = blockIdx.x;
-  const __bf16* x = logits + row * V;
-  __bf16* g = grad + row * V;
+  const T* x = logits + row * V;
+  T* g = grad + row * V;
   const int64_t lab = labels[row];
   const bool valid = lab != ignore;
   const bool vec = (V % 8) == 0;
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(256) void ce_kernel(const __bf16* __restrict__ logi
   if (vec) {
     for (int c = threadIdx.x; c < V / 8; c += 256) {
       float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(x + c * 8), v);
+      load8(x + c * 8, v);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         mx = fmaxf(mx, v[q]);
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) void ce_kernel(const __bf16* __restrict__ logi
   if (vec) {
     for (int c = threadIdx.x; c < V / 8; c += 256) {
       float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(x + c * 8), v);
+      load8(x + c * 8, v);
 #pragma unroll
       for (int q = 0; q < 8; ++q) se += __expf(v[q] - mx);
     }
@@ -97,30 +98,85 @@ __global__ __launch_bounds__(256) void ce_kernel(const __bf16* __restrict__ logi
   if (vec) {
     for (int c = threadIdx.x; c < V / 8; c += 256) {
       float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(x + c * 8), v);
+      load8(x + c * 8, v);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         int col = c * 8 + q;
         float t = base_t + (col == lab ? 1.f - eps : 0.f);
         v[q] = (__expf(v[q] - mx) * inv_se - t) * scale;
       }
-      *reinterpret_cast<uint4*>(g + c * 8) = pack8(v);
+      store8(g + c * 8, v);
     }
   } else {
     for (int c = threadIdx.x; c < V; c += 256) {
       float t = base_t + (c == lab ? 1.f - eps : 0.f);
-      g[c] = (__bf16)((__expf((float)x[c] - mx) * inv_se - t) * scale);
+      g[c] = (T)((__expf((float)x[c] - mx) * inv_se - t) * scale);
     }
   }
 }
 
 void cross_entropy_fwd_bwd(const void* logits, const int64_t* labels, float* loss, void* grad,
                            int R, int V, float smoothing, int64_t ignore_index, int* work,
-                           hipStream_t st) {
+                           hipStream_t st, bool f32) {
   hipMemsetAsync(loss, 0, sizeof(float), st);
   hipLaunchKernelGGL(ce_count_kernel, dim3(1), dim3(256), 0, st, labels, R, ignore_index, work);
-  hipLaunchKernelGGL(ce_kernel, dim3(R), dim3(256), 0, st, (const __bf16*)logits, labels, loss,
-                     (__bf16*)grad, V, smoothing, ignore_index, (const int*)work);
+  if (f32)
+    hipLaunchKernelGGL(ce_kernel<float>, dim3(R), dim3(256), 0, st, (const float*)logits, labels,
+                       loss, (float*)grad, V, smoothing, ignore_index, (const int*)work);
+  else
+    hipLaunchKernelGGL(ce_kernel<__bf16>, dim3(R), dim3(256), 0, st, (const __bf16*)logits, labels,
+                       loss, (__bf16*)grad, V, smoothing, ignore_index, (const int*)work);
+}
+
+// ------------------------------------------------------------------------------ evaluation
+// Top-1 correct count (the reference's eval loop: argmax over classes == label, summed): one
+// wave per row, first maximal index wins (torch.argmax's tie rule), NaN counts as maximal; the
+// per-block count is one integer atomic into *correct (order-independent, so deterministic).
+template <class T>
+__global__ __launch_bounds__(256) void top1_correct_kernel(const T* __restrict__ logits,
+                                                           const int64_t* __restrict__ labels,
+                                                           int R, int V, int* __restrict__ correct) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + wave;
+  int hit = 0;
+  if (row < R) {
+    const T* x = logits + (long)row * V;
+    float best = -INFINITY;
+    int arg = 0x7fffffff;
+    for (int c = lane; c < V; c += 64) {
+      const float v = (float)x[c];
+      if (v > best || (v != v && best == best)) {  // strictly greater keeps the first index
+        best = v;
+        arg = c;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o);
+      const int oa = __shfl_xor(arg, o);
+      const bool onan = ob != ob, mnan = best != best;
+      if ((onan && !mnan) || (onan == mnan && (ob > best || (ob == best && oa < arg)))) {
+        best = ob;
+        arg = oa;
+      }
+    }
+    hit = (lane == 0 && (int64_t)arg == labels[row]) ? 1 : 0;
+  }
+  __shared__ int cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  if (hit) atomicAdd(&cnt, 1);
+  __syncthreads();
+  if (threadIdx.x == 0 && cnt) atomicAdd(correct, cnt);
+}
+
+void top1_correct(const void* logits, const int64_t* labels, int R, int V, int* correct,
+                  hipStream_t st, bool f32) {
+  dim3 g((R + 3) / 4);
+  if (f32)
+    hipLaunchKernelGGL(top1_correct_kernel<float>, g, dim3(256), 0, st, (const float*)logits, labels, R, V, correct);
+  else
+    hipLaunchKernelGGL(top1_correct_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)logits, labels, R, V, correct);
 }
 
 // ------------------------------------------------------------------------------ optimizers
@@ -205,10 +261,10 @@ void adamw_step(float* p, const float* g, float* m, float* v, void* shadow, long
 }
 
 // ------------------------------------------------------------------------------ layout / data
-// x [N][C][H][W] (fp32 or bf16) -> y [N][H][W][Cp] bf16 (channels >= C zero)
-template <bool BF16IN>
+// x [N][C][H][W] (fp32 or bf16) -> y [N][H][W][Cp] T (channels >= C zero)
+template <bool BF16IN, class T>
 __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const void* __restrict__ xin,
-                                                           __bf16* __restrict__ y, int N, int C,
+                                                           T* __restrict__ y, int N, int C,
                                                            int H, int W, int Cp) {
   long total = (long)N * H * W;
   long hw = (long)H * W;
@@ -228,18 +284,22 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const void* __restric
           v[q] = 0.f;
         }
       }
-      *reinterpret_cast<uint4*>(y + t * Cp + c0) = pack8(v);
+      store8(y + t * Cp + c0, v);
     }
   }
 }
 
 void nchw_to_nhwc(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int Cp,
-                  hipStream_t st) {
+                  hipStream_t st, bool y_f32) {
   long total = (long)N * H * W;
-  if (x_is_bf16)
-    hipLaunchKernelGGL(nchw_to_nhwc_kernel<true>, dim3(grid1d(total)), dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, Cp);
-  else
-    hipLaunchKernelGGL(nchw_to_nhwc_kernel<false>, dim3(grid1d(total)), dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, Cp);
+  dim3 g(grid1d(total));
+  if (y_f32) {
+    if (x_is_bf16) hipLaunchKernelGGL((nchw_to_nhwc_kernel<true, float>), g, dim3(256), 0, st, x, (float*)y, N, C, H, W, Cp);
+    else hipLaunchKernelGGL((nchw_to_nhwc_kernel<false, float>), g, dim3(256), 0, st, x, (float*)y, N, C, H, W, Cp);
+  } else {
+    if (x_is_bf16) hipLaunchKernelGGL((nchw_to_nhwc_kernel<true, __bf16>), g, dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, Cp);
+    else hipLaunchKernelGGL((nchw_to_nhwc_kernel<false, __bf16>), g, dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, Cp);
+  }
 }
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
@@ -585,10 +645,10 @@ void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStre
 }
 
 // ------------------------------------------------------------------------------ stem packing
-// One thread per output 16-byte super-pixel: 2 horizontally adjacent padded pixels x 4 channels.
-template <bool IN_BF16>
+// One thread per output super-pixel: 2 horizontally adjacent padded pixels x 4 channels.
+template <bool IN_BF16, class T>
 __global__ __launch_bounds__(256) void stem_pack_kernel(const void* __restrict__ xin,
-                                                        __bf16* __restrict__ y, int N, int C,
+                                                        T* __restrict__ y, int N, int C,
                                                         int H, int W, int pad, int Hp, int Wsp) {
   const long total = (long)N * Hp * Wsp;
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
@@ -614,19 +674,21 @@ __global__ __launch_bounds__(256) void stem_pack_kernel(const void* __restrict__
         v[p * 4 + c] = x;
       }
     }
-    reinterpret_cast<uint4*>(y)[t] = pack8(v);
+    store8(y + t * 8, v);
   }
 }
 
 void stem_pack(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int pad,
-               int Hp, int Wsp, hipStream_t st) {
+               int Hp, int Wsp, hipStream_t st, bool y_f32) {
   const long total = (long)N * Hp * Wsp;
-  if (x_is_bf16)
-    hipLaunchKernelGGL(stem_pack_kernel<true>, dim3(grid1d(total)), dim3(256), 0, st, x,
-                       (__bf16*)y, N, C, H, W, pad, Hp, Wsp);
-  else
-    hipLaunchKernelGGL(stem_pack_kernel<false>, dim3(grid1d(total)), dim3(256), 0, st, x,
-                       (__bf16*)y, N, C, H, W, pad, Hp, Wsp);
+  dim3 g(grid1d(total));
+  if (y_f32) {
+    if (x_is_bf16) hipLaunchKernelGGL((stem_pack_kernel<true, float>), g, dim3(256), 0, st, x, (float*)y, N, C, H, W, pad, Hp, Wsp);
+    else hipLaunchKernelGGL((stem_pack_kernel<false, float>), g, dim3(256), 0, st, x, (float*)y, N, C, H, W, pad, Hp, Wsp);
+  } else {
+    if (x_is_bf16) hipLaunchKernelGGL((stem_pack_kernel<true, __bf16>), g, dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, pad, Hp, Wsp);
+    else hipLaunchKernelGGL((stem_pack_kernel<false, __bf16>), g, dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, pad, Hp, Wsp);
+  }
 }
 
 }  // namespace mipipe

@@ -1,13 +1,14 @@
 // NHWC pooling: max-pool with 1-byte window-argmax (fwd/bwd) and global average pool.
 // Backward max-pool is a gather over the windows covering each input pixel (deterministic,
-// no atomics).  All loads/stores are 16-B vectors of 8 bf16 channels.
+// no atomics).  Each thread moves 8 channels (one 16-B bf16 vector or two fp32 vectors).
 #include "common.hpp"
 #include "launchers.hpp"
 
 namespace mipipe {
 
-__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restrict__ x,
-                                                          __bf16* __restrict__ y,
+template <class T>
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x,
+                                                          T* __restrict__ y,
                                                           uint8_t* __restrict__ idx, int N, int H,
                                                           int W, int C, int Ho, int Wo, int k,
                                                           int s, int p) {
@@ -35,7 +36,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restri
         int wi = wo * s - p + kw;
         if (wi < 0 || wi >= W) continue;
         float v[8];
-        unpack8(*reinterpret_cast<const uint4*>(x + (((long)n * H + hi) * W + wi) * C + c8 * 8), v);
+        load8(x + (((long)n * H + hi) * W + wi) * C + c8 * 8, v);
 #pragma unroll
         for (int q = 0; q < 8; ++q)
           if (v[q] > best[q] || (v[q] != v[q])) {  // NaN propagates like torch
@@ -45,7 +46,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restri
       }
     }
     long o = pix * C + c8 * 8;
-    *reinterpret_cast<uint4*>(y + o) = pack8(best);
+    store8(y + o, best);
     uint2 a;
     a.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | ((uint32_t)arg[3] << 24);
     a.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | ((uint32_t)arg[7] << 24);
@@ -53,9 +54,10 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restri
   }
 }
 
-__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restrict__ dy,
+template <class T>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dy,
                                                           const uint8_t* __restrict__ idx,
-                                                          __bf16* __restrict__ dx, int N, int H,
+                                                          T* __restrict__ dx, int N, int H,
                                                           int W, int C, int Ho, int Wo, int k,
                                                           int s, int p) {
   const int cg = C / 8;
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restri
         long o = (((long)n * Ho + ho) * Wo + wo) * C + c8 * 8;
         uint2 a = *reinterpret_cast<const uint2*>(idx + o);
         float g[8];
-        unpack8(*reinterpret_cast<const uint4*>(dy + o), g);
+        load8(dy + o, g);
         uint32_t w0 = a.x, w1 = a.y;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restri
         }
       }
     }
-    *reinterpret_cast<uint4*>(dx + pix * C + c8 * 8) = pack8(acc);
+    store8(dx + pix * C + c8 * 8, acc);
   }
 }
 
@@ -104,22 +106,31 @@ static int ew_grid(long work) {
 }
 
 void maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int Ho, int Wo,
-                 int k, int stride, int pad, hipStream_t st) {
+                 int k, int stride, int pad, hipStream_t st, bool f32) {
   long work = (long)N * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(ew_grid(work)), dim3(256), 0, st, (const __bf16*)x,
-                     (__bf16*)y, idx, N, H, W, C, Ho, Wo, k, stride, pad);
+  if (f32)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(ew_grid(work)), dim3(256), 0, st,
+                       (const float*)x, (float*)y, idx, N, H, W, C, Ho, Wo, k, stride, pad);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<__bf16>, dim3(ew_grid(work)), dim3(256), 0, st,
+                       (const __bf16*)x, (__bf16*)y, idx, N, H, W, C, Ho, Wo, k, stride, pad);
 }
 
 void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C, int Ho,
-                 int Wo, int k, int stride, int pad, hipStream_t st) {
+                 int Wo, int k, int stride, int pad, hipStream_t st, bool f32) {
   long work = (long)N * H * W * (C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(ew_grid(work)), dim3(256), 0, st, (const __bf16*)dy,
-                     idx, (__bf16*)dx, N, H, W, C, Ho, Wo, k, stride, pad);
+  if (f32)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(ew_grid(work)), dim3(256), 0, st,
+                       (const float*)dy, idx, (float*)dx, N, H, W, C, Ho, Wo, k, stride, pad);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<__bf16>, dim3(ew_grid(work)), dim3(256), 0, st,
+                       (const __bf16*)dy, idx, (__bf16*)dx, N, H, W, C, Ho, Wo, k, stride, pad);
 }
 
 // Global average pool: y[n][c] = mean_hw x[n][hw][c]
-__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const __bf16* __restrict__ x,
-                                                          __bf16* __restrict__ y, int N, int HW,
+template <class T>
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const T* __restrict__ x,
+                                                          T* __restrict__ y, int N, int HW,
                                                           int C) {
   const int cg = C / 8;
   long total = (long)N * cg;
@@ -129,21 +140,22 @@ __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const __bf16* __restri
     int c8 = (int)(t % cg);
     long n = t / cg;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const __bf16* base = x + n * HW * C + c8 * 8;
+    const T* base = x + n * HW * C + c8 * 8;
     for (int i = 0; i < HW; ++i) {
       float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(base + (long)i * C), v);
+      load8(base + (long)i * C, v);
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] += v[q];
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] *= inv;
-    *reinterpret_cast<uint4*>(y + n * C + c8 * 8) = pack8(acc);
+    store8(y + n * C + c8 * 8, acc);
   }
 }
 
-__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const __bf16* __restrict__ dy,
-                                                          __bf16* __restrict__ dx, int N, int HW,
+template <class T>
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const T* __restrict__ dy,
+                                                          T* __restrict__ dx, int N, int HW,
                                                           int C) {
   const int cg = C / 8;
   long total = (long)N * HW * cg;
@@ -154,21 +166,27 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const __bf16* __restri
     long pix = t / cg;
     long n = pix / HW;
     float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(dy + n * C + c8 * 8), v);
+    load8(dy + n * C + c8 * 8, v);
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] *= inv;
-    *reinterpret_cast<uint4*>(dx + pix * C + c8 * 8) = pack8(v);
+    store8(dx + pix * C + c8 * 8, v);
   }
 }
 
-void avgpool_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(ew_grid((long)N * (C / 8))), dim3(256), 0, st,
-                     (const __bf16*)x, (__bf16*)y, N, HW, C);
+void avgpool_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st, bool f32) {
+  dim3 g(ew_grid((long)N * (C / 8)));
+  if (f32)
+    hipLaunchKernelGGL(avgpool_fwd_kernel<float>, g, dim3(256), 0, st, (const float*)x, (float*)y, N, HW, C);
+  else
+    hipLaunchKernelGGL(avgpool_fwd_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)x, (__bf16*)y, N, HW, C);
 }
 
-void avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(ew_grid((long)N * HW * (C / 8))), dim3(256), 0, st,
-                     (const __bf16*)dy, (__bf16*)dx, N, HW, C);
+void avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st, bool f32) {
+  dim3 g(ew_grid((long)N * HW * (C / 8)));
+  if (f32)
+    hipLaunchKernelGGL(avgpool_bwd_kernel<float>, g, dim3(256), 0, st, (const float*)dy, (float*)dx, N, HW, C);
+  else
+    hipLaunchKernelGGL(avgpool_bwd_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)dy, (__bf16*)dx, N, HW, C);
 }
 
 }  // namespace mipipe

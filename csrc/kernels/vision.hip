@@ -157,10 +157,6 @@ __global__ __launch_bounds__(256) void gconv_wgrad_kernel(
 }
 
 // ------------------------------------------------------------------------ depthwise, C % 8 == 0
-__device__ __forceinline__ void load8(const __bf16* p, float* f) {
-  unpack8(*reinterpret_cast<const uint4*>(p), f);
-}
-
 __device__ __forceinline__ void mask8(const __bf16* z, int act, float* g) {
   float zv[8];
   load8(z, zv);

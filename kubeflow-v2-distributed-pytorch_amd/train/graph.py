@@ -12,7 +12,9 @@ Constraints of capture (checked or documented):
 * no host synchronisation inside the step;
 * host-side scalars are frozen at capture: fine for SGD (momentum buffers are on the device),
   NOT for AdamW's bias correction or per-step dropout seeds — :func:`graph_safe` refuses those;
-* single process (eager DDP keeps its overlapped RCCL buckets for N > 1).
+* under mipipe DDP the bucket all-reduces are captured too (RCCL on the process group's
+  stream); capture runs in ``thread_local`` error mode so the RCCL watchdog thread can keep
+  querying its events.
 """
 from __future__ import annotations
 
@@ -62,7 +64,9 @@ class GraphedStep:
         pool = None
         for x, y in self.static:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            # thread_local: the process group's watchdog thread keeps polling its RCCL work
+            # events while this thread captures; global mode would fail those queries
+            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 loss = self.fn(x, y).detach()  # drop the autograd graph: no stale grad nodes
             pool = g.pool()
             self.graphs.append(g)
