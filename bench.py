@@ -262,7 +262,9 @@ def build_cnn(a, world, local, dev, rank):
         if a.distributed:
             model = DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=a.bucket_cap_mb,
                                             force_reduce=a.force_reduce)
-        opt = SGD(model.parameters(), 0.1, momentum=0.9, weight_decay=1e-4)
+        # fp32 compute reads the fp32 master weights directly: no bf16 shadow to refresh
+        opt = SGD(model.parameters(), 0.1, momentum=0.9, weight_decay=1e-4,
+                  shadow_dtype=None if _compute_dtype(a) == torch.float32 else "auto")
 
         def step(x, y):
             opt.zero_grad()

@@ -90,14 +90,6 @@ __device__ __forceinline__ float as_stored(float v) {
   else return bf2f(f2bf(v));
 }
 
-// Split an fp32 value into bf16 hi + bf16 lo (hi = rn(v), lo = rn(v - hi)): hi*b_hi + hi*b_lo +
-// lo*b_hi reproduces an fp32 product to ~2^-16 relative (the lo*lo term is below fp32 rounding
-// of the accumulation) — the "split-bf16" scheme the fp32 GEMM main loop runs on bf16 MFMA.
-__device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
-  hi = f2bf(v);
-  lo = f2bf(v - bf2f(hi));
-}
-
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

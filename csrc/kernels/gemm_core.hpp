@@ -496,22 +496,29 @@ struct MainLoop {
   }
 };
 
-// fp32-operand main loop ("split-bf16", the reference-precision path).  Operands are fp32 in
-// memory; each lane's 8-element chunk (the same chunk the bf16 policies hand to glds) is read
-// into registers one k-step ahead, split into hi = rn(v) and lo = rn(v - hi) and written as TWO
-// bf16 LDS images in exactly the bf16 layouts, so the fragment loaders are unchanged.  Each
-// 16x16x32 tile then takes 3 MFMAs: hi*hi + hi*lo + lo*hi (the lo*lo term is < 2^-16 relative),
-// i.e. fp32-class products at 3x the bf16 MFMA cost — still ~5x the v_mfma_f32_16x16x4_f32 rate.
-// One LDS stage: the register prefetch of step k+1 is what overlaps global latency with step k's
-// MFMAs, and the halved LDS keeps 2 blocks per CU for the 128x128 tile.
+// fp32-operand main loop ("split-bf16x3", the reference-precision path).  Operands are fp32
+// in memory; each lane's 8-element chunk (the same chunk the bf16 policies hand to glds) is read
+// into registers one k-step ahead and split exactly into three bf16 parts
+//   v = v0 + v1 + v2,  v0 = rn(v), v1 = rn(v - v0), v2 = rn(v - v0 - v1)
+// (3 x 8 significant bits = fp32's 24), written as three bf16 LDS images in exactly the bf16
+// layouts, so the fragment loaders are unchanged.  Each 16x16x32 tile takes 6 MFMAs — every
+// partial product down to 2^-16 relative, smallest first:
+//   a0*b2 + a1*b1 + a2*b0,  a0*b1 + a1*b0,  a0*b0
+// bf16 x bf16 products are exact in the fp32 accumulator, so the result carries fp32-class
+// error (~1e-7 relative; measured against float64 in tests/test_fp32_gpu.py) at 1/6 of the bf16
+// MFMA rate — still ~2.6x the v_mfma_f32_16x16x4_f32 peak.  (A two-part split would lose 8 bits
+// per operand: ~1e-5 errors, enough to flip near-zero ReLU decisions the float64 model makes.)
+// One LDS stage: the register prefetch of step k+1 is what overlaps global latency with step
+// k's MFMAs.
 template <int BM, int BN, class OpA, class OpB>
 struct MainLoopF32 {
   static constexpr int MT = BM / 32;
   static constexpr int NT = BN / 32;
+  static constexpr int PARTS = 3;
   static constexpr int A_BYTES = BM * BK * 2;
   static constexpr int B_BYTES = BN * BK * 2;
-  static constexpr int IMG_BYTES = A_BYTES + B_BYTES;  // one precision image (A | B)
-  static constexpr int LDS_BYTES = 2 * IMG_BYTES;      // hi image | lo image
+  static constexpr int IMG_BYTES = A_BYTES + B_BYTES;      // one part's image (A | B)
+  static constexpr int LDS_BYTES = PARTS * IMG_BYTES;      // part 0 | part 1 | part 2
   struct Regs {
     float4 a[OpA::NI][2];
     float4 b[OpB::NI][2];
@@ -534,32 +541,31 @@ struct MainLoopF32 {
     }
   }
 
-  __device__ static void split_store(char* hi_dst, char* lo_dst, const float4 (&v)[2]) {
+  __device__ static void split_store(char* dst, const float4 (&v)[2]) {
     const float f[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
-    bf16x8 h, l;
+    bf16x8 p0, p1, p2;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      __bf16 hq, lq;
-      split_bf16(f[q], hq, lq);
-      h[q] = hq;
-      l[q] = lq;
+      const __bf16 h = f2bf(f[q]);
+      const float r1 = f[q] - bf2f(h);
+      const __bf16 m = f2bf(r1);
+      p0[q] = h;
+      p1[q] = m;
+      p2[q] = f2bf(r1 - bf2f(m));
     }
-    *reinterpret_cast<bf16x8*>(hi_dst) = h;
-    *reinterpret_cast<bf16x8*>(lo_dst) = l;
+    *reinterpret_cast<bf16x8*>(dst) = p0;
+    *reinterpret_cast<bf16x8*>(dst + IMG_BYTES) = p1;
+    *reinterpret_cast<bf16x8*>(dst + 2 * IMG_BYTES) = p2;
   }
 
   // lane-linear destinations, the same bytes a glds16 of this chunk would have written
   __device__ static void store(char* smem, const Regs& r, int wave, int lane) {
 #pragma unroll
-    for (int i = 0; i < OpA::NI; ++i) {
-      char* d = smem + (wave * OpA::NI + i) * 1024 + lane * 16;
-      split_store(d, d + IMG_BYTES, r.a[i]);
-    }
+    for (int i = 0; i < OpA::NI; ++i)
+      split_store(smem + (wave * OpA::NI + i) * 1024 + lane * 16, r.a[i]);
 #pragma unroll
-    for (int i = 0; i < OpB::NI; ++i) {
-      char* d = smem + A_BYTES + (wave * OpB::NI + i) * 1024 + lane * 16;
-      split_store(d, d + IMG_BYTES, r.b[i]);
-    }
+    for (int i = 0; i < OpB::NI; ++i)
+      split_store(smem + A_BYTES + (wave * OpB::NI + i) * 1024 + lane * 16, r.b[i]);
   }
 
   __device__ static void run(char* smem, OpA& a, OpB& b, int kt0, int kt1,
@@ -575,33 +581,33 @@ struct MainLoopF32 {
     load(r, a, b, kt0);
     store(smem, r, wave, lane);
     __syncthreads();
-    const char* ahi = smem;
-    const char* bhi = smem + A_BYTES;
-    const char* alo = smem + IMG_BYTES;
-    const char* blo = smem + IMG_BYTES + A_BYTES;
     for (int kt = kt0; kt < kt1; ++kt) {
       const bool more = kt + 1 < kt1;
       if (more) load(r, a, b, kt + 1);  // in flight under this step's MFMAs
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 ah[MT], al[MT], bh[NT], bl[NT];
+        bf16x8 af[PARTS][MT], bfr[PARTS][NT];
 #pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          ah[i] = FragLoader<OpA::KC, BM>::load(ahi, arow0 + i * 16, ks, lane);
-          al[i] = FragLoader<OpA::KC, BM>::load(alo, arow0 + i * 16, ks, lane);
-        }
+        for (int p = 0; p < PARTS; ++p) {
 #pragma unroll
-        for (int j = 0; j < NT; ++j) {
-          bh[j] = FragLoader<OpB::KC, BN>::load(bhi, bcol0 + j * 16, ks, lane);
-          bl[j] = FragLoader<OpB::KC, BN>::load(blo, bcol0 + j * 16, ks, lane);
+          for (int i = 0; i < MT; ++i)
+            af[p][i] = FragLoader<OpA::KC, BM>::load(smem + p * IMG_BYTES, arow0 + i * 16, ks, lane);
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            bfr[p][j] = FragLoader<OpB::KC, BN>::load(smem + p * IMG_BYTES + A_BYTES,
+                                                      bcol0 + j * 16, ks, lane);
         }
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
           for (int j = 0; j < NT; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], ah[i], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], al[i], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], ah[i], acc[i][j], 0, 0, 0);
+            f32x4 c = acc[i][j];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[2][j], af[0][i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[2][i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[0][i], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[1][i], c, 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[0][i], c, 0, 0, 0);
           }
       }
       if (more) {

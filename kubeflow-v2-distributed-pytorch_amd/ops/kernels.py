@@ -17,7 +17,7 @@ from ._native import native, native_available
 
 __all__ = ["conv_fwd", "conv_dgrad", "conv_wgrad", "bn_finalize", "bn_act_fwd",
            "bn_act_bwd_reduce", "bn_act_bwd_apply", "maxpool_fwd", "maxpool_bwd",
-           "avgpool_fwd", "avgpool_bwd", "gemm", "cross_entropy_fwd_bwd", "sgd_step",
+           "avgpool_fwd", "avgpool_bwd", "gemm", "cross_entropy_fwd_bwd", "top1_correct", "sgd_step",
            "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd", "dropout_fwd", "colsum", "bn_bwd_collect", "stem_pack",
            "embedding_bwd", "gelu_fwd", "gelu_bwd", "nchw_to_nhwc", "use_native",
            "gconv_fwd", "gconv_dgrad", "gconv_wgrad", "chan_stats", "affine_act",
@@ -230,6 +230,18 @@ def cross_entropy_fwd_bwd(logits, labels, label_smoothing=0.0, ignore_index=-100
     return _ref.cross_entropy_fwd_bwd(logits, labels, label_smoothing, ignore_index)
 
 
+def top1_correct(logits, labels, out=None):
+    """``out`` (int32 [1], device) += number of rows whose argmax equals the label — the
+    reference's eval accumulation (task.py:36-44) as one kernel, no host sync."""
+    if use_native(logits):
+        return native().top1_correct(logits.contiguous(), labels.contiguous(), out)
+    n = (logits.argmax(1) == labels).sum().to(torch.int32).reshape(1)
+    if out is None:
+        return n
+    out.add_(n)
+    return out
+
+
 def sgd_step(param, grad, mom, shadow, lr, momentum, dampening, weight_decay, nesterov,
              first_step, grad_scale=1.0):
     if use_native(param):
@@ -320,8 +332,8 @@ def gelu_bwd(dy, x):
 def stem_pack(x, dtype, pad: int, Hp: int, Wsp: int):
     """NCHW image (C <= 4) -> bf16/``dtype`` super-pixels [N, Hp, Wsp, 8]: channel p*4 + c of
     super-pixel (h', j) is x[c, h'-pad, 2j+p-pad] (zero outside the image)."""
-    if use_native(x) and dtype == torch.bfloat16:
-        return native().stem_pack(x.contiguous(), pad, Hp, Wsp)
+    if use_native(x) and dtype in (torch.bfloat16, torch.float32):
+        return native().stem_pack(x.contiguous(), pad, Hp, Wsp, dtype)
     N, C, H, W = x.shape
     P = x.new_zeros(N, 4, Hp, 2 * Wsp, dtype=torch.float64 if x.dtype == torch.float64 else torch.float32)
     hh, ww = min(H, Hp - pad), min(W, 2 * Wsp - pad)

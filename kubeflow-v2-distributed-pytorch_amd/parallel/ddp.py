@@ -107,7 +107,10 @@ class DistributedDataParallel(tnn.Module):
         self._comm = self.world > 1 or self.force_reduce
         params = [p for p in module.parameters() if p.requires_grad]
         dev = params[0].device
-        shadow = torch.bfloat16 if dev.type == "cuda" else None
+        # compute-dtype weight shadow: bf16 on the GPU unless the model computes in fp32 (the
+        # reference's precision), whose kernels read the fp32 master weights directly
+        cdt = getattr(module, "compute_dtype", None)
+        shadow = torch.bfloat16 if dev.type == "cuda" and cdt != torch.float32 else None
         self.space: FlatParamSpace = get_flat_space(params, shadow, module)
         backend = dist.get_backend(process_group) if dist.is_initialized() else "none"
         self._avg_supported = backend == "nccl"

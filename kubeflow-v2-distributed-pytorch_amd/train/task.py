@@ -94,27 +94,27 @@ def _unwrap(model):
 
 @torch.no_grad()
 def evaluate(model, device, test_loader) -> float:
-    """Top-1 accuracy (task.py:30-46) — argmax + correct count stay on the device and the
-    host reads ONE value at the end instead of a ``.item()`` per batch.  Sharded over ranks
-    (each rank's loader holds its shard) and summed with one all-reduce."""
+    """Top-1 accuracy (task.py:30-46) — argmax + correct count run in ONE fused kernel per
+    batch (``top1_correct``, accumulating into a device counter) and the host reads one value
+    at the end instead of a ``.item()`` per batch.  Sharded over ranks (each rank's loader
+    holds its shard) and summed with one all-reduce."""
+    from mipipe.ops import kernels as K
     m = _unwrap(model)
     was_training = m.training
     m.eval()
-    correct = torch.zeros((), dtype=torch.int64, device=device)
-    total = torch.zeros((), dtype=torch.int64, device=device)
+    correct = torch.zeros(1, dtype=torch.int32, device=device)
+    total = 0
     for images, labels in test_loader:
         images, labels = images.to(device), labels.to(device)
         outputs = m(images)
-        predicted = outputs.float().argmax(1)
+        K.top1_correct(outputs, labels, correct)
         total += labels.numel()
-        correct += (predicted == labels).sum()
+    t = torch.stack([correct[0].to(torch.int64), torch.tensor(total, device=device)])
     if dist_utils.get_world_size() > 1:
-        t = torch.stack([correct, total])
         torch.distributed.all_reduce(t)
-        correct, total = t[0], t[1]
     if was_training:
         m.train()
-    return float(correct.item()) / max(1, int(total.item()))
+    return float(t[0].item()) / max(1, int(t[1].item()))
 
 
 def build_parser() -> argparse.ArgumentParser:

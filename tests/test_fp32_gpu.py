@@ -1,0 +1,246 @@
+"""fp32 (the reference's precision, task.py:303-312 has no autocast) on the gfx950 kernels.
+
+GEMM-shaped kernels run the split-bf16x3 main loop (fp32 operands split exactly into three bf16
+parts in LDS, 6 MFMAs per tile, fp32 accumulation); elementwise / reduction kernels read and
+write fp32.  Every kernel is compared against a float64 evaluation of the same op on the same
+fp32 inputs; the bound is 1e-4 relative to the output magnitude (measured ~1e-6, like stock
+fp32 torch; bf16 would be ~1e-2).
+"""
+import math
+
+import pytest
+import torch
+
+from mipipe.ops import _ref
+from mipipe.ops._native import native, native_available
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+TOL = 1e-4
+
+
+@pytest.fixture(autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert native_available(), "mipipe._C must be built for GPU tests (no silent fallback)"
+    torch.manual_seed(4321)
+    yield
+
+
+def rel_err(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+def f32(*shape, scale=1.0):
+    return torch.randn(*shape, device=dev) * scale
+
+
+def d(t):
+    return t.detach().double().cpu()
+
+
+# ResNet-18 on 32x32 inputs (the reference's CIFAR config of record) layer shapes, batch 32,
+# plus odd / strided / 7x7 cases.  N, H, W, Ci, Co, k, s, p
+CONV_CASES = [
+    (32, 16, 16, 8, 64, 3, 1, 1),
+    (32, 8, 8, 64, 64, 3, 1, 1),
+    (32, 8, 8, 64, 128, 3, 2, 1),
+    (32, 8, 8, 64, 128, 1, 2, 0),
+    (32, 4, 4, 128, 128, 3, 1, 1),
+    (32, 4, 4, 128, 256, 3, 2, 1),
+    (32, 2, 2, 256, 512, 3, 2, 1),
+    (32, 1, 1, 512, 512, 3, 1, 1),
+    (4, 14, 14, 256, 1024, 1, 1, 0),
+    (2, 9, 7, 32, 72, 3, 1, 1),
+    (2, 32, 32, 8, 64, 7, 2, 3),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_fp32(case):
+    N, H, W, Ci, Co, k, s, p = case
+    x = f32(N, H, W, Ci)
+    w = f32(Co, k, k, Ci, scale=1.0 / math.sqrt(Ci * k * k))
+    shift = torch.randn(Co, device=dev) * 0.1
+    y, ps, pss = native().conv_fwd(x, w, s, p, shift)
+    assert y.dtype == torch.float32
+    yr, psr, pssr = _ref.conv_fwd(d(x), d(w), s, p, d(shift))
+    assert rel_err(y, yr) < TOL
+    assert rel_err(ps.sum(0), psr[0]) < TOL
+    assert rel_err(pss.sum(0), pssr[0]) < TOL
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_dgrad_fp32(case):
+    N, H, W, Ci, Co, k, s, p = case
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = f32(N, Ho, Wo, Co)
+    w = f32(Co, k, k, Ci, scale=1.0 / math.sqrt(Co * k * k))
+    dx = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p)
+    assert dx.dtype == torch.float32
+    assert rel_err(dx, _ref.conv_dgrad(d(dy), d(w), (N, H, W, Ci), s, p)) < TOL
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_wgrad_fp32(case):
+    N, H, W, Ci, Co, k, s, p = case
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = f32(N, Ho, Wo, Co)
+    x = f32(N, H, W, Ci)
+    dw = native().conv_wgrad(dy, x, k, k, s, p)
+    assert rel_err(dw, _ref.conv_wgrad(d(dy), d(x), k, k, s, p)) < TOL
+
+
+def test_conv_dgrad_fused_epilogue_fp32():
+    # dgrad of a conv whose input was relu(bn(y)) + a residual addend: fp32 epilogue fusions
+    N, H, W, Ci, Co = 8, 8, 8, 64, 64
+    dy = f32(N, H, W, Co)
+    w = f32(Co, 3, 3, Ci, scale=1.0 / math.sqrt(Co * 9))
+    y = f32(N, H, W, Ci)
+    add = f32(N, H, W, Ci)
+    mean = torch.randn(Ci, device=dev) * 0.1
+    invstd = torch.rand(Ci, device=dev) + 0.5
+    gamma = torch.rand(Ci, device=dev) + 0.5
+    beta = torch.randn(Ci, device=dev) * 0.1
+    scale, bias = gamma * invstd, beta - mean * gamma * invstd
+    rep = torch.zeros(3, native().STAT_REPLICAS, Ci, device=dev)
+    g = native().conv_dgrad(dy, w, [N, H, W, Ci], 1, 1, add, y, mean, invstd, scale, bias, rep)
+    sg, sgx = native().bn_bwd_collect(rep, Ci)
+    dx = _ref.conv_dgrad(d(dy), d(w), (N, H, W, Ci), 1, 1) + d(add)
+    z = d(y) * d(scale) + d(bias)
+    gr = dx * (z > 0)
+    assert rel_err(g, gr) < TOL
+    xhat = (d(y) - d(mean)) * d(invstd)
+    assert rel_err(sg, gr.reshape(-1, Ci).sum(0)) < TOL
+    assert rel_err(sgx, (gr * xhat).reshape(-1, Ci).sum(0)) < TOL
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 512, 512), (300, 72, 200), (32, 1000, 512),
+                                   (1024, 10, 512)])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+def test_gemm_fp32(M, N, K, ta, tb):
+    if (ta and M % 8) or (not ta and K % 8) or N % 8 or (tb and K % 8):
+        pytest.skip("layout constraint")
+    a = f32(K, M) if ta else f32(M, K)
+    b = f32(N, K) if tb else f32(K, N)
+    bias = torch.randn(N, device=dev)
+    out = native().gemm(a, b, ta, tb, bias, "relu", torch.float32, None, 0.0)
+    ref = _ref.gemm(d(a), d(b), ta, tb, d(bias), "relu", torch.float64)
+    assert out.dtype == torch.float32 and rel_err(out, ref) < TOL
+    acc = torch.randn(M, N, device=dev)
+    acc0 = d(acc)
+    native().gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0)
+    assert rel_err(acc, acc0 + _ref.gemm(d(a), d(b), ta, tb, None, "none", torch.float64)) < TOL
+
+
+@pytest.mark.parametrize("C", [64, 512])
+def test_bn_kernels_fp32(C):
+    M = 32 * 8 * 8
+    y = f32(M, C) * 2 + 0.5
+    dz = f32(M, C)
+    res = f32(M, C)
+    mean = d(y).mean(0)
+    var = d(y).var(0, unbiased=False)
+    invstd = torch.rsqrt(var + 1e-5)
+    gamma = torch.rand(C, dtype=torch.float64) + 0.5
+    beta = torch.randn(C, dtype=torch.float64) * 0.1
+    scale, bias = gamma * invstd, beta - mean * gamma * invstd
+    g32 = lambda t: t.float().to(dev)  # noqa: E731
+    z = native().bn_act_fwd(y, g32(scale), g32(bias), True, res, None, None)
+    zr = _ref.bn_act_fwd(d(y), scale, bias, True, d(res))
+    assert z.dtype == torch.float32 and rel_err(z, zr) < TOL
+    sg, sgx, _ = native().bn_act_bwd_reduce(dz, z, y, g32(mean), g32(invstd), True)
+    sgr, sgxr = _ref.bn_act_bwd_reduce(d(dz), zr, d(y), mean, invstd, True)
+    assert rel_err(sg, sgr) < TOL and rel_err(sgx, sgxr) < TOL
+    dy, dres = native().bn_act_bwd_apply(dz, z, y, g32(mean), g32(invstd), g32(gamma), sg, sgx,
+                                         M, True, True, None, None, None, None, None)
+    dyr, dresr = _ref.bn_act_bwd_apply(d(dz), zr, d(y), mean, invstd, gamma, sgr, sgxr, M, True,
+                                       True)
+    assert rel_err(dy, dyr) < TOL and rel_err(dres, dresr) < TOL
+
+
+def test_pools_fp32():
+    x = f32(32, 16, 16, 64)
+    y, idx = native().maxpool_fwd(x, 3, 2, 1)
+    yr, _ = _ref.maxpool_fwd(d(x), 3, 2, 1)
+    assert y.dtype == torch.float32 and torch.equal(y.cpu().double(), yr)
+    dy = f32(*y.shape)
+    dx = native().maxpool_bwd_impl(dy, idx, list(x.shape), 3, 2, 1)
+    xr = d(x).permute(0, 3, 1, 2).requires_grad_(True)
+    torch.nn.functional.max_pool2d(xr, 3, 2, 1).backward(d(dy).permute(0, 3, 1, 2))
+    assert rel_err(dx, xr.grad.permute(0, 2, 3, 1)) < TOL
+    a = native().avgpool_fwd(x)
+    assert rel_err(a, _ref.avgpool_fwd(d(x))) < TOL
+    da = f32(32, 64)
+    assert rel_err(native().avgpool_bwd(da, list(x.shape)), _ref.avgpool_bwd(d(da), x.shape)) < TOL
+
+
+@pytest.mark.parametrize("V", [10, 1000])
+def test_cross_entropy_fp32(V):
+    logits = f32(256, V) * 3
+    labels = torch.randint(0, V, (256,), device=dev)
+    loss, grad = native().cross_entropy_fwd_bwd(logits, labels, 0.0, -100)
+    lr, gr = _ref.cross_entropy_fwd_bwd(d(logits), labels.cpu())
+    assert grad.dtype == torch.float32
+    assert abs(loss.item() - lr.item()) / abs(lr.item()) < TOL
+    assert rel_err(grad, gr) < TOL
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("V", [10, 1000])
+def test_top1_correct(dtype, V):
+    R = 777
+    logits = f32(R, V).to(dtype)
+    logits[::7, 3] = logits[::7].float().max(1).values.to(dtype)  # ties: first index wins
+    labels = torch.randint(0, V, (R,), device=dev)
+    labels[::5] = logits[::5].float().argmax(1)
+    out = torch.zeros(1, dtype=torch.int32, device=dev)
+    native().top1_correct(logits, labels, out)
+    native().top1_correct(logits, labels, out)
+    ref = (logits.float().argmax(1) == labels).sum().item()
+    assert out.item() == 2 * ref
+
+
+def test_layout_kernels_fp32():
+    x = torch.rand(8, 3, 32, 32, device=dev)
+    y = native().nchw_to_nhwc(x, torch.float32, 8)
+    assert y.dtype == torch.float32 and torch.equal(y[..., :3], x.permute(0, 2, 3, 1))
+    assert torch.count_nonzero(y[..., 3:]) == 0
+    p = native().stem_pack(x, 3, 37, 19, torch.float32)
+    pb = native().stem_pack(x, 3, 37, 19, torch.bfloat16)
+    assert p.dtype == torch.float32 and rel_err(p, pb.float()) < 1e-2
+
+
+def test_resnet18_cifar_fp32_step_matches_float64():
+    """One ResNet-18 (32x32, 10 classes, batch 64) fwd + bwd in fp32 on the HIP kernels vs the
+    same module tree evaluated in float64 by plain torch ops on the CPU.  Gradients are compared
+    by relative L2 error per tensor: a ReLU whose pre-activation lies within fp32 rounding of 0
+    may legitimately decide differently from float64 and move one tensor's max-abs error."""
+    from mipipe.models import create_model
+    from mipipe.train.task import CrossEntropyLoss
+    torch.manual_seed(0)
+    m = create_model("resnet18", num_classes=10)
+    ref = create_model("resnet18", num_classes=10, compute_dtype=torch.float64).double()
+    ref.load_state_dict(m.state_dict())
+    m = m.to(dev)
+    m.compute_dtype = torch.float32
+    x = torch.randn(64, 3, 32, 32)
+    yl = torch.randint(0, 10, (64,))
+    out = m(x.to(dev))
+    loss = CrossEntropyLoss()(out, yl.to(dev))
+    loss.backward()
+    out_r = ref(x.double())
+    loss_r = torch.nn.functional.cross_entropy(out_r, yl)
+    loss_r.backward()
+    assert out.dtype == torch.float32
+    assert rel_err(out, out_r) < 1e-4
+    assert abs(loss.item() - loss_r.item()) < 1e-5 * max(1.0, abs(loss_r.item()))
+    pr = dict(ref.named_parameters())
+    e2 = sorted(((p.grad.double().cpu() - pr[n].grad).norm() / pr[n].grad.norm()).item()
+                for n, p in m.named_parameters())
+    assert e2[len(e2) // 2] < 1e-4, e2
+    assert e2[-1] < 5e-3, e2
