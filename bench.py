@@ -70,6 +70,9 @@ def parse():
                     help="cpu = gloo backend, fp32 (harness tests without a GPU)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="compute dtype of the mipipe kernels (fp32 = the reference's precision)")
+    ap.add_argument("--tune", type=int, default=1,
+                    help="1: autotune conv tile configs per shape in the warm-up (cudnn.benchmark "
+                         "analogue); 0: heuristic tile choice")
     return ap.parse_args()
 
 
@@ -125,6 +128,12 @@ def main() -> int:
             return 3
     a.distributed = distributed
     torch.manual_seed(0)
+    if not cpu and a.impl == "mipipe":
+        # per-shape conv tile autotuning during the (untimed, eager) warm-up steps — the
+        # analogue of the reference's cudnn.benchmark = True (task.py:244)
+        from mipipe.ops import tuning
+        tuning.from_env()
+        tuning.set_benchmark(a.tune, verbose=False)
     if rank == 0:
         _heartbeat()
 

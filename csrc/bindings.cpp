@@ -7,6 +7,11 @@
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
+#include <pybind11/stl.h>
+
+#include <string>
+#include <unordered_map>
+#include <vector>
 
 #include "kernels/launchers.hpp"
 
@@ -77,13 +82,84 @@ mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int p
   return s;
 }
 
+// ------------------------------------------------------------------------------- tile tuning
+// The cudnn.benchmark analogue (reference task.py:244 sets torch.backends.cudnn.benchmark):
+// with benchmark mode on, the first call of a conv op on a new (op, shape, dtype) times every
+// valid tile config on scratch outputs (hipEvents, eager stream only — never while a stream is
+// being captured into a graph) and remembers the fastest; later calls reuse it.  The table can
+// be exported / imported (mipipe.ops.tuning) so a job can ship a measured table.
+namespace tune {
+bool g_benchmark = false;
+bool g_verbose = false;
+int g_reps = 3;
+std::unordered_map<std::string, int> g_table;
+
+std::string key(const char* op, const mipipe::ConvShape& s) {
+  char buf[200];
+  snprintf(buf, sizeof(buf), "%s|%d,%d,%d,%d,%d,%d,%d,%d,%d,%d,%d|%s", op, s.N, s.H, s.W, s.Ci,
+           s.Co, s.KH, s.KW, s.stride, s.pad, s.stride_w, s.pad_w, s.f32 ? "f32" : "bf16");
+  return buf;
+}
+
+bool capturing() {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream(), &st) != hipSuccess) return true;
+  return st != hipStreamCaptureStatusNone;
+}
+
+std::vector<int> candidates(bool f32, bool wgrad) {
+  if (f32) return {0, 2, 8};
+  std::vector<int> c;
+  for (int i = 0; i < mipipe::kConvTileConfigs; ++i)
+    if (!(wgrad && i == 6)) c.push_back(i);
+  return c;
+}
+
+// cfg for this call: table hit, or (benchmark mode, not capturing) measure all candidates with
+// `run(cfg)` (which must write only scratch outputs) and record the fastest; else -1 (heuristic).
+template <class F>
+int select(const std::string& k, bool f32, bool wgrad, F&& run) {
+  auto it = g_table.find(k);
+  if (it != g_table.end()) return it->second;
+  if (!g_benchmark || capturing()) return -1;
+  hipStream_t st = stream();
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  int best = -1;
+  float best_ms = 1e30f;
+  std::string log;
+  for (int cfg : candidates(f32, wgrad)) {
+    run(cfg);  // warm (first launch of a kernel object loads its code)
+    hipEventRecord(e0, st);
+    for (int r = 0; r < g_reps; ++r) run(cfg);
+    hipEventRecord(e1, st);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    ms /= (float)g_reps;
+    if (g_verbose) log += " " + std::to_string(cfg) + ":" + std::to_string(ms * 1e3f).substr(0, 7);
+    if (ms < best_ms) {
+      best_ms = ms;
+      best = cfg;
+    }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  TORCH_CHECK(hipGetLastError() == hipSuccess, "conv tile tuning: a candidate failed to launch");
+  if (g_verbose) fprintf(stderr, "[mipipe tune] %s -> %d  (us:%s)\n", k.c_str(), best, log.c_str());
+  g_table[k] = best;
+  return best;
+}
+}  // namespace tune
+
 // ------------------------------------------------------------------------------- conv
 std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor w, int stride,
                                                                 int pad, optional<Tensor> shift,
                                                                 optional<Tensor> slab_sum,
                                                                 optional<Tensor> slab_sq,
                                                                 optional<Tensor> bias, bool relu,
-                                                                int stride_w, int pad_w) {
+                                                                int stride_w, int pad_w, int cfg) {
   check_act(x, "x");
   check_same(w, x, "w");
   c10::DeviceGuard g(x.device());
@@ -114,15 +190,29 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
     pssp = pss->data_ptr<float>();
     sh = shift->data_ptr<float>();
   }
-  mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), psp, pssp, sh, s, stream(),
-                   bias.has_value() ? bias->data_ptr<float>() : nullptr, relu);
+  const float* bp = bias.has_value() ? bias->data_ptr<float>() : nullptr;
+  if (cfg < 0) {
+    cfg = tune::select(tune::key("fwd", s), s.f32, false, [&](int c) {
+      auto ys = torch::empty_like(y);
+      optional<Tensor> a, b;
+      if (psp != nullptr) {
+        a = torch::zeros_like(*ps);
+        b = torch::zeros_like(*pss);
+      }
+      mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), ys.data_ptr(),
+                       a.has_value() ? a->data_ptr<float>() : nullptr,
+                       b.has_value() ? b->data_ptr<float>() : nullptr, sh, s, stream(), bp, relu, c);
+    });
+  }
+  mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), psp, pssp, sh, s, stream(), bp, relu,
+                   cfg);
   return {y, ps, pss};
 }
 
 Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride, int pad,
                   optional<Tensor> addend, optional<Tensor> bn_y, optional<Tensor> bn_mean,
                   optional<Tensor> bn_invstd, optional<Tensor> bn_scale, optional<Tensor> bn_bias,
-                  optional<Tensor> bn_rep, optional<Tensor> bn_z, int pad_w) {
+                  optional<Tensor> bn_rep, optional<Tensor> bn_z, int pad_w, int cfg) {
   check_act(dy, "dy");
   check_same(w, dy, "w");
   c10::DeviceGuard g(dy.device());
@@ -172,7 +262,21 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     }
     any = true;
   }
-  mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), any ? &fz : nullptr);
+  if (cfg < 0) {
+    cfg = tune::select(tune::key("dgrad", s), s.f32, false, [&](int c) {
+      auto dxs = torch::empty_like(dx);
+      mipipe::DgradFusion f2 = fz;
+      Tensor reps;
+      if (fz.bn_rep != nullptr) {
+        reps = torch::zeros_like(*bn_rep);
+        f2.bn_rep = reps.data_ptr<float>();
+      }
+      mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dxs.data_ptr(), s, stream(),
+                         any ? &f2 : nullptr, c);
+    });
+  }
+  mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), any ? &fz : nullptr,
+                     cfg);
   return dx;
 }
 
@@ -190,7 +294,7 @@ std::tuple<Tensor, Tensor> bn_bwd_collect(Tensor rep, int64_t C, optional<Tensor
 }
 
 Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, optional<Tensor> out,
-                  int stride_w, int pad_w) {
+                  int stride_w, int pad_w, int cfg) {
   check_act(dy, "dy");
   check_same(x, dy, "x");
   c10::DeviceGuard g(dy.device());
@@ -214,7 +318,13 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
   } else {
     dw = torch::zeros({s.Co, kh, kw, s.Ci}, x.options().dtype(at::kFloat));
   }
-  mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream());
+  if (cfg < 0) {
+    cfg = tune::select(tune::key("wgrad", s), s.f32, true, [&](int c) {
+      auto dws = torch::zeros_like(dw);
+      mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dws.data_ptr<float>(), s, stream(), c);
+    });
+  }
+  mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), cfg);
   return dw;
 }
 
@@ -986,19 +1096,33 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("shift") = py::none(), py::arg("slab_sum") = py::none(),
         py::arg("slab_sq") = py::none(), py::arg("bias") = py::none(), py::arg("relu") = false,
-        py::arg("stride_w") = 0, py::arg("pad_w") = -1);
+        py::arg("stride_w") = 0, py::arg("pad_w") = -1, py::arg("cfg") = -1);
   m.attr("STAT_REPLICAS") = mipipe::kStatReplicas;
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("x_shape"),
         py::arg("stride"), py::arg("pad"), py::arg("addend") = py::none(),
         py::arg("bn_y") = py::none(), py::arg("bn_mean") = py::none(),
         py::arg("bn_invstd") = py::none(), py::arg("bn_scale") = py::none(),
         py::arg("bn_bias") = py::none(), py::arg("bn_rep") = py::none(),
-        py::arg("bn_z") = py::none(), py::arg("pad_w") = -1);
+        py::arg("bn_z") = py::none(), py::arg("pad_w") = -1, py::arg("cfg") = -1);
   m.def("bn_bwd_collect", &bn_bwd_collect, py::arg("rep"), py::arg("C"),
         py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("out") = py::none(), py::arg("stride_w") = 0,
-        py::arg("pad_w") = -1);
+        py::arg("pad_w") = -1, py::arg("cfg") = -1);
+  m.attr("CONV_TILE_CONFIGS") = mipipe::kConvTileConfigs;
+  m.def("set_benchmark", [](bool on, bool verbose, int reps) {
+    tune::g_benchmark = on;
+    tune::g_verbose = verbose;
+    tune::g_reps = std::max(1, reps);
+  }, py::arg("on"), py::arg("verbose") = false, py::arg("reps") = 3);
+  m.def("get_benchmark", []() { return tune::g_benchmark; });
+  m.def("tune_table", []() { return tune::g_table; });
+  m.def("set_tune_entry", [](const std::string& k, int cfg) {
+    TORCH_CHECK(cfg >= -1 && cfg < mipipe::kConvTileConfigs, "bad tile config id");
+    if (cfg < 0) tune::g_table.erase(k);
+    else tune::g_table[k] = cfg;
+  });
+  m.def("clear_tune_table", []() { tune::g_table.clear(); });
   m.def("bn_finalize", &bn_finalize, py::arg("psum"), py::arg("psq"), py::arg("count"),
         py::arg("shift"), py::arg("gamma"), py::arg("beta"), py::arg("rm"), py::arg("rv"),
         py::arg("momentum"), py::arg("eps"), py::arg("zero_after") = true,

@@ -1,0 +1,222 @@
+// Implicit-GEMM convolution (forward, data-grad, weight-grad) for NHWC bf16 / fp32 on gfx950.
+//
+//   forward : M = N*Ho*Wo, N = Co, K = KH*KW*Ci   A = im2col(x) (gathered rows), B = W[Co][K]
+//   dgrad   : M = N*H*W,   N = Ci, K = KH*KW*Co   A = gather(dy), B = W viewed [K=(tap,co)][Ci]
+//   wgrad   : M = Co, N = KH*KW*Ci, K = N*Ho*Wo  A = dy^T (k-major), B = im2col(x)^T, split-K
+//
+// Forward fuses the BatchNorm batch-statistics reduction into its epilogue (shifted per-channel
+// sum / sum-of-squares of the fp32 accumulators), so BN never re-reads y for statistics.
+// 1x1 / stride-1 / pad-0 convolutions take the dense-operand fast path (no gather math).
+//
+// Every kernel is a template over a TILE CONFIG (block tile, LDS stages, wave grid).  The host
+// picks the config per problem: the measured table (conv_tune.cpp: per-shape autotuning, the
+// cudnn.benchmark analogue) when one exists, else the heuristic in default_*_cfg().  The three
+// ops live in separate translation units (conv_fwd.hip / conv_dgrad.hip / conv_wgrad.hip).
+#pragma once
+#include "epilogue.hpp"
+#include "launchers.hpp"
+
+namespace mipipe {
+namespace gk {
+
+// zero page for padding taps / out-of-range rows (one per translation unit: no -fgpu-rdc)
+static __device__ __attribute__((aligned(64))) uint4 g_conv_zero[8];
+
+// Block tile BM x BN, NS LDS stages, WM x WN waves (wave tile (BM/WM) x (BN/WN)).
+template <int BM_, int BN_, int NS_, int WM_, int WN_>
+struct Tile {
+  static constexpr int BM = BM_, BN = BN_, NS = NS_, WM = WM_, WN = WN_;
+  static constexpr int NW = WM * WN;
+  static constexpr int THREADS = 64 * NW;
+};
+
+// The config table.  Ids are stable (they key the tuning table).
+//  0: 128x128, 2 stages, 2x2 waves   — general default
+//  1: 128x128, 1 stage               — short-K / memory-bound (3 blocks per CU)
+//  2: 128x64,  2 stages              — narrow N (<= 64 channels)
+//  3: 256x128, 2 stages, 4x2 waves   — large M: 85 FLOP per L2 byte (128x128: 64)
+//  4: 256x128, 3 stages, 4x2 waves   — same, two k-steps of loads in flight (counted vmcnt)
+//  5: 128x256, 2 stages, 2x4 waves   — large N
+//  6: 256x256, 2 stages, 4x2 waves   — 64x128 wave tiles, 128 FLOP per L2 byte
+//  7: 256x64,  2 stages, 4x1 waves   — large M, narrow N
+//  8: 64x128,  2 stages, 2x2 waves   — narrow M (weight-grad of <= 64 output channels)
+typedef Tile<128, 128, 2, 2, 2> T0;
+typedef Tile<128, 128, 1, 2, 2> T1;
+typedef Tile<128, 64, 2, 2, 2> T2;
+typedef Tile<256, 128, 2, 4, 2> T3;
+typedef Tile<256, 128, 3, 4, 2> T4;
+typedef Tile<128, 256, 2, 2, 4> T5;
+typedef Tile<256, 256, 2, 4, 2> T6;
+typedef Tile<256, 64, 2, 4, 1> T7;
+typedef Tile<64, 128, 2, 2, 2> T8;
+constexpr int kNumTiles = 9;
+
+// fp32 operands run the split-bf16x3 loop (3 LDS images): 4-wave tiles only.
+template <class T>
+constexpr bool tile_ok_for(int cfg) {
+  return std::is_same<T, float>::value ? (cfg == 0 || cfg == 2 || cfg == 8)
+                                       : (cfg >= 0 && cfg < kNumTiles);
+}
+
+template <class T, class C, class OpA, class OpB>
+constexpr int lds_bytes_out() {
+  constexpr int a = MainLoopFor<T, C::BM, C::BN, OpA, OpB, C::NS, C::WM, C::WN>::LDS_BYTES;
+  constexpr int b = kEpiLdsBytes<C::BM, C::BN, T, C::WM>();
+  return a > b ? a : b;
+}
+template <class T, class C, class OpA, class OpB>
+constexpr int lds_bytes_f32out() {
+  constexpr int a = MainLoopFor<T, C::BM, C::BN, OpA, OpB, C::NS, C::WM, C::WN>::LDS_BYTES;
+  constexpr int b = C::BM * (C::BN * 4 + 16);
+  return a > b ? a : b;
+}
+// Minimum resident blocks per CU promised to the register allocator.
+template <class T, class C>
+constexpr int conv_occ() {
+  return C::NW == 8 ? 1 : ((C::NS == 1 && !std::is_same<T, float>::value) ? 3 : 2);
+}
+
+template <class C, bool DENSE, bool ALIGNED, class T>
+__global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_fwd_kernel(
+    const T* __restrict__ x, const T* __restrict__ w, ConvGeom g, uint32_t M,
+    uint32_t tilesN, EpiParams e) {
+  constexpr int BM = C::BM, BN = C::BN, NW = C::NW;
+  typedef typename std::conditional<DENSE, KCDense<BM, T, NW>,
+                                    KCIm2col<BM, ALIGNED, T, NW>>::type OpA;
+  typedef KCDense<BN, T, NW> OpB;
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_out<T, C, OpA, OpB>()];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t tm = id / tilesN, tn = id % tilesN;
+  const uint32_t m0 = tm * BM, n0 = tn * BN;
+  const uint32_t K = (uint32_t)(g.KH * g.KW * g.C);
+  const int nk = (int)((K + BK - 1) / BK);
+  OpA a;
+  if constexpr (DENSE) a.init(x, g.C, M, K, m0, wave, lane, g_conv_zero);
+  else a.init(x, g, M, m0, wave, lane, g_conv_zero);
+  OpB b;
+  b.init(w, K, e.N, K, n0, wave, lane, g_conv_zero);
+  f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
+  MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN>::type::run(smem, a, b, 0, nk, acc, wave,
+                                                                    lane);
+  epilogue_out<BM, BN, false, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
+}
+
+template <class C, bool DENSE, bool ALIGNED, class T>
+__global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_dgrad_kernel(
+    const T* __restrict__ dy, const T* __restrict__ w, int Ho, int Wo, int Co, int taps,
+    FastDiv fCo, DgradClass cls, uint32_t M, uint32_t tilesN, EpiParams e) {
+  constexpr int BM = C::BM, BN = C::BN, NW = C::NW;
+  typedef typename std::conditional<DENSE, KCDense<BM, T, NW>,
+                                    KCDgrad<BM, ALIGNED, T, NW>>::type OpA;
+  typedef typename std::conditional<DENSE, MCDense<BN, T, NW>, MCDgradW<BN, T, NW>>::type OpB;
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_out<T, C, OpA, OpB>()];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t tm = id / tilesN, tn = id % tilesN;
+  const uint32_t m0 = tm * BM, n0 = tn * BN;
+  const uint32_t Ci = e.N;
+  const uint32_t K = (uint32_t)(cls.ntaps * Co);
+  const int nk = (int)((K + BK - 1) / BK);
+  OpA a;
+  OpB b;
+  if constexpr (DENSE) {
+    a.init(dy, Co, M, K, m0, wave, lane, g_conv_zero);
+    b.init(w, Ci, Ci, K, n0, wave, lane, g_conv_zero);
+  } else {
+    a.init(dy, Ho, Wo, Co, fCo, cls, M, m0, wave, lane, g_conv_zero);
+    b.init(w, (uint32_t)Co, (uint32_t)taps, Ci, fCo, cls, n0, wave, lane, g_conv_zero);
+  }
+  f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
+  MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN>::type::run(smem, a, b, 0, nk, acc, wave,
+                                                                    lane);
+  epilogue_out<BM, BN, true, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
+}
+
+template <class C, bool DENSE, class T>
+__global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_wgrad_kernel(
+    const T* __restrict__ dy, const T* __restrict__ x, ConvGeom g, uint32_t tilesN,
+    int kt_per_split, EpiParams e) {
+  constexpr int BM = C::BM, BN = C::BN, NW = C::NW;
+  typedef MCDense<BM, T, NW> OpA;
+  typedef typename std::conditional<DENSE, MCDense<BN, T, NW>, MCIm2colT<BN, T, NW>>::type OpB;
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_f32out<T, C, OpA, OpB>()];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t tm = id / tilesN, tn = id % tilesN;
+  const uint32_t m0 = tm * BM, n0 = tn * BN;
+  const uint32_t Co = e.M;
+  const uint32_t K = (uint32_t)(g.N * g.Ho * g.Wo);
+  const int nk = (int)((K + BK - 1) / BK);
+  const int kt0 = blockIdx.y * kt_per_split;
+  const int kt1 = min(nk, kt0 + kt_per_split);
+  OpA a;
+  a.init(dy, Co, Co, K, m0, wave, lane, g_conv_zero);
+  OpB b;
+  if constexpr (DENSE) b.init(x, g.C, g.C, K, n0, wave, lane, g_conv_zero);
+  else b.init(x, g, n0, wave, lane, g_conv_zero);
+  f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
+  MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN>::type::run(smem, a, b, kt0, kt1, acc,
+                                                                    wave, lane);
+  epilogue_f32<BM, BN, true, C::WM, C::WN>(smem, acc, e, m0, n0, wave, lane);
+}
+
+}  // namespace gk
+
+// ------------------------------------------------------------------------------------ host
+inline gk::ConvGeom make_geom(const ConvShape& s) {
+  gk::ConvGeom g;
+  g.stride_w = s.stride_w > 0 ? s.stride_w : s.stride;
+  g.pad_w = s.pad_w >= 0 ? s.pad_w : s.pad;
+  g.N = s.N; g.H = s.H; g.W = s.W; g.C = s.Ci; g.Ho = s.Ho; g.Wo = s.Wo;
+  g.KH = s.KH; g.KW = s.KW; g.stride = s.stride; g.pad = s.pad;
+  g.fHoWo = FastDiv((uint32_t)(s.Ho * s.Wo));
+  g.fWo = FastDiv((uint32_t)s.Wo);
+  g.fC = FastDiv((uint32_t)s.Ci);
+  g.fKW = FastDiv((uint32_t)s.KW);
+  return g;
+}
+
+inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+inline bool is_dense(const ConvShape& s) {
+  return s.KH == 1 && s.KW == 1 && s.stride == 1 && s.pad == 0 && s.pad_w <= 0 &&
+         (s.stride_w == 0 || s.stride_w == 1);
+}
+
+// Dispatch a runtime config id to a compile-time tile: f(Tile) for valid ids.
+// NO_WIDE: the op cannot stage a 256x256 fp32 tile in LDS (weight-grad): id 6 runs as 3.
+template <class T, bool NO_WIDE = false, class F>
+inline void with_tile(int cfg, F&& f) {
+  using namespace gk;
+  if constexpr (std::is_same<T, float>::value) {
+    if (cfg == 2) f(T2{});
+    else if (cfg == 8) f(T8{});
+    else f(T0{});
+  } else {
+    switch (cfg) {
+      case 1: f(T1{}); break;
+      case 2: f(T2{}); break;
+      case 3: f(T3{}); break;
+      case 4: f(T4{}); break;
+      case 5: f(T5{}); break;
+      case 6:
+        if constexpr (NO_WIDE) f(T3{});
+        else f(T6{});
+        break;
+      case 7: f(T7{}); break;
+      case 8: f(T8{}); break;
+      default: f(T0{}); break;
+    }
+  }
+}
+
+// Heuristic tile choice when the tuning table has no entry (measured round-1 rules).
+int default_fwd_cfg(const ConvShape& s);
+int default_dgrad_cfg(const ConvShape& s, long K_class);
+int default_wgrad_cfg(const ConvShape& s);
+
+}  // namespace mipipe

@@ -1,0 +1,55 @@
+// Convolution forward: implicit GEMM over a tile config (conv_common.hpp), BN-statistics or
+// bias/ReLU epilogue.
+#include "conv_common.hpp"
+
+namespace mipipe {
+using namespace gk;
+
+int conv_fwd_stat_rows(const ConvShape& s) {
+  (void)s;
+  return kStatReplicas;
+}
+
+int default_fwd_cfg(const ConvShape& s) {
+  const bool dense = is_dense(s);
+  const bool ns1 = !s.f32 && (dense ? s.Ci <= g_ns1_max_k
+                                    : (s.Ci % BK == 0 && (long)s.KH * s.KW * s.Ci <= g_ns1_max_k_gather));
+  if (s.Co <= 64) return 2;
+  return ns1 ? 1 : 0;
+}
+
+template <class T>
+static void conv_fwd_t(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
+                       const float* st_shift, const ConvShape& s, hipStream_t st,
+                       const float* bias, bool relu, int cfg) {
+  ConvGeom g = make_geom(s);
+  const uint32_t M = (uint32_t)s.N * s.Ho * s.Wo;
+  EpiParams e{};
+  e.C = y; e.ldc = s.Co; e.M = M; e.N = s.Co; e.bias = bias; e.act = relu ? 1 : 0;
+  e.st_sum = st_sum; e.st_sq = st_sq; e.st_shift = st_shift; e.st_R = g_stat_rows;
+  const bool dense = is_dense(s);
+  const bool aligned = s.Ci % BK == 0;
+  const T* xp = (const T*)x;
+  const T* wp = (const T*)w;
+  if (!tile_ok_for<T>(cfg)) cfg = default_fwd_cfg(s);
+  with_tile<T>(cfg, [&](auto tile) {
+    typedef decltype(tile) C;
+    const uint32_t tN = cdiv(s.Co, C::BN), tiles = cdiv(M, C::BM) * tN;
+    const dim3 grid(tiles), block(C::THREADS);
+    if (dense)
+      hipLaunchKernelGGL((conv_fwd_kernel<C, true, false, T>), grid, block, 0, st, xp, wp, g, M, tN, e);
+    else if (aligned)
+      hipLaunchKernelGGL((conv_fwd_kernel<C, false, true, T>), grid, block, 0, st, xp, wp, g, M, tN, e);
+    else
+      hipLaunchKernelGGL((conv_fwd_kernel<C, false, false, T>), grid, block, 0, st, xp, wp, g, M, tN, e);
+  });
+}
+
+void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
+              const float* st_shift, const ConvShape& s, hipStream_t st, const float* bias,
+              bool relu, int cfg) {
+  if (s.f32) conv_fwd_t<float>(x, w, y, st_sum, st_sq, st_shift, s, st, bias, relu, cfg);
+  else conv_fwd_t<__bf16>(x, w, y, st_sum, st_sq, st_shift, s, st, bias, relu, cfg);
+}
+
+}  // namespace mipipe

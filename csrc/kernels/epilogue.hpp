@@ -58,20 +58,22 @@ template <int BN, class T = __bf16>
 constexpr int kEpiPitch() { return BN * (int)sizeof(T) + 16; }
 template <int BM, int BN, class T = __bf16>
 constexpr int kStatsLdsOffset() { return ((BM * kEpiPitch<BN, T>()) + 255) / 256 * 256; }
-template <int BM, int BN, class T = __bf16>
-constexpr int kEpiLdsBytes() { return kStatsLdsOffset<BM, BN, T>() + 4 * BN * 4; }
+template <int BM, int BN, class T = __bf16, int WM = 2>
+constexpr int kEpiLdsBytes() { return kStatsLdsOffset<BM, BN, T>() + 2 * WM * BN * 4; }
 
 // Output in the activation dtype T (bf16, or fp32 on the reference-precision path).
 // acc layout: lane holds C[m][n..n+3] for tile (i, j).
 // FUSE: compile the dgrad fusions (addend / BN-backward reduction); kernels that never use
 // them keep their register budget.
-template <int BM, int BN, bool FUSE = false, class T = __bf16>
-__device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const EpiParams& e,
-                             uint32_t m0, uint32_t n0, uint32_t prow_base, int wave, int lane) {
-  constexpr int MT = BM / 32, NT = BN / 32;
-  const int wr = wave >> 1, wc = wave & 1;
-  const uint32_t ml0 = wr * (BM / 2) + (lane & 15);
-  const uint32_t nl0 = wc * (BN / 2) + (lane >> 4) * 4;
+template <int BM, int BN, bool FUSE = false, class T = __bf16, int WM = 2, int WN = 2>
+__device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                             const EpiParams& e, uint32_t m0, uint32_t n0, uint32_t prow_base,
+                             int wave, int lane) {
+  constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
+  constexpr int kThreads = 64 * WM * WN;
+  const int wr = wave / WN, wc = wave % WN;
+  const uint32_t ml0 = wr * (BM / WM) + (lane & 15);
+  const uint32_t nl0 = wc * (BN / WN) + (lane >> 4) * 4;
   // dgrad fusions: issue this thread's addend / y loads now so their latency overlaps the
   // accumulator staging below (a thread always owns the same 8-column chunk)
   constexpr int CPR = BN / 8;  // 8-element chunks per row
@@ -124,7 +126,7 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const E
   // and added with fp32 atomics into replica slab (blockIdx % st_R) — 256-B-contiguous
   // wave-instructions, no per-block partial rows to reduce later.
   if (e.st_sum != nullptr) {
-    float* lst = reinterpret_cast<float*>(smem + kStatsLdsOffset<BM, BN, T>());  // [2][2][BN]
+    float* lst = reinterpret_cast<float*>(smem + kStatsLdsOffset<BM, BN, T>());  // [2][WM][BN]
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       uint32_t n = n0 + nl0 + j * 16;
@@ -156,8 +158,8 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const E
         uint32_t nl = nl0 + j * 16;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          lst[(0 * 2 + wr) * BN + nl + q] = s[q];
-          lst[(1 * 2 + wr) * BN + nl + q] = ss[q];
+          lst[(0 * WM + wr) * BN + nl + q] = s[q];
+          lst[(1 * WM + wr) * BN + nl + q] = ss[q];
         }
       }
     }
@@ -190,7 +192,9 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const E
       int arr = t / BN, c = t % BN;
       uint32_t n = n0 + c;
       if (n < e.N) {
-        float v = lst[(arr * 2 + 0) * BN + c] + lst[(arr * 2 + 1) * BN + c];
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) v += lst[(arr * WM + w) * BN + c];
         float* dst = (arr == 0 ? e.st_sum : e.st_sq) + (long)(blockIdx.x % e.st_R) * e.N + n;
         atomicAdd(dst, v);
       }
@@ -253,18 +257,21 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const E
     // threads t, t+CPR, ... share a column chunk: reduce them through LDS, then one atomic
     // per column per block into replica row blockIdx % R
     lds_barrier();  // all staging-tile reads done (red overlaps it)
-    float* red = reinterpret_cast<float*>(smem);  // [kThreads][16]
+    // [16][RP] floats, value-major: the stores (consecutive threads) and the column sums
+    // (8 columns x 8 chunks per wave: bank 8q + cc) are both bank-conflict-free
+    constexpr int RP = kThreads + 8;
+    float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      red[threadIdx.x * 16 + q] = sg[q];
-      red[threadIdx.x * 16 + 8 + q] = sgx[q];
+      red[q * RP + threadIdx.x] = sg[q];
+      red[(8 + q) * RP + threadIdx.x] = sgx[q];
     }
     lds_barrier();
     const uint32_t R = kStatReplicas, Rw = (uint32_t)e.st_R;  // layout rows / rows written
     for (int j = threadIdx.x; j < 2 * BN; j += kThreads) {
       const int arr = j / BN, col = j % BN, cc = col >> 3, q = col & 7;
       float a = 0.f;
-      for (int t = cc; t < kThreads; t += CPR) a += red[t * 16 + arr * 8 + q];
+      for (int t = cc; t < kThreads; t += CPR) a += red[(arr * 8 + q) * RP + t];
       if (n0 + col < e.N)
         atomicAdd(e.bnr_rep + ((long)arr * R + blockIdx.x % Rw) * e.N + n0 + col, a);
     }
@@ -274,17 +281,18 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const E
 template <int BM, int BN, bool FUSE = false>
 __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const EpiParams& e,
                               uint32_t m0, uint32_t n0, uint32_t prow_base, int wave, int lane) {
-  epilogue_out<BM, BN, FUSE, __bf16>(smem, acc, e, m0, n0, prow_base, wave, lane);
+  epilogue_out<BM, BN, FUSE, __bf16, 2, 2>(smem, acc, e, m0, n0, prow_base, wave, lane);
 }
 
 // fp32 output; ATOMIC accumulates into C (split-K), otherwise plain store (beta = 0).
-template <int BM, int BN, bool ATOMIC>
-__device__ void epilogue_f32(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const EpiParams& e,
-                             uint32_t m0, uint32_t n0, int wave, int lane) {
-  constexpr int MT = BM / 32, NT = BN / 32;
-  const int wr = wave >> 1, wc = wave & 1;
-  const uint32_t ml0 = wr * (BM / 2) + (lane & 15);
-  const uint32_t nl0 = wc * (BN / 2) + (lane >> 4) * 4;
+template <int BM, int BN, bool ATOMIC, int WM = 2, int WN = 2>
+__device__ void epilogue_f32(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
+                             const EpiParams& e, uint32_t m0, uint32_t n0, int wave, int lane) {
+  constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
+  constexpr int kThreads = 64 * WM * WN;
+  const int wr = wave / WN, wc = wave % WN;
+  const uint32_t ml0 = wr * (BM / WM) + (lane & 15);
+  const uint32_t nl0 = wc * (BN / WN) + (lane >> 4) * 4;
   // stage fp32 tile: pitch BN*4 + 16 bytes (BM*(BN*4+16) <= LDS of the main loop)
   constexpr int P = BN * 4 + 16;
 #pragma unroll

@@ -37,7 +37,8 @@ __device__ __forceinline__ uint32_t kc_off(uint32_t row, uint32_t chunk) {
 
 template <int W>
 __device__ __forceinline__ uint32_t mc_swz(uint32_t row) {
-  if constexpr (W == 128) return ((row & 3u) << 2) | ((row >> 2) & 3u);
+  if constexpr (W == 256) return ((row & 3u) << 1) | (((row >> 3) & 1u) << 3);
+  else if constexpr (W == 128) return ((row & 3u) << 2) | ((row >> 2) & 3u);
   else return (((row >> 1) & 1u) << 1) | (((row >> 3) & 1u) << 2);
 }
 
@@ -58,16 +59,16 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
 // KC: NI = R/32 instructions per wave, row = (wave*NI+i)*8 + lane/8, chunk = (lane&7)^(lane>>3)
 // MC: NI = W/32, RPI = 512/W rows per instruction, row = (wave*NI+i)*RPI + lane/(W/8)
 
-template <int R>
+template <int R, int NW = 4>
 struct KCGeom {
-  static constexpr int NI = R / 32;
+  static constexpr int NI = R / (8 * NW);
   __device__ static uint32_t row(int wave, int i, int lane) { return (wave * NI + i) * 8 + (lane >> 3); }
   __device__ static uint32_t chunk(int lane) { return (lane & 7) ^ (lane >> 3); }
 };
 
-template <int W>
+template <int W, int NW = 4>
 struct MCGeom {
-  static constexpr int NI = W / 32;
+  static constexpr int NI = W / (8 * NW);
   static constexpr int RPI = 512 / W;
   static constexpr int LPR = W / 8;
   __device__ static uint32_t row(int wave, int i, int lane) { return (wave * NI + i) * RPI + lane / LPR; }
@@ -77,10 +78,10 @@ struct MCGeom {
 };
 
 // Dense K-contiguous rows: element (r, k) at base[r*ld + k].
-template <int R, class T = __bf16>
+template <int R, class T = __bf16, int NW = 4>
 struct KCDense {
   static constexpr bool KC = true;
-  static constexpr int NI = R / 32;
+  static constexpr int NI = R / (8 * NW);
   const T* ptr[NI];
   uint32_t kcol;
   uint32_t K;
@@ -90,10 +91,10 @@ struct KCDense {
                        uint32_t origin, int wave, int lane, const void* zero_page) {
     K = K_;
     zero = zero_page;
-    kcol = KCGeom<R>::chunk(lane) * 8;
+    kcol = KCGeom<R, NW>::chunk(lane) * 8;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      uint32_t r = origin + KCGeom<R>::row(wave, i, lane);
+      uint32_t r = origin + KCGeom<R, NW>::row(wave, i, lane);
       ptr[i] = r < rows_total ? base + (long)r * ld + kcol : nullptr;
     }
   }
@@ -113,10 +114,10 @@ struct ConvGeom {
   int pad_w;             // horizontal padding (== pad for square padding)
 };
 
-template <int R, bool ALIGNED = false, class T = __bf16>
+template <int R, bool ALIGNED = false, class T = __bf16, int NW = 4>
 struct KCIm2col {
   static constexpr bool KC = true;
-  static constexpr int NI = R / 32;
+  static constexpr int NI = R / (8 * NW);
   const T* x;
   int hi0[NI], wi0[NI];
   int rowoff[NI];   // ((img*H + hi0)*W + wi0)*C  (32-bit: host checks numel < 2^31)
@@ -131,10 +132,10 @@ struct KCIm2col {
     g = g_;
     zero = zero_page;
     K = (uint32_t)(g.KH * g.KW * g.C);
-    kcol = KCGeom<R>::chunk(lane) * 8;
+    kcol = KCGeom<R, NW>::chunk(lane) * 8;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      uint32_t m = origin + KCGeom<R>::row(wave, i, lane);
+      uint32_t m = origin + KCGeom<R, NW>::row(wave, i, lane);
       if (m < M) {
         uint32_t img = fdiv(g.fHoWo, m);
         uint32_t rem = m - img * (uint32_t)(g.Ho * g.Wo);
@@ -203,10 +204,10 @@ struct DgradClass {
   FastDiv fHcWc, fWc, fnkw;
 };
 
-template <int R, bool ALIGNED = false, class T = __bf16>
+template <int R, bool ALIGNED = false, class T = __bf16, int NW = 4>
 struct KCDgrad {
   static constexpr bool KC = true;
-  static constexpr int NI = R / 32;
+  static constexpr int NI = R / (8 * NW);
   const T* dy;
   int ib[NI], jb[NI];   // i + dh0, j + dw0 (dy row/col of the class's first tap)
   int rowoff[NI];       // ((img*Ho + ib)*Wo + jb)*Co  (32-bit: host checks numel < 2^31)
@@ -222,10 +223,10 @@ struct KCDgrad {
     dy = dy_; Ho = Ho_; Wo = Wo_; Co = Co_; fCo = fCo_; fnkw = cls.fnkw;
     zero = zero_page;
     K = (uint32_t)(cls.ntaps * Co);
-    kcol = KCGeom<R>::chunk(lane) * 8;
+    kcol = KCGeom<R, NW>::chunk(lane) * 8;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      uint32_t m = origin + KCGeom<R>::row(wave, i, lane);
+      uint32_t m = origin + KCGeom<R, NW>::row(wave, i, lane);
       if (m < M) {
         uint32_t img = fdiv(cls.fHcWc, m);
         uint32_t rem = m - img * (uint32_t)(cls.Hc * cls.Wc);
@@ -273,10 +274,10 @@ struct KCDgrad {
 };
 
 // Dense MN-contiguous operand: element (k, col) at base[k*ld + col]; W columns per tile.
-template <int W, class T = __bf16>
+template <int W, class T = __bf16, int NW = 4>
 struct MCDense {
   static constexpr bool KC = false;
-  static constexpr int NI = W / 32;
+  static constexpr int NI = W / (8 * NW);
   const T* colptr[NI];
   uint32_t krow[NI];
   long ld;
@@ -290,8 +291,8 @@ struct MCDense {
     zero = zero_page;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      krow[i] = MCGeom<W>::row(wave, i, lane);
-      uint32_t col = origin + MCGeom<W>::chunk(wave, i, lane) * 8;
+      krow[i] = MCGeom<W, NW>::row(wave, i, lane);
+      uint32_t col = origin + MCGeom<W, NW>::chunk(wave, i, lane) * 8;
       colptr[i] = col < cols_total ? base + col : nullptr;
     }
   }
@@ -302,10 +303,10 @@ struct MCDense {
 };
 
 // Conv data-grad B operand: B(k = (t, co), n = ci) = W[co][tap(t)][ci] (weights [Co,KH,KW,Ci]).
-template <int W, class T = __bf16>
+template <int W, class T = __bf16, int NW = 4>
 struct MCDgradW {
   static constexpr bool KC = false;
-  static constexpr int NI = W / 32;
+  static constexpr int NI = W / (8 * NW);
   const T* colptr[NI];
   uint32_t krow[NI];
   uint32_t K, Co, taps, Ci;
@@ -322,8 +323,8 @@ struct MCDgradW {
     zero = zero_page;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      krow[i] = MCGeom<W>::row(wave, i, lane);
-      uint32_t col = origin + MCGeom<W>::chunk(wave, i, lane) * 8;
+      krow[i] = MCGeom<W, NW>::row(wave, i, lane);
+      uint32_t col = origin + MCGeom<W, NW>::chunk(wave, i, lane) * 8;
       colptr[i] = col < Ci ? w + col : nullptr;
     }
   }
@@ -340,10 +341,10 @@ struct MCDgradW {
 };
 
 // Conv weight-grad B operand: B(k = output pixel, n = (kh,kw,ci)) = x[img, ho*s-p+kh, wo*s-p+kw, ci].
-template <int W, class T = __bf16>
+template <int W, class T = __bf16, int NW = 4>
 struct MCIm2colT {
   static constexpr bool KC = false;
-  static constexpr int NI = W / 32;
+  static constexpr int NI = W / (8 * NW);
   const T* x;
   uint32_t krow[NI];
   int kh[NI], kw[NI], ci[NI];
@@ -361,8 +362,8 @@ struct MCIm2colT {
     uint32_t Ntot = (uint32_t)(g.KH * g.KW * g.C);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      krow[i] = MCGeom<W>::row(wave, i, lane);
-      uint32_t n = origin + MCGeom<W>::chunk(wave, i, lane) * 8;
+      krow[i] = MCGeom<W, NW>::row(wave, i, lane);
+      uint32_t n = origin + MCGeom<W, NW>::chunk(wave, i, lane) * 8;
       colok[i] = n < Ntot;
       uint32_t tap = fdiv(g.fC, n);
       ci[i] = (int)(n - tap * (uint32_t)g.C);
@@ -418,18 +419,38 @@ struct FragLoader<false, W> {  // MC image: 2 x ds_read_b64_tr_b16
 };
 
 // ---------------------------------------------------------------------------------------------
+// Wait until at most N of this wave's vector-memory operations (the LDS-DMA loads of younger
+// stages) are outstanding.  s_waitcnt immediate on gfx9: vmcnt [3:0] + [15:14], expcnt [6:4],
+// lgkmcnt [11:8]; the other counters are left at their maxima (no wait).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
 // Main loop.  Returns accumulators acc[MT][NT] (swapped orientation: lane holds C[m][n..n+3]).
-// NS = LDS stages.  2: double-buffered (next k-step's glds in flight under this one's MFMAs).
-// 1: single buffer, k-steps strictly serial inside the block — half the LDS, so more blocks fit
-// per CU and the overlap comes from neighbouring blocks (short-K, memory-bound GEMMs).
-template <int BM, int BN, class OpA, class OpB, int NS = 2>
+// WM x WN waves (4 or 8), wave tile (BM/WM) x (BN/WN) of 16x16 MFMA tiles.
+// NS = LDS stages:
+//  1: single buffer, k-steps strictly serial inside the block — the least LDS, so more blocks
+//     fit per CU and the overlap comes from neighbouring blocks (short-K, memory-bound GEMMs);
+//  2: double buffer, the next k-step's LDS-DMA in flight under this one's MFMAs;
+//  3: triple buffer, two k-steps in flight; the wait before each step is a COUNTED vmcnt (the
+//     youngest stage keeps flying) so HBM-latency misses overlap two steps of MFMAs.
+// Per k-step (NS >= 2): wait own loads of stage k -> barrier (everyone's stage k landed, and
+// everyone finished reading stage k-1's buffer) -> issue stage k+NS-1 into that buffer ->
+// fragments + MFMAs of stage k.  One barrier per k-step.
+template <int BM, int BN, class OpA, class OpB, int NS = 2, int WM = 2, int WN = 2>
 struct MainLoop {
-  static constexpr int MT = BM / 32;  // 16-row tiles per wave (wave tile BM/2)
-  static constexpr int NT = BN / 32;
+  static constexpr int NW = WM * WN;
+  static constexpr int MT = BM / WM / 16;  // 16-row tiles per wave
+  static constexpr int NT = BN / WN / 16;
   static constexpr int A_BYTES = BM * BK * 2;
   static constexpr int B_BYTES = BN * BK * 2;
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
-  static constexpr int LDS_BYTES = 2 * STAGE_BYTES;
+  static constexpr int LDS_BYTES = NS * STAGE_BYTES;
+  static constexpr int LOADS = OpA::NI + OpB::NI;  // LDS-DMA instructions per wave per stage
+  static_assert(OpA::NI * 8 * NW == BM && OpB::NI * 8 * NW == BN, "policy wave count");
+  static_assert(NS >= 1 && NS <= 3, "1..3 LDS stages");
 
   __device__ static void stage(char* buf, OpA& a, OpB& b, int kt, int wave) {
     a.prep(kt);  // per-k-step wave-uniform address state (filter tap ...), computed once
@@ -442,6 +463,32 @@ struct MainLoop {
       glds16(b.src(kt, i), buf + A_BYTES + (wave * OpB::NI + i) * 1024);
   }
 
+  __device__ static void compute(const char* cbuf, f32x4 (&acc)[MT][NT], uint32_t arow0,
+                                 uint32_t bcol0, int lane) {
+    const char* aimg = cbuf;
+    const char* bimg = cbuf + A_BYTES;
+    // both k-substeps' fragments are requested up front, so the second substep's LDS reads
+    // are in flight under the first substep's MFMAs (only a counted lgkmcnt before each)
+    bf16x8 af[2][MT], bfr[2][NT];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        af[ks][i] = FragLoader<OpA::KC, BM>::load(aimg, arow0 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        bfr[ks][j] = FragLoader<OpB::KC, BN>::load(bimg, bcol0 + j * 16, ks, lane);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ks][j], af[ks][i], acc[i][j],
+                                                              0, 0, 0);
+  }
+
   __device__ static void run(char* smem, OpA& a, OpB& b, int kt0, int kt1,
                              f32x4 (&acc)[MT][NT], int wave, int lane) {
 #pragma unroll
@@ -449,50 +496,39 @@ struct MainLoop {
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (kt0 >= kt1) return;
-    const int wr = wave >> 1, wc = wave & 1;
-    const uint32_t arow0 = wr * (BM / 2), bcol0 = wc * (BN / 2);
-    stage(smem, a, b, kt0, wave);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      if (NS == 1 && kt > kt0) {  // serial: refill the single buffer (all waves done with it)
+    const int wr = wave / WN, wc = wave % WN;
+    const uint32_t arow0 = wr * (BM / WM), bcol0 = wc * (BN / WN);
+    if constexpr (NS == 1) {
+      for (int kt = kt0; kt < kt1; ++kt) {
+        if (kt > kt0) __syncthreads();  // every wave is done reading the single buffer
         stage(smem, a, b, kt, wave);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wait_vmcnt<0>();
         __syncthreads();
+        compute(smem, acc, arow0, bcol0, lane);
       }
-      char* cbuf = smem + cur * STAGE_BYTES;
-      if (NS == 2 && kt + 1 < kt1) stage(smem + (cur ^ 1) * STAGE_BYTES, a, b, kt + 1, wave);
-      const char* aimg = cbuf;
-      const char* bimg = cbuf + A_BYTES;
-      // both k-substeps' fragments are requested up front, so the second substep's LDS reads
-      // are in flight under the first substep's MFMAs (only a counted lgkmcnt before each)
-      bf16x8 af[2][MT], bfr[2][NT];
+    } else {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-          af[ks][i] = FragLoader<OpA::KC, BM>::load(aimg, arow0 + i * 16, ks, lane);
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-          bfr[ks][j] = FragLoader<OpB::KC, BN>::load(bimg, bcol0 + j * 16, ks, lane);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-          for (int j = 0; j < NT; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ks][j], af[ks][i], acc[i][j],
-                                                                0, 0, 0);
-      if (NS == 2) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int s = 0; s < NS - 1; ++s)
+        if (kt0 + s < kt1) stage(smem + s * STAGE_BYTES, a, b, kt0 + s, wave);
+      int cur = 0;                // buffer of stage kt
+      int nxt = NS - 1;           // buffer the stage kt + NS - 1 goes to
+      for (int kt = kt0; kt < kt1; ++kt) {
+        if constexpr (NS == 3) {
+          if (kt + 1 < kt1) wait_vmcnt<LOADS>();  // stage kt+1 may stay in flight
+          else wait_vmcnt<0>();
+        } else {
+          wait_vmcnt<0>();
+        }
         __syncthreads();
-        cur ^= 1;
-      } else if (kt + 1 < kt1) {
-        __syncthreads();
+        if (kt + NS - 1 < kt1) stage(smem + nxt * STAGE_BYTES, a, b, kt + NS - 1, wave);
+        compute(smem + cur * STAGE_BYTES, acc, arow0, bcol0, lane);
+        cur = cur + 1 == NS ? 0 : cur + 1;
+        nxt = nxt + 1 == NS ? 0 : nxt + 1;
       }
     }
+    // the epilogue reuses the stage buffers (statistics partials, output staging): every wave
+    // must be done reading them
+    __syncthreads();
   }
 };
 
@@ -510,10 +546,10 @@ struct MainLoop {
 // per operand: ~1e-5 errors, enough to flip near-zero ReLU decisions the float64 model makes.)
 // One LDS stage: the register prefetch of step k+1 is what overlaps global latency with step
 // k's MFMAs.
-template <int BM, int BN, class OpA, class OpB>
+template <int BM, int BN, class OpA, class OpB, int WM = 2, int WN = 2>
 struct MainLoopF32 {
-  static constexpr int MT = BM / 32;
-  static constexpr int NT = BN / 32;
+  static constexpr int MT = BM / WM / 16;
+  static constexpr int NT = BN / WN / 16;
   static constexpr int PARTS = 3;
   static constexpr int A_BYTES = BM * BK * 2;
   static constexpr int B_BYTES = BN * BK * 2;
@@ -575,8 +611,8 @@ struct MainLoopF32 {
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (kt0 >= kt1) return;
-    const int wr = wave >> 1, wc = wave & 1;
-    const uint32_t arow0 = wr * (BM / 2), bcol0 = wc * (BN / 2);
+    const int wr = wave / WN, wc = wave % WN;
+    const uint32_t arow0 = wr * (BM / WM), bcol0 = wc * (BN / WN);
     Regs r;
     load(r, a, b, kt0);
     store(smem, r, wave, lane);
@@ -616,19 +652,20 @@ struct MainLoopF32 {
         __syncthreads();
       }
     }
+    __syncthreads();  // the epilogue reuses the images
   }
 };
 
 // Selects the main loop for the operand element type.
-template <class T, int BM, int BN, class OpA, class OpB, int NS = 2>
+template <class T, int BM, int BN, class OpA, class OpB, int NS = 2, int WM = 2, int WN = 2>
 struct MainLoopFor {
-  typedef MainLoop<BM, BN, OpA, OpB, NS> type;
+  typedef MainLoop<BM, BN, OpA, OpB, NS, WM, WN> type;
   static constexpr int LDS_BYTES = NS * (BM + BN) * BK * 2;
 };
-template <int BM, int BN, class OpA, class OpB, int NS>
-struct MainLoopFor<float, BM, BN, OpA, OpB, NS> {
-  typedef MainLoopF32<BM, BN, OpA, OpB> type;
-  static constexpr int LDS_BYTES = MainLoopF32<BM, BN, OpA, OpB>::LDS_BYTES;
+template <int BM, int BN, class OpA, class OpB, int NS, int WM, int WN>
+struct MainLoopFor<float, BM, BN, OpA, OpB, NS, WM, WN> {
+  typedef MainLoopF32<BM, BN, OpA, OpB, WM, WN> type;
+  static constexpr int LDS_BYTES = MainLoopF32<BM, BN, OpA, OpB, WM, WN>::LDS_BYTES;
 };
 
 // Row/col of acc element: lane holds C[m][n + e], e = 0..3, for tile (i, j):

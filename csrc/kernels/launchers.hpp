@@ -36,9 +36,11 @@ extern int g_ns1_max_k_gather;  // same for the gathered (im2col / strided dgrad
 int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 // bias / relu: optional per-channel bias and ReLU in the epilogue (convs without BN: VGG, AlexNet)
+// cfg: tile config id (conv_common.hpp table; < 0 = heuristic default)
+constexpr int kConvTileConfigs = 9;
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
               const float* st_shift, const ConvShape& s, hipStream_t st,
-              const float* bias = nullptr, bool relu = false);
+              const float* bias = nullptr, bool relu = false, int cfg = -1);
 // Optional dgrad epilogue fusions:
 //  addend: [N*H*W][Ci] (activation dtype) added to dx (the block input's other gradient, e.g. the residual);
 //  bn_*:   the conv input was relu(bn(y)) with a single consumer: dx becomes g = dx*[z > 0] and
@@ -51,10 +53,11 @@ struct DgradFusion {
   const void* bn_z = nullptr;  // optional stored relu output: mask = z > 0 (residual blocks)
 };
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
-                const DgradFusion* fz = nullptr);
+                const DgradFusion* fz = nullptr, int cfg = -1);
 // dw is ACCUMULATED into with fp32 atomics (split-K): pass a zeroed buffer, or the parameter's
 // gradient buffer to fuse autograd's accumulation (gradient lands directly in the DDP bucket)
-void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st);
+void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
+                int cfg = -1);
 
 // ---- direct convolution, BatchNorm for any C, k x k average pool (vision.hip) ----------------
 struct GConvShape {

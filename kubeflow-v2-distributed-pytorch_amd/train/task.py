@@ -54,12 +54,24 @@ best_acc1 = 0.0
 
 
 def set_random_seeds(random_seed: int = 0) -> None:
-    """task.py:22-28.  Deterministic kernel choice is the default here (fixed tile tables,
-    no autotuning), so the reference's later ``cudnn.benchmark = True`` override has no
-    analogue."""
+    """task.py:22-28: seed torch / numpy / random.  The reference's
+    ``cudnn.deterministic = True`` maps to mipipe's deterministic mode (``--deterministic``,
+    see :func:`configure_kernels`)."""
     torch.manual_seed(random_seed)
     np.random.seed(random_seed)
     random.seed(random_seed)
+
+
+def configure_kernels(use_gpu: bool) -> None:
+    """task.py:244 ``cudnn.benchmark = True`` -> per-shape tile autotuning of the conv kernels
+    (:mod:`mipipe.ops.tuning`; ``MIPIPE_BENCHMARK=0`` disables it, ``MIPIPE_TUNE_TABLE=path``
+    starts from a saved table)."""
+    if not use_gpu:
+        return
+    from mipipe.ops import tuning
+    tuning.from_env()
+    tuning.set_benchmark(os.environ.get("MIPIPE_BENCHMARK", "1") != "0",
+                         verbose=os.environ.get("MIPIPE_TUNE_VERBOSE", "0") == "1")
 
 
 class CrossEntropyLoss(torch.nn.Module):
@@ -264,6 +276,7 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
         print("Process group initialized", flush=True)
     world = dist_utils.get_world_size()
     set_random_seeds(args.random_seed)  # same seed on every rank -> identical init (task.py:161)
+    configure_kernels(use_gpu)  # cudnn.benchmark analogue (task.py:244)
 
     if args.pretrained:
         print(f"=> pre-trained weights for '{args.arch}' need network access; random init instead")

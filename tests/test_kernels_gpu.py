@@ -363,3 +363,71 @@ def test_stem_superpixel_conv_matches_direct():
     dw_ref = torch.nn.grad.conv2d_weight(x.to(torch.bfloat16).float(), (64, 3, 7, 7),
                                          dy.permute(0, 3, 1, 2).float(), stride=2, padding=3)
     assert rel_err(dw, dw_ref) < 1e-2
+
+
+TILE_CASES = [
+    # N, H, W, Ci, Co, k, s, p  — dense 1x1, gathered 3x3, strided, odd channel counts
+    (4, 14, 14, 256, 512, 1, 1, 0),
+    (4, 15, 13, 64, 192, 3, 1, 1),
+    (4, 16, 16, 128, 256, 3, 2, 1),
+    (2, 9, 7, 40, 72, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("cfg", list(range(9)))
+@pytest.mark.parametrize("case", TILE_CASES)
+def test_conv_every_tile_config(cfg, case):
+    """Every tile config of the tuning table (block tile / LDS stages / 4- or 8-wave grid) gives
+    the same convolution: fwd (+BN statistics), dgrad (+fused BN-backward epilogue), wgrad."""
+    N, H, W, Ci, Co, k, s, p = case
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    x = bf(N, H, W, Ci)
+    w = bf(Co, k, k, Ci, scale=1.0 / math.sqrt(Ci * k * k))
+    shift = torch.randn(Co, device=dev) * 0.1
+    y, ps, pss = native().conv_fwd(x, w, s, p, shift, cfg=cfg)
+    yr, psr, pssr = _ref.conv_fwd(x.float(), w.float(), s, p, shift)
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(ps.sum(0), psr[0]) < 2e-3 and rel_err(pss.sum(0), pssr[0]) < 2e-3
+    dy = bf(N, Ho, Wo, Co)
+    dx = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, cfg=cfg)
+    dxr = _ref.conv_dgrad(dy.float(), w.float(), (N, H, W, Ci), s, p)
+    assert rel_err(dx, dxr) < 1e-2
+    # fused epilogue: dx of relu(bn(yin)) with residual addend, BN-backward sums
+    yin = bf(N, H, W, Ci)
+    add = bf(N, H, W, Ci)
+    mean = torch.randn(Ci, device=dev) * 0.1
+    invstd = torch.rand(Ci, device=dev) + 0.5
+    scale = torch.rand(Ci, device=dev) + 0.5
+    bias = torch.randn(Ci, device=dev) * 0.1
+    rep = torch.zeros(3, native().STAT_REPLICAS, Ci, device=dev)
+    g = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, add, yin, mean, invstd, scale, bias, rep,
+                            cfg=cfg)
+    sg, sgx = native().bn_bwd_collect(rep, Ci)
+    gr = (dxr + add.float()) * ((yin.float() * scale + bias) > 0)
+    assert rel_err(g, gr) < 1e-2
+    grb = gr.to(torch.bfloat16).float()
+    # sums of the stored bf16 g: the kernel's g and the reference's differ by bf16 rounding of
+    # slightly different dx, so the bound is the bf16 sum noise, not fp32's
+    assert rel_err(sg, grb.reshape(-1, Ci).sum(0)) < 5e-3
+    xhat = (yin.float() - mean) * invstd
+    assert rel_err(sgx, (grb * xhat).reshape(-1, Ci).sum(0)) < 5e-3
+    dw = native().conv_wgrad(dy, x, k, k, s, p, cfg=cfg)
+    dwr = _ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)
+    assert rel_err(dw, dwr) < 5e-3
+
+
+def test_tile_benchmark_mode_picks_and_caches():
+    C = native()
+    C.clear_tune_table()
+    C.set_benchmark(True, False, 1)
+    try:
+        x = bf(8, 14, 14, 256)
+        w = bf(256, 3, 3, 256, scale=1 / 48)
+        y, _, _ = C.conv_fwd(x, w, 1, 1)
+        tab = C.tune_table()
+        assert len(tab) == 1 and 0 <= next(iter(tab.values())) < C.CONV_TILE_CONFIGS
+        y2, _, _ = C.conv_fwd(x, w, 1, 1)
+        assert torch.equal(y, y2) and len(C.tune_table()) == 1
+    finally:
+        C.set_benchmark(False)
+        C.clear_tune_table()

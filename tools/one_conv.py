@@ -6,6 +6,7 @@ from mipipe.ops._native import native
 C = native()
 N, H, Ci, Co, k, s, p = [int(v) for v in (sys.argv[1:8] if len(sys.argv) > 7 else [256, 14, 256, 256, 3, 1, 1])]
 which = sys.argv[8] if len(sys.argv) > 8 else "fwd"
+cfg = int(sys.argv[9]) if len(sys.argv) > 9 else -1
 Ho = (H + 2 * p - k) // s + 1
 x = torch.randn(N, H, H, Ci, device="cuda").to(torch.bfloat16)
 w = (torch.randn(Co, k, k, Ci, device="cuda") * 0.05).to(torch.bfloat16)
@@ -14,10 +15,10 @@ sh = torch.zeros(Co, device="cuda")
 out = torch.zeros(Co, k, k, Ci, device="cuda")
 for _ in range(20):
     if which == "fwd":
-        C.conv_fwd(x, w, s, p, sh)
+        C.conv_fwd(x, w, s, p, sh, cfg=cfg)
     elif which == "dgrad":
-        C.conv_dgrad(dy, w, [N, H, H, Ci], s, p)
+        C.conv_dgrad(dy, w, [N, H, H, Ci], s, p, cfg=cfg)
     else:
-        C.conv_wgrad(dy, x, k, k, s, p, out)
+        C.conv_wgrad(dy, x, k, k, s, p, out, cfg=cfg)
 torch.cuda.synchronize()
 print("done", which)
