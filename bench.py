@@ -70,6 +70,8 @@ def parse():
                     help="cpu = gloo backend, fp32 (harness tests without a GPU)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="compute dtype of the mipipe kernels (fp32 = the reference's precision)")
+    ap.add_argument("--deterministic", type=int, default=0,
+                    help="1: fixed-order reductions (no float atomics), bit-reproducible steps")
     ap.add_argument("--tune", type=int, default=1,
                     help="1: autotune conv tile configs per shape in the warm-up (cudnn.benchmark "
                          "analogue); 0: heuristic tile choice")
@@ -134,6 +136,8 @@ def main() -> int:
         from mipipe.ops import tuning
         tuning.from_env()
         tuning.set_benchmark(a.tune, verbose=False)
+        from mipipe.ops import determinism
+        determinism.set_deterministic(bool(a.deterministic))
     if rank == 0:
         _heartbeat()
 
@@ -190,6 +194,7 @@ def main() -> int:
                        "image_size": None if is_bert else a.res, "batch_per_gpu": a.batch,
                        "parallelism": f"dp{world}", "impl": a.impl, "optimizer": opt_s,
                        "hip_graph": bool(getattr(a, "graph_used", False)),
+                       "deterministic": bool(a.deterministic),
                        "force_reduce": bool(a.force_reduce)},
             "final_loss": loss_v}), flush=True)
     if distributed:

@@ -204,6 +204,17 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
                        b.has_value() ? b->data_ptr<float>() : nullptr, sh, s, stream(), bp, relu, c);
     });
   }
+  if (mipipe::g_deterministic && psp != nullptr) {
+    // per-M-tile partial rows (no atomics), then a fixed-order sum into slab row 0; the other
+    // replica rows of the slabs stay zero
+    const int P = mipipe::conv_fwd_tiles_m(s, cfg);
+    auto part = torch::empty({2, P, s.Co}, x.options().dtype(at::kFloat));
+    float* p0 = part.data_ptr<float>();
+    mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), p0, p0 + (long)P * s.Co, sh, s,
+                     stream(), bp, relu, cfg, P);
+    mipipe::det_sum_rows(p0, p0 + (long)P * s.Co, P, s.Co, psp, pssp, false, stream());
+    return {y, ps, pss};
+  }
   mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), psp, pssp, sh, s, stream(), bp, relu,
                    cfg);
   return {y, ps, pss};
@@ -275,6 +286,18 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
                          any ? &f2 : nullptr, c);
     });
   }
+  if (mipipe::g_deterministic && fz.bn_rep != nullptr) {
+    const int P = mipipe::conv_dgrad_tiles_m(s, cfg);
+    auto part = torch::empty({2, P, s.Ci}, dy.options().dtype(at::kFloat));
+    float* rep = fz.bn_rep;
+    fz.bn_rep = part.data_ptr<float>();
+    fz.det_rows = P;
+    mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), &fz, cfg);
+    const long rs = (long)mipipe::kStatReplicas * s.Ci;
+    mipipe::det_sum_rows(fz.bn_rep, fz.bn_rep + (long)P * s.Ci, P, s.Ci, rep, rep + rs, false,
+                         stream());
+    return dx;
+  }
   mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), any ? &fz : nullptr,
                      cfg);
   return dx;
@@ -323,6 +346,13 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
       auto dws = torch::zeros_like(dw);
       mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dws.data_ptr<float>(), s, stream(), c);
     });
+  }
+  if (mipipe::g_deterministic) {
+    const int splits = mipipe::conv_wgrad_splits(s, cfg);
+    auto ws = torch::empty({splits, (int64_t)s.Co * kh * kw * s.Ci}, dy.options().dtype(at::kFloat));
+    mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), cfg,
+                       ws.data_ptr<float>());
+    return dw;
   }
   mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), cfg);
   return dw;
@@ -419,6 +449,9 @@ std::tuple<Tensor, Tensor, optional<Tensor>> bn_act_bwd_reduce(
   } else {
     work = torch::zeros({3L * mipipe::kStatReplicas * C}, o);
   }
+  optional<Tensor> det_ws;
+  if (mipipe::g_deterministic)
+    det_ws = torch::empty({3, (int64_t)mipipe::bn_bwd_reduce_blocks(M, (int)C), C}, o);
   mipipe::bn_act_bwd_reduce(dz.data_ptr(), z.data_ptr(), y.data_ptr(), mean.data_ptr<float>(),
                             invstd.data_ptr<float>(), ptr_or_null(y2),
                             mean2.has_value() ? mean2->data_ptr<float>() : nullptr,
@@ -426,7 +459,8 @@ std::tuple<Tensor, Tensor, optional<Tensor>> bn_act_bwd_reduce(
                             (int)C, sg.data_ptr<float>(), sgx.data_ptr<float>(),
                             sgx2.has_value() ? sgx2->data_ptr<float>() : nullptr,
                             work.data_ptr<float>(), fptr(dgamma, C), fptr(dbeta, C),
-                            fptr(dgamma2, C), fptr(dbeta2, C), stream(), is_f32(y));
+                            fptr(dgamma2, C), fptr(dbeta2, C), stream(), is_f32(y),
+                            det_ws.has_value() ? det_ws->data_ptr<float>() : nullptr);
   return {sg, sgx, sgx2};
 }
 
@@ -580,7 +614,7 @@ std::tuple<Tensor, Tensor> cross_entropy_fwd_bwd(Tensor logits, Tensor labels, d
   int R = logits.size(0), V = logits.size(1);
   auto loss = torch::empty({}, logits.options().dtype(at::kFloat));
   auto grad = torch::empty_like(logits);
-  auto work = torch::empty({4}, logits.options().dtype(at::kInt));
+  auto work = torch::empty({4 + R}, logits.options().dtype(at::kInt));  // count + row losses
   mipipe::cross_entropy_fwd_bwd(logits.data_ptr(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
                                 grad.data_ptr(), R, V, (float)smoothing, ignore_index,
                                 work.data_ptr<int>(), stream(), is_f32(logits));
@@ -787,8 +821,11 @@ Tensor colsum(Tensor x, optional<Tensor> out) {
   } else {
     o = torch::zeros({cols}, x.options().dtype(at::kFloat));
   }
+  optional<Tensor> work;
+  if (mipipe::g_deterministic)
+    work = torch::empty({(int64_t)mipipe::colsum_blocks(rows), cols}, x.options().dtype(at::kFloat));
   mipipe::colsum_f32(x.data_ptr(), x.scalar_type() == at::kBFloat16, o.data_ptr<float>(), rows,
-                     (int)cols, nullptr, stream());
+                     (int)cols, work.has_value() ? work->data_ptr<float>() : nullptr, stream());
   return o;
 }
 
@@ -1116,6 +1153,8 @@ PYBIND11_MODULE(_C, m) {
     tune::g_reps = std::max(1, reps);
   }, py::arg("on"), py::arg("verbose") = false, py::arg("reps") = 3);
   m.def("get_benchmark", []() { return tune::g_benchmark; });
+  m.def("set_deterministic", [](bool on) { mipipe::g_deterministic = on ? 1 : 0; });
+  m.def("get_deterministic", []() { return mipipe::g_deterministic != 0; });
   m.def("tune_table", []() { return tune::g_table; });
   m.def("set_tune_entry", [](const std::string& k, int cfg) {
     TORCH_CHECK(cfg >= -1 && cfg < mipipe::kConvTileConfigs, "bad tile config id");

@@ -201,14 +201,17 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     const T* __restrict__ dz, const T* __restrict__ z, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const T* __restrict__ y2, const float* __restrict__ mean2,
-    const float* __restrict__ invstd2, bool relu, long M, int C, float* __restrict__ rep) {
+    const float* __restrict__ invstd2, bool relu, long M, int C, float* __restrict__ rep,
+    int det_rows) {
   __shared__ float red[3][kT][8];
   const RowMap mp = row_map(C);
   const int t = threadIdx.x;
   const int rg = t / mp.tpr;
   const bool active = rg < mp.rpb;
-  float* rrow = rep + (long)(blockIdx.x % kStatReplicas) * C;
-  const long rstride = (long)kStatReplicas * C;
+  // atomic mode: replica row blockIdx % R of [3][R][C]; deterministic: row blockIdx of
+  // [3][det_rows][C], written (one writer per element)
+  float* rrow = rep + (long)(det_rows > 0 ? blockIdx.x : blockIdx.x % kStatReplicas) * C;
+  const long rstride = (long)(det_rows > 0 ? det_rows : kStatReplicas) * C;
   for (int pass = 0; pass < mp.passes; ++pass) {
     const int cg = pass * mp.tpr + (t % mp.tpr);
     const int c0 = cg * 8;
@@ -268,9 +271,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
         if (TWO) a2 += red[2][k * mp.tpr + owner][q];
       }
       const int cc = pass * mp.tpr * 8 + c;
-      atomicAdd(rrow + cc, a0);
-      atomicAdd(rrow + rstride + cc, a1);
-      if (TWO) atomicAdd(rrow + 2 * rstride + cc, a2);
+      if (det_rows > 0) {
+        rrow[cc] = a0;
+        rrow[rstride + cc] = a1;
+        if (TWO) rrow[2 * rstride + cc] = a2;
+      } else {
+        atomicAdd(rrow + cc, a0);
+        atomicAdd(rrow + rstride + cc, a1);
+        if (TWO) atomicAdd(rrow + 2 * rstride + cc, a2);
+      }
     }
     __syncthreads();
   }
@@ -317,26 +326,39 @@ __global__ void bn_bwd_collect_kernel(float* __restrict__ rep, int C, float* og,
   }
 }
 
+int bn_bwd_reduce_blocks(long M, int C) {
+  RowMap mp = row_map(C);
+  // >= 16 row-iterations per thread, and at most ~1M atomic adds in total
+  long cap = std::max<long>(64, (1l << 20) / (3l * C));
+  return (int)std::max<long>(1, std::min<long>(std::min<long>(1024, cap),
+                                               (M + mp.rpb * 16 - 1) / (mp.rpb * 16)));
+}
+
 void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float* mean,
                        const float* invstd, const void* y2, const float* mean2,
                        const float* invstd2, bool relu, long M, int C, float* out_g,
                        float* out_gx, float* out_gx2, float* rep, float* dgamma, float* dbeta,
-                       float* dgamma2, float* dbeta2, hipStream_t st, bool f32) {
-  RowMap mp = row_map(C);
-  // >= 16 row-iterations per thread, and at most ~1M atomic adds in total
-  long cap = std::max<long>(64, (1l << 20) / (3l * C));
-  int G = (int)std::max<long>(1, std::min<long>(std::min<long>(1024, cap),
-                                                (M + mp.rpb * 16 - 1) / (mp.rpb * 16)));
+                       float* dgamma2, float* dbeta2, hipStream_t st, bool f32, float* det_ws) {
+  const int G = bn_bwd_reduce_blocks(M, C);
+  const int det_rows = det_ws != nullptr ? G : 0;
+  float* part = det_ws != nullptr ? det_ws : rep;
   auto launch = [&](auto tag) {
     typedef decltype(tag) T;
     const T *dzp = (const T*)dz, *zp = (const T*)z, *yp = (const T*)y, *y2p = (const T*)y2;
     if (y2 == nullptr)
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, T>), dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, rep);
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, T>), dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, part, det_rows);
     else
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, T>), dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, rep);
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, T>), dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, part, det_rows);
   };
   if (f32) launch(float{});
   else launch(__bf16{});
+  if (det_ws != nullptr) {
+    // fixed-order sum of the G per-block rows into replica row 0 (the rest of rep stays zero),
+    // then the usual collect
+    const long rs = (long)kStatReplicas * C, ds = (long)G * C;
+    det_sum_rows(det_ws, det_ws + ds, G, C, rep, rep + rs, false, st);
+    if (y2 != nullptr) det_sum_rows(det_ws + 2 * ds, nullptr, G, C, rep + 2 * rs, nullptr, false, st);
+  }
   hipLaunchKernelGGL(bn_bwd_collect_kernel, dim3((C + 255) / 256), dim3(256), 0, st, rep, C, out_g,
                      out_gx, y2 ? out_gx2 : nullptr, dgamma, dbeta, y2 ? dgamma2 : nullptr,
                      y2 ? dbeta2 : nullptr);

@@ -18,20 +18,35 @@ int default_fwd_cfg(const ConvShape& s) {
   return ns1 ? 1 : 0;
 }
 
+static int resolve_fwd_cfg(const ConvShape& s, int cfg) {
+  const bool ok = s.f32 ? tile_ok_for<float>(cfg) : tile_ok_for<__bf16>(cfg);
+  return ok ? cfg : default_fwd_cfg(s);
+}
+
+int conv_fwd_tiles_m(const ConvShape& s, int cfg) {
+  cfg = resolve_fwd_cfg(s, cfg);
+  int bm = 128;
+  auto f = [&](auto tile) { bm = decltype(tile)::BM; };
+  if (s.f32) with_tile<float>(cfg, f);
+  else with_tile<__bf16>(cfg, f);
+  return (int)cdiv((uint64_t)s.N * s.Ho * s.Wo, bm);
+}
+
 template <class T>
 static void conv_fwd_t(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
                        const float* st_shift, const ConvShape& s, hipStream_t st,
-                       const float* bias, bool relu, int cfg) {
+                       const float* bias, bool relu, int cfg, int det_rows) {
   ConvGeom g = make_geom(s);
   const uint32_t M = (uint32_t)s.N * s.Ho * s.Wo;
   EpiParams e{};
   e.C = y; e.ldc = s.Co; e.M = M; e.N = s.Co; e.bias = bias; e.act = relu ? 1 : 0;
   e.st_sum = st_sum; e.st_sq = st_sq; e.st_shift = st_shift; e.st_R = g_stat_rows;
+  e.det_rows = det_rows;
   const bool dense = is_dense(s);
   const bool aligned = s.Ci % BK == 0;
   const T* xp = (const T*)x;
   const T* wp = (const T*)w;
-  if (!tile_ok_for<T>(cfg)) cfg = default_fwd_cfg(s);
+  cfg = resolve_fwd_cfg(s, cfg);
   with_tile<T>(cfg, [&](auto tile) {
     typedef decltype(tile) C;
     const uint32_t tN = cdiv(s.Co, C::BN), tiles = cdiv(M, C::BM) * tN;
@@ -47,9 +62,9 @@ static void conv_fwd_t(const void* x, const void* w, void* y, float* st_sum, flo
 
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
               const float* st_shift, const ConvShape& s, hipStream_t st, const float* bias,
-              bool relu, int cfg) {
-  if (s.f32) conv_fwd_t<float>(x, w, y, st_sum, st_sq, st_shift, s, st, bias, relu, cfg);
-  else conv_fwd_t<__bf16>(x, w, y, st_sum, st_sq, st_shift, s, st, bias, relu, cfg);
+              bool relu, int cfg, int det_rows) {
+  if (s.f32) conv_fwd_t<float>(x, w, y, st_sum, st_sq, st_shift, s, st, bias, relu, cfg, det_rows);
+  else conv_fwd_t<__bf16>(x, w, y, st_sum, st_sq, st_shift, s, st, bias, relu, cfg, det_rows);
 }
 
 }  // namespace mipipe

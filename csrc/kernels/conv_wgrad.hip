@@ -16,36 +16,70 @@ static int pick_splits(uint32_t tiles, int nk, int Ci) {
   return std::min(splits, max_splits);
 }
 
+static int resolve_wgrad_cfg(const ConvShape& s, int cfg) {
+  const bool ok = s.f32 ? tile_ok_for<float>(cfg) : tile_ok_for<__bf16>(cfg);
+  return ok ? cfg : default_wgrad_cfg(s);
+}
+
+template <class C>
+static void wgrad_grid(const ConvShape& s, uint32_t& tN, uint32_t& tiles, int& splits, int& per) {
+  const uint32_t Ntot = (uint32_t)(s.KH * s.KW * s.Ci);
+  const int nk = (int)cdiv((uint64_t)s.N * s.Ho * s.Wo, BK);
+  tN = cdiv(Ntot, C::BN);
+  tiles = cdiv(s.Co, C::BM) * tN;
+  splits = pick_splits(tiles, nk, s.Ci);
+  per = (int)cdiv(nk, splits);
+  splits = (int)cdiv(nk, per);
+}
+
+int conv_wgrad_splits(const ConvShape& s, int cfg) {
+  cfg = resolve_wgrad_cfg(s, cfg);
+  int splits = 1;
+  auto f = [&](auto tile) {
+    uint32_t tN, tiles;
+    int per;
+    wgrad_grid<decltype(tile)>(s, tN, tiles, splits, per);
+  };
+  if (s.f32) with_tile<float, true>(cfg, f);
+  else with_tile<__bf16, true>(cfg, f);
+  return splits;
+}
+
 template <class T>
 static void conv_wgrad_t(const void* dy, const void* x, float* dw, const ConvShape& s,
-                         hipStream_t st, int cfg) {
+                         hipStream_t st, int cfg, float* ws) {
   ConvGeom g = make_geom(s);
   const uint32_t Ntot = (uint32_t)(s.KH * s.KW * s.Ci);
   EpiParams e{};
   e.C = dw; e.ldc = Ntot; e.M = s.Co; e.N = Ntot;
   const bool dense = is_dense(s);
-  const long K = (long)s.N * s.Ho * s.Wo;
-  const int nk = (int)cdiv(K, BK);
   const T* dyp = (const T*)dy;
   const T* xp = (const T*)x;
-  if (!tile_ok_for<T>(cfg)) cfg = default_wgrad_cfg(s);
+  cfg = resolve_wgrad_cfg(s, cfg);
+  int splits_used = 1;
+  if (ws != nullptr) {  // deterministic: partial tiles to the workspace, summed in split order
+    e.C = ws;
+    e.det_rows = 1;
+  }
   with_tile<T, true>(cfg, [&](auto tile) {
     typedef decltype(tile) C;
-    const uint32_t tN = cdiv(Ntot, C::BN), tiles = cdiv(s.Co, C::BM) * tN;
-    int splits = pick_splits(tiles, nk, s.Ci), per = (int)cdiv(nk, splits);
-    splits = (int)cdiv(nk, per);
+    uint32_t tN, tiles;
+    int splits, per;
+    wgrad_grid<C>(s, tN, tiles, splits, per);
+    splits_used = splits;
     const dim3 grid(tiles, splits), block(C::THREADS);
     if (dense)
       hipLaunchKernelGGL((conv_wgrad_kernel<C, true, T>), grid, block, 0, st, dyp, xp, g, tN, per, e);
     else
       hipLaunchKernelGGL((conv_wgrad_kernel<C, false, T>), grid, block, 0, st, dyp, xp, g, tN, per, e);
   });
+  if (ws != nullptr) splitk_sum(ws, splits_used, (long)s.Co * Ntot, dw, st);
 }
 
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
-                int cfg) {
-  if (s.f32) conv_wgrad_t<float>(dy, x, dw, s, st, cfg);
-  else conv_wgrad_t<__bf16>(dy, x, dw, s, st, cfg);
+                int cfg, float* ws) {
+  if (s.f32) conv_wgrad_t<float>(dy, x, dw, s, st, cfg, ws);
+  else conv_wgrad_t<__bf16>(dy, x, dw, s, st, cfg, ws);
 }
 
 }  // namespace mipipe

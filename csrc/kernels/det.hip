@@ -1,0 +1,84 @@
+// Deterministic reductions (the reference's cudnn.deterministic = True, task.py:25-26).
+//
+// In deterministic mode no kernel accumulates a floating-point value with atomics: producers
+// write per-block partial rows, and these kernels sum the rows in a FIXED order (fixed thread ->
+// row assignment, fixed LDS tree), so two identical runs produce bit-identical results.
+#include "common.hpp"
+#include "launchers.hpp"
+
+namespace mipipe {
+
+int g_deterministic = 0;
+
+// out[c] (+)= sum_p in[p][c] for up to two row arrays.  Block: 64 channels x 16 row groups;
+// group g sums rows g, g+16, ... in order, then the 16 group sums are added in index order.
+__global__ __launch_bounds__(1024) void det_sum_rows_kernel(const float* __restrict__ in0,
+                                                            const float* __restrict__ in1, int P,
+                                                            int C, float* __restrict__ out0,
+                                                            float* __restrict__ out1,
+                                                            bool accumulate) {
+  __shared__ float part[16][65];
+  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  const float* in = blockIdx.y == 0 ? in0 : in1;
+  float* out = blockIdx.y == 0 ? out0 : out1;
+  float a = 0.f;
+  if (c < C)
+    for (int p = g; p < P; p += 16) a += in[(long)p * C + c];
+  part[g][lc] = a;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += part[k][lc];
+    out[c] = accumulate ? out[c] + s : s;
+  }
+}
+
+void det_sum_rows(const float* in0, const float* in1, int P, int C, float* out0, float* out1,
+                  bool accumulate, hipStream_t st) {
+  dim3 grid((C + 63) / 64, in1 != nullptr ? 2 : 1);
+  hipLaunchKernelGGL(det_sum_rows_kernel, grid, dim3(1024), 0, st, in0, in1, P, C, out0, out1,
+                     accumulate);
+}
+
+// out[i] += sum_s ws[s][i], s in order (split-K partial tiles of a weight gradient).
+__global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict__ ws, int splits,
+                                                         long n4, float* __restrict__ out) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (long)gridDim.x * blockDim.x) {
+    float4 a = reinterpret_cast<const float4*>(ws)[i];
+    for (int s = 1; s < splits; ++s) {
+      const float4 b = reinterpret_cast<const float4*>(ws + (long)s * n4 * 4)[i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    float4 o = reinterpret_cast<float4*>(out)[i];
+    o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+    reinterpret_cast<float4*>(out)[i] = o;
+  }
+}
+
+__global__ void splitk_sum_tail_kernel(const float* __restrict__ ws, int splits, long n0, long n,
+                                       float* __restrict__ out) {
+  const long i = n0 + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float a = 0.f;
+  for (int s = 0; s < splits; ++s) a += ws[(long)s * n + i];
+  out[i] += a;
+}
+
+void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st) {
+  // the vector path needs n % 4 == 0 and 16-B aligned rows of ws / out
+  const bool vec = (n % 4) == 0 && (reinterpret_cast<uintptr_t>(out) % 16) == 0;
+  if (vec) {
+    const long n4 = n / 4;
+    const long g = std::min<long>(4096, (n4 + 255) / 256);
+    hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)std::max<long>(1, g)), dim3(256), 0, st,
+                       ws, splits, n4, out);
+  } else {
+    hipLaunchKernelGGL(splitk_sum_tail_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       st, ws, splits, 0l, n, out);
+  }
+}
+
+}  // namespace mipipe

@@ -34,6 +34,12 @@ struct EpiParams {
   // when set, the ReLU mask is read from this stored post-activation tensor (z > 0) instead of
   // recomputed from y (needed when a residual was added before the ReLU)
   const void* bnr_z;  // output dtype
+  // deterministic mode (det_rows > 0): no float atomics.  Statistics partials (st_sum / st_sq,
+  // bnr_rep) are WRITTEN at row det_row0 + (m0 / BM) of [det_rows][N] slabs (bnr_rep: two
+  // arrays det_rows apart) and summed in a fixed order afterwards (det.hip); split-K fp32
+  // outputs (epilogue_f32) are written to slice blockIdx.y of a [splits][M][ldc] workspace.
+  int det_rows;
+  int det_row0;
 };
 
 // Workgroup barrier that orders LDS only.  __syncthreads() also drains every outstanding global
@@ -195,8 +201,12 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
         float v = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) v += lst[(arr * WM + w) * BN + c];
-        float* dst = (arr == 0 ? e.st_sum : e.st_sq) + (long)(blockIdx.x % e.st_R) * e.N + n;
-        atomicAdd(dst, v);
+        float* base = arr == 0 ? e.st_sum : e.st_sq;
+        if (e.det_rows > 0) {
+          base[(long)(e.det_row0 + m0 / BM) * e.N + n] = v;
+        } else {
+          atomicAdd(base + (long)(blockIdx.x % e.st_R) * e.N + n, v);
+        }
       }
     }
   }
@@ -272,8 +282,12 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
       const int arr = j / BN, col = j % BN, cc = col >> 3, q = col & 7;
       float a = 0.f;
       for (int t = cc; t < kThreads; t += CPR) a += red[(arr * 8 + q) * RP + t];
-      if (n0 + col < e.N)
-        atomicAdd(e.bnr_rep + ((long)arr * R + blockIdx.x % Rw) * e.N + n0 + col, a);
+      if (n0 + col < e.N) {
+        if (e.det_rows > 0)
+          e.bnr_rep[((long)arr * e.det_rows + e.det_row0 + m0 / BM) * e.N + n0 + col] = a;
+        else
+          atomicAdd(e.bnr_rep + ((long)arr * R + blockIdx.x % Rw) * e.N + n0 + col, a);
+      }
     }
   }
 }
@@ -305,7 +319,15 @@ __device__ void epilogue_f32(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
     }
   __syncthreads();
   float* C = reinterpret_cast<float*>(e.C);
-  if constexpr (ATOMIC) {
+  if (ATOMIC && e.det_rows > 0) {
+    // deterministic split-K: this split's partial tile goes to its own workspace slice
+    C += (long)blockIdx.y * e.M * e.ldc;
+    for (int c = threadIdx.x; c < BM * BN; c += kThreads) {
+      uint32_t r = c / BN, cc = c % BN;
+      uint32_t m = m0 + r, n = n0 + cc;
+      if (m < e.M && n < e.N) C[(long)m * e.ldc + n] = *reinterpret_cast<const float*>(smem + r * P + cc * 4);
+    }
+  } else if constexpr (ATOMIC) {
     // each wave-instruction: 64 lanes x 4 B = 256 contiguous bytes of one row
     for (int c = threadIdx.x; c < BM * BN; c += kThreads) {
       uint32_t r = c / BN, cc = c % BN;

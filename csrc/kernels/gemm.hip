@@ -70,7 +70,8 @@ static void launch_tile(const void* A, long lda, bool a_kc, const void* B, long 
   uint32_t tN = cdiv_u(N, BN), tiles = cdiv_u(M, BM) * tN;
   int nk = (int)cdiv_u(K, 64);
   int splits = 1, per = nk;
-  if (out == 2) {  // split-K until ~g_splitk_target blocks, >= 4 k-steps per split
+  if (out == 2 && !g_deterministic) {  // split-K until ~g_splitk_target blocks, >= 4 k-steps per split
+    // (deterministic mode: one split, so every output element is written by one block)
     splits = std::max<int>(1, std::min<int>(g_splitk_target / std::max<uint32_t>(1, tiles), nk / 4));
     per = (int)cdiv_u(nk, splits);
     splits = (int)cdiv_u(nk, per);

@@ -33,14 +33,25 @@ extern int g_splitk_target;
 // Dense (1x1) conv fwd/dgrad with reduction K <= this use the single-LDS-stage kernels.
 extern int g_ns1_max_k;
 extern int g_ns1_max_k_gather;  // same for the gathered (im2col / strided dgrad) convs
+// Deterministic mode (reference task.py:25-26 cudnn.deterministic): every float reduction runs
+// in a fixed order — no float atomics (det.hip); set from Python (mipipe.ops.set_deterministic).
+extern int g_deterministic;
+// out[c] (+)= sum over P rows of in[p][c] (and in1 -> out1), fixed order.
+void det_sum_rows(const float* in0, const float* in1, int P, int C, float* out0, float* out1,
+                  bool accumulate, hipStream_t st);
+// out[i] += sum_s ws[s][i] over splits in order.
+void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st);
 int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 // bias / relu: optional per-channel bias and ReLU in the epilogue (convs without BN: VGG, AlexNet)
 // cfg: tile config id (conv_common.hpp table; < 0 = heuristic default)
 constexpr int kConvTileConfigs = 9;
+//  det_rows > 0 (deterministic mode): st_sum / st_sq are [det_rows][Co] partial slabs, one row
+//  per M-tile (det_rows = conv_fwd_tiles_m(s, cfg)), written without atomics.
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
               const float* st_shift, const ConvShape& s, hipStream_t st,
-              const float* bias = nullptr, bool relu = false, int cfg = -1);
+              const float* bias = nullptr, bool relu = false, int cfg = -1, int det_rows = 0);
+int conv_fwd_tiles_m(const ConvShape& s, int cfg);
 // Optional dgrad epilogue fusions:
 //  addend: [N*H*W][Ci] (activation dtype) added to dx (the block input's other gradient, e.g. the residual);
 //  bn_*:   the conv input was relu(bn(y)) with a single consumer: dx becomes g = dx*[z > 0] and
@@ -51,13 +62,18 @@ struct DgradFusion {
   const float *bn_mean = nullptr, *bn_invstd = nullptr, *bn_scale = nullptr, *bn_bias = nullptr;
   float* bn_rep = nullptr;
   const void* bn_z = nullptr;  // optional stored relu output: mask = z > 0 (residual blocks)
+  int det_rows = 0;  // deterministic mode: bn_rep is [2][det_rows][Ci] partials, one row per tile
 };
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
                 const DgradFusion* fz = nullptr, int cfg = -1);
+int conv_dgrad_tiles_m(const ConvShape& s, int cfg);  // M-tiles over all stride classes
 // dw is ACCUMULATED into with fp32 atomics (split-K): pass a zeroed buffer, or the parameter's
 // gradient buffer to fuse autograd's accumulation (gradient lands directly in the DDP bucket)
+//  ws != nullptr (deterministic mode): [conv_wgrad_splits(s, cfg)][Co*KH*KW*Ci] workspace for the
+//  split-K partials, summed into dw in split order.
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
-                int cfg = -1);
+                int cfg = -1, float* ws = nullptr);
+int conv_wgrad_splits(const ConvShape& s, int cfg);
 
 // ---- direct convolution, BatchNorm for any C, k x k average pool (vision.hip) ----------------
 struct GConvShape {
@@ -125,7 +141,10 @@ void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float
                        const float* invstd, const void* y2, const float* mean2,
                        const float* invstd2, bool relu, long M, int C, float* out_g,
                        float* out_gx, float* out_gx2, float* rep, float* dgamma, float* dbeta,
-                       float* dgamma2, float* dbeta2, hipStream_t st, bool f32 = false);
+                       float* dgamma2, float* dbeta2, hipStream_t st, bool f32 = false,
+                       float* det_ws = nullptr);
+// grid size of the reduce pass: deterministic mode needs det_ws = [3][blocks][C] floats
+int bn_bwd_reduce_blocks(long M, int C);
 // Sum the replica rows of a bwd slab (filled by a fused dgrad epilogue) into out_g / out_gx,
 // re-zero it, optionally accumulate dγ += Σg·x̂, dβ += Σg.
 void bn_bwd_collect(float* rep, int C, float* out_g, float* out_gx, float* dgamma, float* dbeta,
@@ -146,6 +165,8 @@ void avgpool_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st, b
 void avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st, bool f32 = false);
 
 // ---- loss / optimizer / data -----------------------------------------------------------------
+// work: 4 ints (valid-row count) then R floats (per-row losses, summed in a fixed order: the
+// loss is bit-reproducible)
 void cross_entropy_fwd_bwd(const void* logits, const int64_t* labels, float* loss, void* grad,
                            int R, int V, float smoothing, int64_t ignore_index, int* work,
                            hipStream_t st, bool f32 = false);
@@ -191,7 +212,9 @@ void attention_bwd(const void* dout, const void* qkv, const void* o, const float
 // recomputes the same keep mask from the seed (no mask tensor).
 void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStream_t st);
 void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, hipStream_t st);
+// work (deterministic mode, else null): [colsum_blocks(rows)][cols] floats of per-block partials
 void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
                 hipStream_t st);
+int colsum_blocks(long rows);
 
 }  // namespace mipipe

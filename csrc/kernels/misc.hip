@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void ce_kernel(const T* __restrict__ logits,
                                                  const int64_t* __restrict__ labels,
                                                  float* __restrict__ loss, T* __restrict__ grad,
                                                  int V, float eps, int64_t ignore,
-                                                 const int* __restrict__ nvalid) {
+                                                 const int* __restrict__ nvalid,
+                                                 float* __restrict__ rowloss) {
   __shared__ float sh[8];
   const long row = blockIdx.x;
   const T* x = logits + row * V;
@@ -87,10 +88,13 @@ __global__ __launch_bounds__(256) void ce_kernel(const T* __restrict__ logits,
   se = block_reduce(se, sh, false);
   const float lse = mx + __logf(se);
   const float inv_n = 1.f / (float)max(1, nvalid[0]);
-  if (threadIdx.x == 0 && valid) {
-    float xl = (float)x[lab];
-    float l = (1.f - eps) * (lse - xl) + eps * (lse - sx / (float)V);
-    atomicAdd(loss, l * inv_n);
+  if (threadIdx.x == 0) {  // summed in a fixed order by ce_sum_kernel (no float atomics)
+    float l = 0.f;
+    if (valid) {
+      float xl = (float)x[lab];
+      l = (1.f - eps) * (lse - xl) + eps * (lse - sx / (float)V);
+    }
+    rowloss[row] = l * inv_n;
   }
   const float scale = valid ? inv_n : 0.f;
   const float inv_se = 1.f / se;
@@ -115,17 +119,33 @@ __global__ __launch_bounds__(256) void ce_kernel(const T* __restrict__ logits,
   }
 }
 
+// loss = sum of the per-row losses in a fixed order (thread t: rows t, t+256, ...; then a tree)
+__global__ __launch_bounds__(256) void ce_sum_kernel(const float* __restrict__ rowloss, int R,
+                                                     float* __restrict__ loss) {
+  __shared__ float red[256];
+  float a = 0.f;
+  for (int i = threadIdx.x; i < R; i += 256) a += rowloss[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = red[0];
+}
+
 void cross_entropy_fwd_bwd(const void* logits, const int64_t* labels, float* loss, void* grad,
                            int R, int V, float smoothing, int64_t ignore_index, int* work,
                            hipStream_t st, bool f32) {
-  hipMemsetAsync(loss, 0, sizeof(float), st);
+  float* rowloss = reinterpret_cast<float*>(work + 4);
   hipLaunchKernelGGL(ce_count_kernel, dim3(1), dim3(256), 0, st, labels, R, ignore_index, work);
   if (f32)
     hipLaunchKernelGGL(ce_kernel<float>, dim3(R), dim3(256), 0, st, (const float*)logits, labels,
-                       loss, (float*)grad, V, smoothing, ignore_index, (const int*)work);
+                       loss, (float*)grad, V, smoothing, ignore_index, (const int*)work, rowloss);
   else
     hipLaunchKernelGGL(ce_kernel<__bf16>, dim3(R), dim3(256), 0, st, (const __bf16*)logits, labels,
-                       loss, (__bf16*)grad, V, smoothing, ignore_index, (const int*)work);
+                       loss, (__bf16*)grad, V, smoothing, ignore_index, (const int*)work, rowloss);
+  hipLaunchKernelGGL(ce_sum_kernel, dim3(1), dim3(256), 0, st, rowloss, R, loss);
 }
 
 // ------------------------------------------------------------------------------ evaluation
@@ -393,7 +413,8 @@ void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st) {
 // partials are reduced through LDS and added with one fp32 atomic per column per block.
 __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x, bool bf16,
                                                      float* __restrict__ out, long rows, int cols,
-                                                     long rows_per_block) {
+                                                     long rows_per_block,
+                                                     float* __restrict__ part) {
   __shared__ float red[256 * 8 + 8];
   const int nvec = bf16 ? cols / 8 : cols / 4;  // vectors per row
   const int per = bf16 ? 8 : 4;
@@ -425,17 +446,31 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x,
     for (int c = t; c < ncol; c += 256) {
       float a = 0.f;
       for (int k = 0; k < rpb; ++k) a += red[k * tpr * per + c];
-      atomicAdd(out + (long)vb * per + c, a);
+      if (part != nullptr) part[(long)blockIdx.x * cols + (long)vb * per + c] = a;
+      else atomicAdd(out + (long)vb * per + c, a);
     }
   }
 }
 
-void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* /*work*/,
-                hipStream_t st) {
-  long G = std::max<long>(1, std::min<long>(512, (rows + 31) / 32));
-  long rpb = (rows + G - 1) / G;
+static void colsum_grid(long rows, long& G, long& rpb) {
+  G = std::max<long>(1, std::min<long>(512, (rows + 31) / 32));
+  rpb = (rows + G - 1) / G;
   G = (rows + rpb - 1) / rpb;
-  hipLaunchKernelGGL(colsum_kernel, dim3(G), dim3(256), 0, st, x, bf16, out, rows, cols, rpb);
+}
+
+int colsum_blocks(long rows) {
+  long G, rpb;
+  colsum_grid(rows, G, rpb);
+  return (int)G;
+}
+
+void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
+                hipStream_t st) {
+  long G, rpb;
+  colsum_grid(rows, G, rpb);
+  // work != null (deterministic mode): per-block partial rows, then a fixed-order sum
+  hipLaunchKernelGGL(colsum_kernel, dim3(G), dim3(256), 0, st, x, bf16, out, rows, cols, rpb, work);
+  if (work != nullptr) det_sum_rows(work, nullptr, (int)G, cols, out, nullptr, true, st);
 }
 
 // ------------------------------------------------------------------------------ embedding grad

@@ -62,13 +62,16 @@ def set_random_seeds(random_seed: int = 0) -> None:
     random.seed(random_seed)
 
 
-def configure_kernels(use_gpu: bool) -> None:
-    """task.py:244 ``cudnn.benchmark = True`` -> per-shape tile autotuning of the conv kernels
+def configure_kernels(use_gpu: bool, deterministic: bool = True) -> None:
+    """task.py:25-26 ``cudnn.deterministic = True`` -> mipipe's deterministic mode (fixed-order
+    reductions, no float atomics: :mod:`mipipe.ops.determinism`); task.py:244
+    ``cudnn.benchmark = True`` -> per-shape tile autotuning of the conv kernels
     (:mod:`mipipe.ops.tuning`; ``MIPIPE_BENCHMARK=0`` disables it, ``MIPIPE_TUNE_TABLE=path``
     starts from a saved table)."""
     if not use_gpu:
         return
-    from mipipe.ops import tuning
+    from mipipe.ops import determinism, tuning
+    determinism.set_deterministic(deterministic)
     tuning.from_env()
     tuning.set_benchmark(os.environ.get("MIPIPE_BENCHMARK", "1") != "0",
                          verbose=os.environ.get("MIPIPE_TUNE_VERBOSE", "0") == "1")
@@ -178,6 +181,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--test-samples", type=int, default=None)
     p.add_argument("--num_classes", type=int, default=None,
                    help="classifier width (reference keeps torchvision's 1000)")
+    p.add_argument("--deterministic", dest="deterministic", action="store_true", default=True,
+                   help="fixed-order reductions, bit-reproducible runs (reference task.py:25-26 "
+                        "sets cudnn.deterministic); default on")
+    p.add_argument("--no-deterministic", dest="deterministic", action="store_false",
+                   help="allow float-atomic reductions (faster)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                    help="compute dtype on GPU (master weights stay fp32); CPU runs fp32")
     p.add_argument("--steps", type=int, default=0, help="max training steps per epoch (0 = all)")
@@ -276,7 +284,8 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
         print("Process group initialized", flush=True)
     world = dist_utils.get_world_size()
     set_random_seeds(args.random_seed)  # same seed on every rank -> identical init (task.py:161)
-    configure_kernels(use_gpu)  # cudnn.benchmark analogue (task.py:244)
+    # cudnn.deterministic (task.py:25-26) / cudnn.benchmark (task.py:244) analogues
+    configure_kernels(use_gpu, args.deterministic)
 
     if args.pretrained:
         print(f"=> pre-trained weights for '{args.arch}' need network access; random init instead")
