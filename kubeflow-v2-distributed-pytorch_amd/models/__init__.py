@@ -5,7 +5,9 @@
 """
 from __future__ import annotations
 
-from typing import Callable, Dict, List
+import glob
+import os
+from typing import Callable, Dict, List, Optional
 
 from .resnet import (resnet18, resnet34, resnet50, resnet101, resnet152,  # noqa: F401
                      wide_resnet50_2, wide_resnet101_2, resnext50_32x4d, resnext101_32x8d,
@@ -46,3 +48,27 @@ def create_model(arch: str, **kw):
     if arch not in _REGISTRY:
         raise KeyError(f"unknown arch {arch!r}; choices: {model_names()}")
     return _REGISTRY[arch](**kw)
+
+
+def find_pretrained(arch: str, path: Optional[str] = None) -> Optional[str]:
+    """Locate a torchvision-format weights file for ``arch`` without network access: ``path``
+    when given, else torchvision's download cache ``$TORCH_HOME/hub/checkpoints/<arch>-*.pth``
+    (``~/.cache/torch`` by default) — where ``models.<arch>(pretrained=True)`` (reference
+    task.py:166-168) would have put it."""
+    if path:
+        return path if os.path.exists(path) else None
+    home = os.environ.get("TORCH_HOME", os.path.join(os.path.expanduser("~"), ".cache", "torch"))
+    hits = sorted(glob.glob(os.path.join(home, "hub", "checkpoints", f"{arch}-*.pth")))
+    return hits[0] if hits else None
+
+
+def load_pretrained(model, path: str, strict: bool = True):
+    """Load a torchvision state_dict into a mipipe model (identical parameter / buffer names).
+    Weights-only loader: nothing in the file is executed."""
+    import torch
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(sd, dict) and "state_dict" in sd and isinstance(sd["state_dict"], dict):
+        sd = sd["state_dict"]  # a checkpoint written by task.py's save path
+    sd = {k[len("module."):] if k.startswith("module.") else k: v for k, v in sd.items()}
+    missing, unexpected = model.load_state_dict(sd, strict=strict)
+    return missing, unexpected

@@ -151,7 +151,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--wd", "--weight-decay", default=1e-4, type=float, metavar="W",
                    dest="weight_decay", help="weight decay (default: 1e-4)")
     p.add_argument("--pretrained", dest="pretrained", action="store_true",
-                   help="use pre-trained model (no network here: warns and random-inits)")
+                   help="use pre-trained model: torchvision-format weights from "
+                        "--pretrained-weights or the torchvision cache (no network download)")
+    p.add_argument("--pretrained-weights", dest="pretrained_weights", default=None,
+                   help="path of a torchvision-format state_dict (.pth) for --pretrained")
     p.add_argument("--local_training", dest="local_training", action="store_true",
                    help="save to --model_dir instead of AIP_MODEL_DIR")
     p.add_argument("--rank", default=-1, type=int, help="node rank for distributed training")
@@ -288,8 +291,9 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
     configure_kernels(use_gpu, args.deterministic)
 
     if args.pretrained:
-        print(f"=> pre-trained weights for '{args.arch}' need network access; random init instead")
-    print(f"=> creating model '{args.arch}'")
+        print(f"=> using pre-trained model '{args.arch}'")  # task.py:167
+    else:
+        print(f"=> creating model '{args.arch}'")
     C, H, W, K, N = DATASET_SHAPES[args.dataset]
     if args.image_size:
         H = W = args.image_size
@@ -302,6 +306,15 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
     elif args.arch.startswith(("resnet", "wide_resnet", "resnext")):
         kw["in_chans"] = C
     model = create_model(args.arch, **kw)
+    if args.pretrained:
+        from mipipe.models import find_pretrained, load_pretrained
+        wpath = find_pretrained(args.arch, args.pretrained_weights)
+        if wpath is None:
+            print(f"=> no local pre-trained weights for '{args.arch}' (no network access to "
+                  "download them): random init")
+        else:
+            load_pretrained(model, wpath)
+            print(f"=> loaded pre-trained weights from {wpath}")
     compute_dtype = torch.bfloat16 if (use_gpu and args.dtype == "bf16") else torch.float32
     if hasattr(model, "compute_dtype"):
         model.compute_dtype = compute_dtype

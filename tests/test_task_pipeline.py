@@ -125,3 +125,35 @@ def test_reference_pipeline_end_to_end(gcs_root, tmp_path, monkeypatch):
     assert models, "model not exported to AIP_MODEL_DIR"
     sd = torch.load(models[0], weights_only=True)
     assert any(k.startswith("module.") for k in sd)  # DDP-wrapped, like the reference
+
+
+def test_pretrained_from_local_torchvision_file(tmp_path, monkeypatch, capsys):
+    """--pretrained (task.py:166-168) loads a torchvision-format state_dict from
+    --pretrained-weights or the torchvision cache with a weights-only loader."""
+    from mipipe.models import create_model, find_pretrained, load_pretrained
+    torch.manual_seed(3)
+    src = create_model("resnet18", num_classes=10)
+    path = tmp_path / "hub" / "checkpoints" / "resnet18-f37072fd.pth"
+    path.parent.mkdir(parents=True)
+    torch.save({("module." + k): v for k, v in src.state_dict().items()}, path)
+    monkeypatch.setenv("TORCH_HOME", str(tmp_path))
+    assert find_pretrained("resnet18") == str(path)
+    assert find_pretrained("resnet50") is None
+    dst = create_model("resnet18", num_classes=10)
+    load_pretrained(dst, str(path))
+    for (k, a), (_, b) in zip(src.state_dict().items(), dst.state_dict().items()):
+        assert torch.equal(a, b), k
+    # through task.py: the exported model equals the pre-trained weights after 0 steps
+    monkeypatch.setenv("MIPIPE_FORCE_CPU", "1")
+    monkeypatch.delenv("AIP_MODEL_DIR", raising=False)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    out = tmp_path / "out"
+    rc = T.main(["--arch", "resnet18", "--num_classes", "10", "--pretrained",
+                 "--pretrained-weights", str(path), "--dataset", "cifar10", "--batch_size", "8",
+                 "--train-samples", "8", "--test-samples", "8", "--num_epochs", "1",
+                 "--learning_rate", "0.0", "--momentum", "0", "--wd", "0", "--local_training",
+                 "--model_dir", str(out), "--log-every", "0"])
+    assert rc == 0
+    assert "loaded pre-trained weights" in capsys.readouterr().out
+    sd = torch.load(out / "resnet_distributed.pth", weights_only=True)
+    assert torch.equal(sd["conv1.weight"], src.state_dict()["conv1.weight"])
