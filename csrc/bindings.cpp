@@ -934,15 +934,16 @@ Tensor dw_taps_major(const Tensor& w) {
 
 const void* act_mask_src(const optional<Tensor>& z, int64_t act, const Tensor& like) {
   if (act == 0 || !z.has_value()) return nullptr;
-  check_bf16(*z, "z");
+  check_act(*z, "z");
+  check_same(*z, like, "z");
   TORCH_CHECK(z->sizes() == like.sizes(), "z must match the conv output");
   return z->data_ptr();
 }
 
 Tensor gconv_fwd(Tensor x, Tensor w, std::vector<int64_t> stride, std::vector<int64_t> pad,
                  int64_t groups, optional<Tensor> bias, int64_t act) {
-  check_bf16(x, "x");
-  check_bf16(w, "w");
+  check_act(x, "x");
+  check_same(w, x, "w");
   c10::DeviceGuard g(x.device());
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "gconv expects NHWC x and [Co,KH,KW,Ci/groups] w");
   auto s = gconv_shape(x.size(0), x.size(1), x.size(2), x.size(3), w.size(0), w.size(1),
@@ -953,17 +954,19 @@ Tensor gconv_fwd(Tensor x, Tensor w, std::vector<int64_t> stride, std::vector<in
   const float* bp = bias.has_value() ? bias->data_ptr<float>() : nullptr;
   if (dw_vec8(s)) {
     auto wt = dw_taps_major(w);
-    mipipe::dwconv_fwd(x.data_ptr(), wt.data_ptr(), bp, y.data_ptr(), s, (int)act, stream());
+    mipipe::dwconv_fwd(x.data_ptr(), wt.data_ptr(), bp, y.data_ptr(), s, (int)act,
+                       stream(), is_f32(x));
   } else {
-    mipipe::gconv_fwd(x.data_ptr(), w.data_ptr(), bp, y.data_ptr(), s, (int)act, stream());
+    mipipe::gconv_fwd(x.data_ptr(), w.data_ptr(), bp, y.data_ptr(), s, (int)act,
+                      stream(), is_f32(x));
   }
   return y;
 }
 
 Tensor gconv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, std::vector<int64_t> stride,
                    std::vector<int64_t> pad, int64_t groups, optional<Tensor> z, int64_t act) {
-  check_bf16(dy, "dy");
-  check_bf16(w, "w");
+  check_act(dy, "dy");
+  check_same(w, dy, "w");
   c10::DeviceGuard g(dy.device());
   TORCH_CHECK(x_shape.size() == 4 && w.dim() == 4, "x_shape must be [N,H,W,Ci]");
   auto s = gconv_shape(x_shape[0], x_shape[1], x_shape[2], x_shape[3], w.size(0), w.size(1),
@@ -975,9 +978,11 @@ Tensor gconv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, std::vecto
   auto dx = torch::empty({s.N, s.H, s.W, s.Ci}, dy.options());
   if (dw_vec8(s)) {
     auto wt = dw_taps_major(w);
-    mipipe::dwconv_dgrad(dy.data_ptr(), wt.data_ptr(), zp, dx.data_ptr(), s, (int)act, stream());
+    mipipe::dwconv_dgrad(dy.data_ptr(), wt.data_ptr(), zp, dx.data_ptr(), s, (int)act,
+                         stream(), is_f32(dy));
   } else {
-    mipipe::gconv_dgrad(dy.data_ptr(), w.data_ptr(), zp, dx.data_ptr(), s, (int)act, stream());
+    mipipe::gconv_dgrad(dy.data_ptr(), w.data_ptr(), zp, dx.data_ptr(), s, (int)act,
+                        stream(), is_f32(dy));
   }
   return dx;
 }
@@ -988,8 +993,8 @@ std::tuple<Tensor, optional<Tensor>> gconv_wgrad(Tensor dy, Tensor x, int64_t kh
                                                  optional<Tensor> z, int64_t act,
                                                  optional<Tensor> out, optional<Tensor> dbias,
                                                  bool want_bias) {
-  check_bf16(dy, "dy");
-  check_bf16(x, "x");
+  check_act(dy, "dy");
+  check_same(x, dy, "x");
   c10::DeviceGuard g(dy.device());
   TORCH_CHECK(x.dim() == 4 && dy.dim() == 4, "NHWC tensors expected");
   const int64_t Co = dy.size(3), Ci = x.size(3);
@@ -1019,28 +1024,28 @@ std::tuple<Tensor, optional<Tensor>> gconv_wgrad(Tensor dy, Tensor x, int64_t kh
   float* dbp = db.has_value() ? db->data_ptr<float>() : nullptr;
   if (dw_vec8(s))
     mipipe::dwconv_wgrad(dy.data_ptr(), x.data_ptr(), zp, dw.data_ptr<float>(), dbp, s, (int)act,
-                         stream());
+                         stream(), is_f32(dy));
   else
     mipipe::gconv_wgrad(dy.data_ptr(), x.data_ptr(), zp, dw.data_ptr<float>(), dbp, s, (int)act,
-                        stream());
+                        stream(), is_f32(dy));
   return {dw, db};
 }
 
 // shifted per-channel sums (one zeroed [2, C] allocation; rows returned as [1, C] views)
 std::tuple<Tensor, Tensor> chan_stats(Tensor y, Tensor shift) {
-  check_bf16(y, "y");
+  check_act(y, "y");
   c10::DeviceGuard g(y.device());
   int64_t C = y.size(-1), M = y.numel() / C;
   check_vec(shift, C, "shift");
   auto st = torch::zeros({2, C}, y.options().dtype(at::kFloat));
   auto ps = st.narrow(0, 0, 1), pq = st.narrow(0, 1, 1);
   mipipe::chan_stats(y.data_ptr(), shift.data_ptr<float>(), M, (int)C, ps.data_ptr<float>(),
-                     pq.data_ptr<float>(), stream());
+                     pq.data_ptr<float>(), stream(), is_f32(y));
   return {ps, pq};
 }
 
 Tensor affine_act(Tensor y, Tensor scale, Tensor bias, int64_t act) {
-  check_bf16(y, "y");
+  check_act(y, "y");
   c10::DeviceGuard g(y.device());
   int64_t C = y.size(-1), M = y.numel() / C;
   check_vec(scale, C, "scale");
@@ -1048,14 +1053,14 @@ Tensor affine_act(Tensor y, Tensor scale, Tensor bias, int64_t act) {
   TORCH_CHECK(act >= 0 && act <= 2, "bad act");
   auto z = torch::empty_like(y);
   mipipe::affine_act(y.data_ptr(), scale.data_ptr<float>(), bias.data_ptr<float>(), z.data_ptr(),
-                     M, (int)C, (int)act, stream());
+                     M, (int)C, (int)act, stream(), is_f32(y));
   return z;
 }
 
 std::tuple<Tensor, Tensor> bn_generic_bwd_reduce(Tensor dz, optional<Tensor> z, Tensor y,
                                                  Tensor mean, Tensor invstd, int64_t act) {
-  check_bf16(dz, "dz");
-  check_bf16(y, "y");
+  check_act(y, "y");
+  check_same(dz, y, "dz");
   c10::DeviceGuard g(y.device());
   int64_t C = y.size(-1), M = y.numel() / C;
   TORCH_CHECK(dz.sizes() == y.sizes(), "dz / y shape mismatch");
@@ -1067,15 +1072,15 @@ std::tuple<Tensor, Tensor> bn_generic_bwd_reduce(Tensor dz, optional<Tensor> z, 
   auto sg = st[0], sgx = st[1];
   mipipe::bn_generic_bwd_reduce(dz.data_ptr(), zp, y.data_ptr(), mean.data_ptr<float>(),
                                 invstd.data_ptr<float>(), M, (int)C, (int)act,
-                                sg.data_ptr<float>(), sgx.data_ptr<float>(), stream());
+                                sg.data_ptr<float>(), sgx.data_ptr<float>(), stream(), is_f32(y));
   return {sg, sgx};
 }
 
 Tensor bn_generic_bwd_apply(Tensor dz, optional<Tensor> z, Tensor y, Tensor mean, Tensor invstd,
                             Tensor gamma, optional<Tensor> sum_g, optional<Tensor> sum_gx,
                             int64_t count, int64_t act) {
-  check_bf16(dz, "dz");
-  check_bf16(y, "y");
+  check_act(y, "y");
+  check_same(dz, y, "dz");
   c10::DeviceGuard g(y.device());
   int64_t C = y.size(-1), M = y.numel() / C;
   TORCH_CHECK(dz.sizes() == y.sizes(), "dz / y shape mismatch");
@@ -1093,12 +1098,12 @@ Tensor bn_generic_bwd_apply(Tensor dz, optional<Tensor> z, Tensor y, Tensor mean
                                invstd.data_ptr<float>(), gamma.data_ptr<float>(),
                                sum_g.has_value() ? sum_g->data_ptr<float>() : nullptr,
                                sum_gx.has_value() ? sum_gx->data_ptr<float>() : nullptr, count, M,
-                               (int)C, (int)act, dy.data_ptr(), stream());
+                               (int)C, (int)act, dy.data_ptr(), stream(), is_f32(y));
   return dy;
 }
 
 Tensor avgpool2d_fwd(Tensor x, int64_t k, int64_t s, int64_t p) {
-  check_bf16(x, "x");
+  check_act(x, "x");
   c10::DeviceGuard g(x.device());
   TORCH_CHECK(x.dim() == 4, "x must be NHWC");
   TORCH_CHECK(k >= 1 && s >= 1 && p >= 0 && 2 * p <= k, "bad avgpool geometry");
@@ -1107,12 +1112,12 @@ Tensor avgpool2d_fwd(Tensor x, int64_t k, int64_t s, int64_t p) {
   TORCH_CHECK(Ho > 0 && Wo > 0, "empty avgpool output");
   auto y = torch::empty({N, Ho, Wo, C}, x.options());
   mipipe::avgpool2d_fwd(x.data_ptr(), y.data_ptr(), N, H, W, C, Ho, Wo, (int)k, (int)s, (int)p,
-                        stream());
+                        stream(), is_f32(x));
   return y;
 }
 
 Tensor avgpool2d_bwd(Tensor dy, std::vector<int64_t> xs, int64_t k, int64_t s, int64_t p) {
-  check_bf16(dy, "dy");
+  check_act(dy, "dy");
   c10::DeviceGuard g(dy.device());
   TORCH_CHECK(xs.size() == 4 && dy.dim() == 4, "NHWC shapes expected");
   TORCH_CHECK(k >= 1 && s >= 1 && p >= 0 && 2 * p <= k, "bad avgpool geometry");
@@ -1122,7 +1127,7 @@ Tensor avgpool2d_bwd(Tensor dy, std::vector<int64_t> xs, int64_t k, int64_t s, i
               "avgpool2d_bwd shape mismatch");
   auto dx = torch::empty({N, H, W, C}, dy.options());
   mipipe::avgpool2d_bwd(dy.data_ptr(), dx.data_ptr(), N, H, W, C, Ho, Wo, (int)k, (int)s, (int)p,
-                        stream());
+                        stream(), is_f32(dy));
   return dx;
 }
 

@@ -41,6 +41,12 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
+// scalar element <-> fp32 for kernels templated on the activation dtype
+__device__ __forceinline__ float to_f32(__bf16 v) { return (float)v; }
+__device__ __forceinline__ float to_f32(float v) { return v; }
+template <class T>
+__device__ __forceinline__ T from_f32(float v) { return (T)v; }
+
 // 8-channel vector I/O for both activation dtypes: bf16 = one 16-B access, fp32 = two.  Kernels
 // templated on the element type T (bf16 mixed precision / fp32 reference precision) use these.
 __device__ __forceinline__ void load8(const __bf16* p, float* f) {

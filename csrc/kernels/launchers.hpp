@@ -79,40 +79,41 @@ int conv_wgrad_splits(const ConvShape& s, int cfg);
 struct GConvShape {
   int N, H, W, Ci, Co, KH, KW, sh, sw, ph, pw, groups, Ho, Wo;
 };
-// act: 0 none, 1 relu, 2 relu6.  Weights [Co][KH][KW][Ci/groups].
+// act: 0 none, 1 relu, 2 relu6.  Weights [Co][KH][KW][Ci/groups].  f32: activations and
+// weights are fp32 (the reference's precision) instead of bf16.
 void gconv_fwd(const void* x, const void* w, const float* bias, void* y, const GConvShape& s,
-               int act, hipStream_t st);
+               int act, hipStream_t st, bool f32 = false);
 // z (optional): the forward OUTPUT of a fused activation; dy is masked by act'(z)
 void gconv_dgrad(const void* dy, const void* w, const void* z, void* dx, const GConvShape& s,
-                 int act, hipStream_t st);
+                 int act, hipStream_t st, bool f32 = false);
 // dw [Co][KH][KW][Ci/groups] and dbias [Co] (optional) are ACCUMULATED into (fp32 atomics)
 void gconv_wgrad(const void* dy, const void* x, const void* z, float* dw, float* dbias,
-                 const GConvShape& s, int act, hipStream_t st);
+                 const GConvShape& s, int act, hipStream_t st, bool f32 = false);
 // depthwise (groups == Ci == Co, C % 8 == 0, C <= 2048): taps-major weights wt [KH*KW][C];
 // dw stays in the parameter layout [C][KH][KW]
 void dwconv_fwd(const void* x, const void* wt, const float* bias, void* y, const GConvShape& s,
-                int act, hipStream_t st);
+                int act, hipStream_t st, bool f32 = false);
 void dwconv_dgrad(const void* dy, const void* wt, const void* z, void* dx, const GConvShape& s,
-                  int act, hipStream_t st);
+                  int act, hipStream_t st, bool f32 = false);
 void dwconv_wgrad(const void* dy, const void* x, const void* z, float* dw, float* dbias,
-                  const GConvShape& s, int act, hipStream_t st);
+                  const GConvShape& s, int act, hipStream_t st, bool f32 = false);
 // psum/psq: zeroed [C] accumulators of Σ(y - shift), Σ(y - shift)²
 void chan_stats(const void* y, const float* shift, long M, int C, float* psum, float* psq,
-                hipStream_t st);
+                hipStream_t st, bool f32 = false);
 void affine_act(const void* y, const float* scale, const float* bias, void* z, long M, int C,
-                int act, hipStream_t st);
+                int act, hipStream_t st, bool f32 = false);
 // out_g / out_gx: zeroed [C] accumulators
 void bn_generic_bwd_reduce(const void* dz, const void* z, const void* y, const float* mean,
                            const float* invstd, long M, int C, int act, float* out_g,
-                           float* out_gx, hipStream_t st);
+                           float* out_gx, hipStream_t st, bool f32 = false);
 void bn_generic_bwd_apply(const void* dz, const void* z, const void* y, const float* mean,
                           const float* invstd, const float* gamma, const float* sum_g,
                           const float* sum_gx, long count, long M, int C, int act, void* dy,
-                          hipStream_t st);
+                          hipStream_t st, bool f32 = false);
 void avgpool2d_fwd(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo, int k,
-                   int stride, int pad, hipStream_t st);
+                   int stride, int pad, hipStream_t st, bool f32 = false);
 void avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho, int Wo, int k,
-                   int stride, int pad, hipStream_t st);
+                   int stride, int pad, hipStream_t st, bool f32 = false);
 
 // ---- dense GEMM: C[M][N] = op(A) op(B) --------------------------------------------------------
 //  a_kc: A stored [M][K] (else [K][M]);  b_kc: B stored [N][K] (else [K][N]).

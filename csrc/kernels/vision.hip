@@ -40,9 +40,10 @@ static int grid_for(long work, int per_block = 256, int cap = 8192) {
 // ------------------------------------------------------------------------ grouped conv fwd
 // One thread per output element, co fastest: a wave stores 64 consecutive channels of one
 // pixel; the group's input channels are read as a contiguous run.
+template <class T>
 __global__ __launch_bounds__(256) void gconv_fwd_kernel(
-    const __bf16* __restrict__ x, const __bf16* __restrict__ w, const float* __restrict__ bias,
-    __bf16* __restrict__ y, GConvShape s, int act) {
+    const T* __restrict__ x, const T* __restrict__ w, const float* __restrict__ bias,
+    T* __restrict__ y, GConvShape s, int act) {
   const int Cig = s.Ci / s.groups, Cog = s.Co / s.groups;
   const long total = (long)s.N * s.Ho * s.Wo * s.Co;
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
@@ -61,12 +62,12 @@ __global__ __launch_bounds__(256) void gconv_fwd_kernel(
       for (int kw = 0; kw < s.KW; ++kw) {
         const int wi = wo * s.sw - s.pw + kw;
         if (wi < 0 || wi >= s.W) continue;
-        const __bf16* xp = x + (((long)n * s.H + hi) * s.W + wi) * s.Ci + ci0;
-        const __bf16* wp = w + (((long)co * s.KH + kh) * s.KW + kw) * Cig;
-        for (int c = 0; c < Cig; ++c) acc += bf2f(xp[c]) * bf2f(wp[c]);
+        const T* xp = x + (((long)n * s.H + hi) * s.W + wi) * s.Ci + ci0;
+        const T* wp = w + (((long)co * s.KH + kh) * s.KW + kw) * Cig;
+        for (int c = 0; c < Cig; ++c) acc += to_f32(xp[c]) * to_f32(wp[c]);
       }
     }
-    y[t] = f2bf(act_apply(acc, act));
+    y[t] = from_f32<T>(act_apply(acc, act));
   }
 }
 
@@ -74,9 +75,10 @@ __global__ __launch_bounds__(256) void gconv_fwd_kernel(
 // dx[n,hi,wi,ci] = sum over taps and the group's output channels; a gather (no atomics).
 // ``z`` (optional): the conv's OUTPUT when an activation was fused in forward: dy is masked by
 // act'(z) on the fly (the masked gradient is never materialised).
+template <class T>
 __global__ __launch_bounds__(256) void gconv_dgrad_kernel(
-    const __bf16* __restrict__ dy, const __bf16* __restrict__ w, const __bf16* __restrict__ z,
-    __bf16* __restrict__ dx, GConvShape s, int act) {
+    const T* __restrict__ dy, const T* __restrict__ w, const T* __restrict__ z,
+    T* __restrict__ dx, GConvShape s, int act) {
   const int Cig = s.Ci / s.groups, Cog = s.Co / s.groups;
   const long total = (long)s.N * s.H * s.W * s.Ci;
   const long wstride = (long)s.KH * s.KW * Cig;
@@ -101,15 +103,15 @@ __global__ __launch_bounds__(256) void gconv_dgrad_kernel(
         const int wo = wn / s.sw;
         if (wo >= s.Wo) continue;
         const long o = (((long)n * s.Ho + ho) * s.Wo + wo) * s.Co + co0;
-        const __bf16* wp = w + (((long)co0 * s.KH + kh) * s.KW + kw) * Cig + cil;
+        const T* wp = w + (((long)co0 * s.KH + kh) * s.KW + kw) * Cig + cil;
         for (int j = 0; j < Cog; ++j) {
-          float gv = bf2f(dy[o + j]);
-          if (z != nullptr && !act_pass(bf2f(z[o + j]), act)) gv = 0.f;
-          acc += gv * bf2f(wp[j * wstride]);
+          float gv = to_f32(dy[o + j]);
+          if (z != nullptr && !act_pass(to_f32(z[o + j]), act)) gv = 0.f;
+          acc += gv * to_f32(wp[j * wstride]);
         }
       }
     }
-    dx[t] = f2bf(acc);
+    dx[t] = from_f32<T>(acc);
   }
 }
 
@@ -119,8 +121,9 @@ __global__ __launch_bounds__(256) void gconv_dgrad_kernel(
 // blockIdx.y splits the (n, ho) rows and the partial sums land in dw with fp32 atomics
 // (dw = zeroed buffer, or the parameter's slice of the flat gradient bucket).  Optional act/z
 // mask as in dgrad; optional dbias (Σ masked dy per co, accumulated by the tap-0 threads).
+template <class T>
 __global__ __launch_bounds__(256) void gconv_wgrad_kernel(
-    const __bf16* __restrict__ dy, const __bf16* __restrict__ x, const __bf16* __restrict__ z,
+    const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ z,
     float* __restrict__ dw, float* __restrict__ dbias, GConvShape s, int act, int rows_per) {
   const int Cig = s.Ci / s.groups, Cog = s.Co / s.groups;
   const long nW = (long)s.Co * Cig;  // per tap
@@ -141,15 +144,15 @@ __global__ __launch_bounds__(256) void gconv_wgrad_kernel(
     const int hi = ho * s.sh - s.ph + kh;
     const bool hok = hi >= 0 && hi < s.H;
     if (!hok && !do_bias) continue;
-    const __bf16* dyr = dy + r * s.Wo * s.Co + co;
-    const __bf16* zr = z ? z + r * s.Wo * s.Co + co : nullptr;
-    const __bf16* xr = x + ((long)n * s.H + (hok ? hi : 0)) * s.W * s.Ci + ci;
+    const T* dyr = dy + r * s.Wo * s.Co + co;
+    const T* zr = z ? z + r * s.Wo * s.Co + co : nullptr;
+    const T* xr = x + ((long)n * s.H + (hok ? hi : 0)) * s.W * s.Ci + ci;
     for (int wo = 0; wo < s.Wo; ++wo) {
-      float gv = bf2f(dyr[(long)wo * s.Co]);
-      if (zr != nullptr && !act_pass(bf2f(zr[(long)wo * s.Co]), act)) gv = 0.f;
+      float gv = to_f32(dyr[(long)wo * s.Co]);
+      if (zr != nullptr && !act_pass(to_f32(zr[(long)wo * s.Co]), act)) gv = 0.f;
       accb += gv;
       const int wi = wo * s.sw - s.pw + kw;
-      if (hok && wi >= 0 && wi < s.W) acc += gv * bf2f(xr[(long)wi * s.Ci]);
+      if (hok && wi >= 0 && wi < s.W) acc += gv * to_f32(xr[(long)wi * s.Ci]);
     }
   }
   atomicAdd(dw + (((long)co * s.KH + kh) * s.KW + kw) * Cig + cil, acc);
@@ -157,7 +160,8 @@ __global__ __launch_bounds__(256) void gconv_wgrad_kernel(
 }
 
 // ------------------------------------------------------------------------ depthwise, C % 8 == 0
-__device__ __forceinline__ void mask8(const __bf16* z, int act, float* g) {
+template <class T>
+__device__ __forceinline__ void mask8(const T* z, int act, float* g) {
   float zv[8];
   load8(z, zv);
 #pragma unroll
@@ -167,9 +171,10 @@ __device__ __forceinline__ void mask8(const __bf16* z, int act, float* g) {
 
 // 8 channels of one output pixel per thread: per tap one 16-B activation load and one 16-B
 // weight load (taps-major weights), 8 FMAs.
+template <class T>
 __global__ __launch_bounds__(256) void dwconv_fwd_v8_kernel(
-    const __bf16* __restrict__ x, const __bf16* __restrict__ wt, const float* __restrict__ bias,
-    __bf16* __restrict__ y, GConvShape s, int act) {
+    const T* __restrict__ x, const T* __restrict__ wt, const float* __restrict__ bias,
+    T* __restrict__ y, GConvShape s, int act) {
   const int C = s.Co, cg = C / 8;
   const long total = (long)s.N * s.Ho * s.Wo * cg;
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
@@ -198,13 +203,14 @@ __global__ __launch_bounds__(256) void dwconv_fwd_v8_kernel(
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] = act_apply(acc[q], act);
-    *reinterpret_cast<uint4*>(y + pix * C + c8 * 8) = pack8(acc);
+    store8(y + pix * C + c8 * 8, acc);
   }
 }
 
+template <class T>
 __global__ __launch_bounds__(256) void dwconv_dgrad_v8_kernel(
-    const __bf16* __restrict__ dy, const __bf16* __restrict__ wt, const __bf16* __restrict__ z,
-    __bf16* __restrict__ dx, GConvShape s, int act) {
+    const T* __restrict__ dy, const T* __restrict__ wt, const T* __restrict__ z,
+    T* __restrict__ dx, GConvShape s, int act) {
   const int C = s.Ci, cg = C / 8;
   const long total = (long)s.N * s.H * s.W * cg;
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
@@ -235,7 +241,7 @@ __global__ __launch_bounds__(256) void dwconv_dgrad_v8_kernel(
         for (int q = 0; q < 8; ++q) acc[q] += g[q] * wv[q];
       }
     }
-    *reinterpret_cast<uint4*>(dx + pix * C + c8 * 8) = pack8(acc);
+    store8(dx + pix * C + c8 * 8, acc);
   }
 }
 
@@ -243,8 +249,9 @@ __global__ __launch_bounds__(256) void dwconv_dgrad_v8_kernel(
 // positions of blockIdx.y's (n, ho) row range are strided over the lanes.  Per-block partials
 // are reduced through LDS, then one fp32 atomic per weight element per block lands in dw
 // ([C][KH][KW], the parameter layout).  blockIdx.z = tap; tap-0 blocks also reduce dbias.
+template <class T>
 __global__ __launch_bounds__(256) void dwconv_wgrad_v8_kernel(
-    const __bf16* __restrict__ dy, const __bf16* __restrict__ x, const __bf16* __restrict__ z,
+    const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ z,
     float* __restrict__ dw, float* __restrict__ dbias, GConvShape s, int act, int rows_per) {
   __shared__ float red[256 * 9];  // stride 9: conflict-free column reads
   const int C = s.Co, cg = C / 8;
@@ -309,69 +316,100 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_v8_kernel(
 }
 
 void gconv_fwd(const void* x, const void* w, const float* bias, void* y, const GConvShape& s,
-               int act, hipStream_t st) {
-  long work = (long)s.N * s.Ho * s.Wo * s.Co;
-  hipLaunchKernelGGL(gconv_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, st, (const __bf16*)x,
-                     (const __bf16*)w, bias, (__bf16*)y, s, act);
+               int act, hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    long work = (long)s.N * s.Ho * s.Wo * s.Co;
+    hipLaunchKernelGGL((gconv_fwd_kernel<T>), dim3(grid_for(work)), dim3(256), 0, st, (const T*)x,
+                       (const T*)w, bias, (T*)y, s, act);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 void gconv_dgrad(const void* dy, const void* w, const void* z, void* dx, const GConvShape& s,
-                 int act, hipStream_t st) {
-  long work = (long)s.N * s.H * s.W * s.Ci;
-  hipLaunchKernelGGL(gconv_dgrad_kernel, dim3(grid_for(work)), dim3(256), 0, st,
-                     (const __bf16*)dy, (const __bf16*)w, (const __bf16*)z, (__bf16*)dx, s, act);
+                 int act, hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    long work = (long)s.N * s.H * s.W * s.Ci;
+    hipLaunchKernelGGL((gconv_dgrad_kernel<T>), dim3(grid_for(work)), dim3(256), 0, st,
+                       (const T*)dy, (const T*)w, (const T*)z, (T*)dx, s, act);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 void gconv_wgrad(const void* dy, const void* x, const void* z, float* dw, float* dbias,
-                 const GConvShape& s, int act, hipStream_t st) {
-  const long nW = (long)s.Co * (s.Ci / s.groups);
-  const int bx = (int)((nW + 255) / 256);
-  const int taps = s.KH * s.KW;
-  const long R = (long)s.N * s.Ho;
-  // ~2048 workgroups in total, every split at least 4 rows of (n, ho)
-  long splits = std::max<long>(1, 2048 / std::max<long>(1, (long)bx * taps));
-  splits = std::min<long>(splits, std::max<long>(1, R / 4));
-  splits = std::min<long>(splits, 65535);
-  const int rows_per = (int)((R + splits - 1) / splits);
-  const int by = (int)((R + rows_per - 1) / rows_per);
-  hipLaunchKernelGGL(gconv_wgrad_kernel, dim3(bx, by, taps), dim3(256), 0, st, (const __bf16*)dy,
-                     (const __bf16*)x, (const __bf16*)z, dw, dbias, s, act, rows_per);
+                 const GConvShape& s, int act, hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    const long nW = (long)s.Co * (s.Ci / s.groups);
+    const int bx = (int)((nW + 255) / 256);
+    const int taps = s.KH * s.KW;
+    const long R = (long)s.N * s.Ho;
+    // ~2048 workgroups in total, every split at least 4 rows of (n, ho)
+    long splits = std::max<long>(1, 2048 / std::max<long>(1, (long)bx * taps));
+    splits = std::min<long>(splits, std::max<long>(1, R / 4));
+    splits = std::min<long>(splits, 65535);
+    const int rows_per = (int)((R + splits - 1) / splits);
+    const int by = (int)((R + rows_per - 1) / rows_per);
+    hipLaunchKernelGGL((gconv_wgrad_kernel<T>), dim3(bx, by, taps), dim3(256), 0, st, (const T*)dy,
+                       (const T*)x, (const T*)z, dw, dbias, s, act, rows_per);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 void dwconv_fwd(const void* x, const void* wt, const float* bias, void* y, const GConvShape& s,
-                int act, hipStream_t st) {
-  long work = (long)s.N * s.Ho * s.Wo * (s.Co / 8);
-  hipLaunchKernelGGL(dwconv_fwd_v8_kernel, dim3(grid_for(work)), dim3(256), 0, st,
-                     (const __bf16*)x, (const __bf16*)wt, bias, (__bf16*)y, s, act);
+                int act, hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    long work = (long)s.N * s.Ho * s.Wo * (s.Co / 8);
+    hipLaunchKernelGGL((dwconv_fwd_v8_kernel<T>), dim3(grid_for(work)), dim3(256), 0, st,
+                       (const T*)x, (const T*)wt, bias, (T*)y, s, act);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 void dwconv_dgrad(const void* dy, const void* wt, const void* z, void* dx, const GConvShape& s,
-                  int act, hipStream_t st) {
-  long work = (long)s.N * s.H * s.W * (s.Ci / 8);
-  hipLaunchKernelGGL(dwconv_dgrad_v8_kernel, dim3(grid_for(work)), dim3(256), 0, st,
-                     (const __bf16*)dy, (const __bf16*)wt, (const __bf16*)z, (__bf16*)dx, s, act);
+                  int act, hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    long work = (long)s.N * s.H * s.W * (s.Ci / 8);
+    hipLaunchKernelGGL((dwconv_dgrad_v8_kernel<T>), dim3(grid_for(work)), dim3(256), 0, st,
+                       (const T*)dy, (const T*)wt, (const T*)z, (T*)dx, s, act);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 void dwconv_wgrad(const void* dy, const void* x, const void* z, float* dw, float* dbias,
-                  const GConvShape& s, int act, hipStream_t st) {
-  const int cg = s.Co / 8, lanes = 256 / cg, taps = s.KH * s.KW;
-  const long P = (long)s.N * s.Ho * s.Wo;
-  const long R = (long)s.N * s.Ho;
-  // ~2048 workgroups, each lane covering >= 32 output positions
-  long splits = std::max<long>(1, 2048 / taps);
-  splits = std::min<long>(splits, std::max<long>(1, P / ((long)lanes * 32)));
-  splits = std::min<long>(splits, std::min<long>(R, 65535));
-  const int rows_per = (int)((R + splits - 1) / splits);
-  const int by = (int)((R + rows_per - 1) / rows_per);
-  hipLaunchKernelGGL(dwconv_wgrad_v8_kernel, dim3(1, by, taps), dim3(256), 0, st,
-                     (const __bf16*)dy, (const __bf16*)x, (const __bf16*)z, dw, dbias, s, act,
-                     rows_per);
+                  const GConvShape& s, int act, hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    const int cg = s.Co / 8, lanes = 256 / cg, taps = s.KH * s.KW;
+    const long P = (long)s.N * s.Ho * s.Wo;
+    const long R = (long)s.N * s.Ho;
+    // ~2048 workgroups, each lane covering >= 32 output positions
+    long splits = std::max<long>(1, 2048 / taps);
+    splits = std::min<long>(splits, std::max<long>(1, P / ((long)lanes * 32)));
+    splits = std::min<long>(splits, std::min<long>(R, 65535));
+    const int rows_per = (int)((R + splits - 1) / splits);
+    const int by = (int)((R + rows_per - 1) / rows_per);
+    hipLaunchKernelGGL((dwconv_wgrad_v8_kernel<T>), dim3(1, by, taps), dim3(256), 0, st,
+                       (const T*)dy, (const T*)x, (const T*)z, dw, dbias, s, act,
+                       rows_per);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 // ------------------------------------------------------------------------ BatchNorm, any C
 // Block = 64 channels (one per lane) x 4 waves over rows; per-block partials reduced in LDS
 // and added to the [C] outputs with one atomic per channel per block.
-__global__ __launch_bounds__(256) void chan_stats_kernel(const __bf16* __restrict__ y,
+template <class T>
+__global__ __launch_bounds__(256) void chan_stats_kernel(const T* __restrict__ y,
                                                          const float* __restrict__ shift, long M,
                                                          int C, float* __restrict__ psum,
                                                          float* __restrict__ psq) {
@@ -382,7 +420,7 @@ __global__ __launch_bounds__(256) void chan_stats_kernel(const __bf16* __restric
   if (c < C) {
     const float sf = shift[c];
     for (long r = (long)blockIdx.y * 4 + ty; r < M; r += (long)gridDim.y * 4) {
-      float d = bf2f(y[r * C + c]) - sf;
+      float d = to_f32(y[r * C + c]) - sf;
       s += d;
       q += d * d;
     }
@@ -398,21 +436,23 @@ __global__ __launch_bounds__(256) void chan_stats_kernel(const __bf16* __restric
   }
 }
 
-__global__ __launch_bounds__(256) void affine_act_kernel(const __bf16* __restrict__ y,
+template <class T>
+__global__ __launch_bounds__(256) void affine_act_kernel(const T* __restrict__ y,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ bias,
-                                                         __bf16* __restrict__ z, long n, int C,
+                                                         T* __restrict__ z, long n, int C,
                                                          int act) {
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < n;
        t += (long)gridDim.x * blockDim.x) {
     const int c = (int)(t % C);
-    z[t] = f2bf(act_apply(bf2f(y[t]) * scale[c] + bias[c], act));
+    z[t] = from_f32<T>(act_apply(to_f32(y[t]) * scale[c] + bias[c], act));
   }
 }
 
 // Σg and Σg·x̂ with g = dz·act'(z), x̂ = (y - mean)·invstd
+template <class T>
 __global__ __launch_bounds__(256) void bn_generic_bwd_reduce_kernel(
-    const __bf16* __restrict__ dz, const __bf16* __restrict__ z, const __bf16* __restrict__ y,
+    const T* __restrict__ dz, const T* __restrict__ z, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, long M, int C, int act,
     float* __restrict__ out_g, float* __restrict__ out_gx) {
   __shared__ float sh_g[4][64], sh_x[4][64];
@@ -423,10 +463,10 @@ __global__ __launch_bounds__(256) void bn_generic_bwd_reduce_kernel(
     const float mu = mean[c], is = invstd[c];
     for (long r = (long)blockIdx.y * 4 + ty; r < M; r += (long)gridDim.y * 4) {
       const long i = r * C + c;
-      float g = bf2f(dz[i]);
-      if (act != 0 && !act_pass(bf2f(z[i]), act)) g = 0.f;
+      float g = to_f32(dz[i]);
+      if (act != 0 && !act_pass(to_f32(z[i]), act)) g = 0.f;
       sg += g;
-      sgx += g * (bf2f(y[i]) - mu) * is;
+      sgx += g * (to_f32(y[i]) - mu) * is;
     }
   }
   sh_g[ty][threadIdx.x] = sg;
@@ -441,24 +481,25 @@ __global__ __launch_bounds__(256) void bn_generic_bwd_reduce_kernel(
 }
 
 // dy = γ·invstd·(g - Σg/count - x̂·Σg·x̂/count); sum_g == nullptr: eval-mode BN, dy = γ·invstd·g
+template <class T>
 __global__ __launch_bounds__(256) void bn_generic_bwd_apply_kernel(
-    const __bf16* __restrict__ dz, const __bf16* __restrict__ z, const __bf16* __restrict__ y,
+    const T* __restrict__ dz, const T* __restrict__ z, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, const float* __restrict__ sum_g,
     const float* __restrict__ sum_gx, float inv_count, long n, int C, int act,
-    __bf16* __restrict__ dy) {
+    T* __restrict__ dy) {
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < n;
        t += (long)gridDim.x * blockDim.x) {
     const int c = (int)(t % C);
-    float g = bf2f(dz[t]);
-    if (act != 0 && !act_pass(bf2f(z[t]), act)) g = 0.f;
+    float g = to_f32(dz[t]);
+    if (act != 0 && !act_pass(to_f32(z[t]), act)) g = 0.f;
     const float is = invstd[c];
     float v = g;
     if (sum_g != nullptr) {
-      const float xh = (bf2f(y[t]) - mean[c]) * is;
+      const float xh = (to_f32(y[t]) - mean[c]) * is;
       v = g - sum_g[c] * inv_count - xh * sum_gx[c] * inv_count;
     }
-    dy[t] = f2bf(gamma[c] * is * v);
+    dy[t] = from_f32<T>(gamma[c] * is * v);
   }
 }
 
@@ -483,7 +524,8 @@ __device__ __forceinline__ void lds_reduce_atomic8(float* sh, const float* v, in
   __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void chan_stats_v8_kernel(const __bf16* __restrict__ y,
+template <class T>
+__global__ __launch_bounds__(256) void chan_stats_v8_kernel(const T* __restrict__ y,
                                                             const float* __restrict__ shift,
                                                             long M, int C,
                                                             float* __restrict__ psum,
@@ -512,10 +554,11 @@ __global__ __launch_bounds__(256) void chan_stats_v8_kernel(const __bf16* __rest
   lds_reduce_atomic8(sh, q, tpr, rpb, psq);
 }
 
-__global__ __launch_bounds__(256) void affine_act_v8_kernel(const __bf16* __restrict__ y,
+template <class T>
+__global__ __launch_bounds__(256) void affine_act_v8_kernel(const T* __restrict__ y,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ bias,
-                                                            __bf16* __restrict__ z, long M, int C,
+                                                            T* __restrict__ z, long M, int C,
                                                             int act) {
   const int tpr = C / 8, rpb = 256 / tpr;
   const int t = threadIdx.x, cg = t % tpr, rg = t / tpr;
@@ -532,12 +575,13 @@ __global__ __launch_bounds__(256) void affine_act_v8_kernel(const __bf16* __rest
     load8(y + off, v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = act_apply(v[k] * sc[k] + bi[k], act);
-    *reinterpret_cast<uint4*>(z + off) = pack8(v);
+    store8(z + off, v);
   }
 }
 
+template <class T>
 __global__ __launch_bounds__(256) void bn_generic_bwd_reduce_v8_kernel(
-    const __bf16* __restrict__ dz, const __bf16* __restrict__ z, const __bf16* __restrict__ y,
+    const T* __restrict__ dz, const T* __restrict__ z, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, long M, int C, int act,
     float* __restrict__ out_g, float* __restrict__ out_gx) {
   __shared__ float sh[256 * 9];
@@ -570,12 +614,13 @@ __global__ __launch_bounds__(256) void bn_generic_bwd_reduce_v8_kernel(
 }
 
 // dy = A·g + B + Cc·(y - mean) with A = γ·invstd, B = -A·Σg/n, Cc = -A·invstd·Σg·x̂/n
+template <class T>
 __global__ __launch_bounds__(256) void bn_generic_bwd_apply_v8_kernel(
-    const __bf16* __restrict__ dz, const __bf16* __restrict__ z, const __bf16* __restrict__ y,
+    const T* __restrict__ dz, const T* __restrict__ z, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, const float* __restrict__ sum_g,
     const float* __restrict__ sum_gx, float inv_count, long M, int C, int act,
-    __bf16* __restrict__ dy) {
+    T* __restrict__ dy) {
   const int tpr = C / 8, rpb = 256 / tpr;
   const int t = threadIdx.x, cg = t % tpr, rg = t / tpr;
   if (rg >= rpb) return;
@@ -596,7 +641,7 @@ __global__ __launch_bounds__(256) void bn_generic_bwd_apply_v8_kernel(
     load8(y + off, v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) g[k] = A[k] * g[k] + B[k] + Cc[k] * (v[k] - mu[k]);
-    *reinterpret_cast<uint4*>(dy + off) = pack8(g);
+    store8(dy + off, g);
   }
 }
 
@@ -615,62 +660,83 @@ static dim3 chan_grid(long M, int C) {
 }
 
 void chan_stats(const void* y, const float* shift, long M, int C, float* psum, float* psq,
-                hipStream_t st) {
-  if (bn_v8(C)) {
-    hipLaunchKernelGGL(chan_stats_v8_kernel, dim3(v8_grid(M, C, 512)), dim3(256), 0, st,
-                       (const __bf16*)y, shift, M, C, psum, psq);
-    return;
-  }
-  hipLaunchKernelGGL(chan_stats_kernel, chan_grid(M, C), dim3(64, 4), 0, st, (const __bf16*)y,
-                     shift, M, C, psum, psq);
+                hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    if (bn_v8(C)) {
+      hipLaunchKernelGGL((chan_stats_v8_kernel<T>), dim3(v8_grid(M, C, 512)), dim3(256), 0, st,
+                         (const T*)y, shift, M, C, psum, psq);
+      return;
+    }
+    hipLaunchKernelGGL((chan_stats_kernel<T>), chan_grid(M, C), dim3(64, 4), 0, st, (const T*)y,
+                       shift, M, C, psum, psq);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 void affine_act(const void* y, const float* scale, const float* bias, void* z, long M, int C,
-                int act, hipStream_t st) {
-  if (bn_v8(C)) {
-    hipLaunchKernelGGL(affine_act_v8_kernel, dim3(v8_grid(M, C, 4096)), dim3(256), 0, st,
-                       (const __bf16*)y, scale, bias, (__bf16*)z, M, C, act);
-    return;
-  }
-  long n = M * C;
-  hipLaunchKernelGGL(affine_act_kernel, dim3(grid_for(n)), dim3(256), 0, st, (const __bf16*)y,
-                     scale, bias, (__bf16*)z, n, C, act);
+                int act, hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    if (bn_v8(C)) {
+      hipLaunchKernelGGL((affine_act_v8_kernel<T>), dim3(v8_grid(M, C, 4096)), dim3(256), 0, st,
+                         (const T*)y, scale, bias, (T*)z, M, C, act);
+      return;
+    }
+    long n = M * C;
+    hipLaunchKernelGGL((affine_act_kernel<T>), dim3(grid_for(n)), dim3(256), 0, st, (const T*)y,
+                       scale, bias, (T*)z, n, C, act);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 void bn_generic_bwd_reduce(const void* dz, const void* z, const void* y, const float* mean,
                            const float* invstd, long M, int C, int act, float* out_g,
-                           float* out_gx, hipStream_t st) {
-  if (bn_v8(C)) {
-    hipLaunchKernelGGL(bn_generic_bwd_reduce_v8_kernel, dim3(v8_grid(M, C, 512)), dim3(256), 0,
-                       st, (const __bf16*)dz, (const __bf16*)z, (const __bf16*)y, mean, invstd, M,
-                       C, act, out_g, out_gx);
-    return;
-  }
-  hipLaunchKernelGGL(bn_generic_bwd_reduce_kernel, chan_grid(M, C), dim3(64, 4), 0, st,
-                     (const __bf16*)dz, (const __bf16*)z, (const __bf16*)y, mean, invstd, M, C,
-                     act, out_g, out_gx);
+                           float* out_gx, hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    if (bn_v8(C)) {
+      hipLaunchKernelGGL((bn_generic_bwd_reduce_v8_kernel<T>), dim3(v8_grid(M, C, 512)), dim3(256), 0,
+                         st, (const T*)dz, (const T*)z, (const T*)y, mean, invstd, M,
+                         C, act, out_g, out_gx);
+      return;
+    }
+    hipLaunchKernelGGL((bn_generic_bwd_reduce_kernel<T>), chan_grid(M, C), dim3(64, 4), 0, st,
+                       (const T*)dz, (const T*)z, (const T*)y, mean, invstd, M, C,
+                       act, out_g, out_gx);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 void bn_generic_bwd_apply(const void* dz, const void* z, const void* y, const float* mean,
                           const float* invstd, const float* gamma, const float* sum_g,
                           const float* sum_gx, long count, long M, int C, int act, void* dy,
-                          hipStream_t st) {
-  if (bn_v8(C)) {
-    hipLaunchKernelGGL(bn_generic_bwd_apply_v8_kernel, dim3(v8_grid(M, C, 4096)), dim3(256), 0,
-                       st, (const __bf16*)dz, (const __bf16*)z, (const __bf16*)y, mean, invstd,
-                       gamma, sum_g, sum_gx, 1.f / (float)count, M, C, act, (__bf16*)dy);
-    return;
-  }
-  long n = M * C;
-  hipLaunchKernelGGL(bn_generic_bwd_apply_kernel, dim3(grid_for(n)), dim3(256), 0, st,
-                     (const __bf16*)dz, (const __bf16*)z, (const __bf16*)y, mean, invstd, gamma,
-                     sum_g, sum_gx, 1.f / (float)count, n, C, act, (__bf16*)dy);
+                          hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    if (bn_v8(C)) {
+      hipLaunchKernelGGL((bn_generic_bwd_apply_v8_kernel<T>), dim3(v8_grid(M, C, 4096)), dim3(256), 0,
+                         st, (const T*)dz, (const T*)z, (const T*)y, mean, invstd,
+                         gamma, sum_g, sum_gx, 1.f / (float)count, M, C, act, (T*)dy);
+      return;
+    }
+    long n = M * C;
+    hipLaunchKernelGGL((bn_generic_bwd_apply_kernel<T>), dim3(grid_for(n)), dim3(256), 0, st,
+                       (const T*)dz, (const T*)z, (const T*)y, mean, invstd, gamma,
+                       sum_g, sum_gx, 1.f / (float)count, n, C, act, (T*)dy);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 // ------------------------------------------------------------------------ k x k average pool
 // count_include_pad = True (torch's default, the only mode torchvision uses); any C.
-__global__ __launch_bounds__(256) void avgpool2d_fwd_kernel(const __bf16* __restrict__ x,
-                                                            __bf16* __restrict__ y, int N, int H,
+template <class T>
+__global__ __launch_bounds__(256) void avgpool2d_fwd_kernel(const T* __restrict__ x,
+                                                            T* __restrict__ y, int N, int H,
                                                             int W, int C, int Ho, int Wo, int k,
                                                             int s, int p) {
   const long total = (long)N * Ho * Wo * C;
@@ -690,15 +756,16 @@ __global__ __launch_bounds__(256) void avgpool2d_fwd_kernel(const __bf16* __rest
       for (int kw = 0; kw < k; ++kw) {
         const int wi = wo * s - p + kw;
         if (wi < 0 || wi >= W) continue;
-        acc += bf2f(x[(((long)n * H + hi) * W + wi) * C + c]);
+        acc += to_f32(x[(((long)n * H + hi) * W + wi) * C + c]);
       }
     }
-    y[t] = f2bf(acc * inv);
+    y[t] = from_f32<T>(acc * inv);
   }
 }
 
-__global__ __launch_bounds__(256) void avgpool2d_bwd_kernel(const __bf16* __restrict__ dy,
-                                                            __bf16* __restrict__ dx, int N, int H,
+template <class T>
+__global__ __launch_bounds__(256) void avgpool2d_bwd_kernel(const T* __restrict__ dy,
+                                                            T* __restrict__ dx, int N, int H,
                                                             int W, int C, int Ho, int Wo, int k,
                                                             int s, int p) {
   const long total = (long)N * H * W * C;
@@ -720,23 +787,33 @@ __global__ __launch_bounds__(256) void avgpool2d_bwd_kernel(const __bf16* __rest
       for (int wo = wo_lo; wo <= wo_hi; ++wo) {
         const int kw = wi - (wo * s - p);
         if (kw < 0 || kw >= k) continue;
-        acc += bf2f(dy[(((long)n * Ho + ho) * Wo + wo) * C + c]);
+        acc += to_f32(dy[(((long)n * Ho + ho) * Wo + wo) * C + c]);
       }
     }
-    dx[t] = f2bf(acc * inv);
+    dx[t] = from_f32<T>(acc * inv);
   }
 }
 
 void avgpool2d_fwd(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo, int k,
-                   int stride, int pad, hipStream_t st) {
-  hipLaunchKernelGGL(avgpool2d_fwd_kernel, dim3(grid_for((long)N * Ho * Wo * C)), dim3(256), 0,
-                     st, (const __bf16*)x, (__bf16*)y, N, H, W, C, Ho, Wo, k, stride, pad);
+                   int stride, int pad, hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    hipLaunchKernelGGL((avgpool2d_fwd_kernel<T>), dim3(grid_for((long)N * Ho * Wo * C)), dim3(256), 0,
+                       st, (const T*)x, (T*)y, N, H, W, C, Ho, Wo, k, stride, pad);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 void avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho, int Wo, int k,
-                   int stride, int pad, hipStream_t st) {
-  hipLaunchKernelGGL(avgpool2d_bwd_kernel, dim3(grid_for((long)N * H * W * C)), dim3(256), 0, st,
-                     (const __bf16*)dy, (__bf16*)dx, N, H, W, C, Ho, Wo, k, stride, pad);
+                   int stride, int pad, hipStream_t st, bool f32) {
+  auto run = [&](auto tag) {
+    typedef decltype(tag) T;
+    hipLaunchKernelGGL((avgpool2d_bwd_kernel<T>), dim3(grid_for((long)N * H * W * C)), dim3(256), 0, st,
+                       (const T*)dy, (T*)dx, N, H, W, C, Ho, Wo, k, stride, pad);
+  };
+  if (f32) run(float{});
+  else run(__bf16{});
 }
 
 }  // namespace mipipe

@@ -244,3 +244,105 @@ def test_resnet18_cifar_fp32_step_matches_float64():
                 for n, p in m.named_parameters())
     assert e2[len(e2) // 2] < 1e-4, e2
     assert e2[-1] < 5e-3, e2
+
+
+# vision.hip kernels (grouped / depthwise / non-square direct conv, any-C BatchNorm, k x k avg
+# pool) in fp32: N, H, W, Ci, Co, (kh, kw), (sh, sw), (ph, pw), groups
+GCONV_CASES = [
+    (2, 14, 14, 96, 96, (3, 3), (1, 1), (1, 1), 96),
+    (2, 9, 9, 40, 40, (5, 5), (2, 2), (2, 2), 40),
+    (2, 7, 7, 58, 58, (3, 3), (1, 1), (1, 1), 58),
+    (2, 8, 8, 128, 128, (3, 3), (2, 2), (1, 1), 32),
+    (2, 9, 11, 64, 48, (1, 7), (1, 1), (0, 3), 1),
+]
+
+
+@pytest.mark.parametrize("case", GCONV_CASES)
+def test_gconv_fp32(case):
+    N, H, W, Ci, Co, k, s, p, g = case
+    x = f32(N, H, W, Ci)
+    w = f32(Co, k[0], k[1], Ci // g, scale=1.0 / math.sqrt(Ci // g * k[0] * k[1]))
+    b = torch.randn(Co, device=dev) * 0.1
+    y = native().gconv_fwd(x, w, list(s), list(p), g, b, 2)
+    assert y.dtype == torch.float32
+    assert rel_err(y, _ref.gconv_fwd(d(x), d(w), s, p, g, d(b), "relu6")) < TOL
+    dy = f32(*y.shape)
+    dx = native().gconv_dgrad(dy, w, [N, H, W, Ci], list(s), list(p), g, y, 2)
+    assert rel_err(dx, _ref.gconv_dgrad(d(dy), d(w), (N, H, W, Ci), s, p, g, d(y), "relu6")) < TOL
+    dw, db = native().gconv_wgrad(dy, x, k[0], k[1], list(s), list(p), g, y, 2, None, None, True)
+    dwr, dbr = _ref.gconv_wgrad(d(dy), d(x), k[0], k[1], s, p, g, d(y), "relu6")
+    assert rel_err(dw, dwr) < TOL and rel_err(db, dbr) < TOL
+
+
+@pytest.mark.parametrize("C", [58, 96])
+def test_bn_generic_and_avgpool2d_fp32(C):
+    y = f32(3, 7, 9, C) * 2 + 0.5
+    shift = torch.randn(C, device=dev) * 0.1
+    ps, pq = native().chan_stats(y, shift)
+    psr, pqr = _ref.chan_stats(d(y), d(shift))
+    assert rel_err(ps, psr) < TOL and rel_err(pq, pqr) < TOL
+    scale, bias = torch.randn(C, device=dev), torch.randn(C, device=dev)
+    z = native().affine_act(y, scale, bias, 1)
+    assert z.dtype == torch.float32
+    assert rel_err(z, _ref.affine_act(d(y), d(scale), d(bias), "relu")) < TOL
+    mean, invstd = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    gamma = torch.randn(C, device=dev)
+    dz = f32(*y.shape)
+    sg, sgx = native().bn_generic_bwd_reduce(dz, z, y, mean, invstd, 1)
+    sgr, sgxr = _ref.bn_generic_bwd_reduce(d(dz), d(z), d(y), d(mean), d(invstd), "relu")
+    assert rel_err(sg, sgr) < TOL and rel_err(sgx, sgxr) < TOL
+    n = y.numel() // C
+    dy = native().bn_generic_bwd_apply(dz, z, y, mean, invstd, gamma, sg, sgx, n, 1)
+    dyr = _ref.bn_generic_bwd_apply(d(dz), d(z), d(y), d(mean), d(invstd), d(gamma), sgr, sgxr,
+                                    n, "relu")
+    assert rel_err(dy, dyr) < TOL
+    x = f32(2, 17, 17, C)
+    a = native().avgpool2d_fwd(x, 3, 2, 1)
+    assert a.dtype == torch.float32 and rel_err(a, _ref.avgpool2d_fwd(d(x), 3, 2, 1)) < TOL
+    da = f32(*a.shape)
+    assert rel_err(native().avgpool2d_bwd(da, list(x.shape), 3, 2, 1),
+                   _ref.avgpool2d_bwd(d(da), tuple(x.shape), 3, 2, 1)) < TOL
+
+
+ZOO = [("mobilenet_v2", 64), ("mnasnet1_0", 64), ("shufflenet_v2_x1_0", 64),
+       ("squeezenet1_1", 64), ("densenet121", 64), ("googlenet", 64), ("inception_v3", 299),
+       ("resnext50_32x4d", 64), ("vgg11_bn", 64), ("alexnet", 64)]
+NODROP = {"mobilenet_v2": dict(dropout=0.0), "mnasnet1_0": dict(dropout=0.0),
+          "squeezenet1_1": dict(dropout=0.0), "googlenet": dict(dropout=0.0, dropout_aux=0.0),
+          "inception_v3": dict(dropout=0.0), "vgg11_bn": dict(dropout=0.0),
+          "alexnet": dict(dropout=0.0)}
+
+
+@pytest.mark.parametrize("arch,res", ZOO)
+def test_zoo_fp32_train_step(arch, res):
+    """Every zoo family trains in fp32 on the kernels (the reference's precision): the training-
+    mode forward matches an fp32 torch evaluation of the same weights to fp32-class error, and
+    SGD steps reduce the loss."""
+    from mipipe.models import create_model
+    from mipipe.optim import SGD
+    from mipipe.train.task import CrossEntropyLoss
+    torch.manual_seed(0)
+    m = create_model(arch, num_classes=10, **NODROP.get(arch, {})).to(dev)
+    m.compute_dtype = torch.float32
+    x = torch.randn(8, 3, res, res, device=dev)
+    y = torch.randint(0, 10, (8,), device=dev)
+    if hasattr(m, "reference_forward"):
+        m.eval()
+        with torch.no_grad():
+            out, ref = m(x), m.reference_forward(x)
+        o, r = out.double(), ref.double()
+        assert out.dtype == torch.float32
+        assert ((o - r).norm() / r.norm()).item() < 1e-3
+        m.train()
+    lr = 0.001 if arch.startswith("squeezenet") else 0.005  # no BatchNorm: smaller step
+    opt = SGD(m.parameters(), lr, momentum=0.9, weight_decay=1e-4, shadow_dtype=None)
+    crit = CrossEntropyLoss()
+    losses = []
+    for _ in range(5):
+        opt.zero_grad()
+        loss = crit(m(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.item()))
+    assert all(math.isfinite(v) for v in losses), losses
+    assert min(losses[1:]) < losses[0], losses
