@@ -10,7 +10,9 @@ torch.manual_seed(0)
 m = create_model("bert_base").to(dev)
 m.compute_dtype = torch.bfloat16
 opt = AdamW(m.parameters(), lr=1e-4, weight_decay=0.01)
-B, S, P, V = 32, 128, 20, 30522
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+S = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+P, V = (20 if S == 128 else round(0.15 * S)), 30522
 ids = torch.randint(0, V, (B, S), device=dev)
 am = torch.ones(B, S, device=dev, dtype=torch.int64)
 pos = torch.stack([torch.randperm(S, device=dev)[:P] for _ in range(B)])
@@ -26,10 +28,8 @@ torch.cuda.synchronize()
 with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
     step()
     torch.cuda.synchronize()
-names = ("aten::sum", "aten::add", "aten::add_", "aten::copy_", "aten::to", "aten::_to_copy",
-         "aten::fill_", "aten::zero_", "aten::zeros", "aten::cat", "aten::mul", "aten::sub")
-for ev in prof.key_averages(group_by_stack_n=6):
-    if ev.key in names:
+for ev in sorted(prof.key_averages(group_by_stack_n=6), key=lambda e: -e.device_time_total):
+    if ev.key.startswith("aten::") and ev.device_time_total > 0:
         print(f"{ev.key:16s} n={ev.count:4d} dev_us={ev.device_time_total:9.1f}")
         for fr in ev.stack[:6]:
             print("      ", fr)
