@@ -115,10 +115,10 @@ std::vector<int> candidates(bool f32, bool wgrad) {
   return c;
 }
 
-// cfg for this call: table hit, or (benchmark mode, not capturing) measure all candidates with
+// cfg for this call: table hit, or (benchmark mode, not capturing) measure every candidate with
 // `run(cfg)` (which must write only scratch outputs) and record the fastest; else -1 (heuristic).
 template <class F>
-int select(const std::string& k, bool f32, bool wgrad, F&& run) {
+int select_from(const std::string& k, const std::vector<int>& cands, F&& run) {
   auto it = g_table.find(k);
   if (it != g_table.end()) return it->second;
   if (!g_benchmark || capturing()) return -1;
@@ -129,7 +129,7 @@ int select(const std::string& k, bool f32, bool wgrad, F&& run) {
   int best = -1;
   float best_ms = 1e30f;
   std::string log;
-  for (int cfg : candidates(f32, wgrad)) {
+  for (int cfg : cands) {
     run(cfg);  // warm (first launch of a kernel object loads its code)
     hipEventRecord(e0, st);
     for (int r = 0; r < g_reps; ++r) run(cfg);
@@ -146,10 +146,35 @@ int select(const std::string& k, bool f32, bool wgrad, F&& run) {
   }
   hipEventDestroy(e0);
   hipEventDestroy(e1);
-  TORCH_CHECK(hipGetLastError() == hipSuccess, "conv tile tuning: a candidate failed to launch");
+  TORCH_CHECK(hipGetLastError() == hipSuccess, "tile tuning: a candidate failed to launch");
   if (g_verbose) fprintf(stderr, "[mipipe tune] %s -> %d  (us:%s)\n", k.c_str(), best, log.c_str());
   g_table[k] = best;
   return best;
+}
+
+template <class F>
+int select(const std::string& k, bool f32, bool wgrad, F&& run) {
+  return select_from(k, candidates(f32, wgrad), run);
+}
+
+// GEMM plans: tile id + 16 * split-K count (0 = heuristic split; accumulating GEMMs only)
+constexpr int kPlanSplit = 16;
+std::vector<int> gemm_candidates(bool f32, bool accumulate) {
+  std::vector<int> c;
+  for (int t : candidates(f32, accumulate)) {
+    if (!accumulate) {
+      c.push_back(t);
+      continue;
+    }
+    for (int sp : {1, 2, 4}) c.push_back(t + kPlanSplit * sp);
+  }
+  return c;
+}
+std::string gemm_key(int64_t M, int64_t N, int64_t K, bool akc, bool bkc, int mode, bool f32) {
+  char buf[160];
+  snprintf(buf, sizeof(buf), "gemm|%lld,%lld,%lld,%d,%d,%d|%s", (long long)M, (long long)N,
+           (long long)K, (int)akc, (int)bkc, mode, f32 ? "f32" : "bf16");
+  return buf;
 }
 }  // namespace tune
 
@@ -558,7 +583,8 @@ Tensor avgpool_bwd(Tensor dy, std::vector<int64_t> xs) {
 
 // ------------------------------------------------------------------------------- GEMM
 Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bias,
-            std::string act, at::ScalarType out_dtype, optional<Tensor> c, double beta) {
+            std::string act, at::ScalarType out_dtype, optional<Tensor> c, double beta,
+            int64_t plan) {
   check_act(a, "A");
   check_same(b, a, "B");
   c10::DeviceGuard g(a.device());
@@ -585,6 +611,7 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
     TORCH_CHECK(beta == 1.0, "gemm supports beta in {0, 1}");
     check_f32(*c, "C");
     TORCH_CHECK(c->size(0) == M && c->size(1) == N, "C shape mismatch");
+    TORCH_CHECK(c->stride(1) == 1 && c->stride(0) == N, "accumulated C must be contiguous");
     TORCH_CHECK(bias_p == nullptr && act_i == 0, "accumulating gemm has no epilogue");
     out = *c;
     mode = 2;
@@ -597,9 +624,22 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
     mode = 1;
     TORCH_CHECK(act_i == 0, "fp32 gemm output has no activation epilogue");
   }
-  mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b,
-               out.data_ptr(), N, (int)M, (int)N, (int)K, bias_p, act_i, mode, stream(),
-               is_f32(a));
+  const bool f32 = is_f32(a);
+  auto launch = [&](void* C, int p) {
+    const int cfg = p < 0 ? -1 : p % tune::kPlanSplit;
+    const int sp = p < 0 ? -1 : (p / tune::kPlanSplit > 0 ? p / tune::kPlanSplit : -1);
+    mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b, C, N,
+                 (int)M, (int)N, (int)K, bias_p, act_i, mode, stream(), f32, cfg, sp);
+  };
+  if (plan < 0) {
+    plan = tune::select_from(tune::gemm_key(M, N, K, !trans_a, trans_b, mode, f32),
+                             tune::gemm_candidates(f32, mode == 2), [&](int p) {
+                               auto scratch = mode == 2 ? torch::zeros_like(out)
+                                                        : torch::empty_like(out);
+                               launch(scratch.data_ptr(), p);
+                             });
+  }
+  launch(out.data_ptr(), (int)plan);
   return out;
 }
 
@@ -823,7 +863,7 @@ Tensor colsum(Tensor x, optional<Tensor> out) {
   }
   optional<Tensor> work;
   if (mipipe::g_deterministic)
-    work = torch::empty({(int64_t)mipipe::colsum_blocks(rows), cols}, x.options().dtype(at::kFloat));
+    work = torch::empty({(int64_t)mipipe::colsum_blocks(rows, (int)cols), cols}, x.options().dtype(at::kFloat));
   mipipe::colsum_f32(x.data_ptr(), x.scalar_type() == at::kBFloat16, o.data_ptr<float>(), rows,
                      (int)cols, work.has_value() ? work->data_ptr<float>() : nullptr, stream());
   return o;
@@ -1198,7 +1238,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("maxpool_bwd_impl", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("trans_a"), py::arg("trans_b"),
+        py::arg("bias"), py::arg("act"), py::arg("out_dtype"), py::arg("c"), py::arg("beta"),
+        py::arg("plan") = -1);
   m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
   m.def("sgd_step", &sgd_step);
   m.def("adamw_step", &adamw_step);

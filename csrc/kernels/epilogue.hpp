@@ -40,6 +40,9 @@ struct EpiParams {
   // outputs (epilogue_f32) are written to slice blockIdx.y of a [splits][M][ldc] workspace.
   int det_rows;
   int det_row0;
+  // epilogue_f32 without ATOMIC: add the tile to the existing C (read-modify-write; each
+  // element owned by one block) instead of overwriting it
+  int rmw;
 };
 
 // Workgroup barrier that orders LDS only.  __syncthreads() also drains every outstanding global
@@ -298,7 +301,8 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
   epilogue_out<BM, BN, FUSE, __bf16, 2, 2>(smem, acc, e, m0, n0, prow_base, wave, lane);
 }
 
-// fp32 output; ATOMIC accumulates into C (split-K), otherwise plain store (beta = 0).
+// fp32 output; ATOMIC accumulates into C (split-K), otherwise plain store (beta = 0) or, with
+// e.rmw, a non-atomic accumulate (beta = 1, one block per element).
 template <int BM, int BN, bool ATOMIC, int WM = 2, int WN = 2>
 __device__ void epilogue_f32(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                              const EpiParams& e, uint32_t m0, uint32_t n0, int wave, int lane) {
@@ -344,6 +348,10 @@ __device__ void epilogue_f32(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
       uint32_t m = m0 + r, n = n0 + cc * 4;
       if (m < e.M && n < e.N) {
         float4 v = *reinterpret_cast<const float4*>(smem + r * P + cc * 16);
+        if (e.rmw) {
+          const float4 o = *reinterpret_cast<const float4*>(C + (long)m * e.ldc + n);
+          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
         if (e.bias != nullptr) {
           v.x += e.bias[n]; v.y += e.bias[n + 1]; v.z += e.bias[n + 2]; v.w += e.bias[n + 3];
         }

@@ -1,8 +1,15 @@
-// Dense bf16 / fp32 (split-bf16) GEMM on the shared MFMA core (Linear forward / data-grad / weight-grad).
+// Dense bf16 / fp32 (split-bf16) GEMM on the shared MFMA core (Linear forward / data-grad /
+// weight-grad).
 //   C[M][N] = op(A) op(B);  A stored [M][K] (KC) or [K][M] (MC);  B stored [N][K] (KC) or [K][N] (MC)
-// Output: bf16 (+bias +ReLU epilogue), fp32 store (+bias) or fp32 split-K atomic accumulate.
-#include "epilogue.hpp"
-#include "launchers.hpp"
+// Output modes: 0 activation dtype (+bias +ReLU epilogue), 1 fp32 store (+bias),
+// 2 fp32 accumulate into C (beta = 1): split-K with fp32 atomics (splits > 1) or one block per
+// output element with a plain read-modify-write (splits == 1, no atomics; also the
+// deterministic path).
+// Every kernel is a template over the conv tile table (conv_common.hpp); the host picks a
+// (tile, splits) plan per shape: the benchmark-mode tuning table (bindings.cpp, tune::) or the
+// heuristic below.  Dense GEMMs run the main loop with the raw-barrier / MFMA-priority schedule
+// (tools/gemm_lab: +1..12 % over plain __syncthreads on BERT / square shapes).
+#include "conv_common.hpp"
 
 namespace mipipe {
 int g_splitk_target = 512;
@@ -12,17 +19,19 @@ int g_ns1_max_k = 512;  // measured: tools/sweep_ns1.py (profiles/r1_ns1_sweep.j
 namespace gk {
 
 __device__ __attribute__((aligned(64))) uint4 g_gemm_zero[8];
+constexpr int kGemmLoop = kLoopRawBarrier | kLoopPrio;
 
-template <int BM, int BN, bool A_KC, bool B_KC, int OUT, class T = __bf16>
-__global__ __launch_bounds__(256, 2) void gemm_dense_kernel(const T* __restrict__ A, long lda,
-                                                             const T* __restrict__ B, long ldb,
-                                                             uint32_t K, uint32_t tilesN,
-                                                             int kt_per_split, EpiParams e) {
-  typedef typename std::conditional<A_KC, KCDense<BM, T>, MCDense<BM, T>>::type OpA;
-  typedef typename std::conditional<B_KC, KCDense<BN, T>, MCDense<BN, T>>::type OpB;
-  typedef MainLoopFor<T, BM, BN, OpA, OpB> ML;
+// OUT: 0 activation dtype, 1 fp32 store / read-modify-write (e.rmw), 2 fp32 atomic (split-K)
+template <class C, bool A_KC, bool B_KC, int OUT, class T>
+__global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void gemm_dense_kernel(
+    const T* __restrict__ A, long lda, const T* __restrict__ B, long ldb, uint32_t K,
+    uint32_t tilesN, int kt_per_split, EpiParams e) {
+  constexpr int BM = C::BM, BN = C::BN, NW = C::NW;
+  typedef typename std::conditional<A_KC, KCDense<BM, T, NW>, MCDense<BM, T, NW>>::type OpA;
+  typedef typename std::conditional<B_KC, KCDense<BN, T, NW>, MCDense<BN, T, NW>>::type OpB;
+  typedef MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN, kGemmLoop> ML;
   constexpr int main_lds = ML::LDS_BYTES;
-  constexpr int epi_lds = OUT == 0 ? kEpiLdsBytes<BM, BN, T>() : BM * (BN * 4 + 16);
+  constexpr int epi_lds = OUT == 0 ? kEpiLdsBytes<BM, BN, T, C::WM>() : BM * (BN * 4 + 16);
   __shared__ __attribute__((aligned(16))) char smem[main_lds > epi_lds ? main_lds : epi_lds];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -36,11 +45,10 @@ __global__ __launch_bounds__(256, 2) void gemm_dense_kernel(const T* __restrict_
   a.init(A, lda, e.M, K, m0, wave, lane, g_gemm_zero);
   OpB b;
   b.init(B, ldb, e.N, K, n0, wave, lane, g_gemm_zero);
-  f32x4 acc[BM / 32][BN / 32];
+  f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
   ML::type::run(smem, a, b, kt0, kt1, acc, wave, lane);
-  if constexpr (OUT == 0) epilogue_out<BM, BN, false, T>(smem, acc, e, m0, n0, 0, wave, lane);
-  else if constexpr (OUT == 1) epilogue_f32<BM, BN, false>(smem, acc, e, m0, n0, wave, lane);
-  else epilogue_f32<BM, BN, true>(smem, acc, e, m0, n0, wave, lane);
+  if constexpr (OUT == 0) epilogue_out<BM, BN, false, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
+  else epilogue_f32<BM, BN, OUT == 2, C::WM, C::WN>(smem, acc, e, m0, n0, wave, lane);
 }
 
 }  // namespace gk
@@ -49,55 +57,87 @@ using namespace gk;
 
 static inline uint32_t cdiv_u(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-template <int BM, int BN, bool AK, bool BK_, class T>
+template <class C, bool AK, bool BK_, class T>
 static void launch_out(const void* A, long lda, const void* B, long ldb, int K, uint32_t tN,
                        uint32_t tiles, int splits, int per, int out, const EpiParams& e,
                        hipStream_t st) {
   dim3 grid(tiles, splits);
   const T* a = (const T*)A;
   const T* b = (const T*)B;
-  if (out == 0)
-    hipLaunchKernelGGL((gemm_dense_kernel<BM, BN, AK, BK_, 0, T>), grid, dim3(256), 0, st, a, lda, b, ldb, (uint32_t)K, tN, per, e);
-  else if (out == 1)
-    hipLaunchKernelGGL((gemm_dense_kernel<BM, BN, AK, BK_, 1, T>), grid, dim3(256), 0, st, a, lda, b, ldb, (uint32_t)K, tN, per, e);
-  else
-    hipLaunchKernelGGL((gemm_dense_kernel<BM, BN, AK, BK_, 2, T>), grid, dim3(256), 0, st, a, lda, b, ldb, (uint32_t)K, tN, per, e);
+  // a 256 x 256 fp32 tile does not fit the LDS: those tiles only serve out 0 (with_tile maps
+  // the fp32-output modes to 256 x 128)
+  constexpr bool kWide = C::BM * C::BN > 256 * 128;
+  if (out == 0) {
+    hipLaunchKernelGGL((gemm_dense_kernel<C, AK, BK_, 0, T>), grid, dim3(C::THREADS), 0, st, a, lda, b, ldb, (uint32_t)K, tN, per, e);
+  } else if constexpr (!kWide) {
+    if (out == 1)
+      hipLaunchKernelGGL((gemm_dense_kernel<C, AK, BK_, 1, T>), grid, dim3(C::THREADS), 0, st, a, lda, b, ldb, (uint32_t)K, tN, per, e);
+    else
+      hipLaunchKernelGGL((gemm_dense_kernel<C, AK, BK_, 2, T>), grid, dim3(C::THREADS), 0, st, a, lda, b, ldb, (uint32_t)K, tN, per, e);
+  }
 }
 
-template <int BM, int BN, class T>
+// split count for an accumulating (out == 2) GEMM: `splits` > 0 is the tuned value; else split
+// K until ~g_splitk_target blocks with >= 4 k-steps per split, at most 4 ways (every split
+// adds M*N*4 bytes of atomics, and those run at ~1.3 TB/s chip-wide).
+static int plan_splits(uint32_t tiles, int nk, int splits) {
+  if (g_deterministic) return 1;  // one block per output element: read-modify-write, no atomics
+  if (splits > 0) return std::min(splits, std::max(1, nk));
+  int s = std::min<int>(g_splitk_target / std::max<uint32_t>(1, tiles), nk / 4);
+  return std::max(1, std::min(s, 4));
+}
+
+template <class C, class T>
 static void launch_tile(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc,
-                        int M, int N, int K, int out, const EpiParams& e, hipStream_t st) {
-  uint32_t tN = cdiv_u(N, BN), tiles = cdiv_u(M, BM) * tN;
+                        int M, int N, int K, int out, EpiParams e, int splits_req,
+                        hipStream_t st) {
+  uint32_t tN = cdiv_u(N, C::BN), tiles = cdiv_u(M, C::BM) * tN;
   int nk = (int)cdiv_u(K, 64);
   int splits = 1, per = nk;
-  if (out == 2 && !g_deterministic) {  // split-K until ~g_splitk_target blocks, >= 4 k-steps per split
-    // (deterministic mode: one split, so every output element is written by one block)
-    splits = std::max<int>(1, std::min<int>(g_splitk_target / std::max<uint32_t>(1, tiles), nk / 4));
+  if (out == 2) {
+    splits = plan_splits(tiles, nk, splits_req);
     per = (int)cdiv_u(nk, splits);
     splits = (int)cdiv_u(nk, per);
+    if (splits == 1) {  // sole writer of its tile: plain read-modify-write epilogue
+      out = 1;
+      e.rmw = 1;
+    }
   }
-  if (a_kc && b_kc) launch_out<BM, BN, true, true, T>(A, lda, B, ldb, K, tN, tiles, splits, per, out, e, st);
-  else if (a_kc && !b_kc) launch_out<BM, BN, true, false, T>(A, lda, B, ldb, K, tN, tiles, splits, per, out, e, st);
-  else if (!a_kc && b_kc) launch_out<BM, BN, false, true, T>(A, lda, B, ldb, K, tN, tiles, splits, per, out, e, st);
-  else launch_out<BM, BN, false, false, T>(A, lda, B, ldb, K, tN, tiles, splits, per, out, e, st);
+  if (a_kc && b_kc) launch_out<C, true, true, T>(A, lda, B, ldb, K, tN, tiles, splits, per, out, e, st);
+  else if (a_kc && !b_kc) launch_out<C, true, false, T>(A, lda, B, ldb, K, tN, tiles, splits, per, out, e, st);
+  else if (!a_kc && b_kc) launch_out<C, false, true, T>(A, lda, B, ldb, K, tN, tiles, splits, per, out, e, st);
+  else launch_out<C, false, false, T>(A, lda, B, ldb, K, tN, tiles, splits, per, out, e, st);
+}
+
+// heuristic tile (no tuning-table entry): 64-wide tiles for narrow dimensions, else 128x128
+int default_gemm_cfg(int M, int N, bool f32) {
+  (void)f32;
+  if (N <= 64) return 2;
+  if (M <= 64) return 8;
+  return 0;
 }
 
 template <class T>
-static void gemm_t(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc,
-                   int M, int N, int K, int out, const EpiParams& e, hipStream_t st) {
-  // tile choice: 64-wide tiles for narrow dimensions (MC images support W = 64 and 128)
-  if (N <= 64) launch_tile<128, 64, T>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, st);
-  else if (M <= 64) launch_tile<64, 128, T>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, st);
-  else launch_tile<128, 128, T>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, st);
+static void gemm_t(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, int M,
+                   int N, int K, int out, const EpiParams& e, int cfg, int splits,
+                   hipStream_t st) {
+  if (cfg < 0 || !tile_ok_for<T>(cfg)) cfg = default_gemm_cfg(M, N, std::is_same<T, float>::value);
+  auto go = [&](auto tile) {
+    typedef decltype(tile) C;
+    launch_tile<C, T>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, splits, st);
+  };
+  // fp32-output modes stage BM x BN fp32 in LDS: no 256 x 256 tile there
+  if (out == 0) with_tile<T, false>(cfg, go);
+  else with_tile<T, true>(cfg, go);
 }
 
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
           long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
-          bool f32) {
+          bool f32, int cfg, int splits) {
   EpiParams e{};
   e.C = C; e.ldc = ldc; e.M = (uint32_t)M; e.N = (uint32_t)N; e.bias = bias; e.act = act;
-  if (f32) gemm_t<float>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, st);
-  else gemm_t<__bf16>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, st);
+  if (f32) gemm_t<float>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st);
+  else gemm_t<__bf16>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st);
 }
 
 }  // namespace mipipe

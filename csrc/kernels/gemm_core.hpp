@@ -428,6 +428,15 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// Main-loop schedule variants (bit flags of MainLoop's V).
+constexpr int kLoopRawBarrier = 1;  // lgkmcnt(0) + s_barrier instead of __syncthreads()
+constexpr int kLoopPrio = 2;        // s_setprio(1) around the MFMA block
+constexpr int kLoopSpread = 4;      // next stage's LDS-DMA pieces spread between MFMAs
+#ifndef MIPIPE_LOOP_DEFAULT
+#define MIPIPE_LOOP_DEFAULT 0
+#endif
+constexpr int kLoopDefault = MIPIPE_LOOP_DEFAULT;
+
 // Main loop.  Returns accumulators acc[MT][NT] (swapped orientation: lane holds C[m][n..n+3]).
 // WM x WN waves (4 or 8), wave tile (BM/WM) x (BN/WN) of 16x16 MFMA tiles.
 // NS = LDS stages:
@@ -439,7 +448,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 // Per k-step (NS >= 2): wait own loads of stage k -> barrier (everyone's stage k landed, and
 // everyone finished reading stage k-1's buffer) -> issue stage k+NS-1 into that buffer ->
 // fragments + MFMAs of stage k.  One barrier per k-step.
-template <int BM, int BN, class OpA, class OpB, int NS = 2, int WM = 2, int WN = 2>
+template <int BM, int BN, class OpA, class OpB, int NS = 2, int WM = 2, int WN = 2, int V = kLoopDefault>
 struct MainLoop {
   static constexpr int NW = WM * WN;
   static constexpr int MT = BM / WM / 16;  // 16-row tiles per wave
@@ -449,22 +458,42 @@ struct MainLoop {
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
   static constexpr int LDS_BYTES = NS * STAGE_BYTES;
   static constexpr int LOADS = OpA::NI + OpB::NI;  // LDS-DMA instructions per wave per stage
+  static constexpr int MFMAS = 2 * MT * NT;        // per wave per k-step
+  static constexpr bool RAW_BARRIER = (V & kLoopRawBarrier) != 0;
+  static constexpr bool PRIO = (V & kLoopPrio) != 0;
+  static constexpr bool SPREAD = (V & kLoopSpread) != 0;
   static_assert(OpA::NI * 8 * NW == BM && OpB::NI * 8 * NW == BN, "policy wave count");
   static_assert(NS >= 1 && NS <= 3, "1..3 LDS stages");
+
+  // one LDS-DMA instruction (piece p of LOADS) of stage kt
+  __device__ static void piece(char* buf, OpA& a, OpB& b, int kt, int wave, int p) {
+    if (p < OpA::NI) glds16(a.src(kt, p), buf + (wave * OpA::NI + p) * 1024);
+    else glds16(b.src(kt, p - OpA::NI), buf + A_BYTES + (wave * OpB::NI + p - OpA::NI) * 1024);
+  }
 
   __device__ static void stage(char* buf, OpA& a, OpB& b, int kt, int wave) {
     a.prep(kt);  // per-k-step wave-uniform address state (filter tap ...), computed once
     b.prep(kt);
 #pragma unroll
-    for (int i = 0; i < OpA::NI; ++i)
-      glds16(a.src(kt, i), buf + (wave * OpA::NI + i) * 1024);
-#pragma unroll
-    for (int i = 0; i < OpB::NI; ++i)
-      glds16(b.src(kt, i), buf + A_BYTES + (wave * OpB::NI + i) * 1024);
+    for (int p = 0; p < LOADS; ++p) piece(buf, a, b, kt, wave, p);
   }
 
+  // Block barrier.  RAW: this wave's LDS reads retired + s_barrier, WITHOUT the vmcnt(0) a
+  // __syncthreads() fence adds (which would drain LDS-DMA stages meant to stay in flight).
+  __device__ static void barrier() {
+    if constexpr (RAW_BARRIER) {
+      __builtin_amdgcn_s_waitcnt((7 << 4) | (0 << 8) | 15 | (3 << 14));  // lgkmcnt(0) only
+      __builtin_amdgcn_s_barrier();
+    } else {
+      __syncthreads();
+    }
+  }
+
+  // Fragments + MFMAs of one stage.  With SPREAD, the next stage's LOADS LDS-DMA pieces
+  // (nbuf != nullptr) are issued between MFMA groups instead of in one burst before them.
   __device__ static void compute(const char* cbuf, f32x4 (&acc)[MT][NT], uint32_t arow0,
-                                 uint32_t bcol0, int lane) {
+                                 uint32_t bcol0, int lane, char* nbuf, OpA& a, OpB& b, int nkt,
+                                 int wave) {
     const char* aimg = cbuf;
     const char* bimg = cbuf + A_BYTES;
     // both k-substeps' fragments are requested up front, so the second substep's LDS reads
@@ -479,14 +508,29 @@ struct MainLoop {
       for (int j = 0; j < NT; ++j)
         bfr[ks][j] = FragLoader<OpB::KC, BN>::load(bimg, bcol0 + j * 16, ks, lane);
     }
+    if constexpr (SPREAD) {
+      if (nbuf != nullptr) {
+        a.prep(nkt);
+        b.prep(nkt);
+      }
+    }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < NT; ++j)
+        for (int j = 0; j < NT; ++j) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ks][j], af[ks][i], acc[i][j],
                                                               0, 0, 0);
+          if constexpr (SPREAD) {
+            constexpr int STEP = MFMAS / LOADS > 0 ? MFMAS / LOADS : 1;
+            const int idx = (ks * MT + i) * NT + j;  // compile-time after unrolling
+            if (idx % STEP == STEP - 1 && idx / STEP < LOADS && nbuf != nullptr)
+              piece(nbuf, a, b, nkt, wave, idx / STEP);
+          }
+        }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   }
 
   __device__ static void run(char* smem, OpA& a, OpB& b, int kt0, int kt1,
@@ -504,7 +548,7 @@ struct MainLoop {
         stage(smem, a, b, kt, wave);
         wait_vmcnt<0>();
         __syncthreads();
-        compute(smem, acc, arow0, bcol0, lane);
+        compute(smem, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave);
       }
     } else {
 #pragma unroll
@@ -519,9 +563,15 @@ struct MainLoop {
         } else {
           wait_vmcnt<0>();
         }
-        __syncthreads();
-        if (kt + NS - 1 < kt1) stage(smem + nxt * STAGE_BYTES, a, b, kt + NS - 1, wave);
-        compute(smem + cur * STAGE_BYTES, acc, arow0, bcol0, lane);
+        barrier();
+        const bool more = kt + NS - 1 < kt1;
+        if constexpr (SPREAD) {
+          compute(smem + cur * STAGE_BYTES, acc, arow0, bcol0, lane,
+                  more ? smem + nxt * STAGE_BYTES : nullptr, a, b, kt + NS - 1, wave);
+        } else {
+          if (more) stage(smem + nxt * STAGE_BYTES, a, b, kt + NS - 1, wave);
+          compute(smem + cur * STAGE_BYTES, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave);
+        }
         cur = cur + 1 == NS ? 0 : cur + 1;
         nxt = nxt + 1 == NS ? 0 : nxt + 1;
       }
@@ -657,13 +707,14 @@ struct MainLoopF32 {
 };
 
 // Selects the main loop for the operand element type.
-template <class T, int BM, int BN, class OpA, class OpB, int NS = 2, int WM = 2, int WN = 2>
+template <class T, int BM, int BN, class OpA, class OpB, int NS = 2, int WM = 2, int WN = 2,
+          int V = kLoopDefault>
 struct MainLoopFor {
-  typedef MainLoop<BM, BN, OpA, OpB, NS, WM, WN> type;
+  typedef MainLoop<BM, BN, OpA, OpB, NS, WM, WN, V> type;
   static constexpr int LDS_BYTES = NS * (BM + BN) * BK * 2;
 };
-template <int BM, int BN, class OpA, class OpB, int NS, int WM, int WN>
-struct MainLoopFor<float, BM, BN, OpA, OpB, NS, WM, WN> {
+template <int BM, int BN, class OpA, class OpB, int NS, int WM, int WN, int V>
+struct MainLoopFor<float, BM, BN, OpA, OpB, NS, WM, WN, V> {
   typedef MainLoopF32<BM, BN, OpA, OpB, WM, WN> type;
   static constexpr int LDS_BYTES = MainLoopF32<BM, BN, OpA, OpB, WM, WN>::LDS_BYTES;
 };

@@ -117,12 +117,15 @@ void avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho,
 
 // ---- dense GEMM: C[M][N] = op(A) op(B) --------------------------------------------------------
 //  a_kc: A stored [M][K] (else [K][M]);  b_kc: B stored [N][K] (else [K][N]).
-//  out: 0 = activation-dtype store (bias/act), 1 = fp32 store (bias), 2 = fp32 atomic accumulate
-//  (split-K).
+//  out: 0 = activation-dtype store (bias/act), 1 = fp32 store (bias), 2 = fp32 accumulate into C
+//  (split-K atomics when splits > 1, else a non-atomic read-modify-write).
 //  f32: A and B are fp32 (split-bf16 main loop); out 0 then stores fp32 (the activation dtype).
+//  cfg: tile config id (conv_common.hpp table; -1 = heuristic); splits (out 2): > 0 forces the
+//  split-K count (1 = no split), -1 = heuristic.
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
           long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
-          bool f32 = false);
+          bool f32 = false, int cfg = -1, int splits = -1);
+int default_gemm_cfg(int M, int N, bool f32);
 
 // ---- BatchNorm ------------------------------------------------------------------------------
 // Reduce a [P][C] partial slab pair (shifted sums) and finalize: mean, invstd, scale, bias and
@@ -213,9 +216,9 @@ void attention_bwd(const void* dout, const void* qkv, const void* o, const float
 // recomputes the same keep mask from the seed (no mask tensor).
 void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStream_t st);
 void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, hipStream_t st);
-// work (deterministic mode, else null): [colsum_blocks(rows)][cols] floats of per-block partials
+// work (deterministic mode, else null): [colsum_blocks(rows, cols)][cols] floats of partials
 void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
                 hipStream_t st);
-int colsum_blocks(long rows);
+int colsum_blocks(long rows, int cols);
 
 }  // namespace mipipe

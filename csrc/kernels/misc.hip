@@ -408,68 +408,80 @@ void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------ column sums
-// out[c] += Σ_r x[r][c]  (bias gradients; out may be a view of the flat gradient buffer).
-// tpr threads cover a row in 16-B vectors, rpb = 256/tpr rows per block-iteration; block
-// partials are reduced through LDS and added with one fp32 atomic per column per block.
-__global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x, bool bf16,
+// out[c] += sum_r x[r][c]  (bias gradients; out may be a view of the flat gradient buffer).
+// Grid (column chunks of 512, row blocks): each lane owns 8 consecutive columns (one 16-B bf16
+// / two 16-B fp32 loads per row), the block's 4 waves take interleaved rows with 4 rows of loads
+// in flight per lane, then the 4 wave partials are summed through LDS and added with one fp32
+// atomic per column per block (deterministic mode: written as a partial row instead).
+constexpr int kColsumChunk = 512;
+
+template <class T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x,
                                                      float* __restrict__ out, long rows, int cols,
                                                      long rows_per_block,
                                                      float* __restrict__ part) {
-  __shared__ float red[256 * 8 + 8];
-  const int nvec = bf16 ? cols / 8 : cols / 4;  // vectors per row
-  const int per = bf16 ? 8 : 4;
-  const int tpr = min(nvec, 256), rpb = 256 / tpr;
-  const int t = threadIdx.x, rr = t / tpr, cc = t % tpr;
-  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
-  for (int vb = 0; vb < nvec; vb += tpr) {
-    const int v = vb + cc;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (rr < rpb && v < nvec) {
-      for (long r = r0 + rr; r < r1; r += rpb) {
-        if (bf16) {
-          float f[8];
-          unpack8(reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(x) + r * cols)[v], f);
+  __shared__ float red[4][kColsumChunk + 4];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int c0 = blockIdx.x * kColsumChunk + l * 8;
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min(rows, r0 + rows_per_block);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < cols) {
+    const T* p = x + c0;
+    long r = r0 + w;
+    for (; r + 12 < r1; r += 16) {
+      float v[4][8];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) acc[q] += f[q];
-        } else {
-          float4 f = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x) + r * cols)[v];
-          acc[0] += f.x; acc[1] += f.y; acc[2] += f.z; acc[3] += f.w;
-        }
-      }
+      for (int u = 0; u < 4; ++u) load8(p + (r + 4 * u) * cols, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += v[u][q];
     }
-    __syncthreads();
-    // LDS image [rpb][tpr*per] so the final pass reads/atomics consecutive columns per lane
-    if (rr < rpb)
-      for (int q = 0; q < per; ++q) red[rr * tpr * per + cc * per + q] = acc[q];
-    __syncthreads();
-    const int ncol = min(tpr, nvec - vb) * per;
-    for (int c = t; c < ncol; c += 256) {
-      float a = 0.f;
-      for (int k = 0; k < rpb; ++k) a += red[k * tpr * per + c];
-      if (part != nullptr) part[(long)blockIdx.x * cols + (long)vb * per + c] = a;
-      else atomicAdd(out + (long)vb * per + c, a);
+    for (; r < r1; r += 4) {
+      float v[8];
+      load8(p + r * cols, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += v[q];
     }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[w][l * 8 + q] = acc[q];
+  __syncthreads();
+  for (int c = threadIdx.x; c < kColsumChunk; c += 256) {
+    const int col = blockIdx.x * kColsumChunk + c;
+    if (col >= cols) break;
+    const float s = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    if (part != nullptr) part[(long)blockIdx.y * cols + col] = s;
+    else atomicAdd(out + col, s);
   }
 }
 
-static void colsum_grid(long rows, long& G, long& rpb) {
-  G = std::max<long>(1, std::min<long>(512, (rows + 31) / 32));
+static void colsum_grid(long rows, int cols, long& G, long& rpb) {
+  const long chunks = (cols + kColsumChunk - 1) / kColsumChunk;
+  G = std::max<long>(1, std::min<long>(std::max<long>(1, 1024 / chunks), (rows + 15) / 16));
   rpb = (rows + G - 1) / G;
   G = (rows + rpb - 1) / rpb;
 }
 
-int colsum_blocks(long rows) {
+int colsum_blocks(long rows, int cols) {
   long G, rpb;
-  colsum_grid(rows, G, rpb);
+  colsum_grid(rows, cols, G, rpb);
   return (int)G;
 }
 
 void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
                 hipStream_t st) {
   long G, rpb;
-  colsum_grid(rows, G, rpb);
-  // work != null (deterministic mode): per-block partial rows, then a fixed-order sum
-  hipLaunchKernelGGL(colsum_kernel, dim3(G), dim3(256), 0, st, x, bf16, out, rows, cols, rpb, work);
+  colsum_grid(rows, cols, G, rpb);
+  dim3 grid((cols + kColsumChunk - 1) / kColsumChunk, (unsigned)G);
+  // work != null (deterministic mode): per-row-block partial rows, then a fixed-order sum
+  if (bf16)
+    hipLaunchKernelGGL(colsum_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)x, out, rows,
+                       cols, rpb, work);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, (const float*)x, out, rows,
+                       cols, rpb, work);
   if (work != nullptr) det_sum_rows(work, nullptr, (int)G, cols, out, nullptr, true, st);
 }
 
@@ -566,6 +578,9 @@ void layernorm_fwd(const void* x, const void* res, const float* gamma, const flo
 }
 
 // dx = rstd*(g*γ - mean(g*γ) - x̂*mean(g*γ*x̂)); per-block partials of Σg·x̂ and Σg for dγ, dβ.
+// Each wave walks rows w, w+4, ... of its block with the NEXT row's dy / x loads in flight while
+// it reduces the current one (the kernel is latency-bound otherwise: two dependent wave sums
+// per row); γ is held in registers for the whole block.
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __restrict__ dy,
                                                             const __bf16* __restrict__ x,
                                                             const float* __restrict__ mean,
@@ -577,29 +592,54 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
                                                             int H, int rows_per_block) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nc = H / 8;
-  float accg[LN_MAXC][8], accb[LN_MAXC][8];
+  float accg[LN_MAXC][8], accb[LN_MAXC][8], gam[LN_MAXC][8];
 #pragma unroll
-  for (int k = 0; k < LN_MAXC; ++k)
+  for (int k = 0; k < LN_MAXC; ++k) {
+    const int c = lane + k * 64;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) accg[k][q] = accb[k][q] = 0.f;
-  long r0 = (long)blockIdx.x * rows_per_block;
-  long r1 = min(rows, r0 + rows_per_block);
+    for (int q = 0; q < 8; ++q) {
+      accg[k][q] = accb[k][q] = 0.f;
+      gam[k][q] = c < nc ? gamma[c * 8 + q] : 0.f;
+    }
+  }
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = min(rows, r0 + rows_per_block);
+  uint4 ng[LN_MAXC], nx[LN_MAXC];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](long row) {
+#pragma unroll
+    for (int k = 0; k < LN_MAXC; ++k) {
+      const int c = lane + k * 64;
+      if (c < nc) {
+        ng[k] = *reinterpret_cast<const uint4*>(dy + row * H + c * 8);
+        nx[k] = *reinterpret_cast<const uint4*>(x + row * H + c * 8);
+      }
+    }
+    nmu = mean[row];
+    nrs = rstd[row];
+  };
+  if (r0 + w < r1) fetch(r0 + w);
   for (long row = r0 + w; row < r1; row += 4) {
-    const float mu = mean[row], rs = rstd[row];
+    const float mu = nmu, rs = nrs;
     float g[LN_MAXC][8], xh[LN_MAXC][8];
+#pragma unroll
+    for (int k = 0; k < LN_MAXC; ++k) {
+      if (lane + k * 64 < nc) {
+        unpack8(ng[k], g[k]);
+        unpack8(nx[k], xh[k]);
+      }
+    }
+    if (row + 4 < r1) fetch(row + 4);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < LN_MAXC; ++k) {
-      int c = lane + k * 64;
-      if (c < nc) {
-        unpack8(*reinterpret_cast<const uint4*>(dy + row * H + c * 8), g[k]);
-        unpack8(*reinterpret_cast<const uint4*>(x + row * H + c * 8), xh[k]);
+      if (lane + k * 64 < nc) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           xh[k][q] = (xh[k][q] - mu) * rs;
           accg[k][q] += g[k][q] * xh[k][q];
           accb[k][q] += g[k][q];
-          float gg = g[k][q] * gamma[c * 8 + q];
+          const float gg = g[k][q] * gam[k][q];
           s1 += gg;
           s2 += gg * xh[k][q];
         }
@@ -609,11 +649,11 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
     s2 = wave_sum(s2) / (float)H;
 #pragma unroll
     for (int k = 0; k < LN_MAXC; ++k) {
-      int c = lane + k * 64;
+      const int c = lane + k * 64;
       if (c < nc) {
         float o[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) o[q] = rs * (g[k][q] * gamma[c * 8 + q] - s1 - xh[k][q] * s2);
+        for (int q = 0; q < 8; ++q) o[q] = rs * (g[k][q] * gam[k][q] - s1 - xh[k][q] * s2);
         *reinterpret_cast<uint4*>(dx + row * H + c * 8) = pack8(o);
       }
     }
@@ -640,7 +680,8 @@ void layernorm_bwd(const void* dy, const void* x, const float* mean, const float
                    const float* gamma, void* dx, float* dgamma, float* dbeta, float* work,
                    long rows, int H, hipStream_t st) {
   // dgamma / dbeta are ACCUMULATED into (zeroed buffers or the flat gradient views)
-  int G = (int)std::max<long>(1, std::min<long>(512, (rows + 7) / 8));
+  // >= 8 rows (2 per wave, the second prefetched) per block; <= 4 blocks per CU
+  int G = (int)std::max<long>(1, std::min<long>(1024, (rows + 7) / 8));
   int rpb = (int)((rows + G - 1) / G);
   G = (int)((rows + rpb - 1) / rpb);
   hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(G), dim3(256), 0, st, (const __bf16*)dy,

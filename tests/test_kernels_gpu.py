@@ -125,6 +125,29 @@ def test_gemm(M, N, K, ta, tb):
     assert rel_err(acc, acc0 + ref32) < 2e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (300, 72, 200), (768, 256, 4096)])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
+def test_gemm_every_plan(M, N, K, ta, tb):
+    """Every (tile config x split-K) plan of the GEMM gives the same product: bf16 output with the
+    bias / ReLU epilogue, and fp32 accumulation into C (split-K atomics or the non-atomic
+    read-modify-write of splits == 1)."""
+    if (ta and M % 8) or (not ta and K % 8) or N % 8:
+        pytest.skip("layout constraint")
+    a = bf(K, M) if ta else bf(M, K)
+    b = bf(N, K) if tb else bf(K, N)
+    bias = torch.randn(N, device=dev)
+    ref = _ref.gemm(a.float(), b.float(), ta, tb, bias, "relu", torch.float32)
+    ref32 = _ref.gemm(a.float(), b.float(), ta, tb, None, "none", torch.float32)
+    for cfg in range(native().CONV_TILE_CONFIGS):
+        out = native().gemm(a, b, ta, tb, bias, "relu", torch.bfloat16, None, 0.0, cfg)
+        assert rel_err(out, ref) < 1e-2, cfg
+        for sp in (1, 2, 4):
+            acc = torch.randn(M, N, device=dev)
+            acc0 = acc.clone()
+            native().gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0, cfg + 16 * sp)
+            assert rel_err(acc - acc0, ref32) < 2e-3, (cfg, sp)
+
+
 def test_gemm_identity_asymmetric():
     # A = I with asymmetric B catches transposed C writes (cdna guide §3)
     M = 64
