@@ -645,7 +645,7 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
 
 // ------------------------------------------------------------------------------- loss / optim
 std::tuple<Tensor, Tensor> cross_entropy_fwd_bwd(Tensor logits, Tensor labels, double smoothing,
-                                                 int64_t ignore_index) {
+                                                 int64_t ignore_index, int64_t valid_cols) {
   check_act(logits, "logits");
   check_cuda(labels, "labels");
   c10::DeviceGuard g(logits.device());
@@ -657,7 +657,8 @@ std::tuple<Tensor, Tensor> cross_entropy_fwd_bwd(Tensor logits, Tensor labels, d
   auto work = torch::empty({4 + R}, logits.options().dtype(at::kInt));  // count + row losses
   mipipe::cross_entropy_fwd_bwd(logits.data_ptr(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
                                 grad.data_ptr(), R, V, (float)smoothing, ignore_index,
-                                work.data_ptr<int>(), stream(), is_f32(logits));
+                                work.data_ptr<int>(), stream(), is_f32(logits),
+                                (int)std::min<int64_t>(valid_cols > 0 ? valid_cols : V, V));
   return {loss, grad};
 }
 
@@ -829,9 +830,10 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> layernorm_bwd(
     pg = dg->data_ptr<float>();
     pb = db->data_ptr<float>();
   }
+  auto work = torch::empty({2 * (int64_t)mipipe::layernorm_bwd_blocks(rows), H}, o);
   mipipe::layernorm_bwd(dy.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                        gamma.data_ptr<float>(), dx.data_ptr(), pg, pb, nullptr, rows, (int)H,
-                        stream());
+                        gamma.data_ptr<float>(), dx.data_ptr(), pg, pb, work.data_ptr<float>(),
+                        rows, (int)H, stream());
   return {dx, dg, db};
 }
 
@@ -848,7 +850,7 @@ Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows) {
 }
 
 // out[c] (+)= Σ_rows x[:, c]; accumulates into ``out`` when given (e.g. a flat-grad view)
-Tensor colsum(Tensor x, optional<Tensor> out) {
+Tensor colsum(Tensor x, optional<Tensor> out, bool two_pass) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "colsum dtype");
@@ -862,7 +864,7 @@ Tensor colsum(Tensor x, optional<Tensor> out) {
     o = torch::zeros({cols}, x.options().dtype(at::kFloat));
   }
   optional<Tensor> work;
-  if (mipipe::g_deterministic)
+  if (mipipe::g_deterministic || two_pass)
     work = torch::empty({(int64_t)mipipe::colsum_blocks(rows, (int)cols), cols}, x.options().dtype(at::kFloat));
   mipipe::colsum_f32(x.data_ptr(), x.scalar_type() == at::kBFloat16, o.data_ptr<float>(), rows,
                      (int)cols, work.has_value() ? work->data_ptr<float>() : nullptr, stream());
@@ -1241,7 +1243,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("trans_a"), py::arg("trans_b"),
         py::arg("bias"), py::arg("act"), py::arg("out_dtype"), py::arg("c"), py::arg("beta"),
         py::arg("plan") = -1);
-  m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd);
+  m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd, py::arg("logits"), py::arg("labels"),
+        py::arg("smoothing"), py::arg("ignore_index"), py::arg("valid_cols") = -1);
   m.def("sgd_step", &sgd_step);
   m.def("adamw_step", &adamw_step);
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
@@ -1253,7 +1256,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("rstd"), py::arg("gamma"), py::arg("dgamma") = py::none(),
         py::arg("dbeta") = py::none());
   m.def("embedding_bwd", &embedding_bwd);
-  m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none());
+  m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(),
+        py::arg("two_pass") = false);
+  m.def("set_colsum_row_blocks", [](int v) { mipipe::g_colsum_row_blocks = v; });
   m.def("attention_fwd", &attention_fwd, py::arg("qkv"), py::arg("B"), py::arg("S"), py::arg("H"),
         py::arg("mask") = py::none(), py::arg("scale") = 0.125, py::arg("p_drop") = 0.0,
         py::arg("seed") = 0);

@@ -173,7 +173,7 @@ void avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st,
 // loss is bit-reproducible)
 void cross_entropy_fwd_bwd(const void* logits, const int64_t* labels, float* loss, void* grad,
                            int R, int V, float smoothing, int64_t ignore_index, int* work,
-                           hipStream_t st, bool f32 = false);
+                           hipStream_t st, bool f32 = false, int valid_cols = 0);
 // *correct += #rows whose first maximal logit is at the label (torch.argmax tie rule)
 void top1_correct(const void* logits, const int64_t* labels, int R, int V, int* correct,
                   hipStream_t st, bool f32 = false);
@@ -201,6 +201,7 @@ void layernorm_fwd(const void* x, const void* res, const float* gamma, const flo
 void layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd,
                    const float* gamma, void* dx, float* dgamma, float* dbeta, float* work,
                    long rows, int H, hipStream_t st);
+int layernorm_bwd_blocks(long rows);  // partial rows of layernorm_bwd's work
 void gelu_fwd(const void* x, void* y, long n, hipStream_t st);
 void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st);
 // Fused self-attention, head_dim 64, on the packed projection layout (attention.hip):
@@ -220,5 +221,6 @@ void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H
 void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
                 hipStream_t st);
 int colsum_blocks(long rows, int cols);
+extern int g_colsum_row_blocks;
 
 }  // namespace mipipe

@@ -39,12 +39,13 @@ __device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
   return r;
 }
 
-// one block per row; logits T (bf16 / fp32) [R][V]
+// one block per row; logits T (bf16 / fp32) [R][V] of which the first Vv columns are classes
+// (the rest: tile padding of the vocabulary, excluded from the softmax, gradient 0)
 template <class T>
 __global__ __launch_bounds__(256) void ce_kernel(const T* __restrict__ logits,
                                                  const int64_t* __restrict__ labels,
                                                  float* __restrict__ loss, T* __restrict__ grad,
-                                                 int V, float eps, int64_t ignore,
+                                                 int V, int Vv, float eps, int64_t ignore,
                                                  const int* __restrict__ nvalid,
                                                  float* __restrict__ rowloss) {
   __shared__ float sh[8];
@@ -61,12 +62,14 @@ __global__ __launch_bounds__(256) void ce_kernel(const T* __restrict__ logits,
       load8(x + c * 8, v);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        mx = fmaxf(mx, v[q]);
-        sx += v[q];
+        if (c * 8 + q < Vv) {
+          mx = fmaxf(mx, v[q]);
+          sx += v[q];
+        }
       }
     }
   } else {
-    for (int c = threadIdx.x; c < V; c += 256) {
+    for (int c = threadIdx.x; c < Vv; c += 256) {
       float v = (float)x[c];
       mx = fmaxf(mx, v);
       sx += v;
@@ -80,10 +83,11 @@ __global__ __launch_bounds__(256) void ce_kernel(const T* __restrict__ logits,
       float v[8];
       load8(x + c * 8, v);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) se += __expf(v[q] - mx);
+      for (int q = 0; q < 8; ++q)
+        if (c * 8 + q < Vv) se += __expf(v[q] - mx);
     }
   } else {
-    for (int c = threadIdx.x; c < V; c += 256) se += __expf((float)x[c] - mx);
+    for (int c = threadIdx.x; c < Vv; c += 256) se += __expf((float)x[c] - mx);
   }
   se = block_reduce(se, sh, false);
   const float lse = mx + __logf(se);
@@ -92,13 +96,13 @@ __global__ __launch_bounds__(256) void ce_kernel(const T* __restrict__ logits,
     float l = 0.f;
     if (valid) {
       float xl = (float)x[lab];
-      l = (1.f - eps) * (lse - xl) + eps * (lse - sx / (float)V);
+      l = (1.f - eps) * (lse - xl) + eps * (lse - sx / (float)Vv);
     }
     rowloss[row] = l * inv_n;
   }
   const float scale = valid ? inv_n : 0.f;
   const float inv_se = 1.f / se;
-  const float base_t = eps / (float)V;
+  const float base_t = eps / (float)Vv;
   if (vec) {
     for (int c = threadIdx.x; c < V / 8; c += 256) {
       float v[8];
@@ -107,14 +111,14 @@ __global__ __launch_bounds__(256) void ce_kernel(const T* __restrict__ logits,
       for (int q = 0; q < 8; ++q) {
         int col = c * 8 + q;
         float t = base_t + (col == lab ? 1.f - eps : 0.f);
-        v[q] = (__expf(v[q] - mx) * inv_se - t) * scale;
+        v[q] = col < Vv ? (__expf(v[q] - mx) * inv_se - t) * scale : 0.f;
       }
       store8(g + c * 8, v);
     }
   } else {
     for (int c = threadIdx.x; c < V; c += 256) {
       float t = base_t + (c == lab ? 1.f - eps : 0.f);
-      g[c] = (T)((__expf((float)x[c] - mx) * inv_se - t) * scale);
+      g[c] = (T)(c < Vv ? (__expf((float)x[c] - mx) * inv_se - t) * scale : 0.f);
     }
   }
 }
@@ -136,15 +140,16 @@ __global__ __launch_bounds__(256) void ce_sum_kernel(const float* __restrict__ r
 
 void cross_entropy_fwd_bwd(const void* logits, const int64_t* labels, float* loss, void* grad,
                            int R, int V, float smoothing, int64_t ignore_index, int* work,
-                           hipStream_t st, bool f32) {
+                           hipStream_t st, bool f32, int Vv) {
+  if (Vv <= 0 || Vv > V) Vv = V;
   float* rowloss = reinterpret_cast<float*>(work + 4);
   hipLaunchKernelGGL(ce_count_kernel, dim3(1), dim3(256), 0, st, labels, R, ignore_index, work);
   if (f32)
     hipLaunchKernelGGL(ce_kernel<float>, dim3(R), dim3(256), 0, st, (const float*)logits, labels,
-                       loss, (float*)grad, V, smoothing, ignore_index, (const int*)work, rowloss);
+                       loss, (float*)grad, V, Vv, smoothing, ignore_index, (const int*)work, rowloss);
   else
     hipLaunchKernelGGL(ce_kernel<__bf16>, dim3(R), dim3(256), 0, st, (const __bf16*)logits, labels,
-                       loss, (__bf16*)grad, V, smoothing, ignore_index, (const int*)work, rowloss);
+                       loss, (__bf16*)grad, V, Vv, smoothing, ignore_index, (const int*)work, rowloss);
   hipLaunchKernelGGL(ce_sum_kernel, dim3(1), dim3(256), 0, st, rowloss, R, loss);
 }
 
@@ -457,9 +462,14 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x,
   }
 }
 
+int g_colsum_row_blocks = 0;  // > 0: fixed row-block count (tuning experiments)
+
 static void colsum_grid(long rows, int cols, long& G, long& rpb) {
   const long chunks = (cols + kColsumChunk - 1) / kColsumChunk;
-  G = std::max<long>(1, std::min<long>(std::max<long>(1, 1024 / chunks), (rows + 15) / 16));
+  // measured (tools/r2/colsum_sweep.py): ~64-128 rows per block, <= ~1024 blocks
+  G = g_colsum_row_blocks > 0 ? g_colsum_row_blocks
+                              : std::min<long>((rows + 95) / 96, std::max<long>(1, 1024 / chunks));
+  G = std::max<long>(1, std::min<long>(G, (rows + 15) / 16));
   rpb = (rows + G - 1) / G;
   G = (rows + rpb - 1) / rpb;
 }
@@ -581,6 +591,7 @@ void layernorm_fwd(const void* x, const void* res, const float* gamma, const flo
 // Each wave walks rows w, w+4, ... of its block with the NEXT row's dy / x loads in flight while
 // it reduces the current one (the kernel is latency-bound otherwise: two dependent wave sums
 // per row); γ is held in registers for the whole block.
+template <int NCH>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __restrict__ dy,
                                                             const __bf16* __restrict__ x,
                                                             const float* __restrict__ mean,
@@ -592,9 +603,9 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
                                                             int H, int rows_per_block) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nc = H / 8;
-  float accg[LN_MAXC][8], accb[LN_MAXC][8], gam[LN_MAXC][8];
+  float accg[NCH][8], accb[NCH][8], gam[NCH][8];
 #pragma unroll
-  for (int k = 0; k < LN_MAXC; ++k) {
+  for (int k = 0; k < NCH; ++k) {
     const int c = lane + k * 64;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -604,11 +615,11 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
   }
   const long r0 = (long)blockIdx.x * rows_per_block;
   const long r1 = min(rows, r0 + rows_per_block);
-  uint4 ng[LN_MAXC], nx[LN_MAXC];
+  uint4 ng[NCH], nx[NCH];
   float nmu = 0.f, nrs = 0.f;
   auto fetch = [&](long row) {
 #pragma unroll
-    for (int k = 0; k < LN_MAXC; ++k) {
+    for (int k = 0; k < NCH; ++k) {
       const int c = lane + k * 64;
       if (c < nc) {
         ng[k] = *reinterpret_cast<const uint4*>(dy + row * H + c * 8);
@@ -621,9 +632,9 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
   if (r0 + w < r1) fetch(r0 + w);
   for (long row = r0 + w; row < r1; row += 4) {
     const float mu = nmu, rs = nrs;
-    float g[LN_MAXC][8], xh[LN_MAXC][8];
+    float g[NCH][8], xh[NCH][8];
 #pragma unroll
-    for (int k = 0; k < LN_MAXC; ++k) {
+    for (int k = 0; k < NCH; ++k) {
       if (lane + k * 64 < nc) {
         unpack8(ng[k], g[k]);
         unpack8(nx[k], xh[k]);
@@ -632,7 +643,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
     if (row + 4 < r1) fetch(row + 4);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < LN_MAXC; ++k) {
+    for (int k = 0; k < NCH; ++k) {
       if (lane + k * 64 < nc) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -648,7 +659,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
     s1 = wave_sum(s1) / (float)H;
     s2 = wave_sum(s2) / (float)H;
 #pragma unroll
-    for (int k = 0; k < LN_MAXC; ++k) {
+    for (int k = 0; k < NCH; ++k) {
       const int c = lane + k * 64;
       if (c < nc) {
         float o[8];
@@ -658,35 +669,57 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
       }
     }
   }
-  // block partials of dγ/dβ: the 4 waves reduce through LDS, one atomic per column per block
-  __shared__ float red[4][LN_MAXC * 64 * 8];
+  // block partials of dγ/dβ: the 4 waves reduce through LDS into this block's partial rows
+  // (pg / pb: [gridDim.x][H]); summed in a fixed order by det_sum_rows (no atomics: every
+  // block would otherwise contend on the same 2H addresses)
+  __shared__ float red[4][NCH * 64 * 8];
   for (int arr = 0; arr < 2; ++arr) {
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < LN_MAXC; ++k) {
+    for (int k = 0; k < NCH; ++k) {
       int c = lane + k * 64;
       if (c < nc)
 #pragma unroll
         for (int q = 0; q < 8; ++q) red[w][c * 8 + q] = arr == 0 ? accg[k][q] : accb[k][q];
     }
     __syncthreads();
-    float* dst = arr == 0 ? pg : pb;
+    float* dst = (arr == 0 ? pg : pb) + (long)blockIdx.x * H;
     for (int c = threadIdx.x; c < H; c += 256)
-      atomicAdd(dst + c, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+      dst[c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
   }
+}
+
+static void layernorm_bwd_grid(long rows, int& G, int& rpb) {
+  // >= 8 rows (2 per wave, the second prefetched) per block; <= 4 blocks per CU
+  G = (int)std::max<long>(1, std::min<long>(1024, (rows + 7) / 8));
+  rpb = (int)((rows + G - 1) / G);
+  G = (int)((rows + rpb - 1) / rpb);
+}
+
+int layernorm_bwd_blocks(long rows) {
+  int G, rpb;
+  layernorm_bwd_grid(rows, G, rpb);
+  return G;
 }
 
 void layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd,
                    const float* gamma, void* dx, float* dgamma, float* dbeta, float* work,
                    long rows, int H, hipStream_t st) {
-  // dgamma / dbeta are ACCUMULATED into (zeroed buffers or the flat gradient views)
-  // >= 8 rows (2 per wave, the second prefetched) per block; <= 4 blocks per CU
-  int G = (int)std::max<long>(1, std::min<long>(1024, (rows + 7) / 8));
-  int rpb = (int)((rows + G - 1) / G);
-  G = (int)((rows + rpb - 1) / rpb);
-  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(G), dim3(256), 0, st, (const __bf16*)dy,
-                     (const __bf16*)x, mean, rstd, gamma, (__bf16*)dx, dgamma, dbeta, rows, H,
-                     rpb);
+  // dgamma / dbeta are ACCUMULATED into (zeroed buffers or the flat gradient views) from the
+  // per-block partial rows in work ([2][layernorm_bwd_blocks(rows)][H])
+  int G, rpb;
+  layernorm_bwd_grid(rows, G, rpb);
+  float* wg = work;
+  float* wb = work + (long)G * H;
+  // register arrays sized for H: 2 chunks of 8 per lane up to H = 1024 (BERT-base), else 4
+  if (H <= 1024)
+    hipLaunchKernelGGL(layernorm_bwd_kernel<2>, dim3(G), dim3(256), 0, st, (const __bf16*)dy,
+                       (const __bf16*)x, mean, rstd, gamma, (__bf16*)dx, wg, wb, rows, H, rpb);
+  else
+    hipLaunchKernelGGL(layernorm_bwd_kernel<LN_MAXC>, dim3(G), dim3(256), 0, st,
+                       (const __bf16*)dy, (const __bf16*)x, mean, rstd, gamma, (__bf16*)dx, wg,
+                       wb, rows, H, rpb);
+  det_sum_rows(wg, wb, G, H, dgamma, dbeta, true, st);
 }
 
 // ------------------------------------------------------------------------------ dropout

@@ -161,6 +161,12 @@ class BertForMaskedLM(tnn.Module):
         self._step = 0
         self._vpad = (-c.vocab_size) % 64  # decoder N padded to the GEMM's 64-wide tiles
         self._init_weights()
+        if self._vpad:
+            # the flat parameter space (mipipe.optim) reserves zero rows behind the tied
+            # decoder weight / bias: the padded decoder operand is a view, not a per-step copy
+            vp = c.vocab_size + self._vpad
+            self.bert.embeddings.word_embeddings.weight._mipipe_pad_rows = vp
+            self.cls.predictions.bias._mipipe_pad_rows = vp
         self._register_state_dict_hook(_split_qkv_hook)
         self._register_load_state_dict_pre_hook(_merge_qkv_hook, with_module=True)
 
@@ -188,7 +194,7 @@ class BertForMaskedLM(tnn.Module):
                 masked_positions: Optional[torch.Tensor] = None,
                 labels: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Returns the MLM loss when ``labels`` is given (cross-entropy straight on the
-        tile-padded logits: the pad columns carry -30000 and never win), else the logits."""
+        tile-padded logits, the pad columns excluded), else the logits."""
         c = self.config
         B, S = input_ids.shape
         dt = self.activation_dtype(input_ids)
@@ -217,16 +223,35 @@ class BertForMaskedLM(tnn.Module):
         pr = self.cls.predictions
         t = pr.transform.dense(h, act="gelu")
         t = pr.transform.LayerNorm(t)
-        wd = emb.word_embeddings.compute_weight(dt)  # tied decoder
-        bias = pr.bias
-        if self._vpad:
-            # pad the vocabulary to the GEMM tile width with -inf-like logits (exact softmax)
-            wd = torch.cat([wd, wd.new_zeros(self._vpad, wd.shape[1])], 0)
-            bias = torch.cat([bias, bias.new_full((self._vpad,), -30000.0)])
-        logits = MF.linear(t, emb.word_embeddings.weight, wd, bias, "none")
+        wd, bias_c = self._decoder_operands(dt)  # tied decoder, vocabulary tile-padded
+        logits = MF.linear(t, emb.word_embeddings.weight, wd, pr.bias, "none", bias_c=bias_c)
         if labels is not None:
-            return MF.cross_entropy(logits, labels.reshape(-1), ignore_index=-100)
+            return MF.cross_entropy(logits, labels.reshape(-1), ignore_index=-100,
+                                    valid_cols=c.vocab_size)
         return logits[:, : c.vocab_size] if self._vpad else logits
+
+    def _decoder_operands(self, dt: torch.dtype):
+        """(decoder weight [Vp, H] in dtype dt, bias [Vp] fp32) with Vp = vocab rounded up to the
+        GEMM tile width.  Pad rows / entries are zeros; the loss masks the pad columns.  Views of
+        the flat parameter space's reserved pad rows when the optimizer built one (no copy),
+        else a padded copy (evaluation without an optimizer, CPU)."""
+        from mipipe.optim.flat import flat_space_for
+        wte = self.bert.embeddings.word_embeddings
+        bias = self.cls.predictions.bias
+        if not self._vpad:
+            return wte.compute_weight(dt), None
+        fs = flat_space_for(wte.weight)
+        if fs is not None and fs.padded_rows(wte.weight) and fs.padded_rows(bias) \
+                and flat_space_for(bias) is fs:
+            bias_c = fs.padded_view(fs.flat, bias)
+            if fs.shadow is not None and fs.shadow.dtype == dt:
+                fs.sync_shadow(wte.weight)
+                return fs.padded_view(fs.shadow, wte.weight), bias_c
+            if dt == torch.float32:
+                return fs.padded_view(fs.flat, wte.weight), bias_c
+        wd = wte.compute_weight(dt)
+        wd = torch.cat([wd, wd.new_zeros(self._vpad, wd.shape[1])], 0)
+        return wd, torch.cat([bias.detach(), bias.new_zeros(self._vpad)])
 
     def loss(self, logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         return MF.cross_entropy(logits.contiguous(), labels.reshape(-1), ignore_index=-100)

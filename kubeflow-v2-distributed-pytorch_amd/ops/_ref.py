@@ -177,8 +177,15 @@ def gemm(a: Tensor, b: Tensor, trans_a: bool, trans_b: bool, bias: Optional[Tens
 
 
 def cross_entropy_fwd_bwd(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0,
-                          ignore_index: int = -100) -> Tuple[Tensor, Tensor]:
-    """Mean CE over non-ignored rows and its gradient wrt logits (for grad_output = 1)."""
+                          ignore_index: int = -100,
+                          valid_cols: int = -1) -> Tuple[Tensor, Tensor]:
+    """Mean CE over non-ignored rows and its gradient wrt logits (for grad_output = 1).
+    ``valid_cols`` > 0: only the first columns are classes; the gradient of the rest is 0."""
+    V = logits.shape[-1]
+    if 0 < valid_cols < V:
+        loss, g = cross_entropy_fwd_bwd(logits[:, :valid_cols], labels, label_smoothing,
+                                        ignore_index)
+        return loss, torch.cat([g, g.new_zeros(g.shape[0], V - valid_cols)], 1)
     lf = _f(logits)
     valid = labels != ignore_index
     n = valid.sum().clamp_min(1)

@@ -30,16 +30,24 @@ Tensor = torch.Tensor
 
 
 # ----------------------------------------------------------------------------- conv
-def _direct_grad_target(p: Tensor):
+def _direct_grad_target(p: Tensor, rows: Optional[int] = None):
     """If ``p.grad`` is p's view in a flat gradient buffer, return (space, grad) so a kernel can
-    accumulate straight into it (the DDP bucket), else None."""
+    accumulate straight into it (the DDP bucket), else None.  ``rows``: the caller computes a
+    gradient with dim 0 padded to ``rows`` (a tile-padded vocabulary); the target is then the
+    space's padded view (the pad rows are reserved zeros in the flat buffers), or None."""
     from mipipe.optim.flat import flat_space_for
+    if not p.is_leaf:
+        return None
     fs = flat_space_for(p)
     g = p.grad
     if fs is None or g is None or not g.is_cuda:
         return None
     if g.data_ptr() != fs.flat_grad.data_ptr() + 4 * fs.offset(p):
         return None
+    if rows is not None and rows != p.shape[0]:
+        if fs.padded_rows(p) != rows:
+            return None
+        return fs, fs.padded_view(fs.flat_grad, p)
     return fs, g
 
 
@@ -599,15 +607,16 @@ def global_avg_pool(x: Tensor) -> Tensor:
 # ----------------------------------------------------------------------------- linear
 class _LinearFn(Function):
     @staticmethod
-    def forward(ctx, x, weight, w_c, bias, act):
+    def forward(ctx, x, weight, w_c, bias, act, bias_c):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
+        bk = bias if bias_c is None else bias_c  # bias_c: the kernel's (padded) bias vector
         if act == "gelu":
-            h = K.gemm(x2, w_c, False, True, bias, "none", x.dtype)
+            h = K.gemm(x2, w_c, False, True, bk, "none", x.dtype)
             y = K.gelu_fwd(h)
             ctx.save_for_backward(x2, w_c, h)
         else:
-            y = K.gemm(x2, w_c, False, True, bias, act, x.dtype)
+            y = K.gemm(x2, w_c, False, True, bk, act, x.dtype)
             ctx.save_for_backward(x2, w_c, y if act == "relu" else None)
         ctx.act, ctx.shp, ctx.has_bias = act, shp, bias is not None
         ctx.weight, ctx.bias = weight, bias
@@ -626,19 +635,21 @@ class _LinearFn(Function):
             dx = K.gemm(dy2, w_c, False, False, None, "none", dy2.dtype).reshape(ctx.shp)
         gdt = torch.float64 if dy2.dtype == torch.float64 else torch.float32
         if ctx.needs_input_grad[1]:
-            padded = w_c.shape[0] != ctx.weight.shape[0]  # e.g. vocab padded to the tile width
-            tgt = _direct_grad_target(ctx.weight) if K.use_native(dy2) and not padded else None
+            # w_c may carry more rows than the parameter (vocabulary padded to the tile width):
+            # then the target is the flat space's padded gradient view
+            tgt = _direct_grad_target(ctx.weight, w_c.shape[0]) if K.use_native(dy2) else None
             if tgt is not None:
                 fs, g = tgt
-                K.gemm(dy2, x2, True, False, None, "none", torch.float32, g, 1.0)
+                K.gemm(dy2, x2, True, False, None, "none", torch.float32,
+                       g.reshape(w_c.shape[0], -1), 1.0)
                 fs.grad_ready(ctx.weight)
             else:
                 dw = K.gemm(dy2, x2, True, False, None, "none", gdt)
-                if padded:
+                if w_c.shape[0] != ctx.weight.shape[0]:
                     dw = dw[: ctx.weight.shape[0]]
         if ctx.has_bias and ctx.needs_input_grad[3]:
-            tb = _direct_grad_target(ctx.bias) if K.use_native(dy2) else None
-            if tb is not None and tb[1].shape == (dy2.shape[1],):
+            tb = _direct_grad_target(ctx.bias, dy2.shape[1]) if K.use_native(dy2) else None
+            if tb is not None:
                 K.colsum(dy2, tb[1])
                 tb[0].grad_ready(ctx.bias)
             else:
@@ -646,32 +657,37 @@ class _LinearFn(Function):
                 if ctx.bias.shape[0] != db.shape[0]:
                     db = db[: ctx.bias.shape[0]]
                 db = db.to(gdt)
-        return dx, dw, None, db, None
+        return dx, dw, None, db, None, None
 
 
-def linear(x: Tensor, weight: Tensor, w_c: Tensor, bias: Optional[Tensor], act: str = "none"):
-    return _LinearFn.apply(x, weight, w_c, bias, act)
+def linear(x: Tensor, weight: Tensor, w_c: Tensor, bias: Optional[Tensor], act: str = "none",
+           bias_c: Optional[Tensor] = None):
+    """y = act(x @ w_c^T + bias).  ``weight`` / ``bias``: the parameters (gradient targets);
+    ``w_c``: the compute-dtype operand, ``bias_c``: the bias vector the kernel reads (both may
+    be padded along the output dimension — a vocabulary rounded up to the tile width)."""
+    return _LinearFn.apply(x, weight, w_c, bias, act, bias_c)
 
 
 # ----------------------------------------------------------------------------- loss
 class _CrossEntropyFn(Function):
     @staticmethod
-    def forward(ctx, logits, labels, label_smoothing, ignore_index):
+    def forward(ctx, logits, labels, label_smoothing, ignore_index, valid_cols):
         loss, grad = K.cross_entropy_fwd_bwd(logits.contiguous(), labels.contiguous(),
-                                             label_smoothing, ignore_index)
+                                             label_smoothing, ignore_index, valid_cols)
         ctx.save_for_backward(grad)
         return loss
 
     @staticmethod
     def backward(ctx, g):
         (grad,) = ctx.saved_tensors
-        return (grad * g.to(grad.dtype)), None, None, None
+        return (grad * g.to(grad.dtype)), None, None, None, None
 
 
 def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0,
-                  ignore_index: int = -100) -> Tensor:
-    """Fused log-softmax + NLL (mean) whose backward costs one scale."""
-    return _CrossEntropyFn.apply(logits, labels, label_smoothing, ignore_index)
+                  ignore_index: int = -100, valid_cols: int = -1) -> Tensor:
+    """Fused log-softmax + NLL (mean) whose backward costs one scale.  ``valid_cols``: classes
+    are the first columns only (tile-padded vocabulary)."""
+    return _CrossEntropyFn.apply(logits, labels, label_smoothing, ignore_index, int(valid_cols))
 
 
 # ----------------------------------------------------------------------------- transformer ops

@@ -224,10 +224,13 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, act="none", out_dtype=No
     return _ref.gemm(a, b, trans_a, trans_b, bias, act, out_dtype, c, beta)
 
 
-def cross_entropy_fwd_bwd(logits, labels, label_smoothing=0.0, ignore_index=-100):
+def cross_entropy_fwd_bwd(logits, labels, label_smoothing=0.0, ignore_index=-100, valid_cols=-1):
+    """``valid_cols``: only the first columns are classes (the rest pad a vocabulary to the GEMM
+    tile width: excluded from the softmax, gradient 0)."""
     if use_native(logits):
-        return native().cross_entropy_fwd_bwd(logits, labels, label_smoothing, ignore_index)
-    return _ref.cross_entropy_fwd_bwd(logits, labels, label_smoothing, ignore_index)
+        return native().cross_entropy_fwd_bwd(logits, labels, label_smoothing, ignore_index,
+                                              valid_cols)
+    return _ref.cross_entropy_fwd_bwd(logits, labels, label_smoothing, ignore_index, valid_cols)
 
 
 def top1_correct(logits, labels, out=None):

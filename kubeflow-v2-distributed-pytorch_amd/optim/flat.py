@@ -14,6 +14,11 @@ offset in all three.  Consequences on MI355X:
 
 Offsets are aligned to 64 elements (256 B) so every view starts on a 16-byte boundary for
 vectorised kernel access.
+
+A parameter tagged ``p._mipipe_pad_rows = R`` (R > p.shape[0]) gets R rows reserved: the extra
+rows are zeros in all three buffers (no gradient ever lands there, so the optimizer keeps them
+zero), and :meth:`FlatParamSpace.padded_view` exposes the [R, ...] view — e.g. a vocabulary
+embedding used as the tied MLM decoder, padded to the GEMM tile width without a per-step copy.
 """
 from __future__ import annotations
 
@@ -37,6 +42,19 @@ def _view(buf: torch.Tensor, off: int, like: torch.Tensor) -> torch.Tensor:
     return buf.as_strided(like.shape, like.stride(), buf.storage_offset() + off)
 
 
+def _pad_rows(p: torch.Tensor) -> Optional[int]:
+    r = getattr(p, "_mipipe_pad_rows", None)
+    if r is None or p.dim() == 0 or r <= p.shape[0] or not p.is_contiguous():
+        return None
+    return int(r)
+
+
+def _reserved(p: torch.Tensor) -> int:
+    r = _pad_rows(p)
+    n = p.numel() if r is None else r * (p.numel() // p.shape[0])
+    return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
 class FlatParamSpace:
     def __init__(self, params: Iterable[tnn.Parameter], shadow_dtype: Optional[torch.dtype] = None):
         self.params: List[tnn.Parameter] = [p for p in params]
@@ -55,7 +73,7 @@ class FlatParamSpace:
         off = 0
         for p in order:
             self.offsets[id(p)] = off
-            off += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
+            off += _reserved(p)
         self.numel = off
         self.device = dev
         self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
@@ -98,12 +116,26 @@ class FlatParamSpace:
             return None
         return _view(self.shadow, self.offsets[id(p)], p)
 
+    def padded_rows(self, p: torch.Tensor) -> Optional[int]:
+        """Rows reserved for ``p`` when it was registered padded (``_mipipe_pad_rows``)."""
+        return _pad_rows(p) if id(p) in self.offsets else None
+
+    def padded_view(self, buf: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
+        """[padded_rows, *p.shape[1:]] view of ``p``'s slot in ``buf`` (flat / flat_grad /
+        shadow); rows beyond p.shape[0] are the reserved zeros."""
+        r = self.padded_rows(p)
+        if r is None:
+            raise ValueError("parameter was not registered with padded rows")
+        o = self.offsets[id(p)]
+        n = r * (p.numel() // p.shape[0])
+        return buf[o: o + n].view(r, *p.shape[1:])
+
     def ranges(self) -> List[Tuple[int, int, tnn.Parameter]]:
         """(start, end_aligned, param) in flat order."""
         out = []
         for p in self.order:
             o = self.offsets[id(p)]
-            out.append((o, o + (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN, p))
+            out.append((o, o + _reserved(p), p))
         return out
 
     # ------------------------------------------------------------------ maintenance

@@ -133,3 +133,43 @@ def test_bert_base_training_step_reduces_loss():
         losses.append(loss.item())
     assert all(math.isfinite(v) for v in losses)
     assert losses[-1] < losses[0], losses
+
+
+def test_bert_padded_decoder_views_match_copy_path():
+    """The tied MLM decoder reads the vocabulary-padded weight / bias as views of the flat
+    parameter space's reserved pad rows (optimizer present) and writes its weight / bias
+    gradients straight into the padded flat-gradient views; without an optimizer it pads a
+    copy.  Both give the same loss and gradients, and the pad rows stay zero through steps."""
+    from mipipe.models import create_model
+    from mipipe.optim import AdamW
+    from mipipe.optim.flat import flat_space_for
+    torch.manual_seed(0)
+    kw = dict(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    m1 = create_model("bert_tiny", **kw).cuda()
+    m2 = create_model("bert_tiny", **kw).cuda()
+    m2.load_state_dict(m1.state_dict())
+    for m in (m1, m2):
+        m.compute_dtype = torch.bfloat16
+    opt = AdamW(m1.parameters(), lr=1e-3, weight_decay=0.01)
+    fs = flat_space_for(m1.bert.embeddings.word_embeddings.weight)
+    assert fs is not None and fs.padded_rows(m1.cls.predictions.bias) == 30528
+    B, S = 4, 64
+    ids = torch.randint(0, 30522, (B, S), device=dev)
+    pos = torch.stack([torch.randperm(S, device=dev)[:10] for _ in range(B)])
+    labels = torch.randint(0, 30522, (B * 10,), device=dev)
+    opt.zero_grad()
+    l1 = m1(ids, masked_positions=pos, labels=labels)
+    l2 = m2(ids, masked_positions=pos, labels=labels)
+    assert abs(l1.item() - l2.item()) < 1e-3
+    l1.backward()
+    l2.backward()
+    w1, w2 = m1.bert.embeddings.word_embeddings.weight, m2.bert.embeddings.word_embeddings.weight
+    b1, b2 = m1.cls.predictions.bias, m2.cls.predictions.bias
+    assert rel_err(w1.grad, w2.grad) < 1e-2 and rel_err(b1.grad, b2.grad) < 1e-2
+    for _ in range(2):
+        opt.step()
+        opt.zero_grad()
+        m1(ids, masked_positions=pos, labels=labels).backward()
+    for p in (w1, b1):
+        assert torch.count_nonzero(fs.padded_view(fs.flat, p)[p.shape[0]:]) == 0
+        assert torch.count_nonzero(fs.padded_view(fs.flat_grad, p)[p.shape[0]:]) == 0

@@ -120,3 +120,32 @@ def test_bert_trains_on_cpu():
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < losses[0]
+
+
+def test_padded_decoder_views_match_copy_path_cpu():
+    """Flat-space padded decoder views (optimizer present) vs the padded-copy path: same loss
+    and gradients; the reserved pad rows stay zero through optimizer steps."""
+    from mipipe.optim import AdamW
+    from mipipe.optim.flat import flat_space_for
+    torch.manual_seed(0)
+    kw = dict(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    m1, m2 = create_model("bert_tiny", **kw), create_model("bert_tiny", **kw)
+    m2.load_state_dict(m1.state_dict())
+    opt = AdamW(m1.parameters(), lr=1e-3, weight_decay=0.01)
+    fs = flat_space_for(m1.cls.predictions.bias)
+    assert fs.padded_rows(m1.bert.embeddings.word_embeddings.weight) == 30528
+    B, S = 2, 16
+    ids = torch.randint(0, 30522, (B, S))
+    pos = torch.stack([torch.randperm(S)[:3] for _ in range(B)])
+    labels = torch.randint(0, 30522, (B * 3,))
+    opt.zero_grad()
+    l1 = m1(ids, masked_positions=pos, labels=labels)
+    l2 = m2(ids, masked_positions=pos, labels=labels)
+    assert abs(l1.item() - l2.item()) < 1e-5
+    l1.backward()
+    l2.backward()
+    for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p1.grad, p2.grad, atol=1e-6, rtol=1e-4), n
+    opt.step()
+    for p in (m1.bert.embeddings.word_embeddings.weight, m1.cls.predictions.bias):
+        assert torch.count_nonzero(fs.padded_view(fs.flat, p)[p.shape[0]:]) == 0
