@@ -584,7 +584,7 @@ Tensor avgpool_bwd(Tensor dy, std::vector<int64_t> xs) {
 // ------------------------------------------------------------------------------- GEMM
 Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bias,
             std::string act, at::ScalarType out_dtype, optional<Tensor> c, double beta,
-            int64_t plan) {
+            int64_t plan, optional<Tensor> addend) {
   check_act(a, "A");
   check_same(b, a, "B");
   c10::DeviceGuard g(a.device());
@@ -625,14 +625,23 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
     TORCH_CHECK(act_i == 0, "fp32 gemm output has no activation epilogue");
   }
   const bool f32 = is_f32(a);
+  const void* add_p = nullptr;
+  if (addend.has_value()) {
+    TORCH_CHECK(mode == 0 && !trans_a && !trans_b && bias_p == nullptr && act_i == 0,
+                "gemm addend: activation-dtype output of A[M][K] @ B[K][N], no bias / act");
+    check_same(*addend, a, "addend");
+    TORCH_CHECK(addend->dim() == 2 && addend->size(0) == M && addend->size(1) == N &&
+                addend->is_contiguous(), "addend must be a contiguous [M, N] tensor");
+    add_p = addend->data_ptr();
+  }
   auto launch = [&](void* C, int p) {
     const int cfg = p < 0 ? -1 : p % tune::kPlanSplit;
     const int sp = p < 0 ? -1 : (p / tune::kPlanSplit > 0 ? p / tune::kPlanSplit : -1);
     mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b, C, N,
-                 (int)M, (int)N, (int)K, bias_p, act_i, mode, stream(), f32, cfg, sp);
+                 (int)M, (int)N, (int)K, bias_p, act_i, mode, stream(), f32, cfg, sp, add_p);
   };
   if (plan < 0) {
-    plan = tune::select_from(tune::gemm_key(M, N, K, !trans_a, trans_b, mode, f32),
+    plan = tune::select_from(tune::gemm_key(M, N, K, !trans_a, trans_b, add_p != nullptr ? 3 : mode, f32),
                              tune::gemm_candidates(f32, mode == 2), [&](int p) {
                                auto scratch = mode == 2 ? torch::zeros_like(out)
                                                         : torch::empty_like(out);
@@ -837,16 +846,23 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> layernorm_bwd(
   return {dx, dg, db};
 }
 
-Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows) {
+Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows, optional<Tensor> out) {
   check_bf16(dy, "dy");
   check_cuda(idx, "idx");
   c10::DeviceGuard g(dy.device());
   int64_t H = dy.size(-1), n = dy.numel() / H;
   TORCH_CHECK(idx.numel() == n && idx.scalar_type() == at::kLong, "embedding_bwd idx mismatch");
-  auto out = torch::zeros({num_rows, H}, dy.options().dtype(at::kFloat));
-  mipipe::embedding_bwd(dy.data_ptr(), idx.data_ptr<int64_t>(), out.data_ptr<float>(), n, (int)H,
-                        stream());
-  return out;
+  Tensor o;
+  if (out.has_value()) {  // accumulate into (e.g. the flat-gradient view of the table)
+    check_f32(*out, "out");
+    TORCH_CHECK(out->is_contiguous() && out->numel() == num_rows * H, "out must be [rows, H]");
+    o = *out;
+  } else {
+    o = torch::zeros({num_rows, H}, dy.options().dtype(at::kFloat));
+  }
+  mipipe::embedding_bwd(dy.data_ptr(), idx.data_ptr<int64_t>(), o.data_ptr<float>(), n, (int)H,
+                        (int)num_rows, stream());
+  return o;
 }
 
 // out[c] (+)= Σ_rows x[:, c]; accumulates into ``out`` when given (e.g. a flat-grad view)
@@ -1242,7 +1258,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("trans_a"), py::arg("trans_b"),
         py::arg("bias"), py::arg("act"), py::arg("out_dtype"), py::arg("c"), py::arg("beta"),
-        py::arg("plan") = -1);
+        py::arg("plan") = -1, py::arg("addend") = py::none());
   m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd, py::arg("logits"), py::arg("labels"),
         py::arg("smoothing"), py::arg("ignore_index"), py::arg("valid_cols") = -1);
   m.def("sgd_step", &sgd_step);
@@ -1255,7 +1271,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("mean"),
         py::arg("rstd"), py::arg("gamma"), py::arg("dgamma") = py::none(),
         py::arg("dbeta") = py::none());
-  m.def("embedding_bwd", &embedding_bwd);
+  m.def("embedding_bwd", &embedding_bwd, py::arg("dy"), py::arg("idx"), py::arg("num_rows"),
+        py::arg("out") = py::none());
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(),
         py::arg("two_pass") = false);
   m.def("set_colsum_row_blocks", [](int v) { mipipe::g_colsum_row_blocks = v; });

@@ -238,10 +238,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(FwdArgs a) {
   }
 }
 
-// δ[b,h,q] = Σ_d dO·O  (one thread per (token, head))
+// δ[b,h,q] = Σ_d dO·O  (one thread per (token, head)); also zeroes that (token, head)'s 64
+// fp32 dQ accumulators (the backward kernel adds into them) — no separate memset
 __global__ __launch_bounds__(256) void attn_delta_kernel(const __bf16* __restrict__ dout,
                                                          const __bf16* __restrict__ o,
-                                                         float* __restrict__ delta, int B, int S,
+                                                         float* __restrict__ delta,
+                                                         float* __restrict__ dq_acc, int B, int S,
                                                          int H) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)B * S * H) return;
@@ -260,6 +262,9 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const __bf16* __restric
     for (int e = 0; e < 8; ++e) acc += x[e] * y[e];
   }
   delta[((long)b * H + h) * S + q] = acc;
+  float4* dq = reinterpret_cast<float4*>(dq_acc + tok * H * D + h * D);
+#pragma unroll
+  for (int c = 0; c < D / 4; ++c) dq[c] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 struct BwdArgs {
@@ -473,8 +478,7 @@ void attention_bwd(const void* dout, const void* qkv, const void* o, const float
                    int H, float scale, float p_drop, uint32_t seed, hipStream_t st) {
   const long rows = (long)B * S * H;
   hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
-                     (const __bf16*)dout, (const __bf16*)o, delta, B, S, H);
-  hipMemsetAsync(dq_acc, 0, sizeof(float) * (size_t)B * S * H * attn::D, st);
+                     (const __bf16*)dout, (const __bf16*)o, delta, dq_acc, B, S, H);
   attn::BwdArgs a{(const __bf16*)qkv, (const __bf16*)dout, lse, delta, mask, dq_acc,
                   (__bf16*)dqkv, B, S, H, scale, scale * attn::kLog2e, p_drop,
                   drop_threshold(p_drop), seed};

@@ -21,7 +21,9 @@ namespace gk {
 __device__ __attribute__((aligned(64))) uint4 g_gemm_zero[8];
 constexpr int kGemmLoop = kLoopRawBarrier | kLoopPrio;
 
-// OUT: 0 activation dtype, 1 fp32 store / read-modify-write (e.rmw), 2 fp32 atomic (split-K)
+// OUT: 0 activation dtype, 1 fp32 store / read-modify-write (e.rmw), 2 fp32 atomic (split-K),
+// 3 activation dtype + e.addend (a same-shape tensor added in the epilogue: the second gradient
+// of a tensor consumed twice, e.g. a residual stream, without a separate add)
 template <class C, bool A_KC, bool B_KC, int OUT, class T>
 __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void gemm_dense_kernel(
     const T* __restrict__ A, long lda, const T* __restrict__ B, long ldb, uint32_t K,
@@ -31,7 +33,8 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void gemm_dense_ker
   typedef typename std::conditional<B_KC, KCDense<BN, T, NW>, MCDense<BN, T, NW>>::type OpB;
   typedef MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN, kGemmLoop> ML;
   constexpr int main_lds = ML::LDS_BYTES;
-  constexpr int epi_lds = OUT == 0 ? kEpiLdsBytes<BM, BN, T, C::WM>() : BM * (BN * 4 + 16);
+  constexpr int epi_lds =
+      (OUT == 0 || OUT == 3) ? kEpiLdsBytes<BM, BN, T, C::WM>() : BM * (BN * 4 + 16);
   __shared__ __attribute__((aligned(16))) char smem[main_lds > epi_lds ? main_lds : epi_lds];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -48,6 +51,7 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void gemm_dense_ker
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
   ML::type::run(smem, a, b, kt0, kt1, acc, wave, lane);
   if constexpr (OUT == 0) epilogue_out<BM, BN, false, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
+  else if constexpr (OUT == 3) epilogue_out<BM, BN, true, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
   else epilogue_f32<BM, BN, OUT == 2, C::WM, C::WN>(smem, acc, e, m0, n0, wave, lane);
 }
 
@@ -67,7 +71,10 @@ static void launch_out(const void* A, long lda, const void* B, long ldb, int K, 
   // a 256 x 256 fp32 tile does not fit the LDS: those tiles only serve out 0 (with_tile maps
   // the fp32-output modes to 256 x 128)
   constexpr bool kWide = C::BM * C::BN > 256 * 128;
-  if (out == 0) {
+  if (out == 3) {  // addend epilogue: instantiated for the data-grad layout (A [M][K], B [K][N])
+    if constexpr (AK && !BK_)
+      hipLaunchKernelGGL((gemm_dense_kernel<C, AK, BK_, 3, T>), grid, dim3(C::THREADS), 0, st, a, lda, b, ldb, (uint32_t)K, tN, per, e);
+  } else if (out == 0) {
     hipLaunchKernelGGL((gemm_dense_kernel<C, AK, BK_, 0, T>), grid, dim3(C::THREADS), 0, st, a, lda, b, ldb, (uint32_t)K, tN, per, e);
   } else if constexpr (!kWide) {
     if (out == 1)
@@ -127,15 +134,19 @@ static void gemm_t(const void* A, long lda, bool a_kc, const void* B, long ldb, 
     launch_tile<C, T>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, splits, st);
   };
   // fp32-output modes stage BM x BN fp32 in LDS: no 256 x 256 tile there
-  if (out == 0) with_tile<T, false>(cfg, go);
+  if (out == 0 || out == 3) with_tile<T, false>(cfg, go);
   else with_tile<T, true>(cfg, go);
 }
 
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
           long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
-          bool f32, int cfg, int splits) {
+          bool f32, int cfg, int splits, const void* addend) {
   EpiParams e{};
   e.C = C; e.ldc = ldc; e.M = (uint32_t)M; e.N = (uint32_t)N; e.bias = bias; e.act = act;
+  if (addend != nullptr && out == 0 && a_kc && !b_kc) {
+    e.addend = addend;
+    out = 3;
+  }
   if (f32) gemm_t<float>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st);
   else gemm_t<__bf16>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st);
 }

@@ -433,7 +433,7 @@ constexpr int kLoopRawBarrier = 1;  // lgkmcnt(0) + s_barrier instead of __synct
 constexpr int kLoopPrio = 2;        // s_setprio(1) around the MFMA block
 constexpr int kLoopSpread = 4;      // next stage's LDS-DMA pieces spread between MFMAs
 #ifndef MIPIPE_LOOP_DEFAULT
-#define MIPIPE_LOOP_DEFAULT 0
+#define MIPIPE_LOOP_DEFAULT 3
 #endif
 constexpr int kLoopDefault = MIPIPE_LOOP_DEFAULT;
 

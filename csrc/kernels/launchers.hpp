@@ -121,10 +121,11 @@ void avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho,
 //  (split-K atomics when splits > 1, else a non-atomic read-modify-write).
 //  f32: A and B are fp32 (split-bf16 main loop); out 0 then stores fp32 (the activation dtype).
 //  cfg: tile config id (conv_common.hpp table; -1 = heuristic); splits (out 2): > 0 forces the
-//  split-K count (1 = no split), -1 = heuristic.
+//  split-K count (1 = no split), -1 = heuristic.  addend (out 0, A [M][K], B [K][N] only): a
+//  [M][ldc] tensor of the output dtype added to the product in the epilogue.
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
           long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
-          bool f32 = false, int cfg = -1, int splits = -1);
+          bool f32 = false, int cfg = -1, int splits = -1, const void* addend = nullptr);
 int default_gemm_cfg(int M, int N, bool f32);
 
 // ---- BatchNorm ------------------------------------------------------------------------------
@@ -216,7 +217,8 @@ void attention_bwd(const void* dout, const void* qkv, const void* o, const float
 // Elementwise dropout keyed by (seed, element index): y = x * keep / (1 - p); the backward
 // recomputes the same keep mask from the seed (no mask tensor).
 void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStream_t st);
-void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, hipStream_t st);
+void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, int rows,
+                   hipStream_t st);
 // work (deterministic mode, else null): [colsum_blocks(rows, cols)][cols] floats of partials
 void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
                 hipStream_t st);

@@ -496,6 +496,10 @@ void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float
 }
 
 // ------------------------------------------------------------------------------ embedding grad
+// out[idx[r]][:] += dy[r][:] (out fp32, zeroed or the flat gradient view).  Large tables: one
+// fp32 atomic per element (rows rarely collide).  Small tables (token types, <= 8 rows): every
+// token hits the same few rows, so each block first reduces its tokens into an LDS copy of the
+// table (LDS atomics) and adds it to out once — thousands-way global contention otherwise.
 __global__ __launch_bounds__(256) void embedding_bwd_kernel(const __bf16* __restrict__ dy,
                                                             const int64_t* __restrict__ idx,
                                                             float* __restrict__ out, long n, int H) {
@@ -508,7 +512,33 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const __bf16* __rest
   }
 }
 
-void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, hipStream_t st) {
+constexpr int kEmbSmallRows = 8;
+
+__global__ __launch_bounds__(256) void embedding_bwd_small_kernel(
+    const __bf16* __restrict__ dy, const int64_t* __restrict__ idx, float* __restrict__ out,
+    long n, int H, int rows, long tok_per_block) {
+  extern __shared__ float tab[];  // [rows][H]
+  for (int i = threadIdx.x; i < rows * H; i += 256) tab[i] = 0.f;
+  __syncthreads();
+  const long t0 = (long)blockIdx.x * tok_per_block, t1 = min(n, t0 + tok_per_block);
+  for (long t = t0; t < t1; ++t) {
+    const long r = idx[t];
+    for (int c = threadIdx.x; c < H; c += 256) atomicAdd(&tab[r * H + c], (float)dy[t * H + c]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < rows * H; i += 256) atomicAdd(out + i, tab[i]);
+}
+
+void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, int rows,
+                   hipStream_t st) {
+  if (rows > 0 && rows <= kEmbSmallRows) {
+    const long G = std::max<long>(1, std::min<long>(256, (n + 31) / 32));
+    const long per = (n + G - 1) / G;
+    hipLaunchKernelGGL(embedding_bwd_small_kernel, dim3((unsigned)((n + per - 1) / per)),
+                       dim3(256), (size_t)rows * H * 4, st, (const __bf16*)dy, idx, out, n, H,
+                       rows, per);
+    return;
+  }
   hipLaunchKernelGGL(embedding_bwd_kernel, dim3(grid1d(n * H)), dim3(256), 0, st,
                      (const __bf16*)dy, idx, out, n, H);
 }

@@ -99,16 +99,19 @@ class BertLayer(tnn.Module):
     def forward(self, h: torch.Tensor, B: int, S: int, mask: Optional[torch.Tensor],
                 seeds) -> torch.Tensor:
         train = self.training
-        qkv = self.attention.self.qkv(h)
+        # h and h1 each feed a projection AND a post-LN residual: the LayerNorm backward hands
+        # the residual gradient to the projection, whose data-grad GEMM adds it (no extra add)
+        s_h, s_h1 = MF.ResidualSlot(), MF.ResidualSlot()
+        qkv = self.attention.self.qkv(h, res_take=s_h)
         ctx = MF.attention(qkv, B, S, self.heads, mask, p_drop=self.p_attn if train else 0.0,
                            seed=seeds[0])
         a = self.attention.output.dense(ctx)
         a = MF.dropout(a, self.p_hidden, seeds[1], train)
-        h1 = self.attention.output.LayerNorm(a, residual=h)
-        f = self.intermediate.dense(h1, act="gelu")
+        h1 = self.attention.output.LayerNorm(a, residual=h, res_give=s_h)
+        f = self.intermediate.dense(h1, act="gelu", res_take=s_h1)
         f2 = self.output.dense(f)
         f2 = MF.dropout(f2, self.p_hidden, seeds[2], train)
-        return self.output.LayerNorm(f2, residual=h1)
+        return self.output.LayerNorm(f2, residual=h1, res_give=s_h1)
 
 
 class _Encoder(tnn.Module):
@@ -161,6 +164,9 @@ class BertForMaskedLM(tnn.Module):
         self._step = 0
         self._vpad = (-c.vocab_size) % 64  # decoder N padded to the GEMM's 64-wide tiles
         self._init_weights()
+        # the tied decoder's weight-gradient GEMM runs before the embedding lookup's scatter in
+        # the backward: only the latter may report the shared gradient complete (DDP buckets)
+        self.bert.embeddings.word_embeddings.weight._mipipe_tied_later = True
         if self._vpad:
             # the flat parameter space (mipipe.optim) reserves zero rows behind the tied
             # decoder weight / bias: the padded decoder operand is a view, not a per-step copy

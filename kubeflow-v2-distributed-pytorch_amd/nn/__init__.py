@@ -249,10 +249,10 @@ class AdaptiveAvgPool2d(tnn.AdaptiveAvgPool2d):
 class Linear(ShadowMixin, tnn.Linear):
     """``torch.nn.Linear`` state; GEMM on the MFMA kernel with the bias in the epilogue."""
 
-    def forward(self, x: torch.Tensor, act: str = "none") -> torch.Tensor:
+    def forward(self, x: torch.Tensor, act: str = "none", res_take=None) -> torch.Tensor:
         w_c = self.compute_weight(x.dtype)
         b = None if self.bias is None else self.bias
-        return MF.linear(x, self.weight, w_c, b, act)
+        return MF.linear(x, self.weight, w_c, b, act, res_take=res_take)
 
 
 class Embedding(ShadowMixin, tnn.Embedding):
@@ -261,8 +261,9 @@ class Embedding(ShadowMixin, tnn.Embedding):
 
 
 class LayerNorm(tnn.LayerNorm):
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-        return MF.layer_norm(x, self.weight, self.bias, self.eps, residual)
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                res_give=None) -> torch.Tensor:
+        return MF.layer_norm(x, self.weight, self.bias, self.eps, residual, res_give)
 
 
 class Dropout(tnn.Dropout):

@@ -607,7 +607,7 @@ def global_avg_pool(x: Tensor) -> Tensor:
 # ----------------------------------------------------------------------------- linear
 class _LinearFn(Function):
     @staticmethod
-    def forward(ctx, x, weight, w_c, bias, act, bias_c):
+    def forward(ctx, x, weight, w_c, bias, act, bias_c, res_take):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         bk = bias if bias_c is None else bias_c  # bias_c: the kernel's (padded) bias vector
@@ -620,6 +620,7 @@ class _LinearFn(Function):
             ctx.save_for_backward(x2, w_c, y if act == "relu" else None)
         ctx.act, ctx.shp, ctx.has_bias = act, shp, bias is not None
         ctx.weight, ctx.bias = weight, bias
+        ctx.res_take = res_take
         return y.reshape(*shp[:-1], y.shape[-1])
 
     @staticmethod
@@ -632,7 +633,13 @@ class _LinearFn(Function):
             dy2 = (dy2.float() * (aux > 0)).to(dy2.dtype)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = K.gemm(dy2, w_c, False, False, None, "none", dy2.dtype).reshape(ctx.shp)
+            # the input's other gradient (residual stream), handed over by the consumer that ran
+            # first, is added in the data-grad GEMM's epilogue
+            add = ctx.res_take.take() if ctx.res_take is not None else None
+            if add is not None:
+                add = add.reshape(-1, add.shape[-1]).to(dy2.dtype).contiguous()
+            dx = K.gemm(dy2, w_c, False, False, None, "none", dy2.dtype,
+                        addend=add).reshape(ctx.shp)
         gdt = torch.float64 if dy2.dtype == torch.float64 else torch.float32
         if ctx.needs_input_grad[1]:
             # w_c may carry more rows than the parameter (vocabulary padded to the tile width):
@@ -642,7 +649,11 @@ class _LinearFn(Function):
                 fs, g = tgt
                 K.gemm(dy2, x2, True, False, None, "none", torch.float32,
                        g.reshape(w_c.shape[0], -1), 1.0)
-                fs.grad_ready(ctx.weight)
+                # a tied weight (``_mipipe_tied_later``: an MLM decoder sharing the input
+                # embedding) gets another contribution later in the backward — that writer
+                # reports it ready, else DDP would all-reduce a partial gradient
+                if not getattr(ctx.weight, "_mipipe_tied_later", False):
+                    fs.grad_ready(ctx.weight)
             else:
                 dw = K.gemm(dy2, x2, True, False, None, "none", gdt)
                 if w_c.shape[0] != ctx.weight.shape[0]:
@@ -657,15 +668,17 @@ class _LinearFn(Function):
                 if ctx.bias.shape[0] != db.shape[0]:
                     db = db[: ctx.bias.shape[0]]
                 db = db.to(gdt)
-        return dx, dw, None, db, None, None
+        return dx, dw, None, db, None, None, None
 
 
 def linear(x: Tensor, weight: Tensor, w_c: Tensor, bias: Optional[Tensor], act: str = "none",
-           bias_c: Optional[Tensor] = None):
+           bias_c: Optional[Tensor] = None, res_take: Optional["ResidualSlot"] = None):
     """y = act(x @ w_c^T + bias).  ``weight`` / ``bias``: the parameters (gradient targets);
     ``w_c``: the compute-dtype operand, ``bias_c``: the bias vector the kernel reads (both may
-    be padded along the output dimension — a vocabulary rounded up to the tile width)."""
-    return _LinearFn.apply(x, weight, w_c, bias, act, bias_c)
+    be padded along the output dimension — a vocabulary rounded up to the tile width).
+    ``res_take``: x is also consumed elsewhere (a residual stream); that consumer's gradient
+    wrt x, handed over through the slot, is added in this layer's data-grad GEMM."""
+    return _LinearFn.apply(x, weight, w_c, bias, act, bias_c, res_take)
 
 
 # ----------------------------------------------------------------------------- loss
@@ -693,11 +706,12 @@ def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0,
 # ----------------------------------------------------------------------------- transformer ops
 class _LayerNormFn(Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps, residual):
+    def forward(ctx, x, gamma, beta, eps, residual, res_give):
         y, mean, rstd, xs = K.layernorm_fwd(x, gamma, beta, eps, residual)
         ctx.save_for_backward(x if xs is None else xs, mean, rstd, gamma)
         ctx.beta = beta
         ctx.has_res = residual is not None
+        ctx.res_give = res_give
         return y
 
     @staticmethod
@@ -709,18 +723,25 @@ class _LayerNormFn(Function):
             if tg is not None and tb is not None:
                 acc = (tg[1], tb[1])
         dx, dgamma, dbeta = K.layernorm_bwd(dy.contiguous(), x, mean, rstd, gamma, acc)
+        dres = None
+        if ctx.has_res:
+            # d/d residual = d/dx; handed to the residual's other consumer when it fuses the add
+            dres = ctx.res_give.produce(dx) if ctx.res_give is not None else dx
         if acc is not None:
             fs = _direct_grad_target(gamma)[0]
             fs.grad_ready(gamma)
             fs.grad_ready(ctx.beta)
-            return dx, None, None, None, (dx if ctx.has_res else None)
-        return dx, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), None, (dx if ctx.has_res else None)
+            return dx, None, None, None, dres, None
+        return dx, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), None, dres, None
 
 
 def layer_norm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float = 1e-12,
-               residual: Optional[Tensor] = None) -> Tensor:
-    """LN(x [+ residual]) — the BERT post-LN residual add fused into the norm."""
-    return _LayerNormFn.apply(x, gamma, beta, eps, residual)
+               residual: Optional[Tensor] = None,
+               res_give: Optional["ResidualSlot"] = None) -> Tensor:
+    """LN(x [+ residual]) — the BERT post-LN residual add fused into the norm.  ``res_give``:
+    the residual's gradient goes to the slot (for the residual's other consumer to add in its
+    own kernel) instead of through autograd."""
+    return _LayerNormFn.apply(x, gamma, beta, eps, residual, res_give)
 
 
 class _GeluFn(Function):
@@ -796,11 +817,18 @@ class _EmbeddingFn(Function):
     def forward(ctx, idx, weight, w_c):
         ctx.save_for_backward(idx)
         ctx.rows = weight.shape[0]
+        ctx.weight = weight
         return w_c[idx]
 
     @staticmethod
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
+        if ctx.needs_input_grad[1] and K.use_native(dy):
+            tgt = _direct_grad_target(ctx.weight)
+            if tgt is not None:  # scatter straight into the flat gradient buffer
+                K.embedding_bwd(dy.contiguous(), idx, ctx.rows, tgt[1])
+                tgt[0].grad_ready(ctx.weight)
+                return None, None, None
         return None, K.embedding_bwd(dy.contiguous(), idx, ctx.rows), None
 
 

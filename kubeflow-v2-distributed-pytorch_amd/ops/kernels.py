@@ -195,7 +195,21 @@ def _pad2(t, r, c):
 
 
 def gemm(a, b, trans_a=False, trans_b=False, bias=None, act="none", out_dtype=None, c=None,
-         beta=0.0):
+         beta=0.0, addend=None):
+    """act(op(a) @ op(b) + bias) [+ beta * c] [+ addend]; ``addend`` (same shape / dtype as the
+    output; a @ b form, no bias / act) is added in the GEMM epilogue."""
+    if addend is not None:
+        M = a.shape[1] if trans_a else a.shape[0]
+        N = b.shape[0] if trans_b else b.shape[1]
+        Kd = a.shape[0] if trans_a else a.shape[1]
+        fusable = (use_native(a) and not trans_a and not trans_b and bias is None
+                   and act == "none" and c is None and (out_dtype in (None, a.dtype))
+                   and M % 8 == 0 and N % 8 == 0 and Kd % 8 == 0
+                   and addend.dtype == a.dtype and addend.is_contiguous())
+        if fusable:
+            return native().gemm(a, b, False, False, None, "none", a.dtype, None, 0.0, -1,
+                                 addend.reshape(M, N))
+        return gemm(a, b, trans_a, trans_b, bias, act, out_dtype, c, beta) + addend.reshape(M, N)
     if use_native(a):
         odt = out_dtype if out_dtype is not None else a.dtype
         M = a.shape[1] if trans_a else a.shape[0]
@@ -314,10 +328,16 @@ def dropout_fwd(x, p, seed):
     return _ref.dropout_fwd(x, p, seed)
 
 
-def embedding_bwd(dy, idx, num_rows):
+def embedding_bwd(dy, idx, num_rows, out=None):
+    """Scatter-add of dy rows into a [num_rows, H] fp32 table gradient (``out``: accumulate into
+    it, e.g. the parameter's flat-gradient view; else a fresh zeroed tensor)."""
     if use_native(dy):
-        return native().embedding_bwd(dy, idx, num_rows)
-    return _ref.embedding_bwd(dy, idx, num_rows)
+        return native().embedding_bwd(dy, idx, num_rows, out)
+    g = _ref.embedding_bwd(dy, idx, num_rows)
+    if out is not None:
+        out.add_(g.to(out.dtype))
+        return out
+    return g
 
 
 def gelu_fwd(x):

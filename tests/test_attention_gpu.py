@@ -173,3 +173,29 @@ def test_bert_padded_decoder_views_match_copy_path():
     for p in (w1, b1):
         assert torch.count_nonzero(fs.padded_view(fs.flat, p)[p.shape[0]:]) == 0
         assert torch.count_nonzero(fs.padded_view(fs.flat_grad, p)[p.shape[0]:]) == 0
+
+
+def test_tied_embedding_reported_ready_only_when_complete():
+    """The MLM decoder and the input embedding share one weight; both write its gradient
+    straight into the flat buffer.  The readiness signal DDP buckets wait for must come after
+    the LAST contribution: the gradient seen at notification time equals the final one."""
+    from mipipe.models import create_model
+    from mipipe.optim import AdamW
+    from mipipe.optim.flat import flat_space_for
+    torch.manual_seed(0)
+    m = create_model("bert_tiny", hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0).cuda()
+    m.compute_dtype = torch.bfloat16
+    opt = AdamW(m.parameters(), lr=1e-3)  # owns the flat space (kept alive)
+    w = m.bert.embeddings.word_embeddings.weight
+    fs = flat_space_for(w)
+    seen = []
+    fs.add_ready_listener(lambda p: seen.append(fs.grad_view(p).clone()) if p is w else None)
+    B, S = 4, 64
+    ids = torch.randint(0, 30522, (B, S), device=dev)
+    pos = torch.stack([torch.randperm(S, device=dev)[:10] for _ in range(B)])
+    labels = torch.randint(0, 30522, (B * 10,), device=dev)
+    fs.zero_grad()
+    m(ids, masked_positions=pos, labels=labels).backward()
+    assert len(seen) == 1
+    assert torch.equal(seen[0], w.grad)
+    del opt

@@ -148,6 +148,17 @@ def test_gemm_every_plan(M, N, K, ta, tb):
             assert rel_err(acc - acc0, ref32) < 2e-3, (cfg, sp)
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (4096, 768, 3072), (200, 64, 136)])
+def test_gemm_addend_epilogue(M, N, K):
+    """dx = dy @ W + addend in one GEMM (the residual-stream gradient fused into the data-grad
+    epilogue), for every tile config."""
+    a, b, add = bf(M, K), bf(K, N, scale=0.05), bf(M, N)
+    ref = a.float() @ b.float() + add.float()
+    for cfg in range(native().CONV_TILE_CONFIGS):
+        out = native().gemm(a, b, False, False, None, "none", torch.bfloat16, None, 0.0, cfg, add)
+        assert rel_err(out, ref) < 1e-2, cfg
+
+
 def test_gemm_identity_asymmetric():
     # A = I with asymmetric B catches transposed C writes (cdna guide §3)
     M = 64
