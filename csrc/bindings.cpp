@@ -366,20 +366,35 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
   } else {
     dw = torch::zeros({s.Co, kh, kw, s.Ci}, x.options().dtype(at::kFloat));
   }
-  if (cfg < 0) {
-    cfg = tune::select(tune::key("wgrad", s), s.f32, true, [&](int c) {
+  // plan = tile id + 16 * split count (0: heuristic split)
+  int plan = cfg;
+  if (plan < 0) {
+    std::vector<int> cands;
+    for (int t : tune::candidates(s.f32, true))
+      for (int sp : {0, 1, 2, 4, 8, 16}) cands.push_back(t + tune::kPlanSplit * sp);
+    plan = tune::select_from(tune::key("wgrad", s), cands, [&](int p) {
       auto dws = torch::zeros_like(dw);
-      mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dws.data_ptr<float>(), s, stream(), c);
+      const int sp = p / tune::kPlanSplit;
+      mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dws.data_ptr<float>(), s, stream(),
+                         p % tune::kPlanSplit, nullptr, sp > 0 ? sp : -1);
     });
   }
+  const int tile = plan < 0 ? -1 : plan % tune::kPlanSplit;
+  const int sp = plan < 0 ? -1 : (plan / tune::kPlanSplit > 0 ? plan / tune::kPlanSplit : -1);
   if (mipipe::g_deterministic) {
-    const int splits = mipipe::conv_wgrad_splits(s, cfg);
+    const int splits = mipipe::conv_wgrad_splits(s, tile, sp);
+    if (splits == 1) {  // one writer per element: the plain read-modify-write is deterministic
+      mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), tile,
+                         nullptr, 1);
+      return dw;
+    }
     auto ws = torch::empty({splits, (int64_t)s.Co * kh * kw * s.Ci}, dy.options().dtype(at::kFloat));
-    mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), cfg,
-                       ws.data_ptr<float>());
+    mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), tile,
+                       ws.data_ptr<float>(), sp);
     return dw;
   }
-  mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), cfg);
+  mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), tile,
+                     nullptr, sp);
   return dw;
 }
 

@@ -17,6 +17,7 @@ namespace mipipe {
 namespace {
 
 constexpr int kT = 256;
+constexpr int kRowU = 4;  // rows per thread-iteration of bn_bwd_reduce (loads in flight)
 
 struct RowMap {
   int tpr;   // threads per row (C/8), capped at 256 per pass
@@ -229,27 +230,40 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
           is2[q] = invstd2[c0 + q];
         }
       }
-      for (long row = (long)blockIdx.x * mp.rpb + rg; row < M; row += (long)gridDim.x * mp.rpb) {
-        long off = row * C + c0;
-        float g[8], yv[8];
-        load8(dz + off, g);
-        if (relu) {
-          float zv[8];
-          load8(z + off, zv);
+      const long stride = (long)gridDim.x * mp.rpb;
+      for (long row0 = (long)blockIdx.x * mp.rpb + rg; row0 < M; row0 += kRowU * stride) {
+        Raw8<T> rg_[kRowU], rz[kRowU], ry[kRowU], ry2[kRowU];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) g[q] = zv[q] > 0.f ? g[q] : 0.f;
+        for (int u = 0; u < kRowU; ++u) {
+          const long off = min(row0 + u * stride, M - 1) * C + c0;
+          rg_[u] = ld_raw8(dz + off);
+          if (relu) rz[u] = ld_raw8(z + off);
+          ry[u] = ld_raw8(y + off);
+          if (TWO) ry2[u] = ld_raw8(y2 + off);
         }
-        load8(y + off, yv);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          sg[q] += g[q];
-          sx[q] += g[q] * (yv[q] - mu[q]) * is[q];
-        }
-        if (TWO) {
-          float y2v[8];
-          load8(y2 + off, y2v);
+        for (int u = 0; u < kRowU; ++u) {
+          if (row0 + u * stride >= M) break;
+          float g[8], yv[8];
+          unpack_raw(rg_[u], g);
+          if (relu) {
+            float zv[8];
+            unpack_raw(rz[u], zv);
 #pragma unroll
-          for (int q = 0; q < 8; ++q) sx2[q] += g[q] * (y2v[q] - mu2[q]) * is2[q];
+            for (int q = 0; q < 8; ++q) g[q] = zv[q] > 0.f ? g[q] : 0.f;
+          }
+          unpack_raw(ry[u], yv);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            sg[q] += g[q];
+            sx[q] += g[q] * (yv[q] - mu[q]) * is[q];
+          }
+          if (TWO) {
+            float y2v[8];
+            unpack_raw(ry2[u], y2v);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sx2[q] += g[q] * (y2v[q] - mu2[q]) * is2[q];
+          }
         }
       }
     }

@@ -135,7 +135,9 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_dgrad_ker
   epilogue_out<BM, BN, true, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
-template <class C, bool DENSE, class T>
+// ATOMIC: split-K partial tiles added with fp32 atomics; else the block owns its output tile
+// (no split) and adds it with a plain read-modify-write (e.rmw) or writes a workspace slice
+template <class C, bool DENSE, class T, bool ATOMIC = true>
 __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_wgrad_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, ConvGeom g, uint32_t tilesN,
     int kt_per_split, EpiParams e) {
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_wgrad_ker
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
   MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN>::type::run(smem, a, b, kt0, kt1, acc,
                                                                     wave, lane);
-  epilogue_f32<BM, BN, true, C::WM, C::WN>(smem, acc, e, m0, n0, wave, lane);
+  epilogue_f32<BM, BN, ATOMIC, C::WM, C::WN>(smem, acc, e, m0, n0, wave, lane);
 }
 
 }  // namespace gk

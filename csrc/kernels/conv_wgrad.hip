@@ -1,5 +1,6 @@
 // Convolution weight-grad: dw[Co][(kh,kw,ci)] += dy^T im2col(x), split-K over output pixels with
-// fp32 atomics into the (flat DDP bucket) gradient.
+// fp32 atomics into the (flat DDP bucket) gradient — or, unsplit, one block per output tile with
+// a plain read-modify-write (no atomics).  The (tile, split count) plan is tuned per shape.
 #include "conv_common.hpp"
 
 namespace mipipe {
@@ -22,23 +23,24 @@ static int resolve_wgrad_cfg(const ConvShape& s, int cfg) {
 }
 
 template <class C>
-static void wgrad_grid(const ConvShape& s, uint32_t& tN, uint32_t& tiles, int& splits, int& per) {
+static void wgrad_grid(const ConvShape& s, uint32_t& tN, uint32_t& tiles, int& splits, int& per,
+                       int splits_req) {
   const uint32_t Ntot = (uint32_t)(s.KH * s.KW * s.Ci);
   const int nk = (int)cdiv((uint64_t)s.N * s.Ho * s.Wo, BK);
   tN = cdiv(Ntot, C::BN);
   tiles = cdiv(s.Co, C::BM) * tN;
-  splits = pick_splits(tiles, nk, s.Ci);
+  splits = splits_req > 0 ? std::min(splits_req, nk) : pick_splits(tiles, nk, s.Ci);
   per = (int)cdiv(nk, splits);
   splits = (int)cdiv(nk, per);
 }
 
-int conv_wgrad_splits(const ConvShape& s, int cfg) {
+int conv_wgrad_splits(const ConvShape& s, int cfg, int splits_req) {
   cfg = resolve_wgrad_cfg(s, cfg);
   int splits = 1;
   auto f = [&](auto tile) {
     uint32_t tN, tiles;
     int per;
-    wgrad_grid<decltype(tile)>(s, tN, tiles, splits, per);
+    wgrad_grid<decltype(tile)>(s, tN, tiles, splits, per, splits_req);
   };
   if (s.f32) with_tile<float, true>(cfg, f);
   else with_tile<__bf16, true>(cfg, f);
@@ -47,7 +49,7 @@ int conv_wgrad_splits(const ConvShape& s, int cfg) {
 
 template <class T>
 static void conv_wgrad_t(const void* dy, const void* x, float* dw, const ConvShape& s,
-                         hipStream_t st, int cfg, float* ws) {
+                         hipStream_t st, int cfg, float* ws, int splits_req) {
   ConvGeom g = make_geom(s);
   const uint32_t Ntot = (uint32_t)(s.KH * s.KW * s.Ci);
   EpiParams e{};
@@ -65,21 +67,29 @@ static void conv_wgrad_t(const void* dy, const void* x, float* dw, const ConvSha
     typedef decltype(tile) C;
     uint32_t tN, tiles;
     int splits, per;
-    wgrad_grid<C>(s, tN, tiles, splits, per);
+    wgrad_grid<C>(s, tN, tiles, splits, per, splits_req);
     splits_used = splits;
     const dim3 grid(tiles, splits), block(C::THREADS);
-    if (dense)
-      hipLaunchKernelGGL((conv_wgrad_kernel<C, true, T>), grid, block, 0, st, dyp, xp, g, tN, per, e);
-    else
-      hipLaunchKernelGGL((conv_wgrad_kernel<C, false, T>), grid, block, 0, st, dyp, xp, g, tN, per, e);
+    EpiParams ee = e;
+    // unsplit (and not the deterministic workspace path): the block owns its output tile ->
+    // non-atomic read-modify-write; the ATOMIC template also carries the workspace-slice store
+    const bool atomic = splits > 1 || ws != nullptr;
+    if (!atomic) ee.rmw = 1;
+    if (dense) {
+      if (atomic) hipLaunchKernelGGL((conv_wgrad_kernel<C, true, T, true>), grid, block, 0, st, dyp, xp, g, tN, per, ee);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<C, true, T, false>), grid, block, 0, st, dyp, xp, g, tN, per, ee);
+    } else {
+      if (atomic) hipLaunchKernelGGL((conv_wgrad_kernel<C, false, T, true>), grid, block, 0, st, dyp, xp, g, tN, per, ee);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<C, false, T, false>), grid, block, 0, st, dyp, xp, g, tN, per, ee);
+    }
   });
   if (ws != nullptr) splitk_sum(ws, splits_used, (long)s.Co * Ntot, dw, st);
 }
 
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
-                int cfg, float* ws) {
-  if (s.f32) conv_wgrad_t<float>(dy, x, dw, s, st, cfg, ws);
-  else conv_wgrad_t<__bf16>(dy, x, dw, s, st, cfg, ws);
+                int cfg, float* ws, int splits) {
+  if (s.f32) conv_wgrad_t<float>(dy, x, dw, s, st, cfg, ws, splits);
+  else conv_wgrad_t<__bf16>(dy, x, dw, s, st, cfg, ws, splits);
 }
 
 }  // namespace mipipe

@@ -67,13 +67,14 @@ struct DgradFusion {
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
                 const DgradFusion* fz = nullptr, int cfg = -1);
 int conv_dgrad_tiles_m(const ConvShape& s, int cfg);  // M-tiles over all stride classes
-// dw is ACCUMULATED into with fp32 atomics (split-K): pass a zeroed buffer, or the parameter's
-// gradient buffer to fuse autograd's accumulation (gradient lands directly in the DDP bucket)
-//  ws != nullptr (deterministic mode): [conv_wgrad_splits(s, cfg)][Co*KH*KW*Ci] workspace for the
-//  split-K partials, summed into dw in split order.
+// dw is ACCUMULATED into (split-K fp32 atomics, or a plain read-modify-write when unsplit): pass
+// a zeroed buffer, or the parameter's gradient buffer to fuse autograd's accumulation (gradient
+// lands directly in the DDP bucket).  splits: > 0 forces the split-K count, -1 = heuristic.
+//  ws != nullptr (deterministic mode): [conv_wgrad_splits(s, cfg, splits)][Co*KH*KW*Ci] workspace
+//  for the split-K partials, summed into dw in split order.
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
-                int cfg = -1, float* ws = nullptr);
-int conv_wgrad_splits(const ConvShape& s, int cfg);
+                int cfg = -1, float* ws = nullptr, int splits = -1);
+int conv_wgrad_splits(const ConvShape& s, int cfg, int splits = -1);
 
 // ---- direct convolution, BatchNorm for any C, k x k average pool (vision.hip) ----------------
 struct GConvShape {

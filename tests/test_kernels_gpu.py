@@ -445,9 +445,13 @@ def test_conv_every_tile_config(cfg, case):
     assert rel_err(sg, grb.reshape(-1, Ci).sum(0)) < 5e-3
     xhat = (yin.float() - mean) * invstd
     assert rel_err(sgx, (grb * xhat).reshape(-1, Ci).sum(0)) < 5e-3
-    dw = native().conv_wgrad(dy, x, k, k, s, p, cfg=cfg)
     dwr = _ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)
-    assert rel_err(dw, dwr) < 5e-3
+    for sp in (0, 1, 3):  # weight-grad plans: heuristic split, unsplit (read-modify-write), 3-way
+        dw = native().conv_wgrad(dy, x, k, k, s, p, cfg=cfg + 16 * sp)
+        assert rel_err(dw, dwr) < 5e-3, sp
+        acc = torch.ones_like(dw)
+        native().conv_wgrad(dy, x, k, k, s, p, acc, cfg=cfg + 16 * sp)
+        assert rel_err(acc - 1, dwr) < 5e-3, sp
 
 
 def test_tile_benchmark_mode_picks_and_caches():
