@@ -248,7 +248,8 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
 Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride, int pad,
                   optional<Tensor> addend, optional<Tensor> bn_y, optional<Tensor> bn_mean,
                   optional<Tensor> bn_invstd, optional<Tensor> bn_scale, optional<Tensor> bn_bias,
-                  optional<Tensor> bn_rep, optional<Tensor> bn_z, int pad_w, int cfg) {
+                  optional<Tensor> bn_rep, optional<Tensor> bn_z, int pad_w, int cfg,
+                  optional<Tensor> bn_mask) {
   check_act(dy, "dy");
   check_same(w, dy, "w");
   c10::DeviceGuard g(dy.device());
@@ -291,6 +292,12 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     fz.bn_mean = bn_mean->data_ptr<float>(); fz.bn_invstd = bn_invstd->data_ptr<float>();
     fz.bn_scale = bn_scale->data_ptr<float>(); fz.bn_bias = bn_bias->data_ptr<float>();
     fz.bn_rep = bn_rep->data_ptr<float>();
+    if (bn_mask.has_value()) {  // the ReLU mask as bits, written by bn_act_fwd
+      check_cuda(*bn_mask, "bn_mask");
+      TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->is_contiguous() &&
+                      bn_mask->numel() * 8 == dx.numel(), "bn_mask must be uint8 [rows, Ci/8]");
+      fz.bn_mask = bn_mask->data_ptr<uint8_t>();
+    }
     if (bn_z.has_value()) {
       check_same(*bn_z, dy, "bn_z");
       TORCH_CHECK(bn_z->sizes() == dx.sizes(), "bn_z must match dx");
@@ -435,7 +442,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_finalize(Tensor psum, Tensor psq, 
 }
 
 Tensor bn_act_fwd(Tensor y, Tensor scale, Tensor bias, bool relu, optional<Tensor> r,
-                  optional<Tensor> rscale, optional<Tensor> rbias) {
+                  optional<Tensor> rscale, optional<Tensor> rbias, optional<Tensor> mask) {
   check_act(y, "y");
   c10::DeviceGuard g(y.device());
   int64_t C = y.size(-1), M = y.numel() / C;
@@ -450,11 +457,18 @@ Tensor bn_act_fwd(Tensor y, Tensor scale, Tensor bias, bool relu, optional<Tenso
     check_vec(*rscale, C, "res_scale");
     check_vec(*rbias, C, "res_bias");
   }
+  uint8_t* mp = nullptr;
+  if (mask.has_value()) {  // also write the ReLU mask of z as bits
+    check_cuda(*mask, "mask");
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() * 8 == y.numel(), "mask must be uint8 [rows, C/8]");
+    mp = mask->data_ptr<uint8_t>();
+  }
   auto z = torch::empty_like(y);
   mipipe::bn_act_fwd(y.data_ptr(), scale.data_ptr<float>(), bias.data_ptr<float>(), ptr_or_null(r),
                      rscale.has_value() ? rscale->data_ptr<float>() : nullptr,
                      rbias.has_value() ? rbias->data_ptr<float>() : nullptr, z.data_ptr(), M,
-                     (int)C, relu, stream(), is_f32(y));
+                     (int)C, relu, stream(), is_f32(y), mp);
   return z;
 }
 
@@ -1218,7 +1232,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bn_y") = py::none(), py::arg("bn_mean") = py::none(),
         py::arg("bn_invstd") = py::none(), py::arg("bn_scale") = py::none(),
         py::arg("bn_bias") = py::none(), py::arg("bn_rep") = py::none(),
-        py::arg("bn_z") = py::none(), py::arg("pad_w") = -1, py::arg("cfg") = -1);
+        py::arg("bn_z") = py::none(), py::arg("pad_w") = -1, py::arg("cfg") = -1,
+        py::arg("bn_mask") = py::none());
   m.def("bn_bwd_collect", &bn_bwd_collect, py::arg("rep"), py::arg("C"),
         py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
@@ -1244,7 +1259,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift"), py::arg("gamma"), py::arg("beta"), py::arg("rm"), py::arg("rv"),
         py::arg("momentum"), py::arg("eps"), py::arg("zero_after") = true,
         py::arg("nbt") = py::none());
-  m.def("bn_act_fwd", &bn_act_fwd);
+  m.def("bn_act_fwd", &bn_act_fwd, py::arg("y"), py::arg("scale"), py::arg("bias"),
+        py::arg("relu"), py::arg("r"), py::arg("rscale"), py::arg("rbias"),
+        py::arg("mask") = py::none());
   m.def("bn_act_bwd_reduce", &bn_act_bwd_reduce, py::arg("dz"), py::arg("z"), py::arg("y"),
         py::arg("mean"), py::arg("invstd"), py::arg("relu"), py::arg("y2") = py::none(),
         py::arg("mean2") = py::none(), py::arg("invstd2") = py::none(),

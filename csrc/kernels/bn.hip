@@ -132,7 +132,8 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y
                                                          const float* __restrict__ rscale,
                                                          const float* __restrict__ rbias,
                                                          T* __restrict__ z, long M, int C,
-                                                         bool relu) {
+                                                         bool relu,
+                                                         uint8_t* __restrict__ mask) {
   const RowMap mp = row_map(C);
   const int t = threadIdx.x;
   const int rg = t / mp.tpr;
@@ -167,6 +168,12 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
       }
+      if (mask != nullptr) {  // 1 bit per element of the STORED z: the backward's ReLU mask
+        uint32_t b = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) b |= (as_stored<T>(v[q]) > 0.f ? 1u : 0u) << q;
+        mask[row * (C / 8) + cg] = (uint8_t)b;
+      }
       store8(z + off, v);
     }
   }
@@ -175,25 +182,25 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y
 template <class T>
 static void bn_act_fwd_t(const void* y, const float* scale, const float* bias, const void* r,
                          const float* rscale, const float* rbias, void* z, long M, int C,
-                         bool relu, hipStream_t st) {
+                         bool relu, hipStream_t st, uint8_t* mask) {
   RowMap mp = row_map(C);
   int grid = grid_for_rows(M, mp.rpb);
   const T* yp = (const T*)y;
   const T* rp = (const T*)r;
   T* zp = (T*)z;
   if (r == nullptr)
-    hipLaunchKernelGGL((bn_act_fwd_kernel<0, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<0, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask);
   else if (rscale == nullptr)
-    hipLaunchKernelGGL((bn_act_fwd_kernel<1, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<1, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask);
   else
-    hipLaunchKernelGGL((bn_act_fwd_kernel<2, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<2, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask);
 }
 
 void bn_act_fwd(const void* y, const float* scale, const float* bias, const void* r,
                 const float* rscale, const float* rbias, void* z, long M, int C, bool relu,
-                hipStream_t st, bool f32) {
-  if (f32) bn_act_fwd_t<float>(y, scale, bias, r, rscale, rbias, z, M, C, relu, st);
-  else bn_act_fwd_t<__bf16>(y, scale, bias, r, rscale, rbias, z, M, C, relu, st);
+                hipStream_t st, bool f32, uint8_t* mask) {
+  if (f32) bn_act_fwd_t<float>(y, scale, bias, r, rscale, rbias, z, M, C, relu, st, mask);
+  else bn_act_fwd_t<__bf16>(y, scale, bias, r, rscale, rbias, z, M, C, relu, st, mask);
 }
 
 // ----------------------------------------------------------------------------- backward
@@ -358,7 +365,7 @@ void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float
   float* part = det_ws != nullptr ? det_ws : rep;
   auto launch = [&](auto tag) {
     typedef decltype(tag) T;
-    const T *dzp = (const T*)dz, *zp = (const T*)z, *yp = (const T*)y, *y2p = (const T*)y2;
+      const T *dzp = (const T*)dz, *zp = (const T*)z, *yp = (const T*)y, *y2p = (const T*)y2;
     if (y2 == nullptr)
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, T>), dim3(G), dim3(256), 0, st, dzp, zp, yp, mean, invstd, y2p, mean2, invstd2, relu, M, C, part, det_rows);
     else
@@ -450,7 +457,7 @@ void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float*
   float inv_n = 1.f / (float)count;
   auto launch = [&](auto tag) {
     typedef decltype(tag) T;
-    const T *dzp = (const T*)dz, *zp = (const T*)z, *yp = (const T*)y, *y2p = (const T*)y2;
+      const T *dzp = (const T*)dz, *zp = (const T*)z, *yp = (const T*)y, *y2p = (const T*)y2;
     T *dyp = (T*)dy, *dop = (T*)dother;
     if (y2 != nullptr)
       hipLaunchKernelGGL((bn_bwd_apply_kernel<2, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C);

@@ -81,6 +81,7 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
         e.bnr_mean = fz->bn_mean; e.bnr_invstd = fz->bn_invstd;
         e.bnr_scale = fz->bn_scale; e.bnr_bias = fz->bn_bias; e.bnr_rep = fz->bn_rep; e.st_R = g_stat_rows;
         e.bnr_z = fz->bn_z;
+        e.bnr_mask = fz->bn_mask;
         e.det_rows = fz->det_rows;
         e.det_row0 = row0;
       }

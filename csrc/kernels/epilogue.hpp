@@ -34,6 +34,7 @@ struct EpiParams {
   // when set, the ReLU mask is read from this stored post-activation tensor (z > 0) instead of
   // recomputed from y (needed when a residual was added before the ReLU)
   const void* bnr_z;  // output dtype
+  const uint8_t* bnr_mask;  // or the mask as bits: [rows][ldc / 8] bytes, bit q = column 8c+q
   // deterministic mode (det_rows > 0): no float atomics.  Statistics partials (st_sum / st_sq,
   // bnr_rep) are WRITTEN at row det_row0 + (m0 / BM) of [det_rows][N] slabs (bnr_rep: two
   // arrays det_rows apart) and summed in a fixed order afterwards (det.hip); split-K fp32
@@ -70,14 +71,51 @@ constexpr int kStatsLdsOffset() { return ((BM * kEpiPitch<BN, T>()) + 255) / 256
 template <int BM, int BN, class T = __bf16, int WM = 2>
 constexpr int kEpiLdsBytes() { return kStatsLdsOffset<BM, BN, T>() + 2 * WM * BN * 4; }
 
+// The fused epilogue's operand ring: each thread's addend / y / z chunks (PF iterations ahead).
+// (Priming it before a short main loop was measured slower in round 2: the seven ResNet-50
+// layer-1 1x1 data-grads went from ~1.9 ms to 3.4 ms per step — the early loads stretch the main
+// loop's vmcnt waits and the registers' lifetime.)
+template <int BM, int BN, bool FUSE, class T, int WM, int WN>
+struct EpiOps {
+  static constexpr int kThreads = 64 * WM * WN;
+  static constexpr int CPR = BN / 8;  // 8-element chunks per row
+  static constexpr int ITER = BM * CPR / kThreads;
+  static constexpr int PF = FUSE ? (ITER < 4 ? ITER : 4) : 1;
+  Raw8<T> ad[PF], y[PF], z[PF];
+  uint32_t mk[PF];
+  __device__ __forceinline__ void issue(const EpiParams& e, uint32_t m0, uint32_t n0, int it,
+                                        int slot) {
+    const uint32_t my_n = n0 + (threadIdx.x % CPR) * 8;
+    const uint32_t ld_n = my_n < e.N ? my_n : 0;
+    const uint32_t r = (threadIdx.x + it * kThreads) / CPR;
+    const uint32_t m = min(m0 + r, e.M - 1);
+    const long orow = out_row(e, m);
+    if (e.addend != nullptr) ad[slot] = ld_raw8(reinterpret_cast<const T*>(e.addend) + orow * e.ldc + ld_n);
+    if (e.bnr_rep != nullptr) {
+      y[slot] = ld_raw8(reinterpret_cast<const T*>(e.bnr_y) + orow * e.ldc + ld_n);
+      if (e.bnr_mask != nullptr)
+        mk[slot] = e.bnr_mask[orow * (e.ldc / 8) + ld_n / 8];
+      else if (e.bnr_z != nullptr)
+        z[slot] = ld_raw8(reinterpret_cast<const T*>(e.bnr_z) + orow * e.ldc + ld_n);
+    }
+  }
+  __device__ __forceinline__ void prime(const EpiParams& e, uint32_t m0, uint32_t n0) {
+    if (FUSE && (e.addend != nullptr || e.bnr_rep != nullptr)) {
+#pragma unroll
+      for (int it = 0; it < PF; ++it) issue(e, m0, n0, it, it);
+    }
+  }
+};
+
 // Output in the activation dtype T (bf16, or fp32 on the reference-precision path).
 // acc layout: lane holds C[m][n..n+3] for tile (i, j).
 // FUSE: compile the dgrad fusions (addend / BN-backward reduction); kernels that never use
-// them keep their register budget.
+// them keep their register budget.  early: an operand ring the kernel already primed.
 template <int BM, int BN, bool FUSE = false, class T = __bf16, int WM = 2, int WN = 2>
 __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                              const EpiParams& e, uint32_t m0, uint32_t n0, uint32_t prow_base,
-                             int wave, int lane) {
+                             int wave, int lane,
+                             EpiOps<BM, BN, FUSE, T, WM, WN>* early = nullptr) {
   constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
   constexpr int kThreads = 64 * WM * WN;
   const int wr = wave / WN, wc = wave % WN;
@@ -90,28 +128,18 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
   static_assert(kThreads % CPR == 0 && (BM * CPR) % kThreads == 0, "epilogue thread map");
   const bool bnr = FUSE && e.bnr_rep != nullptr;
   const bool has_add = FUSE && e.addend != nullptr;
-  const bool zmask = bnr && e.bnr_z != nullptr;
+  const bool zmask = bnr && e.bnr_z != nullptr && e.bnr_mask == nullptr;
+  const bool bmask = bnr && e.bnr_mask != nullptr;
   const uint32_t my_cc = threadIdx.x % CPR, my_n = n0 + my_cc * 8;
   const uint32_t ld_n = my_n < e.N ? my_n : 0;
-  // software-pipelined operand ring: PF iterations in flight; the first PF are issued now so
-  // their latency overlaps the accumulator staging below
-  constexpr int PF = FUSE ? (ITER < 4 ? ITER : 4) : 1;
-  Raw8<T> ad_raw[PF], y_raw[PF], z_raw[PF];
-  const T* addend = reinterpret_cast<const T*>(e.addend);
-  const T* bnr_y = reinterpret_cast<const T*>(e.bnr_y);
-  const T* bnr_z = reinterpret_cast<const T*>(e.bnr_z);
-  auto issue = [&](int it, int slot) {
-    const uint32_t r = (threadIdx.x + it * kThreads) / CPR;
-    const uint32_t m = min(m0 + r, e.M - 1);
-    const long orow = out_row(e, m);
-    if (has_add) ad_raw[slot] = ld_raw8(addend + orow * e.ldc + ld_n);
-    if (bnr) y_raw[slot] = ld_raw8(bnr_y + orow * e.ldc + ld_n);
-    if (zmask) z_raw[slot] = ld_raw8(bnr_z + orow * e.ldc + ld_n);
-  };
-  if (FUSE && (has_add || bnr)) {
-#pragma unroll
-    for (int it = 0; it < PF; ++it) issue(it, it);
-  }
+  // software-pipelined operand ring: PF iterations in flight; the first PF are issued now (unless
+  // the kernel primed them before its main loop) so their latency overlaps the staging below
+  typedef EpiOps<BM, BN, FUSE, T, WM, WN> Ops;
+  constexpr int PF = Ops::PF;
+  Ops local;
+  Ops& ops = early != nullptr ? *early : local;
+  if (early == nullptr) ops.prime(e, m0, n0);
+  (void)ld_n;
   // bias / activation
   if (e.bias != nullptr || e.act) {
 #pragma unroll
@@ -240,17 +268,19 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
         unpack_raw(v, f);
         if (has_add) {
           float a[8];
-          unpack_raw(ad_raw[it % PF], a);
+          unpack_raw(ops.ad[it % PF], a);
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] += a[q];
         }
         if (bnr) {
           float yv[8], zv[8];
-          unpack_raw(y_raw[it % PF], yv);
-          if (zmask) unpack_raw(z_raw[it % PF], zv);
+          unpack_raw(ops.y[it % PF], yv);
+          if (zmask) unpack_raw(ops.z[it % PF], zv);
+          const uint32_t bits = bmask ? ops.mk[it % PF] : 0u;
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const float zq = zmask ? zv[q] : yv[q] * b_sc[q] + b_bi[q];
+            const float zq = bmask ? (float)((bits >> q) & 1u)
+                                   : (zmask ? zv[q] : yv[q] * b_sc[q] + b_bi[q]);
             const float gq = zq > 0.f ? as_stored<T>(f[q]) : 0.f;  // stats of the stored g
             f[q] = gq;
             sg[q] += gq;
@@ -264,7 +294,7 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
           reinterpret_cast<uint4*>(C + orow * e.ldc + n)[h] = v.v[h];
       }
     }
-    if (FUSE && (has_add || bnr) && it + PF < ITER) issue(it + PF, it % PF);
+    if (FUSE && (has_add || bnr) && it + PF < ITER) ops.issue(e, m0, n0, it + PF, it % PF);
   }
   if (FUSE && bnr) {
     // threads t, t+CPR, ... share a column chunk: reduce them through LDS, then one atomic

@@ -62,6 +62,7 @@ struct DgradFusion {
   const float *bn_mean = nullptr, *bn_invstd = nullptr, *bn_scale = nullptr, *bn_bias = nullptr;
   float* bn_rep = nullptr;
   const void* bn_z = nullptr;  // optional stored relu output: mask = z > 0 (residual blocks)
+  const uint8_t* bn_mask = nullptr;  // or that mask as bits ([rows][Ci/8] bytes, bit q = chan q)
   int det_rows = 0;  // deterministic mode: bn_rep is [2][det_rows][Ci] partials, one row per tile
 };
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
@@ -140,7 +141,7 @@ void bn_finalize(float* psum, float* psq, int P, int C, long count, const float*
 // z = act(y*scale + bias [+ r | + r*rscale + rbias])   (M rows of C channels, bf16 or f32)
 void bn_act_fwd(const void* y, const float* scale, const float* bias, const void* r,
                 const float* rscale, const float* rbias, void* z, long M, int C, bool relu,
-                hipStream_t st, bool f32 = false);
+                hipStream_t st, bool f32 = false, uint8_t* mask = nullptr);
 // sums: out_g[C], out_gx[C], out_gx2[C] (if y2).  rep: zeroed [3][kStatReplicas][C] slab,
 // left zeroed on return.
 void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float* mean,

@@ -18,6 +18,8 @@ back in fp32.
 from __future__ import annotations
 
 import math
+import os
+import weakref
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -27,6 +29,10 @@ from torch.autograd import Function
 from . import kernels as K
 
 Tensor = torch.Tensor
+
+
+# block-output ReLU masks kept as bits for the fused backward (MIPIPE_RELU_BITMASK=0: read z)
+_RELU_BITMASK = os.environ.get("MIPIPE_RELU_BITMASK", "1") != "0"
 
 
 # ----------------------------------------------------------------------------- conv
@@ -80,13 +86,25 @@ class BNActToken:
     """Links a BN(+ReLU) output to its single consuming conv: the conv's backward computes the
     BN-backward reductions in its dgrad epilogue and flags the BN's backward to skip them."""
 
-    __slots__ = ("bn", "st", "y", "z", "pre_reduced")
+    __slots__ = ("bn", "st", "y", "_z", "mask", "pre_reduced")
+
+    @property
+    def z(self):
+        return None if self._z is None else self._z()
+
+    @z.setter
+    def z(self, t):
+        # weak: z carries this token as ``z._mipipe_bnact``; a strong back-reference would make
+        # a z <-> token cycle that holds every block output until the next gc pass
+        self._z = None if t is None else weakref.ref(t)
 
     def __init__(self, bn, st, y, z=None):
         # z set: BN + residual + ReLU block output.  Its consumer conv also feeds the next
         # block's identity path, so the fusion is valid only when that conv's dgrad also adds
-        # the identity gradient (residual slot delivered) - the mask comes from stored z.
+        # the identity gradient (residual slot delivered) - the mask comes from stored z, or
+        # from its 1-bit copy (``mask``, written by the BN-apply kernel: 1/16 of z's bytes).
         self.bn, self.st, self.y, self.z = bn, st, y, z
+        self.mask = None
         self.pre_reduced = False
 
 
@@ -127,7 +145,7 @@ class _ConvFn(Function):
                     st = tok.st
                     bnr = (tok.y, st.mean, st.invstd, st.scale, st.bias, rep)
                     if tok.z is not None:
-                        bnr = bnr + (tok.z,)
+                        bnr = bnr + (tok.mask if tok.mask is not None else tok.z,)
             dx = K.conv_dgrad(dy, w_c, x.shape, stride, pad, addend=addend, bnr=bnr)
             if bnr is not None:
                 tok.pre_reduced = True
@@ -392,9 +410,16 @@ class _BNActFn(Function):
     @staticmethod
     def forward(ctx, y, gamma, beta, residual, y2, gamma2, beta2, st, st2, relu, bn=None,
                 token=None, res_give=None):
+        mask = None
+        if (_RELU_BITMASK and token is not None and relu
+                and (residual is not None or y2 is not None) and K.use_native(y)):
+            # block output: its fused backward reads the ReLU mask as bits, not z
+            mask = torch.empty(y.numel() // 8, dtype=torch.uint8, device=y.device)
+            token.mask = mask
         z = K.bn_act_fwd(y, st.scale, st.bias, relu,
                          residual if y2 is None else y2,
-                         None if st2 is None else st2.scale, None if st2 is None else st2.bias)
+                         None if st2 is None else st2.scale, None if st2 is None else st2.bias,
+                         mask=mask)
         ctx.save_for_backward(y, z, y2, gamma, gamma2)
         ctx.st, ctx.st2, ctx.relu = st, st2, relu
         ctx.has_res = residual is not None

@@ -64,16 +64,20 @@ def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None, bias=None, relu=Fa
 def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None):
     """dx of an NHWC conv.  ``addend``: tensor added to dx in the epilogue (residual gradient).
     ``bnr = (y, mean, invstd, scale, bias, rep[, z])``: the conv input was relu(bn(y)[+res]);
-    dx becomes g = dx·[z > 0] (z recomputed from y unless given) and Σg, Σg·x̂ accumulate into
-    ``rep`` rows 0/1 (native only)."""
+    dx becomes g = dx·[z > 0] (z recomputed from y unless given — as the stored tensor, or as
+    its uint8 bit mask from ``bn_act_fwd(mask=)``) and Σg, Σg·x̂ accumulate into ``rep`` rows
+    0/1 (native only)."""
     if use_native(dy):
         ph, pw = _pads(pad)
         if bnr is None:
             return native().conv_dgrad(dy, w, list(x_shape), stride, ph, addend, pad_w=pw)
         y, mean, invstd, scale, bias, rep = bnr[:6]
         z = bnr[6] if len(bnr) > 6 else None
+        mask = None
+        if z is not None and z.dtype == torch.uint8:
+            z, mask = None, z
         return native().conv_dgrad(dy, w, list(x_shape), stride, ph, addend, y, mean, invstd,
-                                   scale, bias, rep, z, pw)
+                                   scale, bias, rep, z, pw, bn_mask=mask)
     if bnr is not None:
         raise RuntimeError("BN-reduce dgrad fusion is a native-kernel path")
     dx = _ref.conv_dgrad(dy, w, x_shape, stride, pad if isinstance(pad, int) else tuple(pad))
@@ -117,9 +121,12 @@ def bn_finalize(psum, psumsq, count, shift, gamma, beta, running_mean, running_v
                             running_var, momentum, eps)
 
 
-def bn_act_fwd(y, scale, bias, relu, residual=None, res_scale=None, res_bias=None):
+def bn_act_fwd(y, scale, bias, relu, residual=None, res_scale=None, res_bias=None, mask=None):
+    """z = relu?(y*scale + bias [+ residual | + residual*res_scale + res_bias]).  ``mask``
+    (native, uint8 [rows, C/8]): also receives z > 0 as bits (bit q of byte c = channel 8c+q),
+    the ReLU mask the backward reads instead of z."""
     if use_native(y):
-        return native().bn_act_fwd(y, scale, bias, relu, residual, res_scale, res_bias)
+        return native().bn_act_fwd(y, scale, bias, relu, residual, res_scale, res_bias, mask)
     return _ref.bn_act_fwd(y, scale, bias, relu, residual, res_scale, res_bias)
 
 

@@ -402,6 +402,7 @@ def test_stem_superpixel_conv_matches_direct():
 TILE_CASES = [
     # N, H, W, Ci, Co, k, s, p  — dense 1x1, gathered 3x3, strided, odd channel counts
     (4, 14, 14, 256, 512, 1, 1, 0),
+    (8, 14, 14, 256, 64, 1, 1, 0),  # short-K 1x1 data-grad: epilogue operands primed early
     (4, 15, 13, 64, 192, 3, 1, 1),
     (4, 16, 16, 128, 256, 3, 2, 1),
     (2, 9, 7, 40, 72, 3, 1, 1),
@@ -469,3 +470,33 @@ def test_tile_benchmark_mode_picks_and_caches():
     finally:
         C.set_benchmark(False)
         C.clear_tune_table()
+
+
+@pytest.mark.parametrize("C", [64, 256])
+def test_relu_bitmask_matches_stored_z(C):
+    """bn_act_fwd(mask=) writes z > 0 as bits; the fused BN-backward dgrad epilogue reading the
+    bits gives exactly what it gives reading z (g and the Σg, Σg·x̂ partials)."""
+    N, H, W, Co = 4, 14, 14, 64
+    y = bf(N, H, W, C, scale=2.0)
+    res = bf(N, H, W, C)
+    scale = torch.rand(C, device=dev) + 0.5
+    bias = torch.randn(C, device=dev) * 0.1
+    mask = torch.empty(N * H * W * C // 8, dtype=torch.uint8, device=dev)
+    z = native().bn_act_fwd(y, scale, bias, True, res, None, None, mask)
+    bits = (z.reshape(-1, C // 8, 8) > 0).to(torch.int32)
+    expect = (bits << torch.arange(8, device=dev, dtype=torch.int32)).sum(-1).to(torch.uint8)
+    assert torch.equal(mask, expect.reshape(-1))
+    dy = bf(N, H, W, Co)
+    w = bf(Co, 1, 1, C, scale=1.0 / math.sqrt(Co))
+    add = bf(N, H, W, C)
+    mean = torch.randn(C, device=dev) * 0.1
+    invstd = torch.rand(C, device=dev) + 0.5
+    outs = []
+    for kw in (dict(bn_z=z), dict(bn_mask=mask)):
+        rep = torch.zeros(3, native().STAT_REPLICAS, C, device=dev)
+        g = native().conv_dgrad(dy, w, [N, H, W, C], 1, 0, add, y, mean, invstd, scale, bias, rep,
+                                **kw)
+        outs.append((g, *native().bn_bwd_collect(rep, C)))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-5)
+    assert torch.allclose(outs[0][2], outs[1][2], rtol=1e-5, atol=1e-5)
