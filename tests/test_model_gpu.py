@@ -204,3 +204,52 @@ def test_graphed_step_bit_identical_in_deterministic_mode():
             assert torch.equal(p, q), n
     finally:
         determinism.set_deterministic(False)
+
+
+@pytest.mark.parametrize("arch,res", [("resnet50", 64), ("resnext50_32x4d", 64),
+                                      ("mobilenet_v2", 64), ("densenet121", 64),
+                                      ("bert_tiny", 0)])
+def test_eager_training_memory_is_flat(arch, res):
+    """Eager training steps must not accumulate device memory.  The garbage collector is off:
+    anything a step leaves in a reference cycle (tensors that only gc would free) shows up as
+    growth."""
+    import gc
+    from mipipe.optim import AdamW
+    from mipipe.train.task import CrossEntropyLoss
+    torch.manual_seed(0)
+    if arch.startswith("bert"):
+        m = create_model(arch).cuda()
+        opt = AdamW(m.parameters(), lr=1e-4)
+        ids = torch.randint(0, 30522, (4, 64), device="cuda")
+        pos = torch.stack([torch.randperm(64, device="cuda")[:8] for _ in range(4)])
+        lab = torch.randint(0, 30522, (32,), device="cuda")
+
+        def step():
+            opt.zero_grad()
+            m(ids, masked_positions=pos, labels=lab).backward()
+            opt.step()
+    else:
+        m = create_model(arch, num_classes=10).cuda()
+        opt = SGD(m.parameters(), 0.01, momentum=0.9, weight_decay=1e-4)
+        x = torch.randn(8, 3, res, res, device="cuda")
+        y = torch.randint(0, 10, (8,), device="cuda")
+        crit = CrossEntropyLoss()
+
+        def step():
+            opt.zero_grad()
+            crit(m(x), y).backward()
+            opt.step()
+    gc.collect()
+    gc.disable()
+    try:
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated()
+        for _ in range(4):
+            step()
+        torch.cuda.synchronize()
+        grown = torch.cuda.memory_allocated() - base
+    finally:
+        gc.enable()
+    assert grown <= 1 << 20, f"{grown / 2**20:.1f} MiB retained over 4 steps"
