@@ -40,6 +40,9 @@ struct Tile {
 //  6: 256x256, 2 stages, 4x2 waves   — 64x128 wave tiles, 128 FLOP per L2 byte
 //  7: 256x64,  2 stages, 4x1 waves   — large M, narrow N
 //  8: 64x128,  2 stages, 2x2 waves   — narrow M (weight-grad of <= 64 output channels)
+//  9: 128x64,  1 stage               — short-K streaming convs (one or two k-steps, large M):
+//     24.6 KB of LDS -> 6 blocks per CU to keep more epilogue traffic in flight
+// 10: 64x128,  1 stage               — same for narrow M
 typedef Tile<128, 128, 2, 2, 2> T0;
 typedef Tile<128, 128, 1, 2, 2> T1;
 typedef Tile<128, 64, 2, 2, 2> T2;
@@ -49,7 +52,9 @@ typedef Tile<128, 256, 2, 2, 4> T5;
 typedef Tile<256, 256, 2, 4, 2> T6;
 typedef Tile<256, 64, 2, 4, 1> T7;
 typedef Tile<64, 128, 2, 2, 2> T8;
-constexpr int kNumTiles = 9;
+typedef Tile<128, 64, 1, 2, 2> T9;
+typedef Tile<64, 128, 1, 2, 2> T10;
+constexpr int kNumTiles = 11;
 
 // fp32 operands run the split-bf16x3 loop (3 LDS images): 4-wave tiles only.
 template <class T>
@@ -73,6 +78,7 @@ constexpr int lds_bytes_f32out() {
 // Minimum resident blocks per CU promised to the register allocator.
 template <class T, class C>
 constexpr int conv_occ() {
+  // (asking 5-6 blocks of the single-stage half-size tiles 9/10 spills: they need ~100 VGPRs)
   return C::NW == 8 ? 1 : ((C::NS == 1 && !std::is_same<T, float>::value) ? 3 : 2);
 }
 
@@ -211,6 +217,8 @@ inline void with_tile(int cfg, F&& f) {
         break;
       case 7: f(T7{}); break;
       case 8: f(T8{}); break;
+      case 9: f(T9{}); break;
+      case 10: f(T10{}); break;
       default: f(T0{}); break;
     }
   }

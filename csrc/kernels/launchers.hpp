@@ -45,7 +45,7 @@ int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 // bias / relu: optional per-channel bias and ReLU in the epilogue (convs without BN: VGG, AlexNet)
 // cfg: tile config id (conv_common.hpp table; < 0 = heuristic default)
-constexpr int kConvTileConfigs = 9;
+constexpr int kConvTileConfigs = 11;
 //  det_rows > 0 (deterministic mode): st_sum / st_sq are [det_rows][Co] partial slabs, one row
 //  per M-tile (det_rows = conv_fwd_tiles_m(s, cfg)), written without atomics.
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
