@@ -1308,6 +1308,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(),
         py::arg("two_pass") = false);
   m.def("set_colsum_row_blocks", [](int v) { mipipe::g_colsum_row_blocks = v; });
+  m.def("set_attn_waves", [](int v) { mipipe::g_attn_waves = v; });
   m.def("attention_fwd", &attention_fwd, py::arg("qkv"), py::arg("B"), py::arg("S"), py::arg("H"),
         py::arg("mask") = py::none(), py::arg("scale") = 0.125, py::arg("p_drop") = 0.0,
         py::arg("seed") = 0);

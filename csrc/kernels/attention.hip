@@ -115,11 +115,14 @@ struct FwdArgs {
 constexpr int kFwdTile = 16384;  // K (8 KB) + V (8 KB) for 64 keys
 constexpr int kMaxS = 2048;
 
-__global__ __launch_bounds__(256) void attn_fwd_kernel(FwdArgs a) {
+// NW waves per block (32 queries each): 4 (default) or 2 (see attn_waves()).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(FwdArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kFwdTile + kMaxS * 4];
+  constexpr int QB = 32 * NW;  // queries per block
   const int S = a.S, H = a.H;
   const long ld = 3l * H * D, ldo = (long)H * D;
-  const int nqt = (S + 127) / 128;
+  const int nqt = (S + QB - 1) / QB;
   const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);  // a head's q-tiles share an XCD's L2
   const int qt = bid % nqt, bh = bid / nqt, h = bh % H, b = bh / H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, r = lane & 31;
@@ -128,24 +131,24 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(FwdArgs a) {
   const __bf16* vb = kb + (long)H * D;
   const int nkt = (S + 63) / 64;
   float* maskl = reinterpret_cast<float*>(smem + 2 * kFwdTile);
-  for (int i = tid; i < nkt * 64; i += 256)
+  for (int i = tid; i < nkt * 64; i += 64 * NW)
     maskl[i] = i < S ? (a.mask ? a.mask[(long)b * S + i] * kLog2e : 0.f) : -INFINITY;
-  const int q = qt * 128 + wave * 32 + r;
+  const int q = qt * QB + wave * 32 + r;
   const int qc = min(q, S - 1);
   bf16x8 qf[4];
 #pragma unroll
   for (int st = 0; st < 4; ++st)
     qf[st] = *reinterpret_cast<const bf16x8*>(qb + (long)qc * ld + 16 * st + 8 * hl);
 
-  auto stage = [&](char* buf, int k0) {
+  auto stage = [&](char* buf, int k0) {  // 64 keys x 8 chunks of K and of V
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int t = (i * 4 + wave) * 64 + lane;
+    for (int i = 0; i < 8 / NW; ++i) {
+      const int t = (i * NW + wave) * 64 + lane;
       const int row = t >> 3, pos = t & 7;
       const int chunk = pos ^ swz(row);
       const long key = min(k0 + row, S - 1);
-      glds16(kb + key * ld + chunk * 8, buf + (i * 4 + wave) * 1024);
-      glds16(vb + key * ld + chunk * 8, buf + 8192 + (i * 4 + wave) * 1024);
+      glds16(kb + key * ld + chunk * 8, buf + (i * NW + wave) * 1024);
+      glds16(vb + key * ld + chunk * 8, buf + 8192 + (i * NW + wave) * 1024);
     }
   };
 
@@ -230,7 +233,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(FwdArgs a) {
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
     const int row = it * 4 + (lane >> 4), piece = lane & 15;
-    const int qq = qt * 128 + wave * 32 + row;
+    const int qq = qt * QB + wave * 32 + row;
     if (qq < S) {
       uint2 v = *reinterpret_cast<const uint2*>(ow + row * 136 + piece * 8);
       *reinterpret_cast<uint2*>(a.o + ((long)b * S + qq) * ldo + h * D + piece * 4) = v;
@@ -282,17 +285,19 @@ struct BwdArgs {
   uint32_t seed;
 };
 
-// LDS: K tile (128 keys) | 2 x {Q 4 KB, dO 4 KB, lse 128 B, delta 128 B} | dSᵀ [128][32] bf16
-constexpr int kKT = 16384;
+// LDS: K tile (KB keys) | 2 x {Q 4 KB, dO 4 KB, lse 128 B, delta 128 B} | dSᵀ [KB][32] bf16
 constexpr int kQStage = 8192 + 256;
-constexpr int kDsOff = kKT + 2 * kQStage;
-constexpr int kBwdLds = kDsOff + 128 * 64;
 
-__global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[kBwdLds];
+// NW waves per block (32 keys each; 4 by default, as in the forward)
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(BwdArgs a) {
+  constexpr int KB = 32 * NW;  // keys per block
+  constexpr int kKT = KB * 128;
+  constexpr int kDsOff = kKT + 2 * kQStage;
+  __shared__ __attribute__((aligned(16))) char smem[kDsOff + KB * 64];
   const int S = a.S, H = a.H;
   const long ld = 3l * H * D, ldq = (long)H * D;
-  const int nkb = (S + 127) / 128;
+  const int nkb = (S + KB - 1) / KB;
   const uint32_t bid = xcd_remap(blockIdx.x, gridDim.x);
   const int kbk = bid % nkb, bh = bid / nkb, h = bh % H, b = bh / H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5, r = lane & 31;
@@ -302,7 +307,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
   const __bf16* dob = a.dout + (long)b * S * ldq + h * D;
   const float* lseb = a.lse + ((long)b * H + h) * S;
   const float* delb = a.delta + ((long)b * H + h) * S;
-  const int key = kbk * 128 + wave * 32 + r;
+  const int key = kbk * KB + wave * 32 + r;
   const int kc = min(key, S - 1);
   // this lane's key: K and V rows as B operands, its mask bias
   bf16x8 kf[4], vf[4];
@@ -312,21 +317,24 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
     vf[st] = *reinterpret_cast<const bf16x8*>(vb + (long)kc * ld + 16 * st + 8 * hl);
   }
   const float mk = key < S ? (a.mask ? a.mask[(long)b * S + key] * kLog2e : 0.f) : -INFINITY;
-  // K tile [128 keys][64] for the dQ product (4 glds per thread)
+  // K tile [KB keys][64] for the dQ product (4 glds per thread)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int t = (i * 4 + wave) * 64 + lane;
+    const int t = (i * NW + wave) * 64 + lane;
     const int row = t >> 3, pos = t & 7;
-    const long kk = min(kbk * 128 + row, S - 1);
-    glds16(kb + kk * ld + ((pos ^ swz(row)) * 8), smem + (i * 4 + wave) * 1024);
+    const long kk = min(kbk * KB + row, S - 1);
+    glds16(kb + kk * ld + ((pos ^ swz(row)) * 8), smem + (i * NW + wave) * 1024);
   }
   const int nqt = (S + 31) / 32;
   auto stage = [&](char* buf, int q0) {
-    const int t = wave * 64 + lane;  // 256 chunks of 16 B per 32x64 tile
-    const int row = t >> 3, pos = t & 7;
-    const long qq = min(q0 + row, S - 1);
-    glds16(qb + qq * ld + ((pos ^ swz(row)) * 8), buf + wave * 1024);
-    glds16(dob + qq * ldq + ((pos ^ swz(row)) * 8), buf + 4096 + wave * 1024);
+#pragma unroll
+    for (int i = 0; i < 4 / NW; ++i) {  // 256 chunks of 16 B per 32x64 tile
+      const int t = (i * NW + wave) * 64 + lane;
+      const int row = t >> 3, pos = t & 7;
+      const long qq = min(q0 + row, S - 1);
+      glds16(qb + qq * ld + ((pos ^ swz(row)) * 8), buf + (i * NW + wave) * 1024);
+      glds16(dob + qq * ldq + ((pos ^ swz(row)) * 8), buf + 4096 + (i * NW + wave) * 1024);
+    }
     if (wave == 0) {
       const int qi = min(q0 + (lane & 31), S - 1);
       glds4(lane < 32 ? lseb + qi : delb + qi, buf + 8192);
@@ -386,13 +394,17 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // raw barrier: keeps the next tile's glds in flight
     asm volatile("" ::: "memory");
-    // dQ[32 q][64 d] += dS[q][128 keys]·K[keys][d]: wave -> q rows 16(w&1), d cols 32(w>>1)
+    // dQ[32 q][64 d] += dS[q][KB keys]·K[keys][d]: wave -> q rows 16(w&1), d cols
+    // (128/NW)(w>>1) in DT 16-column MFMA tiles
     {
-      const int qr0 = 16 * (wave & 1), dc0 = 32 * (wave >> 1);
+      constexpr int DT = 128 / NW / 16;
+      const int qr0 = 16 * (wave & 1), dc0 = (128 / NW) * (wave >> 1);
       const int g = lane >> 4, li = lane & 15, qq = li >> 2, p = li & 3;
-      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+      f32x4 cacc[DT];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
+      for (int dt = 0; dt < DT; ++dt) cacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NW; ++ks) {
         const int k0 = ks * 32 + 8 * g + qq;
         // A = dS[q][key]: transposed read of dSᵀ rows k0, k0+4, columns qr0 + 4p..
         const char* a0 = dsT + k0 * 64 + (qr0 + 4 * p) * 2;
@@ -401,7 +413,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
         s16x8 av = {alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
         const bf16x8 af = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
+        for (int dt = 0; dt < DT; ++dt) {
           const int col = dc0 + 16 * dt + 4 * p;
           const char* b0 = smem + off(k0, col >> 3) + 8 * (p & 1);
           const char* b1 = smem + off(k0 + 4, col >> 3) + 8 * (p & 1);
@@ -409,8 +421,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
           s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)b1);
           s16x8 bv = {blo[0], blo[1], blo[2], blo[3], bhi[0], bhi[1], bhi[2], bhi[3]};
           const bf16x8 bfr = __builtin_bit_cast(bf16x8, bv);
-          if (dt == 0) c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, c0, 0, 0, 0);
-          else c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, c1, 0, 0, 0);
+          cacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, cacc[dt], 0, 0, 0);
         }
       }
       // C: col = lane&15 (d), row = 4(lane>>4) + i (q)
@@ -419,8 +430,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
         const int qg = it * 32 + qr0 + 4 * g + i;
         if (qg < S) {
           float* dst = a.dq_acc + ((long)b * S + qg) * ldq + h * D + dc0 + li;
-          atomicAdd(dst, c0[i]);
-          atomicAdd(dst + 16, c1[i]);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) atomicAdd(dst + 16 * dt, cacc[dt][i]);
         }
       }
     }
@@ -460,6 +471,17 @@ __global__ __launch_bounds__(256) void attn_dq_store_kernel(const float* __restr
 
 }  // namespace attn
 
+int g_attn_waves = 0;  // 0: default (4); 2 / 4: forced (tests, A/B)
+
+// waves (32 rows each) per attention block.  4 by default: measured on BERT-base 8x512, the
+// 2-wave blocks (twice the grid, even spread over the CUs) run the step 7 % slower — sharing
+// each staged K/V (fwd) / Q-dO (bwd) tile across 4 waves matters more than occupancy
+// (tools/r2/bench_attn_waves.py).
+static int attn_waves(int B, int S, int H) {
+  (void)B; (void)S; (void)H;
+  return g_attn_waves == 2 ? 2 : 4;
+}
+
 static uint32_t drop_threshold(float p) {
   double t = (double)p * 4294967296.0;
   return t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
@@ -469,8 +491,10 @@ void attention_fwd(const void* qkv, const float* mask, void* o, float* lse, int 
                    float scale, float p_drop, uint32_t seed, hipStream_t st) {
   attn::FwdArgs a{(const __bf16*)qkv, (__bf16*)o, lse, mask, B, S, H, scale * attn::kLog2e,
                   p_drop, drop_threshold(p_drop), seed};
-  const int blocks = B * H * ((S + 127) / 128);
-  hipLaunchKernelGGL(attn::attn_fwd_kernel, dim3(blocks), dim3(256), 0, st, a);
+  if (attn_waves(B, S, H) == 2)
+    hipLaunchKernelGGL(attn::attn_fwd_kernel<2>, dim3(B * H * ((S + 63) / 64)), dim3(128), 0, st, a);
+  else
+    hipLaunchKernelGGL(attn::attn_fwd_kernel<4>, dim3(B * H * ((S + 127) / 128)), dim3(256), 0, st, a);
 }
 
 void attention_bwd(const void* dout, const void* qkv, const void* o, const float* lse,
@@ -482,8 +506,10 @@ void attention_bwd(const void* dout, const void* qkv, const void* o, const float
   attn::BwdArgs a{(const __bf16*)qkv, (const __bf16*)dout, lse, delta, mask, dq_acc,
                   (__bf16*)dqkv, B, S, H, scale, scale * attn::kLog2e, p_drop,
                   drop_threshold(p_drop), seed};
-  const int blocks = B * H * ((S + 127) / 128);
-  hipLaunchKernelGGL(attn::attn_bwd_kernel, dim3(blocks), dim3(256), 0, st, a);
+  if (attn_waves(B, S, H) == 2)
+    hipLaunchKernelGGL(attn::attn_bwd_kernel<2>, dim3(B * H * ((S + 63) / 64)), dim3(128), 0, st, a);
+  else
+    hipLaunchKernelGGL(attn::attn_bwd_kernel<4>, dim3(B * H * ((S + 127) / 128)), dim3(256), 0, st, a);
   const long chunks = (long)B * S * H * attn::D / 8;
   hipLaunchKernelGGL(attn::attn_dq_store_kernel, dim3((chunks + 255) / 256), dim3(256), 0, st,
                      dq_acc, (__bf16*)dqkv, (long)B * S, H * attn::D);

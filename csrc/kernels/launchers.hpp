@@ -210,6 +210,7 @@ void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st);
 // Fused self-attention, head_dim 64, on the packed projection layout (attention.hip):
 //   qkv [B*S][3*H*64] bf16, o [B*S][H*64] bf16, lse [B][H][S] fp32, mask [B][S] additive or null.
 // p_drop > 0 applies attention-probability dropout keyed by (seed, b, h, q, k).
+extern int g_attn_waves;  // attention block size override (0 auto, 2, 4)
 void attention_fwd(const void* qkv, const float* mask, void* o, float* lse, int B, int S, int H,
                    float scale, float p_drop, uint32_t seed, hipStream_t st);
 // dqkv [B*S][3*H*64]; delta [B][H][S] and dq_acc [B*S][H*64] fp32 are scratch.

@@ -24,9 +24,17 @@ def rel_err(a, b):
     return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
 
 
+@pytest.fixture(params=[2, 4], ids=["2waves", "4waves"])
+def attn_waves(request):
+    """Both attention block shapes (32 rows per wave; the launcher picks by grid size)."""
+    native().set_attn_waves(request.param)
+    yield request.param
+    native().set_attn_waves(0)
+
+
 @pytest.mark.parametrize("B,S,H", [(2, 128, 2), (1, 100, 3), (2, 512, 2), (1, 64, 1), (3, 200, 2)])
 @pytest.mark.parametrize("masked", [False, True])
-def test_attention_fwd_bwd(B, S, H, masked):
+def test_attention_fwd_bwd(B, S, H, masked, attn_waves):
     D = 64
     qkv = (torch.randn(B * S, 3 * H * D, device=dev) * 1.5).to(torch.bfloat16)
     mask = None
@@ -47,7 +55,7 @@ def test_attention_fwd_bwd(B, S, H, masked):
         assert rel_err(a, b) < 3e-2, name
 
 
-def test_attention_dropout_matches_reference_mask():
+def test_attention_dropout_matches_reference_mask(attn_waves):
     B, S, H, D = 2, 128, 2, 64
     qkv = torch.randn(B * S, 3 * H * D, device=dev).to(torch.bfloat16)
     p, seed = 0.1, 77
