@@ -1250,7 +1250,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("get_deterministic", []() { return mipipe::g_deterministic != 0; });
   m.def("tune_table", []() { return tune::g_table; });
   m.def("set_tune_entry", [](const std::string& k, int cfg) {
-    TORCH_CHECK(cfg >= -1 && cfg < mipipe::kConvTileConfigs, "bad tile config id");
+    // plans: tile id + 16 * (split-K count | direct-epilogue flag)
+    TORCH_CHECK(cfg == -1 || (cfg >= 0 && cfg % 16 < mipipe::kConvTileConfigs),
+                "bad tile plan id");
     if (cfg < 0) tune::g_table.erase(k);
     else tune::g_table[k] = cfg;
   });
