@@ -349,7 +349,9 @@ std::tuple<Tensor, Tensor> bn_bwd_collect(Tensor rep, int64_t C, optional<Tensor
 }
 
 Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, optional<Tensor> out,
-                  int stride_w, int pad_w, int cfg) {
+                  int stride_w, int pad_w, int cfg, optional<Tensor> col_rep,
+                  optional<Tensor> col_out, optional<Tensor> col_dgamma,
+                  optional<Tensor> col_dbeta) {
   check_act(dy, "dy");
   check_same(x, dy, "x");
   c10::DeviceGuard g(dy.device());
@@ -373,6 +375,24 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
   } else {
     dw = torch::zeros({s.Co, kh, kw, s.Ci}, x.options().dtype(at::kFloat));
   }
+  // optional BN-backward collect riding in the launch (bn_bwd_collect's work, BnCollect)
+  mipipe::BnCollect col;
+  const mipipe::BnCollect* colp = nullptr;
+  if (col_rep.has_value()) {
+    check_f32(*col_rep, "col_rep");
+    const int64_t C = col_rep->numel() / (3ll * mipipe::kStatReplicas);
+    TORCH_CHECK(col_rep->numel() == 3ll * mipipe::kStatReplicas * C, "col_rep must be [3,R,C]");
+    TORCH_CHECK(col_out.has_value(), "col_out needed");
+    check_f32(*col_out, "col_out");
+    TORCH_CHECK(col_out->numel() == 2 * C && col_out->is_contiguous(), "col_out must be [2,C]");
+    TORCH_CHECK(col_dgamma.has_value() == col_dbeta.has_value(), "pass both accumulators or none");
+    col.rep = col_rep->data_ptr<float>();
+    col.C = (int)C;
+    col.out = col_out->data_ptr<float>();
+    col.dgamma = fptr(col_dgamma, C);
+    col.dbeta = fptr(col_dbeta, C);
+    colp = &col;
+  }
   // plan = tile id + 16 * split count (0: heuristic split)
   int plan = cfg;
   if (plan < 0) {
@@ -392,16 +412,16 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
     const int splits = mipipe::conv_wgrad_splits(s, tile, sp);
     if (splits == 1) {  // one writer per element: the plain read-modify-write is deterministic
       mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), tile,
-                         nullptr, 1);
+                         nullptr, 1, colp);
       return dw;
     }
     auto ws = torch::empty({splits, (int64_t)s.Co * kh * kw * s.Ci}, dy.options().dtype(at::kFloat));
     mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), tile,
-                       ws.data_ptr<float>(), sp);
+                       ws.data_ptr<float>(), sp, colp);
     return dw;
   }
   mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), tile,
-                     nullptr, sp);
+                     nullptr, sp, colp);
   return dw;
 }
 
@@ -1238,7 +1258,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("out") = py::none(), py::arg("stride_w") = 0,
-        py::arg("pad_w") = -1, py::arg("cfg") = -1);
+        py::arg("pad_w") = -1, py::arg("cfg") = -1, py::arg("col_rep") = py::none(),
+        py::arg("col_out") = py::none(), py::arg("col_dgamma") = py::none(),
+        py::arg("col_dbeta") = py::none());
   m.attr("CONV_TILE_CONFIGS") = mipipe::kConvTileConfigs;
   m.def("set_benchmark", [](bool on, bool verbose, int reps) {
     tune::g_benchmark = on;

@@ -161,6 +161,7 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_wgrad_ker
   const int nk = (int)((K + BK - 1) / BK);
   const int kt0 = blockIdx.y * kt_per_split;
   const int kt1 = min(nk, kt0 + kt_per_split);
+  if (e.col.rep != nullptr && blockIdx.x == 0 && blockIdx.y == 0) bn_collect_block<C::THREADS>(e.col);
   OpA a;
   a.init(dy, Co, Co, K, m0, wave, lane, g_conv_zero);
   OpB b;

@@ -49,11 +49,13 @@ int conv_wgrad_splits(const ConvShape& s, int cfg, int splits_req) {
 
 template <class T>
 static void conv_wgrad_t(const void* dy, const void* x, float* dw, const ConvShape& s,
-                         hipStream_t st, int cfg, float* ws, int splits_req) {
+                         hipStream_t st, int cfg, float* ws, int splits_req,
+                         const BnCollect* col) {
   ConvGeom g = make_geom(s);
   const uint32_t Ntot = (uint32_t)(s.KH * s.KW * s.Ci);
   EpiParams e{};
   e.C = dw; e.ldc = Ntot; e.M = s.Co; e.N = Ntot;
+  if (col != nullptr) e.col = *col;
   const bool dense = is_dense(s);
   const T* dyp = (const T*)dy;
   const T* xp = (const T*)x;
@@ -87,9 +89,9 @@ static void conv_wgrad_t(const void* dy, const void* x, float* dw, const ConvSha
 }
 
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
-                int cfg, float* ws, int splits) {
-  if (s.f32) conv_wgrad_t<float>(dy, x, dw, s, st, cfg, ws, splits);
-  else conv_wgrad_t<__bf16>(dy, x, dw, s, st, cfg, ws, splits);
+                int cfg, float* ws, int splits, const BnCollect* col) {
+  if (s.f32) conv_wgrad_t<float>(dy, x, dw, s, st, cfg, ws, splits, col);
+  else conv_wgrad_t<__bf16>(dy, x, dw, s, st, cfg, ws, splits, col);
 }
 
 }  // namespace mipipe

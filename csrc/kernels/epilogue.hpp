@@ -44,7 +44,40 @@ struct EpiParams {
   // epilogue_f32 without ATOMIC: add the tile to the existing C (read-modify-write; each
   // element owned by one block) instead of overwriting it
   int rmw;
+  // optional BN-backward collect done by block (0,0) of this launch (launchers.hpp BnCollect)
+  BnCollect col;
 };
+
+// BnCollect riding in a kernel: the block sums the replica rows of a bwd slab that the previous
+// kernel filled, re-zeroes them and writes Σg / Σg·x̂ (+ dβ, dγ).  Each thread issues all of a
+// channel's replica loads before any add (one memory latency per channel group).
+template <int THREADS>
+__device__ void bn_collect_block(const BnCollect c) {
+  constexpr int R = kStatReplicas;
+  const long rs = (long)R * c.C;
+  for (int ch = threadIdx.x; ch < c.C; ch += THREADS) {
+    float va[R], vb[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      va[r] = c.rep[(long)r * c.C + ch];
+      vb[r] = c.rep[rs + (long)r * c.C + ch];
+    }
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {  // fixed order: deterministic
+      a += va[r];
+      b += vb[r];
+      c.rep[(long)r * c.C + ch] = 0.f;
+      c.rep[rs + (long)r * c.C + ch] = 0.f;
+    }
+    c.out[ch] = a;
+    c.out[c.C + ch] = b;
+    if (c.dgamma != nullptr) {
+      c.dgamma[ch] += b;
+      c.dbeta[ch] += a;
+    }
+  }
+}
 
 // Workgroup barrier that orders LDS only.  __syncthreads() also drains every outstanding global
 // load / store / atomic (s_waitcnt vmcnt(0)), which here would expose the latency of the

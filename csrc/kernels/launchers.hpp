@@ -73,8 +73,21 @@ int conv_dgrad_tiles_m(const ConvShape& s, int cfg);  // M-tiles over all stride
 // lands directly in the DDP bucket).  splits: > 0 forces the split-K count, -1 = heuristic.
 //  ws != nullptr (deterministic mode): [conv_wgrad_splits(s, cfg, splits)][Co*KH*KW*Ci] workspace
 //  for the split-K partials, summed into dw in split order.
+// BN-backward collect riding in another kernel: block (0,0) of the kernel sums the replica rows
+// of a bwd slab that the PREVIOUS kernel filled (the fused dgrad of the same conv), writes
+// out[0][C] = Σg, out[1][C] = Σg·x̂, re-zeroes the slab and accumulates dβ += Σg, dγ += Σg·x̂
+// (dgamma / dbeta may be null) — the work of a separate bn_bwd_collect launch, whose ~6 us
+// standalone cost grows to 10-15 us right after a large kernel (tools/r2/collect_probe.py), hidden
+// in the weight-grad kernel that runs between the dgrad and the BN apply anyway.
+struct BnCollect {
+  float* rep = nullptr;  // [3][kStatReplicas][C] slab; null: nothing to collect
+  int C = 0;
+  float* out = nullptr;
+  float *dgamma = nullptr, *dbeta = nullptr;
+};
+// col: optional collect riding in this launch (see BnCollect)
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
-                int cfg = -1, float* ws = nullptr, int splits = -1);
+                int cfg = -1, float* ws = nullptr, int splits = -1, const BnCollect* col = nullptr);
 int conv_wgrad_splits(const ConvShape& s, int cfg, int splits = -1);
 
 // ---- direct convolution, BatchNorm for any C, k x k average pool (vision.hip) ----------------

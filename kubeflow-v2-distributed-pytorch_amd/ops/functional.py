@@ -86,7 +86,7 @@ class BNActToken:
     """Links a BN(+ReLU) output to its single consuming conv: the conv's backward computes the
     BN-backward reductions in its dgrad epilogue and flags the BN's backward to skip them."""
 
-    __slots__ = ("bn", "st", "y", "_z", "mask", "pre_reduced")
+    __slots__ = ("bn", "st", "y", "_z", "mask", "pre_reduced", "collected")
 
     @property
     def z(self):
@@ -106,6 +106,9 @@ class BNActToken:
         self.bn, self.st, self.y, self.z = bn, st, y, z
         self.mask = None
         self.pre_reduced = False
+        # (Σg/Σg·x̂ [2, C], direct dγ/dβ accumulated) when the consuming conv's weight-grad
+        # launch already collected the bwd slab (BnCollect), else None
+        self.collected = None
 
 
 class _ConvFn(Function):
@@ -132,6 +135,7 @@ class _ConvFn(Function):
         stride, pad, kh, kw, ci = ctx.conf
         dy = dy.contiguous()
         dx = dw = None
+        bnr = tok = None
         if ctx.needs_input_grad[0]:
             if not isinstance(stride, int):
                 raise NotImplementedError("dgrad of a non-square-stride conv")
@@ -153,16 +157,29 @@ class _ConvFn(Function):
                 dx = ctx.res_give.produce(dx)
         if ctx.needs_input_grad[1]:
             weight = ctx.weight
+            collect = None
+            if bnr is not None:
+                # the weight-grad launch also collects the slab the fused dgrad just filled
+                # (one of its blocks; no separate bn_bwd_collect launch)
+                bn = tok.bn
+                out2 = torch.empty(2, bn.num_features, device=dy.device, dtype=torch.float32)
+                tg = _direct_grad_target(bn.weight) if bn.weight is not None else None
+                tb = _direct_grad_target(bn.bias) if bn.bias is not None else None
+                direct = (tg is not None and tb is not None and bn.weight.requires_grad
+                          and bn.bias.requires_grad)
+                collect = (bnr[5], out2, tg[1] if direct else None, tb[1] if direct else None)
+                tok.collected = (out2, direct)
             tgt = (_direct_grad_target(weight)
                    if x.shape[-1] == ci and ctx.wmap is None and K.use_native(dy) else None)
             if tgt is not None:
                 # gradient accumulates straight into the flat DDP bucket: no zero-fill, no
                 # autograd AccumulateGrad add; tell the reducer the gradient is ready.
                 fs, g = tgt
-                K.conv_wgrad(dy, x, kh, kw, stride, pad, out=g.permute(0, 2, 3, 1))
+                K.conv_wgrad(dy, x, kh, kw, stride, pad, out=g.permute(0, 2, 3, 1),
+                             collect=collect)
                 fs.grad_ready(weight)
             else:
-                dw = K.conv_wgrad(dy, x, kh, kw, stride, pad)
+                dw = K.conv_wgrad(dy, x, kh, kw, stride, pad, collect=collect)
                 if ctx.wmap is not None:  # kernel layout -> parameter layout (packed stem)
                     dw = ctx.wmap(dw)
                 else:
@@ -494,11 +511,17 @@ class _BNActFn(Function):
         rep = bn.__dict__["_mipipe_ws_bwd"]
         C = y.shape[-1]
         direct = None
-        if ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
-            tg, tb = _direct_grad_target(gamma), _direct_grad_target(ctx.beta)
-            if tg is not None and tb is not None:
-                direct = (tg[1], tb[1])
-        sg, sgx = K.bn_bwd_collect(rep, C, direct)
+        if tok.collected is not None:  # collected by the consuming conv's weight-grad launch
+            out2, used_direct = tok.collected
+            tok.collected = None
+            sg, sgx = out2[0], out2[1]
+            direct = (True,) if used_direct else None
+        else:
+            if ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
+                tg, tb = _direct_grad_target(gamma), _direct_grad_target(ctx.beta)
+                if tg is not None and tb is not None:
+                    direct = (tg[1], tb[1])
+            sg, sgx = K.bn_bwd_collect(rep, C, direct)
         _ws_done(bn, "bwd")
         if direct is not None:
             fs = _direct_grad_target(gamma)[0]

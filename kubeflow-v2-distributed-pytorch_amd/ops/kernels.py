@@ -90,13 +90,18 @@ def bn_bwd_collect(rep, C, acc=None):
     return native().bn_bwd_collect(rep, C, *a)
 
 
-def conv_wgrad(dy, x, kh, kw, stride, pad, out=None):
+def conv_wgrad(dy, x, kh, kw, stride, pad, out=None, collect=None):
     """``out``: accumulate into this fp32 [Co,KH,KW,Ci] buffer (the parameter's flat gradient).
-    ``stride``: int or (vertical, horizontal)."""
+    ``stride``: int or (vertical, horizontal).  ``collect = (rep, out2, dgamma, dbeta)`` (native):
+    one block of the launch also does :func:`bn_bwd_collect` of ``rep`` into ``out2`` [2, C]
+    (Σg, Σg·x̂; dgamma / dbeta accumulators or None) — the slab a fused dgrad just filled."""
     sh, sw = (stride, 0) if isinstance(stride, int) else (stride[0], stride[1])
     if use_native(dy):
         ph, pw = _pads(pad)
-        return native().conv_wgrad(dy, x, kh, kw, sh, ph, out, sw, pw)
+        c = collect if collect is not None else (None, None, None, None)
+        return native().conv_wgrad(dy, x, kh, kw, sh, ph, out, sw, pw, -1, *c)
+    if collect is not None:
+        raise RuntimeError("collect-in-wgrad is a native-kernel path")
     dw = _ref.conv_wgrad(dy, x, kh, kw, stride if isinstance(stride, int) else tuple(stride),
                          pad if isinstance(pad, int) else tuple(pad))
     if out is not None:

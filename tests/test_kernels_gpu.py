@@ -358,6 +358,43 @@ def test_conv_dgrad_fused_epilogues(case):
     assert rel_err(only_add, dx) < 2e-2
 
 
+@pytest.mark.parametrize("case", [(2, 16, 16, 64, 64, 3, 1, 1), (2, 14, 14, 64, 256, 1, 2, 0),
+                                  (4, 7, 7, 512, 2048, 1, 1, 0)])
+def test_bn_collect_rides_in_wgrad(case):
+    """The weight-grad launch collects the slab the fused dgrad filled (BnCollect): same Σg /
+    Σg·x̂ / dγ / dβ as bn_bwd_collect, slab re-zeroed, weight gradient unchanged."""
+    N, H, W, Ci, Co, k, s, p = case
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = bf(N, Ho, Wo, Co)
+    w = bf(Co, k, k, Ci, scale=0.1)
+    x = bf(N, H, W, Ci)
+    y = bf(N, H, W, Ci)
+    mean = torch.randn(Ci, device=dev) * 0.1
+    invstd = torch.rand(Ci, device=dev) + 0.5
+    scale = torch.randn(Ci, device=dev)
+    bias = torch.randn(Ci, device=dev) * 0.3
+    R = native().STAT_REPLICAS
+    reps = [torch.zeros(3, R, Ci, device=dev) for _ in range(2)]
+    for rep in reps:
+        native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, None, y, mean, invstd, scale, bias, rep)
+    dgam, dbet = torch.zeros(Ci, device=dev), torch.ones(Ci, device=dev)
+    sg, sgx = native().bn_bwd_collect(reps[0], Ci, dgam, dbet)
+    dgam2, dbet2 = torch.zeros(Ci, device=dev), torch.ones(Ci, device=dev)
+    out2 = torch.full((2, Ci), float("nan"), device=dev)
+    dw = native().conv_wgrad(dy, x, k, k, s, p, col_rep=reps[1], col_out=out2,
+                             col_dgamma=dgam2, col_dbeta=dbet2)
+    dw_ref = native().conv_wgrad(dy, x, k, k, s, p)
+    assert rel_err(dw, dw_ref) < 1e-5
+    assert rel_err(out2[0], sg) < 1e-4 and rel_err(out2[1], sgx) < 1e-4
+    assert rel_err(dgam2, dgam) < 1e-4 and rel_err(dbet2 - 1, dbet - 1) < 1e-4
+    assert float(reps[1].abs().max()) == 0.0
+    # without accumulators
+    native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, None, y, mean, invstd, scale, bias, reps[1])
+    out3 = torch.empty(2, Ci, device=dev)
+    native().conv_wgrad(dy, x, k, k, s, p, col_rep=reps[1], col_out=out3)
+    assert rel_err(out3[1], sgx) < 1e-3 and float(reps[1].abs().max()) == 0.0
+
+
 def test_conv_fwd_bias_relu_epilogue():
     N, H, W, Ci, Co = 2, 12, 12, 64, 96
     x = bf(N, H, W, Ci)
