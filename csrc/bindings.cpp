@@ -288,6 +288,9 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     check_vec(*bn_bias, s.Ci, "bn_bias");
     check_f32(*bn_rep, "bn_rep");
     TORCH_CHECK(bn_rep->numel() == 3ll * mipipe::kStatReplicas * s.Ci, "bn_rep must be [3,R,Ci]");
+    for (const Tensor* t : {&*bn_mean, &*bn_invstd, &*bn_scale, &*bn_bias})
+      TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                  "BN fusion vectors must be 16-byte aligned (the epilogue reads them as float4)");
     fz.bn_y = bn_y->data_ptr();
     fz.bn_mean = bn_mean->data_ptr<float>(); fz.bn_invstd = bn_invstd->data_ptr<float>();
     fz.bn_scale = bn_scale->data_ptr<float>(); fz.bn_bias = bn_bias->data_ptr<float>();

@@ -24,6 +24,14 @@ __device__ __forceinline__ float bf16_bits_to_f(uint16_t b) {
   return __uint_as_float(((uint32_t)b) << 16);
 }
 
+// 8 consecutive fp32 (16-B aligned) as two 16-B loads.
+__device__ __forceinline__ void ld_f32x8(const float* p, float* f) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0];
+  const float4 b = reinterpret_cast<const float4*>(p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+  f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
 // Unpack 8 bf16 held in a uint4 to floats.
 __device__ __forceinline__ void unpack8(const uint4& u, float* f) {
   f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);

@@ -173,6 +173,24 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
   Ops& ops = early != nullptr ? *early : local;
   if (early == nullptr) ops.prime(e, m0, n0);
   (void)ld_n;
+  // BN-backward coefficients of this thread's 8 columns, requested now (16-B vector loads; the
+  // host checks N % 8 == 0 and 16-B alignment) so their latency hides under the staging below:
+  // issued as 32 scalar loads at the store loop they cost the layer-1 fused data-grads ~35 %
+  // (tools/r2/knob_probe.py).  scale / bias only when the ReLU mask is recomputed from y.
+  float b_sc[8], b_bi[8], b_mu[8], b_is[8];
+  if (bnr) {
+    const bool okc = my_n < e.N;
+    const uint32_t cn = okc ? my_n : 0;
+    if (!bmask && !zmask) {
+      ld_f32x8(e.bnr_scale + cn, b_sc);
+      ld_f32x8(e.bnr_bias + cn, b_bi);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) b_sc[q] = b_bi[q] = 0.f;
+    }
+    ld_f32x8(e.bnr_mean + cn, b_mu);
+    ld_f32x8(e.bnr_invstd + cn, b_is);
+  }
   // bias / activation
   if (e.bias != nullptr || e.act) {
 #pragma unroll
@@ -275,16 +293,9 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
     }
   }
   T* C = reinterpret_cast<T*>(e.C);
-  float b_sc[8], b_bi[8], b_mu[8], b_is[8], sg[8], sgx[8];
+  float sg[8], sgx[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    sg[q] = sgx[q] = 0.f;
-    const bool ok = bnr && my_n + q < e.N;
-    b_sc[q] = ok ? e.bnr_scale[my_n + q] : 0.f;
-    b_bi[q] = ok ? e.bnr_bias[my_n + q] : 0.f;
-    b_mu[q] = ok ? e.bnr_mean[my_n + q] : 0.f;
-    b_is[q] = ok ? e.bnr_invstd[my_n + q] : 0.f;
-  }
+  for (int q = 0; q < 8; ++q) sg[q] = sgx[q] = 0.f;
 #pragma unroll
   for (int it = 0; it < ITER; ++it) {
     const int c = threadIdx.x + it * kThreads;
