@@ -104,6 +104,22 @@ __device__ __forceinline__ float as_stored(float v) {
   else return bf2f(f2bf(v));
 }
 
+// DPP lane move within 16-lane rows (VALU only; no LDS crossbar like ds_bpermute).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xF, 0xF, false));
+}
+// Sum over each 16-lane DPP row (lanes 16r .. 16r+15); every lane of the row gets the total.
+// quad_perm [1,0,3,2] (xor 1), [2,3,0,1] (xor 2), then row_ror 4 and row_ror 8.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x124>(v);
+  v += dpp_f<0x128>(v);
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

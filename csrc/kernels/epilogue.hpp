@@ -235,12 +235,9 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
         }
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s[q] += __shfl_xor(s[q], o);
-          ss[q] += __shfl_xor(ss[q], o);
-        }
+      for (int q = 0; q < 4; ++q) {  // over the 16 lanes (rows) of each DPP row: VALU only
+        s[q] = row16_sum(s[q]);
+        ss[q] = row16_sum(ss[q]);
       }
       if ((lane & 15) == 0) {
         uint32_t nl = nl0 + j * 16;
