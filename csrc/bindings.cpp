@@ -600,6 +600,79 @@ std::tuple<Tensor, Tensor> maxpool_fwd(Tensor x, int k, int s, int p, bool ceil_
   return {y, idx};
 }
 
+// Stem fusion: max-pool of relu(y*scale + bias) without storing the normalised activation.
+std::tuple<Tensor, Tensor> pool_bn_fwd(Tensor y, Tensor scale, Tensor bias, int k, int s, int p) {
+  check_act(y, "y");
+  c10::DeviceGuard g(y.device());
+  int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0 && k <= 15, "pool_bn: C % 8 == 0, 256 % (C/8) == 0");
+  TORCH_CHECK(k >= 1 && s >= 1 && p >= 0 && 2 * p <= k, "bad maxpool geometry");
+  check_vec(scale, C, "scale");
+  check_vec(bias, C, "bias");
+  for (const Tensor* t : {&scale, &bias})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "pool_bn vectors: 16-B aligned");
+  int Ho = pool_out(H, k, s, p, false), Wo = pool_out(W, k, s, p, false);
+  TORCH_CHECK(Ho > 0 && Wo > 0, "empty maxpool output");
+  auto out = torch::empty({N, Ho, Wo, C}, y.options());
+  auto idx = torch::empty({N, Ho, Wo, C}, y.options().dtype(at::kByte));
+  mipipe::pool_bn_fwd(y.data_ptr(), scale.data_ptr<float>(), bias.data_ptr<float>(), out.data_ptr(),
+                      idx.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, k, s, p, stream(), is_f32(y));
+  return {out, idx};
+}
+
+// Its backward: Σg, Σg·x̂ (replica slab `rep`, re-zeroed) -> (+ dγ, dβ accumulators) -> dy.
+// Returns (dy, Σg, Σg·x̂).
+std::tuple<Tensor, Tensor, Tensor> pool_bn_bwd(Tensor dp, Tensor idx, Tensor pout, Tensor y,
+                                               Tensor mean, Tensor invstd, Tensor gamma, Tensor rep,
+                                               int64_t count, int k, int s, int p,
+                                               optional<Tensor> dgamma, optional<Tensor> dbeta) {
+  check_act(dp, "dp");
+  check_same(pout, dp, "pout");
+  check_same(y, dp, "y");
+  check_cuda(idx, "idx");
+  c10::DeviceGuard g(dp.device());
+  int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  int Ho = dp.size(1), Wo = dp.size(2);
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "pool_bn: C % 8 == 0, 256 % (C/8) == 0");
+  TORCH_CHECK(idx.sizes() == dp.sizes() && pout.sizes() == dp.sizes() && dp.size(3) == C,
+              "pool_bn_bwd shape mismatch");
+  TORCH_CHECK(Ho == pool_out(H, k, s, p, false) && Wo == pool_out(W, k, s, p, false),
+              "pool_bn_bwd geometry mismatch");
+  for (const Tensor* t : {&mean, &invstd, &gamma}) check_vec(*t, C, "BN vector");
+  for (const Tensor* t : {&mean, &invstd})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "pool_bn vectors: 16-B aligned");
+  check_f32(rep, "rep");
+  TORCH_CHECK(rep.numel() == 3ll * mipipe::kStatReplicas * C, "rep must be [3,R,C]");
+  TORCH_CHECK(dgamma.has_value() == dbeta.has_value(), "pass both accumulators or none");
+  const bool f32 = is_f32(dp);
+  const long pixels = (long)N * H * W;
+  if (mipipe::g_deterministic) {
+    const int G = mipipe::pool_bn_bwd_reduce_blocks(pixels, C);
+    auto part = torch::empty({2, G, C}, dp.options().dtype(at::kFloat));
+    float* p0 = part.data_ptr<float>();
+    mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), pout.data_ptr(), y.data_ptr(),
+                               mean.data_ptr<float>(), invstd.data_ptr<float>(), N, H, W, C, Ho, Wo,
+                               k, s, p, p0, G, stream(), f32);
+    float* r = rep.data_ptr<float>();
+    mipipe::det_sum_rows(p0, p0 + (long)G * C, G, C, r, r + (long)mipipe::kStatReplicas * C, false,
+                         stream());
+  } else {
+    mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), pout.data_ptr(), y.data_ptr(),
+                               mean.data_ptr<float>(), invstd.data_ptr<float>(), N, H, W, C, Ho, Wo,
+                               k, s, p, rep.data_ptr<float>(), 0, stream(), f32);
+  }
+  auto o = rep.options();
+  auto sg = torch::empty({C}, o), sgx = torch::empty({C}, o);
+  mipipe::bn_bwd_collect(rep.data_ptr<float>(), C, sg.data_ptr<float>(), sgx.data_ptr<float>(),
+                         fptr(dgamma, C), fptr(dbeta, C), stream());
+  auto dy = torch::empty_like(y);
+  mipipe::pool_bn_bwd_apply(dp.data_ptr(), idx.data_ptr<uint8_t>(), pout.data_ptr(), y.data_ptr(),
+                            mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                            gamma.data_ptr<float>(), sg.data_ptr<float>(), sgx.data_ptr<float>(),
+                            count, dy.data_ptr(), N, H, W, C, Ho, Wo, k, s, p, stream(), f32);
+  return {dy, sg, sgx};
+}
+
 Tensor maxpool_bwd(Tensor dy, Tensor idx, std::vector<int64_t> xs, int k, int s, int p) {
   check_act(dy, "dy");
   check_cuda(idx, "idx");
@@ -1313,6 +1386,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("avgpool2d_fwd", &avgpool2d_fwd);
   m.def("avgpool2d_bwd", &avgpool2d_bwd);
   m.def("maxpool_bwd_impl", &maxpool_bwd);
+  m.def("pool_bn_fwd", &pool_bn_fwd, py::arg("y"), py::arg("scale"), py::arg("bias"), py::arg("k"),
+        py::arg("s"), py::arg("p"));
+  m.def("pool_bn_bwd", &pool_bn_bwd, py::arg("dp"), py::arg("idx"), py::arg("pout"), py::arg("y"),
+        py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("rep"), py::arg("count"),
+        py::arg("k"), py::arg("s"), py::arg("p"), py::arg("dgamma") = py::none(),
+        py::arg("dbeta") = py::none());
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("trans_a"), py::arg("trans_b"),

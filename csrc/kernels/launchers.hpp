@@ -181,6 +181,24 @@ void maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int 
                  int k, int stride, int pad, hipStream_t st, bool f32 = false);
 void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int N, int H, int W, int C, int Ho,
                  int Wo, int k, int stride, int pad, hipStream_t st, bool f32 = false);
+// Stem fusion (pool.hip): out = maxpool_k,s,p(relu(y*scale + bias)) + window argmax idx, and
+// the backward as gathers over the windows (g = Σ dp over windows whose argmax is the pixel and
+// whose output is > 0): Σg, Σg·x̂ into the replica slab rep ([3][kStatReplicas][C]; det_rows > 0:
+// rep is [2][det_rows][C] partial rows, one per block), then dy = A·g + B·y + C.
+// C % 8 == 0 and 256 % (C / 8) == 0.
+void pool_bn_fwd(const void* y, const float* scale, const float* bias, void* out, uint8_t* idx,
+                 int N, int H, int W, int C, int Ho, int Wo, int k, int stride, int pad,
+                 hipStream_t st, bool f32 = false);
+int pool_bn_bwd_reduce_blocks(long pixels, int C);
+void pool_bn_bwd_reduce(const void* dp, const uint8_t* idx, const void* pout, const void* y,
+                        const float* mean, const float* invstd, int N, int H, int W, int C,
+                        int Ho, int Wo, int k, int stride, int pad, float* rep, int det_rows,
+                        hipStream_t st, bool f32 = false);
+void pool_bn_bwd_apply(const void* dp, const uint8_t* idx, const void* pout, const void* y,
+                       const float* mean, const float* invstd, const float* gamma,
+                       const float* sum_g, const float* sum_gx, long count, void* dy, int N, int H,
+                       int W, int C, int Ho, int Wo, int k, int stride, int pad, hipStream_t st,
+                       bool f32 = false);
 void avgpool_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st, bool f32 = false);
 void avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st, bool f32 = false);
 

@@ -219,8 +219,7 @@ class ResNet(tnn.Module):
     def forward_features(self, x: torch.Tensor) -> torch.Tensor:
         """NCHW float input -> NHWC features of layer4."""
         x = self.conv1.pack_input(x, self.activation_dtype(x))
-        x = mnn.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-        x = self.maxpool(x)
+        x = mnn.conv_bn_relu_maxpool(x, self.conv1, self.bn1, self.maxpool)
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)

@@ -233,12 +233,32 @@ class ReLU(tnn.ReLU):
     pass
 
 
+def conv_bn_relu_maxpool(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d,
+                         pool: "MaxPool2d") -> torch.Tensor:
+    """maxpool(relu(bn(conv(x)))) — the ResNet stem — with BN-apply, ReLU and the pool in one
+    kernel (the normalised activation is never stored) and a gather-based fused backward."""
+    if pool.ceil_mode or pool.dilation not in (1, (1, 1)):
+        return pool(conv_bn_act(x, conv, bn, relu=True))
+    use_batch = bn.training
+    if use_batch:
+        ws = MF.bn_workspace(bn, "fwd", x.device)
+        y, ps, pss = conv(x, bn.running_mean, None if ws is None else (ws[0], ws[1]))
+    else:
+        y, ps, pss = conv(x), None, None
+    st = MF.bn_stats_from_partials(ps, pss, y.numel() // y.shape[-1], bn, use_batch)
+    k, s, p = pool.geometry()
+    return MF.bn_relu_maxpool(y, st, bn, k, s, p)
+
+
 class MaxPool2d(tnn.MaxPool2d):
-    def forward(self, x):  # NHWC
+    def geometry(self):
         k = self.kernel_size if isinstance(self.kernel_size, int) else self.kernel_size[0]
         s = self.stride if isinstance(self.stride, int) else self.stride[0]
         p = self.padding if isinstance(self.padding, int) else self.padding[0]
-        return MF.max_pool2d(x, k, s, p)
+        return k, s, p
+
+    def forward(self, x):  # NHWC
+        return MF.max_pool2d(x, *self.geometry())
 
 
 class AdaptiveAvgPool2d(tnn.AdaptiveAvgPool2d):

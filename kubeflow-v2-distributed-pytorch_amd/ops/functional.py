@@ -615,6 +615,54 @@ class _MaxPoolFn(Function):
         return K.maxpool_bwd(dy.contiguous(), idx, ctx.xshape, *ctx.conf), None, None, None, None
 
 
+class _PoolBNFn(Function):
+    """maxpool_k,s,p(relu(bn(y))) in one pass (the ResNet stem: BN1 + ReLU + 3x3/2 max-pool);
+    the backward gathers over the pooling windows twice (Σg / Σg·x̂, then dy) instead of
+    scattering dz, reducing and applying over the full-resolution tensors (pool.hip)."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, st, bn, k, stride, pad):
+        out, idx = K.pool_bn_fwd(y, st.scale, st.bias, k, stride, pad)
+        ctx.save_for_backward(y, out, idx, gamma)
+        ctx.st, ctx.bn, ctx.beta, ctx.conf = st, bn, beta, (k, stride, pad)
+        ctx.mark_non_differentiable(idx)
+        return out, idx
+
+    @staticmethod
+    def backward(ctx, dp, _didx):
+        y, out, idx, gamma = ctx.saved_tensors
+        st, bn = ctx.st, ctx.bn
+        if not st.batch_stats:
+            raise RuntimeError("pool_bn backward needs batch statistics (training mode)")
+        rep = bn_workspace(bn, "bwd", dp.device)
+        direct = None
+        if ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
+            tg, tb = _direct_grad_target(gamma), _direct_grad_target(ctx.beta)
+            if tg is not None and tb is not None:
+                direct = (tg[1], tb[1])
+        dy, sg, sgx = K.pool_bn_bwd(dp.contiguous(), idx, out, y, st.mean, st.invstd,
+                                    gamma.detach().float(), rep, st.count, *ctx.conf, acc=direct)
+        _ws_done(bn, "bwd")
+        if direct is not None:
+            fs = _direct_grad_target(gamma)[0]
+            fs.grad_ready(gamma)
+            fs.grad_ready(ctx.beta)
+            return dy, None, None, None, None, None, None, None
+        return (dy, sgx.to(gamma.dtype) if ctx.needs_input_grad[1] else None,
+                sg.to(gamma.dtype) if ctx.needs_input_grad[2] else None,
+                None, None, None, None, None)
+
+
+def bn_relu_maxpool(y: Tensor, st: BNStats, bn, k: int, stride: int, pad: int) -> Tensor:
+    """maxpool(relu(bn(y))) on NHWC ``y``: fused kernels on the GPU (training with batch
+    statistics or eval), the unfused BN-apply + max-pool otherwise."""
+    if (K.pool_bn_supported(y) and (st.batch_stats or not torch.is_grad_enabled())
+            and st.scale.dtype == torch.float32):
+        out, _ = _PoolBNFn.apply(y, bn.weight, bn.bias, st, bn, k, stride, pad)
+        return out
+    return max_pool2d(batchnorm_act(y, st, bn, relu=True), k, stride, pad)
+
+
 def max_pool2d(x: Tensor, k: int, stride: int, pad: int, ceil_mode: bool = False) -> Tensor:
     return _MaxPoolFn.apply(x, k, stride, pad, bool(ceil_mode))
 

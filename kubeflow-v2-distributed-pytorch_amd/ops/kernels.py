@@ -17,7 +17,7 @@ from ._native import native, native_available
 
 __all__ = ["conv_fwd", "conv_dgrad", "conv_wgrad", "bn_finalize", "bn_act_fwd",
            "bn_act_bwd_reduce", "bn_act_bwd_apply", "maxpool_fwd", "maxpool_bwd",
-           "avgpool_fwd", "avgpool_bwd", "gemm", "cross_entropy_fwd_bwd", "top1_correct", "sgd_step",
+           "avgpool_fwd", "avgpool_bwd", "pool_bn_fwd", "pool_bn_bwd", "pool_bn_supported", "gemm", "cross_entropy_fwd_bwd", "top1_correct", "sgd_step",
            "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd", "dropout_fwd", "colsum", "bn_bwd_collect", "stem_pack",
            "embedding_bwd", "gelu_fwd", "gelu_bwd", "nchw_to_nhwc", "use_native",
            "gconv_fwd", "gconv_dgrad", "gconv_wgrad", "chan_stats", "affine_act",
@@ -183,6 +183,25 @@ def maxpool_bwd(dy, idx, x_shape, k, stride, pad):
     if use_native(dy):
         return native().maxpool_bwd_impl(dy, idx, list(x_shape), k, stride, pad)
     return _ref.maxpool_bwd(dy, idx, x_shape)
+
+
+def pool_bn_fwd(y, scale, bias, k, stride, pad):
+    """(maxpool(relu(y*scale + bias)), window argmax) without storing the normalised
+    activation (native; NHWC, C % 8 == 0 and 256 % (C/8) == 0)."""
+    return native().pool_bn_fwd(y, scale, bias, k, stride, pad)
+
+
+def pool_bn_bwd(dp, idx, pout, y, mean, invstd, gamma, rep, count, k, stride, pad, acc=None):
+    """Backward of :func:`pool_bn_fwd` + the BN statistics: (dy, Σg, Σg·x̂); ``acc`` = (dγ, dβ)
+    accumulators (the flat gradient buffer) or None.  ``rep``: zeroed bwd replica slab."""
+    a = acc if acc is not None else (None, None)
+    return native().pool_bn_bwd(dp, idx, pout, y, mean, invstd, gamma, rep, count, k, stride, pad,
+                                *a)
+
+
+def pool_bn_supported(y) -> bool:
+    C = y.shape[-1]
+    return use_native(y) and C % 8 == 0 and 256 % (C // 8) == 0
 
 
 def avgpool_fwd(x):

@@ -36,6 +36,18 @@ def graph_safe(model: torch.nn.Module, optimizer) -> Tuple[bool, str]:
     return True, ""
 
 
+def _drain_collective_watchdog(wait_s: float = 0.5) -> None:
+    """Let the process group's watchdog thread retire the (completed) work of the eager warm-up
+    collectives before capture starts: it polls every ~100 ms with event queries, and a query
+    that lands inside the capture window can fail and abort the process (seen once in ~10
+    world-1 RCCL captures, tests/test_ddp_gpu.py).  The device is idle here, so every pending
+    work object completes on its next poll."""
+    import time
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        time.sleep(wait_s)
+
+
 class GraphedStep:
     """Capture ``step_fn(x, y) -> loss`` into hipGraph(s) after ``warmup`` eager steps.
 
@@ -59,6 +71,7 @@ class GraphedStep:
                 self.fn(x, y).detach()
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
+        _drain_collective_watchdog()
         self.graphs: List[torch.cuda.CUDAGraph] = []
         self.losses: List[torch.Tensor] = []
         pool = None

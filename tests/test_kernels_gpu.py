@@ -540,3 +540,43 @@ def test_relu_bitmask_matches_stored_z(C):
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-5)
     assert torch.allclose(outs[0][2], outs[1][2], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape", [(4, 32, 32, 64), (2, 17, 15, 64), (3, 12, 12, 128)])
+@pytest.mark.parametrize("det", [0, 1])
+def test_pool_bn_fused_matches_unfused(shape, det):
+    """Stem fusion: maxpool(relu(bn(y))) in one kernel + gather backward == the unfused
+    BN-apply -> max-pool -> max-pool backward -> BN reduce -> BN apply chain."""
+    from mipipe.ops import kernels as Kx
+    from mipipe.ops import determinism
+    N, H, W, C = shape
+    y = bf(N, H, W, C)
+    scale = torch.randn(C, device=dev)
+    bias = torch.randn(C, device=dev) * 0.5
+    mean = torch.randn(C, device=dev) * 0.1
+    invstd = torch.rand(C, device=dev) + 0.5
+    gamma = torch.randn(C, device=dev)
+    count = N * H * W
+    R = native().STAT_REPLICAS
+    old = determinism.deterministic_enabled()
+    determinism.set_deterministic(bool(det))
+    try:
+        out, idx = Kx.pool_bn_fwd(y, scale, bias, 3, 2, 1)
+        z = Kx.bn_act_fwd(y, scale, bias, True)
+        out2, idx2 = Kx.maxpool_fwd(z, 3, 2, 1)
+        assert torch.equal(out, out2) and torch.equal(idx, idx2)
+        dp = bf(*out.shape)
+        rep = torch.zeros(3, R, C, device=dev)
+        dg, db = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        dy, sg, sgx = Kx.pool_bn_bwd(dp, idx, out, y, mean, invstd, gamma, rep, count, 3, 2, 1,
+                                     acc=(dg, db))
+        assert float(rep.abs().max()) == 0.0
+        dz = Kx.maxpool_bwd(dp, idx2, z.shape, 3, 2, 1)
+        rep2 = torch.zeros(3, R, C, device=dev)
+        sg2, sgx2, _ = Kx.bn_act_bwd_reduce(dz, z, y, mean, invstd, True, rep=rep2)
+        dy2, _ = Kx.bn_act_bwd_apply(dz, z, y, mean, invstd, gamma, sg2, sgx2, count, True)
+        assert rel_err(sg, sg2) < 1e-4 and rel_err(sgx, sgx2) < 1e-4
+        assert rel_err(dg, sgx2) < 1e-4 and rel_err(db - 1, sg2) < 1e-4
+        assert rel_err(dy, dy2) < 1e-2
+    finally:
+        determinism.set_deterministic(old)
