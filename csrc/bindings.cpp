@@ -249,7 +249,8 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
                   optional<Tensor> addend, optional<Tensor> bn_y, optional<Tensor> bn_mean,
                   optional<Tensor> bn_invstd, optional<Tensor> bn_scale, optional<Tensor> bn_bias,
                   optional<Tensor> bn_rep, optional<Tensor> bn_z, int pad_w, int cfg,
-                  optional<Tensor> bn_mask) {
+                  optional<Tensor> bn_mask, optional<Tensor> bn_y2, optional<Tensor> bn_mean2,
+                  optional<Tensor> bn_invstd2) {
   check_act(dy, "dy");
   check_same(w, dy, "w");
   c10::DeviceGuard g(dy.device());
@@ -306,6 +307,21 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
       TORCH_CHECK(bn_z->sizes() == dx.sizes(), "bn_z must match dx");
       fz.bn_z = bn_z->data_ptr();
     }
+    if (bn_y2.has_value()) {  // two-branch block output: relu(bn(y) + bn2(y2))
+      TORCH_CHECK(bn_mean2.has_value() && bn_invstd2.has_value(), "bn_y2 needs mean2/invstd2");
+      TORCH_CHECK(!s.f32 && s.KH == 1 && s.KW == 1 && stride == 1 && pad == 0 && pw == 0,
+                  "two-branch BN fusion: bf16 1x1 stride-1 data-grads only");
+      check_same(*bn_y2, dy, "bn_y2");
+      TORCH_CHECK(bn_y2->sizes() == dx.sizes(), "bn_y2 must match dx");
+      check_vec(*bn_mean2, s.Ci, "bn_mean2");
+      check_vec(*bn_invstd2, s.Ci, "bn_invstd2");
+      for (const Tensor* t : {&*bn_mean2, &*bn_invstd2})
+        TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                    "BN fusion vectors must be 16-byte aligned");
+      fz.bn_y2 = bn_y2->data_ptr();
+      fz.bn_mean2 = bn_mean2->data_ptr<float>();
+      fz.bn_invstd2 = bn_invstd2->data_ptr<float>();
+    }
     any = true;
   }
   if (cfg < 0) {
@@ -323,14 +339,17 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
   }
   if (mipipe::g_deterministic && fz.bn_rep != nullptr) {
     const int P = mipipe::conv_dgrad_tiles_m(s, cfg);
-    auto part = torch::empty({2, P, s.Ci}, dy.options().dtype(at::kFloat));
+    const bool two = fz.bn_y2 != nullptr;
+    auto part = torch::empty({two ? 3 : 2, P, s.Ci}, dy.options().dtype(at::kFloat));
     float* rep = fz.bn_rep;
     fz.bn_rep = part.data_ptr<float>();
     fz.det_rows = P;
     mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), &fz, cfg);
-    const long rs = (long)mipipe::kStatReplicas * s.Ci;
-    mipipe::det_sum_rows(fz.bn_rep, fz.bn_rep + (long)P * s.Ci, P, s.Ci, rep, rep + rs, false,
-                         stream());
+    const long rs = (long)mipipe::kStatReplicas * s.Ci, ps = (long)P * s.Ci;
+    mipipe::det_sum_rows(fz.bn_rep, fz.bn_rep + ps, P, s.Ci, rep, rep + rs, false, stream());
+    if (two)
+      mipipe::det_sum_rows(fz.bn_rep + 2 * ps, nullptr, P, s.Ci, rep + 2 * rs, nullptr, false,
+                           stream());
     return dx;
   }
   mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), any ? &fz : nullptr,
@@ -354,7 +373,8 @@ std::tuple<Tensor, Tensor> bn_bwd_collect(Tensor rep, int64_t C, optional<Tensor
 Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, optional<Tensor> out,
                   int stride_w, int pad_w, int cfg, optional<Tensor> col_rep,
                   optional<Tensor> col_out, optional<Tensor> col_dgamma,
-                  optional<Tensor> col_dbeta) {
+                  optional<Tensor> col_dbeta, bool col_two, optional<Tensor> col_dgamma2,
+                  optional<Tensor> col_dbeta2) {
   check_act(dy, "dy");
   check_same(x, dy, "x");
   c10::DeviceGuard g(dy.device());
@@ -387,13 +407,18 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
     TORCH_CHECK(col_rep->numel() == 3ll * mipipe::kStatReplicas * C, "col_rep must be [3,R,C]");
     TORCH_CHECK(col_out.has_value(), "col_out needed");
     check_f32(*col_out, "col_out");
-    TORCH_CHECK(col_out->numel() == 2 * C && col_out->is_contiguous(), "col_out must be [2,C]");
+    TORCH_CHECK(col_out->numel() == (col_two ? 3 : 2) * C && col_out->is_contiguous(),
+                "col_out must be [2,C] ([3,C] with col_two)");
     TORCH_CHECK(col_dgamma.has_value() == col_dbeta.has_value(), "pass both accumulators or none");
+    TORCH_CHECK(col_dgamma2.has_value() == col_dbeta2.has_value(), "pass both accumulators or none");
     col.rep = col_rep->data_ptr<float>();
     col.C = (int)C;
     col.out = col_out->data_ptr<float>();
     col.dgamma = fptr(col_dgamma, C);
     col.dbeta = fptr(col_dbeta, C);
+    col.two = col_two;
+    col.dgamma2 = fptr(col_dgamma2, C);
+    col.dbeta2 = fptr(col_dbeta2, C);
     colp = &col;
   }
   // plan = tile id + 16 * split count (0: heuristic split)
@@ -1329,14 +1354,16 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bn_invstd") = py::none(), py::arg("bn_scale") = py::none(),
         py::arg("bn_bias") = py::none(), py::arg("bn_rep") = py::none(),
         py::arg("bn_z") = py::none(), py::arg("pad_w") = -1, py::arg("cfg") = -1,
-        py::arg("bn_mask") = py::none());
+        py::arg("bn_mask") = py::none(), py::arg("bn_y2") = py::none(),
+        py::arg("bn_mean2") = py::none(), py::arg("bn_invstd2") = py::none());
   m.def("bn_bwd_collect", &bn_bwd_collect, py::arg("rep"), py::arg("C"),
         py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("out") = py::none(), py::arg("stride_w") = 0,
         py::arg("pad_w") = -1, py::arg("cfg") = -1, py::arg("col_rep") = py::none(),
         py::arg("col_out") = py::none(), py::arg("col_dgamma") = py::none(),
-        py::arg("col_dbeta") = py::none());
+        py::arg("col_dbeta") = py::none(), py::arg("col_two") = false,
+        py::arg("col_dgamma2") = py::none(), py::arg("col_dbeta2") = py::none());
   m.attr("CONV_TILE_CONFIGS") = mipipe::kConvTileConfigs;
   m.def("set_benchmark", [](bool on, bool verbose, int reps) {
     tune::g_benchmark = on;

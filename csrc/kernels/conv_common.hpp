@@ -109,7 +109,8 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_fwd_kerne
   epilogue_out<BM, BN, false, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
-template <class C, bool DENSE, bool ALIGNED, class T>
+// TWO: BN-backward fusion of a two-branch block output (dense bf16 data-grads only)
+template <class C, bool DENSE, bool ALIGNED, class T, bool TWO = false>
 __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_dgrad_kernel(
     const T* __restrict__ dy, const T* __restrict__ w, int Ho, int Wo, int Co, int taps,
     FastDiv fCo, DgradClass cls, uint32_t M, uint32_t tilesN, EpiParams e) {
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_dgrad_ker
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
   MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN>::type::run(smem, a, b, 0, nk, acc, wave,
                                                                     lane);
-  epilogue_out<BM, BN, true, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
+  epilogue_out<BM, BN, true, T, C::WM, C::WN, TWO>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
 // ATOMIC: split-K partial tiles added with fp32 atomics; else the block owns its output tile

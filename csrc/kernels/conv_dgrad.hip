@@ -82,6 +82,9 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
         e.bnr_scale = fz->bn_scale; e.bnr_bias = fz->bn_bias; e.bnr_rep = fz->bn_rep; e.st_R = g_stat_rows;
         e.bnr_z = fz->bn_z;
         e.bnr_mask = fz->bn_mask;
+        e.bnr_y2 = fz->bn_y2;
+        e.bnr_mean2 = fz->bn_mean2;
+        e.bnr_invstd2 = fz->bn_invstd2;
         e.det_rows = fz->det_rows;
         e.det_row0 = row0;
       }
@@ -96,7 +99,10 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
         const uint32_t tN = cdiv(s.Ci, C::BN), tiles = cdiv(M, C::BM) * tN;
         row0 += (int)cdiv(M, C::BM);
         const dim3 grid(tiles), block(C::THREADS);
-        if (dense)
+        if (e.bnr_y2 != nullptr) {  // two-branch block output (host checks: dense, bf16)
+          if constexpr (std::is_same<T, __bf16>::value)
+            hipLaunchKernelGGL((conv_dgrad_kernel<C, true, false, T, true>), grid, block, 0, st, dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
+        } else if (dense)
           hipLaunchKernelGGL((conv_dgrad_kernel<C, true, false, T>), grid, block, 0, st, dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else if (aligned)
           hipLaunchKernelGGL((conv_dgrad_kernel<C, false, true, T>), grid, block, 0, st, dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);

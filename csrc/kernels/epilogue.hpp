@@ -34,6 +34,10 @@ struct EpiParams {
   // when set, the ReLU mask is read from this stored post-activation tensor (z > 0) instead of
   // recomputed from y (needed when a residual was added before the ReLU)
   const void* bnr_z;  // output dtype
+  // two-branch BN (ResNet downsample block output relu(bn(y) + bn2(y2))): Σg·x̂₂ goes to the
+  // third slab array (TWO epilogues only)
+  const void* bnr_y2;
+  const float *bnr_mean2, *bnr_invstd2;
   const uint8_t* bnr_mask;  // or the mask as bits: [rows][ldc / 8] bytes, bit q = column 8c+q
   // deterministic mode (det_rows > 0): no float atomics.  Statistics partials (st_sum / st_sq,
   // bnr_rep) are WRITTEN at row det_row0 + (m0 / BM) of [det_rows][N] slabs (bnr_rep: two
@@ -76,6 +80,19 @@ __device__ void bn_collect_block(const BnCollect c) {
       c.dgamma[ch] += b;
       c.dbeta[ch] += a;
     }
+    if (c.two) {  // Σg·x̂₂ of the second branch (dβ₂ = Σg as well)
+      float d = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        d += c.rep[2 * rs + (long)r * c.C + ch];
+        c.rep[2 * rs + (long)r * c.C + ch] = 0.f;
+      }
+      c.out[2 * c.C + ch] = d;
+      if (c.dgamma2 != nullptr) {
+        c.dgamma2[ch] += d;
+        c.dbeta2[ch] += a;
+      }
+    }
   }
 }
 
@@ -108,13 +125,13 @@ constexpr int kEpiLdsBytes() { return kStatsLdsOffset<BM, BN, T>() + 2 * WM * BN
 // (Priming it before a short main loop was measured slower in round 2: the seven ResNet-50
 // layer-1 1x1 data-grads went from ~1.9 ms to 3.4 ms per step — the early loads stretch the main
 // loop's vmcnt waits and the registers' lifetime.)
-template <int BM, int BN, bool FUSE, class T, int WM, int WN>
+template <int BM, int BN, bool FUSE, class T, int WM, int WN, bool TWO = false>
 struct EpiOps {
   static constexpr int kThreads = 64 * WM * WN;
   static constexpr int CPR = BN / 8;  // 8-element chunks per row
   static constexpr int ITER = BM * CPR / kThreads;
   static constexpr int PF = FUSE ? (ITER < 4 ? ITER : 4) : 1;
-  Raw8<T> ad[PF], y[PF], z[PF];
+  Raw8<T> ad[PF], y[PF], z[PF], y2[TWO ? PF : 1];
   uint32_t mk[PF];
   __device__ __forceinline__ void issue(const EpiParams& e, uint32_t m0, uint32_t n0, int it,
                                         int slot) {
@@ -126,6 +143,8 @@ struct EpiOps {
     if (e.addend != nullptr) ad[slot] = ld_raw8(reinterpret_cast<const T*>(e.addend) + orow * e.ldc + ld_n);
     if (e.bnr_rep != nullptr) {
       y[slot] = ld_raw8(reinterpret_cast<const T*>(e.bnr_y) + orow * e.ldc + ld_n);
+      if constexpr (TWO)
+        y2[slot] = ld_raw8(reinterpret_cast<const T*>(e.bnr_y2) + orow * e.ldc + ld_n);
       if (e.bnr_mask != nullptr)
         mk[slot] = e.bnr_mask[orow * (e.ldc / 8) + ld_n / 8];
       else if (e.bnr_z != nullptr)
@@ -144,11 +163,13 @@ struct EpiOps {
 // acc layout: lane holds C[m][n..n+3] for tile (i, j).
 // FUSE: compile the dgrad fusions (addend / BN-backward reduction); kernels that never use
 // them keep their register budget.  early: an operand ring the kernel already primed.
-template <int BM, int BN, bool FUSE = false, class T = __bf16, int WM = 2, int WN = 2>
+// TWO: the BN-backward fusion of a two-branch block output (e.bnr_y2 set, FUSE only).
+template <int BM, int BN, bool FUSE = false, class T = __bf16, int WM = 2, int WN = 2,
+          bool TWO = false>
 __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                              const EpiParams& e, uint32_t m0, uint32_t n0, uint32_t prow_base,
                              int wave, int lane,
-                             EpiOps<BM, BN, FUSE, T, WM, WN>* early = nullptr) {
+                             EpiOps<BM, BN, FUSE, T, WM, WN, TWO>* early = nullptr) {
   constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
   constexpr int kThreads = 64 * WM * WN;
   const int wr = wave / WN, wc = wave % WN;
@@ -167,7 +188,7 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
   const uint32_t ld_n = my_n < e.N ? my_n : 0;
   // software-pipelined operand ring: PF iterations in flight; the first PF are issued now (unless
   // the kernel primed them before its main loop) so their latency overlaps the staging below
-  typedef EpiOps<BM, BN, FUSE, T, WM, WN> Ops;
+  typedef EpiOps<BM, BN, FUSE, T, WM, WN, TWO> Ops;
   constexpr int PF = Ops::PF;
   Ops local;
   Ops& ops = early != nullptr ? *early : local;
@@ -190,6 +211,14 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
     }
     ld_f32x8(e.bnr_mean + cn, b_mu);
     ld_f32x8(e.bnr_invstd + cn, b_is);
+  }
+  float b_mu2[TWO ? 8 : 1], b_is2[TWO ? 8 : 1], sgx2[TWO ? 8 : 1];
+  if constexpr (TWO) {
+    const uint32_t cn = my_n < e.N ? my_n : 0;
+    ld_f32x8(e.bnr_mean2 + cn, b_mu2);
+    ld_f32x8(e.bnr_invstd2 + cn, b_is2);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sgx2[q] = 0.f;
   }
   // bias / activation
   if (e.bias != nullptr || e.act) {
@@ -327,6 +356,12 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
             sg[q] += gq;
             sgx[q] += gq * (yv[q] - b_mu[q]) * b_is[q];
           }
+          if constexpr (TWO) {
+            float y2v[8];
+            unpack_raw(ops.y2[it % PF], y2v);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sgx2[q] += f[q] * (y2v[q] - b_mu2[q]) * b_is2[q];
+          }
         }
         store8(C + orow * e.ldc + n, f);
       } else {
@@ -361,6 +396,23 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
           e.bnr_rep[((long)arr * e.det_rows + e.det_row0 + m0 / BM) * e.N + n0 + col] = a;
         else
           atomicAdd(e.bnr_rep + ((long)arr * R + blockIdx.x % Rw) * e.N + n0 + col, a);
+      }
+    }
+    if constexpr (TWO) {  // Σg·x̂₂: third array, through the same LDS rows
+      lds_barrier();
+#pragma unroll
+      for (int q = 0; q < 8; ++q) red[q * RP + threadIdx.x] = sgx2[q];
+      lds_barrier();
+      for (int col = threadIdx.x; col < BN; col += kThreads) {
+        const int cc = col >> 3, q = col & 7;
+        float a = 0.f;
+        for (int t = cc; t < kThreads; t += CPR) a += red[q * RP + t];
+        if (n0 + col < e.N) {
+          if (e.det_rows > 0)
+            e.bnr_rep[((long)2 * e.det_rows + e.det_row0 + m0 / BM) * e.N + n0 + col] = a;
+          else
+            atomicAdd(e.bnr_rep + ((long)2 * R + blockIdx.x % Rw) * e.N + n0 + col, a);
+        }
       }
     }
   }

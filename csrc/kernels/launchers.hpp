@@ -63,6 +63,9 @@ struct DgradFusion {
   float* bn_rep = nullptr;
   const void* bn_z = nullptr;  // optional stored relu output: mask = z > 0 (residual blocks)
   const uint8_t* bn_mask = nullptr;  // or that mask as bits ([rows][Ci/8] bytes, bit q = chan q)
+  // two-branch block output relu(bn(y) + bn2(y2)): Σg·x̂₂ to rep array 2 (bf16, 1x1 convs)
+  const void* bn_y2 = nullptr;
+  const float *bn_mean2 = nullptr, *bn_invstd2 = nullptr;
   int det_rows = 0;  // deterministic mode: bn_rep is [2][det_rows][Ci] partials, one row per tile
 };
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
@@ -82,8 +85,11 @@ int conv_dgrad_tiles_m(const ConvShape& s, int cfg);  // M-tiles over all stride
 struct BnCollect {
   float* rep = nullptr;  // [3][kStatReplicas][C] slab; null: nothing to collect
   int C = 0;
-  float* out = nullptr;
+  float* out = nullptr;  // [2][C], or [3][C] with `two`
   float *dgamma = nullptr, *dbeta = nullptr;
+  // two-branch block output: also Σg·x̂₂ (slab array 2) -> out[2][C]; dγ₂ += Σg·x̂₂, dβ₂ += Σg
+  bool two = false;
+  float *dgamma2 = nullptr, *dbeta2 = nullptr;
 };
 // col: optional collect riding in this launch (see BnCollect)
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,

@@ -216,7 +216,17 @@ def conv_bn_act(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d, relu: bool = Tru
         else:
             yb, psb, pssb = convb(xb, res_give=res_give), None, None
         stb = MF.bn_stats_from_partials(psb, pssb, count, bnb, bnb.training)
-        return MF.batchnorm_act(y, st, bn, relu, y2=yb, st2=stb, bn2=bnb)
+        token = None
+        if relu and use_batch and bnb.training:
+            # the block output's consumer (next block's conv1, which also adds the identity
+            # gradient) reduces both BNs' backward in its dgrad epilogue (two-branch fusion)
+            token = MF.BNActToken(bn, st, y)
+            token.y2, token.st2, token.bn2 = yb, stb, bnb
+        z = MF.batchnorm_act(y, st, bn, relu, y2=yb, st2=stb, bn2=bnb, token=token)
+        if token is not None:
+            token.z = z
+            z._mipipe_bnact = token
+        return z
     token = None
     if relu and use_batch:
         token = MF.BNActToken(bn, st, y)

@@ -86,7 +86,7 @@ class BNActToken:
     """Links a BN(+ReLU) output to its single consuming conv: the conv's backward computes the
     BN-backward reductions in its dgrad epilogue and flags the BN's backward to skip them."""
 
-    __slots__ = ("bn", "st", "y", "_z", "mask", "pre_reduced", "collected")
+    __slots__ = ("bn", "st", "y", "_z", "mask", "pre_reduced", "collected", "y2", "st2", "bn2")
 
     @property
     def z(self):
@@ -106,9 +106,11 @@ class BNActToken:
         self.bn, self.st, self.y, self.z = bn, st, y, z
         self.mask = None
         self.pre_reduced = False
-        # (Σg/Σg·x̂ [2, C], direct dγ/dβ accumulated) when the consuming conv's weight-grad
-        # launch already collected the bwd slab (BnCollect), else None
+        # (Σg/Σg·x̂[/Σg·x̂₂] [2|3, C], direct dγ/dβ accumulated, direct dγ₂/dβ₂ accumulated) when
+        # the consuming conv's weight-grad launch already collected the bwd slab (BnCollect)
         self.collected = None
+        # two-branch block output relu(bn(y) + bn2(y2)) (ResNet downsample block)
+        self.y2 = self.st2 = self.bn2 = None
 
 
 class _ConvFn(Function):
@@ -142,7 +144,13 @@ class _ConvFn(Function):
             addend = ctx.res_take.take() if ctx.res_take is not None else None
             bnr = None
             tok = ctx.prev
-            if (tok is not None and K.use_native(dy) and tok.st.batch_stats
+            two = tok is not None and tok.y2 is not None
+            # the two-branch fusion: bf16 1x1 stride-1 data-grads whose weight-grad launch (which
+            # collects the third slab array) follows
+            two_ok = (not two or (kh == 1 and kw == 1 and stride == 1 and pad == 0
+                                  and dy.dtype == torch.bfloat16 and ctx.needs_input_grad[1]
+                                  and tok.st2.batch_stats))
+            if (tok is not None and K.use_native(dy) and tok.st.batch_stats and two_ok
                     and (tok.z is None or addend is not None)):
                 rep = bn_workspace(tok.bn, "bwd", dy.device)  # zeroed; pending until collect
                 if rep is not None:
@@ -150,7 +158,8 @@ class _ConvFn(Function):
                     bnr = (tok.y, st.mean, st.invstd, st.scale, st.bias, rep)
                     if tok.z is not None:
                         bnr = bnr + (tok.mask if tok.mask is not None else tok.z,)
-            dx = K.conv_dgrad(dy, w_c, x.shape, stride, pad, addend=addend, bnr=bnr)
+            bnr2 = (tok.y2, tok.st2.mean, tok.st2.invstd) if bnr is not None and two else None
+            dx = K.conv_dgrad(dy, w_c, x.shape, stride, pad, addend=addend, bnr=bnr, bnr2=bnr2)
             if bnr is not None:
                 tok.pre_reduced = True
             if ctx.res_give is not None:
@@ -161,14 +170,21 @@ class _ConvFn(Function):
             if bnr is not None:
                 # the weight-grad launch also collects the slab the fused dgrad just filled
                 # (one of its blocks; no separate bn_bwd_collect launch)
+                two = tok.y2 is not None
                 bn = tok.bn
-                out2 = torch.empty(2, bn.num_features, device=dy.device, dtype=torch.float32)
-                tg = _direct_grad_target(bn.weight) if bn.weight is not None else None
-                tb = _direct_grad_target(bn.bias) if bn.bias is not None else None
-                direct = (tg is not None and tb is not None and bn.weight.requires_grad
-                          and bn.bias.requires_grad)
-                collect = (bnr[5], out2, tg[1] if direct else None, tb[1] if direct else None)
-                tok.collected = (out2, direct)
+                out2 = torch.empty(3 if two else 2, bn.num_features, device=dy.device,
+                                   dtype=torch.float32)
+
+                def targets(m):
+                    tg = _direct_grad_target(m.weight) if m.weight is not None else None
+                    tb = _direct_grad_target(m.bias) if m.bias is not None else None
+                    ok = (tg is not None and tb is not None and m.weight.requires_grad
+                          and m.bias.requires_grad)
+                    return (tg[1], tb[1]) if ok else (None, None)
+                t1 = targets(bn)
+                t2 = targets(tok.bn2) if two else (None, None)
+                collect = (bnr[5], out2) + t1 + ((True,) + t2 if two else ())
+                tok.collected = (out2, t1[0] is not None, t2[0] is not None)
             tgt = (_direct_grad_target(weight)
                    if x.shape[-1] == ci and ctx.wmap is None and K.use_native(dy) else None)
             if tgt is not None:
@@ -452,7 +468,7 @@ class _BNActFn(Function):
         dz = dz.contiguous()
         tok = ctx.token
         if tok is not None and tok.pre_reduced:
-            return _BNActFn._backward_pre_reduced(ctx, dz, y, gamma)
+            return _BNActFn._backward_pre_reduced(ctx, dz, y, gamma, y2, gamma2)
         rep = bn_workspace(ctx.bn, "bwd", dz.device) if ctx.bn is not None else None
         # BN affine grads accumulate straight into the flat gradient buffer when possible
         direct = None
@@ -502,17 +518,36 @@ class _BNActFn(Function):
                 None, None)
 
     @staticmethod
-    def _backward_pre_reduced(ctx, g, y, gamma):
-        """The consuming conv's dgrad already produced g = dz·relu'(z) and Σg, Σg·x̂ in the
-        bwd replica slab: collect them (+ direct dγ/dβ) and apply, no reduction pass."""
+    def _backward_pre_reduced(ctx, g, y, gamma, y2=None, gamma2=None):
+        """The consuming conv's dgrad already produced g = dz·relu'(z) and Σg, Σg·x̂ (and
+        Σg·x̂₂ of a two-branch output) in the bwd replica slab: collect them (+ direct dγ/dβ)
+        and apply, no reduction pass."""
         tok = ctx.token
         tok.pre_reduced = False
         st, bn = ctx.st, ctx.bn
         rep = bn.__dict__["_mipipe_ws_bwd"]
         C = y.shape[-1]
         direct = None
+        if y2 is not None:  # two-branch: always collected by the weight-grad launch
+            out3, d1, d2 = tok.collected
+            tok.collected = None
+            sg, sgx, sgx2 = out3[0], out3[1], out3[2]
+            _ws_done(bn, "bwd")
+            st2 = ctx.st2
+            for used, (ga, be) in ((d1, (gamma, ctx.beta)), (d2, (gamma2, ctx.beta2))):
+                if used:
+                    fs = _direct_grad_target(ga)[0]
+                    fs.grad_ready(ga)
+                    fs.grad_ready(be)
+            dy, dy2 = K.bn_act_bwd_apply(g, g, y, st.mean, st.invstd, gamma.detach(), sg, sgx,
+                                         st.count, False, y2=y2, mean2=st2.mean,
+                                         invstd2=st2.invstd, gamma2=gamma2.detach(),
+                                         sum_gx2=sgx2)
+            return (dy, None if d1 else sgx.to(gamma.dtype), None if d1 else sg.to(gamma.dtype),
+                    None, dy2, None if d2 else sgx2.to(gamma2.dtype),
+                    None if d2 else sg.to(gamma2.dtype), None, None, None, None, None, None)
         if tok.collected is not None:  # collected by the consuming conv's weight-grad launch
-            out2, used_direct = tok.collected
+            out2, used_direct, _ = tok.collected
             tok.collected = None
             sg, sgx = out2[0], out2[1]
             direct = (True,) if used_direct else None

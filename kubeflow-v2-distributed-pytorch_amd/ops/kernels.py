@@ -61,12 +61,13 @@ def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None, bias=None, relu=Fa
     return y, a, b
 
 
-def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None):
+def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None, bnr2=None):
     """dx of an NHWC conv.  ``addend``: tensor added to dx in the epilogue (residual gradient).
     ``bnr = (y, mean, invstd, scale, bias, rep[, z])``: the conv input was relu(bn(y)[+res]);
     dx becomes g = dx·[z > 0] (z recomputed from y unless given — as the stored tensor, or as
     its uint8 bit mask from ``bn_act_fwd(mask=)``) and Σg, Σg·x̂ accumulate into ``rep`` rows
-    0/1 (native only)."""
+    0/1 (native only).  ``bnr2 = (y2, mean2, invstd2)``: the input was relu(bn(y) + bn2(y2))
+    (ResNet downsample block output): Σg·x̂₂ into ``rep`` array 2 (bf16 1x1 convs)."""
     if use_native(dy):
         ph, pw = _pads(pad)
         if bnr is None:
@@ -76,8 +77,10 @@ def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None):
         mask = None
         if z is not None and z.dtype == torch.uint8:
             z, mask = None, z
+        y2, mean2, invstd2 = bnr2 if bnr2 is not None else (None, None, None)
         return native().conv_dgrad(dy, w, list(x_shape), stride, ph, addend, y, mean, invstd,
-                                   scale, bias, rep, z, pw, bn_mask=mask)
+                                   scale, bias, rep, z, pw, bn_mask=mask, bn_y2=y2,
+                                   bn_mean2=mean2, bn_invstd2=invstd2)
     if bnr is not None:
         raise RuntimeError("BN-reduce dgrad fusion is a native-kernel path")
     dx = _ref.conv_dgrad(dy, w, x_shape, stride, pad if isinstance(pad, int) else tuple(pad))
@@ -92,13 +95,16 @@ def bn_bwd_collect(rep, C, acc=None):
 
 def conv_wgrad(dy, x, kh, kw, stride, pad, out=None, collect=None):
     """``out``: accumulate into this fp32 [Co,KH,KW,Ci] buffer (the parameter's flat gradient).
-    ``stride``: int or (vertical, horizontal).  ``collect = (rep, out2, dgamma, dbeta)`` (native):
-    one block of the launch also does :func:`bn_bwd_collect` of ``rep`` into ``out2`` [2, C]
-    (Σg, Σg·x̂; dgamma / dbeta accumulators or None) — the slab a fused dgrad just filled."""
+    ``stride``: int or (vertical, horizontal).  ``collect = (rep, out2, dgamma, dbeta[, True,
+    dgamma2, dbeta2])`` (native): one block of the launch also does :func:`bn_bwd_collect` of
+    ``rep`` into ``out2`` [2, C] (Σg, Σg·x̂; dgamma / dbeta accumulators or None) — the slab a
+    fused dgrad just filled; the 7-tuple form also collects Σg·x̂₂ (out2 [3, C])."""
     sh, sw = (stride, 0) if isinstance(stride, int) else (stride[0], stride[1])
     if use_native(dy):
         ph, pw = _pads(pad)
-        c = collect if collect is not None else (None, None, None, None)
+        c = tuple(collect) if collect is not None else (None, None, None, None)
+        if len(c) == 4:
+            c = c + (False, None, None)
         return native().conv_wgrad(dy, x, kh, kw, sh, ph, out, sw, pw, -1, *c)
     if collect is not None:
         raise RuntimeError("collect-in-wgrad is a native-kernel path")

@@ -580,3 +580,51 @@ def test_pool_bn_fused_matches_unfused(shape, det):
         assert rel_err(dy, dy2) < 1e-2
     finally:
         determinism.set_deterministic(old)
+
+
+@pytest.mark.parametrize("case", [(2, 16, 16, 256, 64), (4, 7, 7, 2048, 512), (8, 28, 28, 512, 128)])
+@pytest.mark.parametrize("det", [0, 1])
+def test_conv_dgrad_two_branch_bn_fusion(case, det):
+    """Downsample-block output relu(bn(y) + bn2(y2)) consumed by a 1x1 conv: its dgrad epilogue
+    masks g with the stored ReLU bits, adds the identity gradient and reduces Σg, Σg·x̂, Σg·x̂₂;
+    the weight-grad launch collects all three (dγ/dβ, dγ₂/dβ₂ accumulated)."""
+    from mipipe.ops import determinism
+    N, H, W, Ci, Co = case
+    dy = bf(N, H, W, Co)
+    w = bf(Co, 1, 1, Ci, scale=0.05)
+    x = bf(N, H, W, Ci)
+    add = bf(N, H, W, Ci)
+    y, y2 = bf(N, H, W, Ci), bf(N, H, W, Ci)
+    mean, mean2 = torch.randn(Ci, device=dev) * 0.1, torch.randn(Ci, device=dev) * 0.1
+    invstd, invstd2 = torch.rand(Ci, device=dev) + 0.5, torch.rand(Ci, device=dev) + 0.5
+    scale, bias = torch.randn(Ci, device=dev), torch.randn(Ci, device=dev) * 0.3
+    z = bf(N, H, W, Ci)  # any tensor: the mask is its sign
+    bits = torch.empty(z.numel() // 8, dtype=torch.uint8, device=dev)
+    zz = native().bn_act_fwd(z, torch.ones(Ci, device=dev), torch.zeros(Ci, device=dev), True,
+                             None, None, None, bits)
+    R = native().STAT_REPLICAS
+    rep = torch.zeros(3, R, Ci, device=dev)
+    old = determinism.deterministic_enabled()
+    determinism.set_deterministic(bool(det))
+    try:
+        g = native().conv_dgrad(dy, w, [N, H, W, Ci], 1, 0, add, y, mean, invstd, scale, bias,
+                                rep, None, bn_mask=bits, bn_y2=y2, bn_mean2=mean2,
+                                bn_invstd2=invstd2)
+        out3 = torch.empty(3, Ci, device=dev)
+        dg, db, dg2, db2 = (torch.zeros(Ci, device=dev) for _ in range(4))
+        native().conv_wgrad(dy, x, 1, 1, 1, 0, col_rep=rep, col_out=out3, col_dgamma=dg,
+                            col_dbeta=db, col_two=True, col_dgamma2=dg2, col_dbeta2=db2)
+    finally:
+        determinism.set_deterministic(old)
+    dx = _ref.conv_dgrad(dy.float(), w.float(), (N, H, W, Ci), 1, 0) + add.float()
+    g_ref = dx * (zz.float() > 0)
+    assert rel_err(g, g_ref) < 2e-2
+    gb = g.float().reshape(-1, Ci)
+    sg = gb.sum(0)
+    sgx = (gb * ((y.float() - mean) * invstd).reshape(-1, Ci)).sum(0)
+    sgx2 = (gb * ((y2.float() - mean2) * invstd2).reshape(-1, Ci)).sum(0)
+    assert rel_err(out3[0], sg) < 1e-3 and rel_err(out3[1], sgx) < 1e-3
+    assert rel_err(out3[2], sgx2) < 1e-3
+    assert rel_err(dg, sgx) < 1e-3 and rel_err(db, sg) < 1e-3
+    assert rel_err(dg2, sgx2) < 1e-3 and rel_err(db2, sg) < 1e-3
+    assert float(rep.abs().max()) == 0.0
