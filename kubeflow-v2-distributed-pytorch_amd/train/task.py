@@ -104,7 +104,8 @@ class CrossEntropyLoss(torch.nn.Module):
 
 
 def _unwrap(model):
-    return model.module if isinstance(model, (DistributedDataParallel, torch.nn.DataParallel)) else model
+    return model.module if isinstance(model, (DistributedDataParallel, DataParallel,
+                                          torch.nn.DataParallel)) else model
 
 
 @torch.no_grad()
