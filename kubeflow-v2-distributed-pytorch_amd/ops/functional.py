@@ -86,7 +86,8 @@ class BNActToken:
     """Links a BN(+ReLU) output to its single consuming conv: the conv's backward computes the
     BN-backward reductions in its dgrad epilogue and flags the BN's backward to skip them."""
 
-    __slots__ = ("bn", "st", "y", "_z", "mask", "pre_reduced", "collected", "y2", "st2", "bn2")
+    __slots__ = ("bn", "st", "y", "_z", "mask", "pre_reduced", "collected", "y2", "st2", "bn2",
+                 "rep")
 
     @property
     def z(self):
@@ -111,6 +112,7 @@ class BNActToken:
         self.collected = None
         # two-branch block output relu(bn(y) + bn2(y2)) (ResNet downsample block)
         self.y2 = self.st2 = self.bn2 = None
+        self.rep = None  # the bwd slab the consuming dgrad filled (this pass's own slab)
 
 
 class _ConvFn(Function):
@@ -153,6 +155,7 @@ class _ConvFn(Function):
             if (tok is not None and K.use_native(dy) and tok.st.batch_stats and two_ok
                     and (tok.z is None or addend is not None)):
                 rep = bn_workspace(tok.bn, "bwd", dy.device)  # zeroed; pending until collect
+                tok.rep = rep
                 if rep is not None:
                     st = tok.st
                     bnr = (tok.y, st.mean, st.invstd, st.scale, st.bias, rep)
@@ -399,7 +402,11 @@ class BNStats:
 def bn_workspace(bn, kind: str, device) -> Optional[Tensor]:
     """Persistent zero-initialised replica slab for BN statistics on the GPU ('fwd': [2,R,C],
     'bwd': [3,R,C]).  Kernels that accumulate into it are always followed by the kernel that
-    reads AND re-zeroes it; a per-module 'pending' flag re-zeroes after an interrupted step."""
+    reads AND re-zeroes it.  A per-module 'pending' flag marks a slab between those two kernels:
+    if it is still set when the slab is requested again, either a step was interrupted or the
+    module is used twice in one graph (a chunk loop, shared weights) and the two backward passes
+    interleave — a FRESH slab then replaces the cached one (the in-flight user keeps its own),
+    instead of re-zeroing a slab another pass is still accumulating into."""
     if device.type != "cuda" or not K.native_available():
         return None
     C = bn.num_features
@@ -412,7 +419,8 @@ def bn_workspace(bn, kind: str, device) -> Optional[Tensor]:
         bn.__dict__[attr] = ws
     pend = "_mipipe_pending_" + kind
     if bn.__dict__.get(pend):
-        ws.zero_()
+        ws = torch.zeros_like(ws)
+        bn.__dict__[attr] = ws
     bn.__dict__[pend] = True
     return ws
 
@@ -525,7 +533,8 @@ class _BNActFn(Function):
         tok = ctx.token
         tok.pre_reduced = False
         st, bn = ctx.st, ctx.bn
-        rep = bn.__dict__["_mipipe_ws_bwd"]
+        rep = tok.rep if tok.rep is not None else bn.__dict__["_mipipe_ws_bwd"]
+        tok.rep = None
         C = y.shape[-1]
         direct = None
         if y2 is not None:  # two-branch: always collected by the weight-grad launch

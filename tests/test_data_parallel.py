@@ -91,33 +91,46 @@ def test_dp_single_device_passthrough():
 
 
 @pytest.mark.gpu
-def test_dp_gpu_replicas_match_chunked_module():
-    """bf16 HIP-kernel ResNet-18 under DataParallel([0, 0]) vs the same module run per chunk:
-    replica kernels read their own flat bf16 shadow and write their own flat gradients."""
+def test_dp_gpu_replicas_match_per_chunk_copies():
+    """bf16 HIP-kernel ResNet-18 under DataParallel([0, 0]) vs one deep copy of the module per
+    chunk (what DataParallel computes; deterministic kernels, copies re-synced each step): the
+    replica reads its own flat bf16 shadow, writes its own flat gradients, and the reduction sums
+    them into the master's.  (A single module looped over both chunks is not the oracle in bf16:
+    its second chunk normalises around the running mean the first chunk just moved, and batch-8
+    bf16 BatchNorm gradients are sensitive to that at the 10 % level — fp32 agrees to 1e-5,
+    tools/r2/dp_debug.py.)"""
+    from mipipe.ops.determinism import deterministic
     torch.manual_seed(0)
     dev = torch.device("cuda", 0)
     model = create_model("resnet18", num_classes=10).to(dev)
     model.compute_dtype = torch.bfloat16
-    ref = copy.deepcopy(model)
+    copies = [copy.deepcopy(model) for _ in range(2)]
     dp = DataParallel(model, device_ids=[0, 0])
     opt = SGD(dp.parameters(), 0.05, momentum=0.9)
-    ropt = SGD(ref.parameters(), 0.05, momentum=0.9)
+    keep = [SGD(c.parameters(), 0.05) for c in copies]
     x = torch.randn(16, 3, 32, 32, device=dev)
     y = torch.randint(0, 10, (16,), device=dev)
-    for _ in range(2):
-        opt.zero_grad()
-        ropt.zero_grad()
-        loss = cross_entropy(dp(x), y)
-        loss.backward()
-        _, rloss = _chunked_reference(ref, x, y, 2)
-        rloss.backward()
-        torch.cuda.synchronize()
-        assert abs(float(loss) - float(rloss)) < 2e-2 * max(1.0, abs(float(rloss)))
-        g = torch.cat([p.grad.flatten() for p in model.parameters()])
-        rg = torch.cat([p.grad.flatten() for p in ref.parameters()])
-        cos = float(torch.nn.functional.cosine_similarity(g, rg, dim=0))
-        assert cos > 0.99, cos
-        opt.step()
-        ropt.step()
-    assert dp._rep_spaces[0].shadow is not None
-    assert dp._rep_spaces[0].flat.device == dev
+    with deterministic(True):
+        for _ in range(3):
+            with torch.no_grad():
+                for c in copies:
+                    for a, b in zip(c.state_dict().values(), model.state_dict().values()):
+                        a.copy_(b)
+            opt.zero_grad()
+            for o in keep:
+                o.zero_grad()
+            loss = cross_entropy(dp(x), y)
+            loss.backward()
+            rloss = cross_entropy(torch.cat([c(xc) for c, xc in zip(copies, x.chunk(2))]), y)
+            rloss.backward()
+            torch.cuda.synchronize()
+            lv, rv = float(loss.detach()), float(rloss.detach())
+            assert abs(lv - rv) < 1e-4 * max(1.0, abs(rv)), (lv, rv)
+            g = torch.cat([p.grad.flatten() for p in model.parameters()])
+            rg = sum(torch.cat([p.grad.flatten() for p in c.parameters()]) for c in copies)
+            err = float((g - rg).norm() / rg.norm())
+            assert err < 1e-3, err
+            opt.step()
+    rs = dp._rep_spaces[0]
+    assert rs is not None and rs.shadow is not None and rs.flat.device == dev
+    assert float(rs.flat_grad.abs().max()) == 0.0  # drained into the master
