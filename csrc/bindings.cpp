@@ -270,6 +270,20 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
   TORCH_CHECK(dy.numel() < (1ll << 31), "conv dgrad dy too large for 32-bit gather offsets");
   TORCH_CHECK(s.pad < s.KH && pw < s.KW, "conv dgrad expects padding < kernel size");
   auto dx = torch::empty({s.N, s.H, s.W, s.Ci}, dy.options());
+  // stride-1 non-1x1 data-grads run as forward convolutions over the tap-flipped weight
+  // (MIPIPE_DGRAD_FWD=0: the parity-class data-grad kernels for every stride)
+  static const bool fwd_style_on = [] {
+    const char* v = getenv("MIPIPE_DGRAD_FWD");
+    return v == nullptr || v[0] != '0';
+  }();
+  Tensor wflip;
+  const void* wfp = nullptr;
+  if (fwd_style_on && mipipe::conv_dgrad_fwd_style(s)) {
+    wflip = torch::empty({s.Ci, s.KH, s.KW, s.Co}, w.options());  // w: contiguous [Co,KH,KW,Ci]
+    mipipe::conv_weight_flip(w.data_ptr(), wflip.data_ptr(), s.Co, s.KH, s.KW, s.Ci, s.f32,
+                             stream());
+    wfp = wflip.data_ptr();
+  }
   mipipe::DgradFusion fz;
   bool any = false;
   if (addend.has_value()) {
@@ -334,7 +348,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
         f2.bn_rep = reps.data_ptr<float>();
       }
       mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dxs.data_ptr(), s, stream(),
-                         any ? &f2 : nullptr, c);
+                         any ? &f2 : nullptr, c, wfp);
     });
   }
   if (mipipe::g_deterministic && fz.bn_rep != nullptr) {
@@ -344,7 +358,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     float* rep = fz.bn_rep;
     fz.bn_rep = part.data_ptr<float>();
     fz.det_rows = P;
-    mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), &fz, cfg);
+    mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), &fz, cfg, wfp);
     const long rs = (long)mipipe::kStatReplicas * s.Ci, ps = (long)P * s.Ci;
     mipipe::det_sum_rows(fz.bn_rep, fz.bn_rep + ps, P, s.Ci, rep, rep + rs, false, stream());
     if (two)
@@ -353,7 +367,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     return dx;
   }
   mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), any ? &fz : nullptr,
-                     cfg);
+                     cfg, wfp);
   return dx;
 }
 

@@ -82,7 +82,9 @@ constexpr int conv_occ() {
   return C::NW == 8 ? 1 : ((C::NS == 1 && !std::is_same<T, float>::value) ? 3 : 2);
 }
 
-template <class C, bool DENSE, bool ALIGNED, class T>
+// DGRAD_EPI: the same im2col main loop run as a stride-1 data-grad (x = dy, w = the tap-flipped
+// [Ci][KH][KW][Co] weight, pad = K-1-pad) with the data-grad epilogue and its fusions
+template <class C, bool DENSE, bool ALIGNED, class T, bool DGRAD_EPI = false>
 __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_fwd_kernel(
     const T* __restrict__ x, const T* __restrict__ w, ConvGeom g, uint32_t M,
     uint32_t tilesN, EpiParams e) {
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_fwd_kerne
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
   MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN>::type::run(smem, a, b, 0, nk, acc, wave,
                                                                     lane);
-  epilogue_out<BM, BN, false, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
+  epilogue_out<BM, BN, DGRAD_EPI, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
 // TWO: BN-backward fusion of a two-branch block output (dense bf16 data-grads only)

@@ -62,6 +62,86 @@ int conv_dgrad_tiles_m(const ConvShape& s, int cfg_in) {
   return total;
 }
 
+// ----------------------------------------------------------------------------------------
+// Stride-1 data-grads as forward convolutions.  With stride 1 there is a single parity class
+// and dx = conv(dy, flip(W)ᵀ, pad = K-1-pad): the forward kernel's im2col A operand (dy rows
+// gathered per tap, K-contiguous) and its K-contiguous weight operand replace the data-grad
+// gather and the N-contiguous (transposed-read) weight operand.  Measured per shape by the tile
+// tuner on the ResNet-50 b256 3x3 layers (tools/r2/tune_dump.py): the dgrad main loop ran at
+// 15-23 % of the dense bf16 peak where the forward loop runs at 26-35 %.
+bool conv_dgrad_fwd_style(const ConvShape& s) {
+  const bool s1 = s.stride == 1 && (s.stride_w == 0 || s.stride_w == 1);
+  return s1 && !is_dense(s);
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void conv_weight_flip_kernel(const T* __restrict__ w,
+                                                               T* __restrict__ wt, int Co, int KH,
+                                                               int KW, int Ci) {
+  // wt[ci][kh][kw][co] = w[co][KH-1-kh][KW-1-kw][ci]; one thread per output element
+  const long total = (long)Co * KH * KW * Ci;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % Co);
+    long r = i / Co;
+    const int kw = (int)(r % KW);
+    r /= KW;
+    const int kh = (int)(r % KH);
+    const int ci = (int)(r / KH);
+    wt[i] = w[(((long)co * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)) * Ci + ci];
+  }
+}
+
+void conv_weight_flip(const void* w, void* wt, int Co, int KH, int KW, int Ci, bool f32,
+                      hipStream_t st) {
+  const long total = (long)Co * KH * KW * Ci;
+  const int grid = (int)std::min<long>((total + 255) / 256, 2048);
+  if (f32)
+    hipLaunchKernelGGL((conv_weight_flip_kernel<float>), dim3(grid), dim3(256), 0, st,
+                       (const float*)w, (float*)wt, Co, KH, KW, Ci);
+  else
+    hipLaunchKernelGGL((conv_weight_flip_kernel<__bf16>), dim3(grid), dim3(256), 0, st,
+                       (const __bf16*)w, (__bf16*)wt, Co, KH, KW, Ci);
+}
+
+template <class T>
+static void conv_dgrad_fwd_t(const void* dy, const void* wflip, void* dx, const ConvShape& s,
+                             hipStream_t st, const DgradFusion* fz, int cfg_in) {
+  ConvShape s2 = s;  // the forward convolution dy -> dx
+  s2.H = s.Ho; s2.W = s.Wo; s2.Ci = s.Co; s2.Co = s.Ci;
+  s2.Ho = s.H; s2.Wo = s.W;
+  s2.stride = 1; s2.stride_w = 0;
+  s2.pad = s.KH - 1 - s.pad;
+  s2.pad_w = s.KW - 1 - (s.pad_w >= 0 ? s.pad_w : s.pad);
+  const ConvGeom g = make_geom(s2);
+  const uint32_t M = (uint32_t)s.N * s.H * s.W;
+  EpiParams e{};
+  e.C = dx; e.ldc = s.Ci; e.M = M; e.N = s.Ci;
+  if (fz != nullptr) {
+    e.addend = fz->addend;
+    e.bnr_y = fz->bn_y;
+    e.bnr_mean = fz->bn_mean; e.bnr_invstd = fz->bn_invstd;
+    e.bnr_scale = fz->bn_scale; e.bnr_bias = fz->bn_bias; e.bnr_rep = fz->bn_rep; e.st_R = g_stat_rows;
+    e.bnr_z = fz->bn_z;
+    e.bnr_mask = fz->bn_mask;
+    e.det_rows = fz->det_rows;
+    e.det_row0 = 0;
+  }
+  const bool aligned = s.Co % BK == 0;
+  const T* dyp = (const T*)dy;
+  const T* wp = (const T*)wflip;
+  const int cfg = resolve_dgrad_cfg(s, cfg_in, (long)s.KH * s.KW * s.Co);
+  with_tile<T>(cfg, [&](auto tile) {
+    typedef decltype(tile) C;
+    const uint32_t tN = cdiv(s.Ci, C::BN), tiles = cdiv(M, C::BM) * tN;
+    const dim3 grid(tiles), block(C::THREADS);
+    if (aligned)
+      hipLaunchKernelGGL((conv_fwd_kernel<C, false, true, T, true>), grid, block, 0, st, dyp, wp, g, M, tN, e);
+    else
+      hipLaunchKernelGGL((conv_fwd_kernel<C, false, false, T, true>), grid, block, 0, st, dyp, wp, g, M, tN, e);
+  });
+}
+
 template <class T>
 static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShape& s,
                          hipStream_t st, const DgradFusion* fz, int cfg_in) {
@@ -113,7 +193,12 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
 }
 
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
-                const DgradFusion* fz, int cfg) {
+                const DgradFusion* fz, int cfg, const void* w_flip) {
+  if (w_flip != nullptr && conv_dgrad_fwd_style(s) && (fz == nullptr || fz->bn_y2 == nullptr)) {
+    if (s.f32) conv_dgrad_fwd_t<float>(dy, w_flip, dx, s, st, fz, cfg);
+    else conv_dgrad_fwd_t<__bf16>(dy, w_flip, dx, s, st, fz, cfg);
+    return;
+  }
   if (s.f32) conv_dgrad_t<float>(dy, w, dx, s, st, fz, cfg);
   else conv_dgrad_t<__bf16>(dy, w, dx, s, st, fz, cfg);
 }
