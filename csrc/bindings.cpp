@@ -270,18 +270,17 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
   TORCH_CHECK(dy.numel() < (1ll << 31), "conv dgrad dy too large for 32-bit gather offsets");
   TORCH_CHECK(s.pad < s.KH && pw < s.KW, "conv dgrad expects padding < kernel size");
   auto dx = torch::empty({s.N, s.H, s.W, s.Ci}, dy.options());
-  // stride-1 non-1x1 data-grads run as forward convolutions over the tap-flipped weight
-  // (MIPIPE_DGRAD_FWD=0: the parity-class data-grad kernels for every stride)
-  static const bool fwd_style_on = [] {
+  // data-grads run as forward convolutions over tap-flipped (sub-)kernels, per stride-parity
+  // class; MIPIPE_DGRAD_FWD=0: the data-grad gather kernels everywhere, =2: also 1x1 stride-1
+  static const int fwd_style_mode = [] {
     const char* v = getenv("MIPIPE_DGRAD_FWD");
-    return v == nullptr || v[0] != '0';
+    return v == nullptr ? 1 : atoi(v);
   }();
   Tensor wflip;
-  const void* wfp = nullptr;
-  if (fwd_style_on && mipipe::conv_dgrad_fwd_style(s)) {
-    wflip = torch::empty({s.Ci, s.KH, s.KW, s.Co}, w.options());  // w: contiguous [Co,KH,KW,Ci]
-    mipipe::conv_weight_flip(w.data_ptr(), wflip.data_ptr(), s.Co, s.KH, s.KW, s.Ci, s.f32,
-                             stream());
+  void* wfp = nullptr;
+  if (fwd_style_mode > 0 && mipipe::conv_dgrad_fwd_style(s, fwd_style_mode >= 2) &&
+      !bn_y2.has_value()) {
+    wflip = torch::empty({(int64_t)s.Ci * s.KH * s.KW * s.Co}, w.options());  // w: [Co,KH,KW,Ci]
     wfp = wflip.data_ptr();
   }
   mipipe::DgradFusion fz;

@@ -63,89 +63,55 @@ int conv_dgrad_tiles_m(const ConvShape& s, int cfg_in) {
 }
 
 // ----------------------------------------------------------------------------------------
-// Stride-1 data-grads as forward convolutions.  With stride 1 there is a single parity class
-// and dx = conv(dy, flip(W)ᵀ, pad = K-1-pad): the forward kernel's im2col A operand (dy rows
-// gathered per tap, K-contiguous) and its K-contiguous weight operand replace the data-grad
-// gather and the N-contiguous (transposed-read) weight operand.  Measured per shape by the tile
-// tuner on the ResNet-50 b256 3x3 layers (tools/r2/tune_dump.py): the dgrad main loop ran at
-// 15-23 % of the dense bf16 peak where the forward loop runs at 26-35 %.
-bool conv_dgrad_fwd_style(const ConvShape& s) {
-  const bool s1 = s.stride == 1 && (s.stride_w == 0 || s.stride_w == 1);
-  return s1 && !is_dense(s);
+// Data-grads as forward convolutions.  A stride-S data-grad splits into S² parity classes; the
+// class (ph, pw) is a STRIDE-1 convolution of dy with the taps kh = kh0 + S·a, kw = kw0 + S·b,
+// flipped: dx[S·i+ph][S·j+pw] = Σ_{a',b'} dy[i - pad_h + a'][j - pad_w + b'] · W'[a'][b'] with
+// W'[ci][a'][b'][co] = W[co][kh0 + S(nkh-1-a')][kw0 + S(nkw-1-b')][ci] and pad = nk-1-d0.  The
+// forward kernel's im2col A operand (dy rows gathered per tap, K-contiguous) and K-contiguous
+// weight operand then replace the data-grad gather and its N-contiguous (transposed-read)
+// weight operand; the epilogue (row remap of the class, BN-backward fusions) is unchanged.
+// Measured per shape by the tile tuner on the ResNet-50 b256 3x3 layers (tools/r2/tune_dump.py):
+// the dgrad main loop ran at 15-23 % of the dense bf16 peak where the forward loop runs at
+// 26-35 %; switching the stride-1 3x3s: 10.84k -> 11.24k img/s.
+bool conv_dgrad_fwd_style(const ConvShape& s, bool dense_too) {
+  const bool sq = s.stride_w == 0 || s.stride_w == s.stride;
+  return sq && (dense_too || !is_dense(s));
 }
 
 template <class T>
 __global__ __launch_bounds__(256) void conv_weight_flip_kernel(const T* __restrict__ w,
                                                                T* __restrict__ wt, int Co, int KH,
-                                                               int KW, int Ci) {
-  // wt[ci][kh][kw][co] = w[co][KH-1-kh][KW-1-kw][ci]; one thread per output element
-  const long total = (long)Co * KH * KW * Ci;
+                                                               int KW, int Ci, int kh0, int kw0,
+                                                               int S, int nkh, int nkw) {
+  // wt[ci][a][b][co] = w[co][kh0 + S(nkh-1-a)][kw0 + S(nkw-1-b)][ci]; one thread per output
+  const long total = (long)Co * nkh * nkw * Ci;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
     const int co = (int)(i % Co);
     long r = i / Co;
-    const int kw = (int)(r % KW);
-    r /= KW;
-    const int kh = (int)(r % KH);
-    const int ci = (int)(r / KH);
-    wt[i] = w[(((long)co * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)) * Ci + ci];
+    const int b = (int)(r % nkw);
+    r /= nkw;
+    const int a = (int)(r % nkh);
+    const int ci = (int)(r / nkh);
+    const int kh = kh0 + S * (nkh - 1 - a), kw = kw0 + S * (nkw - 1 - b);
+    wt[i] = w[(((long)co * KH + kh) * KW + kw) * Ci + ci];
   }
-}
-
-void conv_weight_flip(const void* w, void* wt, int Co, int KH, int KW, int Ci, bool f32,
-                      hipStream_t st) {
-  const long total = (long)Co * KH * KW * Ci;
-  const int grid = (int)std::min<long>((total + 255) / 256, 2048);
-  if (f32)
-    hipLaunchKernelGGL((conv_weight_flip_kernel<float>), dim3(grid), dim3(256), 0, st,
-                       (const float*)w, (float*)wt, Co, KH, KW, Ci);
-  else
-    hipLaunchKernelGGL((conv_weight_flip_kernel<__bf16>), dim3(grid), dim3(256), 0, st,
-                       (const __bf16*)w, (__bf16*)wt, Co, KH, KW, Ci);
 }
 
 template <class T>
-static void conv_dgrad_fwd_t(const void* dy, const void* wflip, void* dx, const ConvShape& s,
-                             hipStream_t st, const DgradFusion* fz, int cfg_in) {
-  ConvShape s2 = s;  // the forward convolution dy -> dx
-  s2.H = s.Ho; s2.W = s.Wo; s2.Ci = s.Co; s2.Co = s.Ci;
-  s2.Ho = s.H; s2.Wo = s.W;
-  s2.stride = 1; s2.stride_w = 0;
-  s2.pad = s.KH - 1 - s.pad;
-  s2.pad_w = s.KW - 1 - (s.pad_w >= 0 ? s.pad_w : s.pad);
-  const ConvGeom g = make_geom(s2);
-  const uint32_t M = (uint32_t)s.N * s.H * s.W;
-  EpiParams e{};
-  e.C = dx; e.ldc = s.Ci; e.M = M; e.N = s.Ci;
-  if (fz != nullptr) {
-    e.addend = fz->addend;
-    e.bnr_y = fz->bn_y;
-    e.bnr_mean = fz->bn_mean; e.bnr_invstd = fz->bn_invstd;
-    e.bnr_scale = fz->bn_scale; e.bnr_bias = fz->bn_bias; e.bnr_rep = fz->bn_rep; e.st_R = g_stat_rows;
-    e.bnr_z = fz->bn_z;
-    e.bnr_mask = fz->bn_mask;
-    e.det_rows = fz->det_rows;
-    e.det_row0 = 0;
-  }
-  const bool aligned = s.Co % BK == 0;
-  const T* dyp = (const T*)dy;
-  const T* wp = (const T*)wflip;
-  const int cfg = resolve_dgrad_cfg(s, cfg_in, (long)s.KH * s.KW * s.Co);
-  with_tile<T>(cfg, [&](auto tile) {
-    typedef decltype(tile) C;
-    const uint32_t tN = cdiv(s.Ci, C::BN), tiles = cdiv(M, C::BM) * tN;
-    const dim3 grid(tiles), block(C::THREADS);
-    if (aligned)
-      hipLaunchKernelGGL((conv_fwd_kernel<C, false, true, T, true>), grid, block, 0, st, dyp, wp, g, M, tN, e);
-    else
-      hipLaunchKernelGGL((conv_fwd_kernel<C, false, false, T, true>), grid, block, 0, st, dyp, wp, g, M, tN, e);
-  });
+static void weight_flip(const T* w, T* wt, const ConvShape& s, const DgradClass& c, int nkh,
+                        hipStream_t st) {
+  const long total = (long)s.Co * nkh * c.nkw * s.Ci;
+  const int grid = (int)std::min<long>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL((conv_weight_flip_kernel<T>), dim3(grid), dim3(256), 0, st, w, wt, s.Co,
+                     s.KH, s.KW, s.Ci, c.kh0, c.kw0, c.S, nkh, c.nkw);
 }
 
 template <class T>
 static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShape& s,
-                         hipStream_t st, const DgradFusion* fz, int cfg_in) {
+                         hipStream_t st, const DgradFusion* fz, int cfg_in, void* wflip) {
   const bool dense = is_dense(s);
+  long flip_off = 0;  // this class's slice of the flipped-weight workspace
   const bool aligned = s.Co % BK == 0;
   const T* dyp = (const T*)dy;
   const T* wp = (const T*)w;
@@ -174,12 +140,42 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
       }
       const int taps = s.KH * s.KW;
       const int cfg = resolve_dgrad_cfg(s, cfg_in, (long)c.ntaps * s.Co);
+      const int nkh = c.kh0 < s.KH ? (s.KH - c.kh0 + S - 1) / S : 0;
+      if (wflip != nullptr && c.ntaps > 0 && e.bnr_y2 == nullptr) {
+        // this class as a stride-1 forward convolution of dy (see conv_dgrad_fwd_style)
+        T* wt = (T*)wflip + flip_off;
+        flip_off += (long)s.Ci * c.ntaps * s.Co;
+        weight_flip<T>(wp, wt, s, c, nkh, st);
+        ConvShape s2 = s;
+        s2.H = s.Ho; s2.W = s.Wo; s2.Ci = s.Co; s2.Co = s.Ci;
+        s2.Ho = c.Hc; s2.Wo = c.Wc;
+        s2.KH = nkh; s2.KW = c.nkw;
+        s2.stride = 1; s2.stride_w = 0;
+        s2.pad = nkh - 1 - c.dh0;
+        s2.pad_w = c.nkw - 1 - c.dw0;
+        const ConvGeom g2 = make_geom(s2);
+        const bool dense2 = dense && S == 1;
+        with_tile<T>(cfg, [&](auto tile) {
+          typedef decltype(tile) C;
+          const uint32_t tN = cdiv(s.Ci, C::BN), tiles = cdiv(M, C::BM) * tN;
+          row0 += (int)cdiv(M, C::BM);
+          const dim3 grid(tiles), block(C::THREADS);
+          if (dense2)
+            hipLaunchKernelGGL((conv_fwd_kernel<C, true, false, T, true>), grid, block, 0, st, dyp, wt, g2, M, tN, e);
+          else if (aligned)
+            hipLaunchKernelGGL((conv_fwd_kernel<C, false, true, T, true>), grid, block, 0, st, dyp, wt, g2, M, tN, e);
+          else
+            hipLaunchKernelGGL((conv_fwd_kernel<C, false, false, T, true>), grid, block, 0, st, dyp, wt, g2, M, tN, e);
+        });
+        return;
+      }
       with_tile<T>(cfg, [&](auto tile) {
         typedef decltype(tile) C;
         const uint32_t tN = cdiv(s.Ci, C::BN), tiles = cdiv(M, C::BM) * tN;
         row0 += (int)cdiv(M, C::BM);
         const dim3 grid(tiles), block(C::THREADS);
-        if (e.bnr_y2 != nullptr) {  // two-branch block output (host checks: dense, bf16)
+        if (e.bnr_y2 != nullptr) {
+  // two-branch block output (host checks: dense, bf16)
           if constexpr (std::is_same<T, __bf16>::value)
             hipLaunchKernelGGL((conv_dgrad_kernel<C, true, false, T, true>), grid, block, 0, st, dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         } else if (dense)
@@ -193,14 +189,9 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
 }
 
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
-                const DgradFusion* fz, int cfg, const void* w_flip) {
-  if (w_flip != nullptr && conv_dgrad_fwd_style(s) && (fz == nullptr || fz->bn_y2 == nullptr)) {
-    if (s.f32) conv_dgrad_fwd_t<float>(dy, w_flip, dx, s, st, fz, cfg);
-    else conv_dgrad_fwd_t<__bf16>(dy, w_flip, dx, s, st, fz, cfg);
-    return;
-  }
-  if (s.f32) conv_dgrad_t<float>(dy, w, dx, s, st, fz, cfg);
-  else conv_dgrad_t<__bf16>(dy, w, dx, s, st, fz, cfg);
+                const DgradFusion* fz, int cfg, void* w_flip) {
+  if (s.f32) conv_dgrad_t<float>(dy, w, dx, s, st, fz, cfg, w_flip);
+  else conv_dgrad_t<__bf16>(dy, w, dx, s, st, fz, cfg, w_flip);
 }
 
 }  // namespace mipipe

@@ -68,13 +68,12 @@ struct DgradFusion {
   const float *bn_mean2 = nullptr, *bn_invstd2 = nullptr;
   int det_rows = 0;  // deterministic mode: bn_rep is [2][det_rows][Ci] partials, one row per tile
 };
-// w_flip: the tap-flipped [Ci][KH][KW][Co] weight (conv_weight_flip) — when given, a stride-1
-// data-grad runs as a forward im2col convolution of dy (conv_dgrad_fwd_style(s) must hold)
+// w_flip: a workspace of Co*KH*KW*Ci elements — when given, every stride-parity class with taps
+// runs as a stride-1 FORWARD im2col convolution of dy over its tap-flipped sub-kernel (written
+// into the workspace by this call); allocate it only when conv_dgrad_fwd_style(s, ...) holds
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
-                const DgradFusion* fz = nullptr, int cfg = -1, const void* w_flip = nullptr);
-bool conv_dgrad_fwd_style(const ConvShape& s);
-void conv_weight_flip(const void* w, void* wt, int Co, int KH, int KW, int Ci, bool f32,
-                      hipStream_t st);
+                const DgradFusion* fz = nullptr, int cfg = -1, void* w_flip = nullptr);
+bool conv_dgrad_fwd_style(const ConvShape& s, bool dense_too);
 int conv_dgrad_tiles_m(const ConvShape& s, int cfg);  // M-tiles over all stride classes
 // dw is ACCUMULATED into (split-K fp32 atomics, or a plain read-modify-write when unsplit): pass
 // a zeroed buffer, or the parameter's gradient buffer to fuse autograd's accumulation (gradient

@@ -38,15 +38,19 @@ def nccl_pg():
 
 
 def test_rccl_ddp_graphed_matches_eager(nccl_pg):
+    """DDP (RCCL, world 1, every bucket forced through the collective) replayed from a hipGraph
+    == the same steps run eagerly.  Deterministic kernels: without them a batch-32 bf16
+    BatchNorm net amplifies atomic-order noise to ~0.98 cosine between two EAGER runs within
+    four SGD steps, which is no basis for comparing graph against eager."""
     from mipipe.models import create_model
+    from mipipe.ops.determinism import deterministic
     from mipipe.ops.functional import cross_entropy
     from mipipe.optim import SGD
     from mipipe.parallel import DistributedDataParallel
     from mipipe.train.graph import GraphedStep, graph_safe
     torch.manual_seed(0)
     base = create_model("resnet18", num_classes=10).cuda()
-    mods = [copy.deepcopy(base) for _ in range(3)]
-    init = [p.detach().clone() for p in base.parameters()]
+    mods = [copy.deepcopy(base) for _ in range(2)]
     ddps = [DistributedDataParallel(m, device_ids=[0], force_reduce=True, bucket_cap_mb=8)
             for m in mods]
     for d in ddps:
@@ -65,29 +69,22 @@ def test_rccl_ddp_graphed_matches_eager(nccl_pg):
             return loss
         return step
 
-    la = [make_step(ddps[0], opts[0])(x, y).item() for _ in range(4)]
-    lc = [make_step(ddps[2], opts[2])(x, y).item() for _ in range(4)]
-    n0 = ddps[0]._clog.count
-    # per eager step: one buffer broadcast per dtype + one all-reduce per bucket
-    assert n0 >= 4 * len(ddps[0].buckets)
-    c0 = ddps[1]._clog.count
-    gs = GraphedStep(make_step(ddps[1], opts[1]), (x, y), warmup=1, inputs=[(x, y)])
-    assert ddps[1]._clog.count - c0 >= 2 * len(ddps[1].buckets)  # eager warmup + capture
-    lb = [gs.replay(0).item() for _ in range(3)]
-    torch.cuda.synchronize()
-    assert abs(la[-1] - lb[-1]) < 3 * abs(la[-1] - lc[-1]) + 0.02 * abs(la[0]), (la, lb, lc)
-    vp, vq, vr = [], [], []
-    for (n, p), (_, q), (_, r), p0 in zip(mods[0].named_parameters(), mods[1].named_parameters(),
-                                          mods[2].named_parameters(), init):
-        if p.dim() == 1:
-            vp.append((p.detach() - p0).flatten())
-            vq.append((q.detach() - p0).flatten())
-            vr.append((r.detach() - p0).flatten())
-            continue
-        assert cos(p, q) > min(0.999, cos(p, r) - 0.01), (n, cos(p, q), cos(p, r))
-    va, vb, vc = torch.cat(vp), torch.cat(vq), torch.cat(vr)
-    assert cos(va, vb) > min(0.99, cos(va, vc) - 0.02), (cos(va, vb), cos(va, vc))
-
+    with deterministic(True):
+        la = [make_step(ddps[0], opts[0])(x, y).item() for _ in range(4)]
+        n0 = ddps[0]._clog.count
+        # per eager step: one buffer broadcast per dtype + one all-reduce per bucket
+        assert n0 >= 4 * len(ddps[0].buckets)
+        c0 = ddps[1]._clog.count
+        gs = GraphedStep(make_step(ddps[1], opts[1]), (x, y), warmup=1, inputs=[(x, y)])
+        assert ddps[1]._clog.count - c0 >= 2 * len(ddps[1].buckets)  # eager warmup + capture
+        lb = [gs.replay(0).item() for _ in range(3)]
+        torch.cuda.synchronize()
+    assert abs(la[-1] - lb[-1]) <= 1e-5 * abs(la[-1]), (la, lb)
+    for (n, p), (_, q) in zip(mods[0].named_parameters(), mods[1].named_parameters()):
+        assert cos(p, q) > 0.99999, (n, cos(p, q))
+    for (n, b), (_, c) in zip(mods[0].named_buffers(), mods[1].named_buffers()):
+        if b.is_floating_point():
+            torch.testing.assert_close(b, c, rtol=1e-4, atol=1e-5, msg=n)
 
 def test_rccl_bf16_comm_dtype(nccl_pg):
     """comm_dtype=bf16 halves the bytes on the wire; the averaged gradient equals the fp32
