@@ -78,33 +78,43 @@ bool conv_dgrad_fwd_style(const ConvShape& s, bool dense_too) {
   return sq && (dense_too || !is_dense(s));
 }
 
+// Tap-flipped sub-kernel as 64x64 LDS-tiled transposes, one per tap: wt[ci][a][b][co] =
+// w[co][kh0 + S(nkh-1-a)][kw0 + S(nkw-1-b)][ci].  Reads run along ci and writes along co (both
+// coalesced; the one-thread-per-element gather it replaces cost ~7 us per call).
 template <class T>
 __global__ __launch_bounds__(256) void conv_weight_flip_kernel(const T* __restrict__ w,
                                                                T* __restrict__ wt, int Co, int KH,
                                                                int KW, int Ci, int kh0, int kw0,
                                                                int S, int nkh, int nkw) {
-  // wt[ci][a][b][co] = w[co][kh0 + S(nkh-1-a)][kw0 + S(nkw-1-b)][ci]; one thread per output
-  const long total = (long)Co * nkh * nkw * Ci;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const int co = (int)(i % Co);
-    long r = i / Co;
-    const int b = (int)(r % nkw);
-    r /= nkw;
-    const int a = (int)(r % nkh);
-    const int ci = (int)(r / nkh);
-    const int kh = kh0 + S * (nkh - 1 - a), kw = kw0 + S * (nkw - 1 - b);
-    wt[i] = w[(((long)co * KH + kh) * KW + kw) * Ci + ci];
+  __shared__ T tile[64][65];
+  const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64, tap = blockIdx.z;
+  const int a = tap / nkw, b = tap % nkw;
+  const int kh = kh0 + S * (nkh - 1 - a), kw = kw0 + S * (nkw - 1 - b);
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  // all 16 loads in flight at once: a launch this small is one memory latency, not sixteen
+  T v[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int co = co0 + ty + 4 * u, ci = ci0 + tx;
+    v[u] = (co < Co && ci < Ci) ? w[(((long)co * KH + kh) * KW + kw) * Ci + ci] : T(0.f);
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) tile[ty + 4 * u][tx] = v[u];
+  __syncthreads();
+  const long taps = (long)nkh * nkw;
+#pragma unroll
+  for (int r = ty; r < 64; r += 4) {
+    const int ci = ci0 + r, co = co0 + tx;
+    if (co < Co && ci < Ci) wt[((long)ci * taps + tap) * Co + co] = tile[tx][r];
   }
 }
 
 template <class T>
 static void weight_flip(const T* w, T* wt, const ConvShape& s, const DgradClass& c, int nkh,
                         hipStream_t st) {
-  const long total = (long)s.Co * nkh * c.nkw * s.Ci;
-  const int grid = (int)std::min<long>((total + 255) / 256, 2048);
-  hipLaunchKernelGGL((conv_weight_flip_kernel<T>), dim3(grid), dim3(256), 0, st, w, wt, s.Co,
-                     s.KH, s.KW, s.Ci, c.kh0, c.kw0, c.S, nkh, c.nkw);
+  const dim3 grid((s.Ci + 63) / 64, (s.Co + 63) / 64, nkh * c.nkw);
+  hipLaunchKernelGGL((conv_weight_flip_kernel<T>), grid, dim3(256), 0, st, w, wt, s.Co, s.KH,
+                     s.KW, s.Ci, c.kh0, c.kw0, c.S, nkh, c.nkw);
 }
 
 template <class T>
