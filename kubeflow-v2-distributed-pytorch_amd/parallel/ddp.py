@@ -17,7 +17,8 @@ MI355X design: gradients already live in one flat fp32 buffer in gradient-ready 
 (every rank issues the same collective sequence) from post-accumulate-grad hooks, on the
 process group's communication stream; the step's end waits on them with stream semantics only
 (no host sync).  Bucket size defaults to 32 MiB (≈7 links × ~4.5 MiB chunks per ring step on
-the 8-GPU xGMI mesh) with a small first bucket so communication starts early; the optional
+the 8-GPU xGMI mesh) with a small first bucket so communication starts early and a small last
+bucket so little is left to all-reduce after the final backward kernel; the optional
 ``comm_dtype=torch.bfloat16`` halves the bytes on the wire.
 
 Debug aid (SURVEY §5.2 hazard): ``check_collectives=True`` (or ``MIPIPE_CHECK_COLLECTIVES=1``)
@@ -79,6 +80,7 @@ class DistributedDataParallel(tnn.Module):
     def __init__(self, module: tnn.Module, device_ids: Optional[List[int]] = None,
                  output_device=None, broadcast_buffers: bool = True,
                  process_group=None, bucket_cap_mb: float = 32.0, first_bucket_mb: float = 1.0,
+                 last_bucket_mb: float = 2.0,
                  comm_dtype: Optional[torch.dtype] = None, find_unused_parameters: bool = False,
                  check_collectives: Optional[bool] = None, check_every: int = 50,
                  gradient_as_bucket_view: bool = True, static_graph: bool = False,
@@ -117,7 +119,8 @@ class DistributedDataParallel(tnn.Module):
         if self._comm:
             self._verify_shapes(params)
             self._sync_module_states()
-        self.buckets = self._build_buckets(bucket_cap_mb * 2 ** 20, first_bucket_mb * 2 ** 20)
+        self.buckets = self._build_buckets(bucket_cap_mb * 2 ** 20, first_bucket_mb * 2 ** 20,
+                                           last_bucket_mb * 2 ** 20)
         self._bucket_of = {}
         for b in self.buckets:
             for p in b.params:
@@ -174,23 +177,52 @@ class DistributedDataParallel(tnn.Module):
         for flat in self._flat_bufs:
             self._broadcast(flat)
 
-    def _build_buckets(self, cap_bytes: float, first_bytes: float) -> List[Bucket]:
+    def _build_buckets(self, cap_bytes: float, first_bytes: float,
+                       last_bytes: float = 0.0) -> List[Bucket]:
+        """Contiguous flat-gradient slices in gradient-ready order: a small FIRST bucket (the
+        classifier: communication starts as soon as backward does), a small LAST bucket (the
+        stem and first layers: the only all-reduce that cannot overlap backward is this one, so
+        its bytes are the exposed communication of the step), and the rest split into equal
+        buckets of at most ``cap_bytes``.  With a plain greedy cut the tail of ResNet-50 would be
+        a ~27 MB remainder (layer 2 + layer 1 + stem) all-reduced after the last kernel."""
+        ranges = list(self.space.ranges())
+        n = len(ranges)
+        cuts = []  # exclusive end index of each bucket
+        i, acc = 0, 0
+        while i < n:  # first bucket
+            acc += (ranges[i][1] - ranges[i][0]) * 4
+            i += 1
+            if acc >= first_bytes:
+                break
+        cuts.append(i)
+        j, acc = n, 0
+        if last_bytes > 0:
+            while j > i:  # last bucket, from the end
+                acc += (ranges[j - 1][1] - ranges[j - 1][0]) * 4
+                j -= 1
+                if acc >= last_bytes:
+                    break
+        if j > i:  # middle: equal buckets of <= cap_bytes
+            mid = sum((ranges[k][1] - ranges[k][0]) * 4 for k in range(i, j))
+            nb = max(1, int(-(-mid // max(cap_bytes, 1.0))))
+            target = mid / nb
+            acc = 0
+            for k in range(i, j):
+                acc += (ranges[k][1] - ranges[k][0]) * 4
+                if acc >= target and k + 1 < j:
+                    cuts.append(k + 1)
+                    acc = 0
+            cuts.append(j)
+        if cuts[-1] != n:
+            cuts.append(n)
         buckets: List[Bucket] = []
-        cur: List[tnn.Parameter] = []
-        start = None
-        end = 0
-        limit = first_bytes
-        for (s, e, p) in self.space.ranges():
-            if start is None:
-                start = s
-            cur.append(p)
-            end = e
-            if (end - start) * 4 >= limit:
-                buckets.append(Bucket(len(buckets), start, end, cur))
-                cur, start = [], None
-                limit = cap_bytes
-        if cur:
-            buckets.append(Bucket(len(buckets), start, end, cur))
+        lo = 0
+        for hi in cuts:
+            if hi <= lo:
+                continue
+            ps = [r[2] for r in ranges[lo:hi]]
+            buckets.append(Bucket(len(buckets), ranges[lo][0], ranges[hi - 1][1], ps))
+            lo = hi
         return buckets
 
     # ------------------------------------------------------------------ forward

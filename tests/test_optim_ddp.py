@@ -160,3 +160,30 @@ def test_data_parallel_passthrough_and_unwrap():
     torch.testing.assert_close(dp(x), inner(x))
     assert _unwrap(dp) is inner
     assert set(inner.state_dict()) == set(_unwrap(dp).state_dict())
+
+
+def _bucket_layout_worker(rank, world, port, out):
+    import torch.distributed as dist
+    from mipipe.models import create_model
+    from mipipe.parallel import DistributedDataParallel
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    d = DistributedDataParallel(create_model("resnet50", num_classes=1000), force_reduce=True)
+    out[rank] = [(b.start, b.end, len(b.params)) for b in d.buckets]
+    dist.destroy_process_group()
+
+
+def test_ddp_bucket_layout_small_tail():
+    """ResNet-50 buckets: contiguous slices covering the flat gradient buffer, a small first
+    bucket (classifier), a small LAST bucket (stem + first layer: the all-reduce left exposed
+    after the final backward kernel) and middle buckets within the cap."""
+    out = mp.Manager().dict()
+    mp.spawn(_bucket_layout_worker, args=(1, 29300 + os.getpid() % 500, out), nprocs=1)
+    b = out[0]
+    assert b[0][0] == 0
+    assert all(b[k][1] == b[k + 1][0] for k in range(len(b) - 1))
+    mb = [(e - s) * 4 / 2 ** 20 for s, e, _ in b]
+    assert mb[-1] <= 4.0 and mb[0] <= 10.0, mb
+    assert all(m <= 32.0 for m in mb[1:-1]), mb
+    assert len(b) >= 4
