@@ -1258,8 +1258,10 @@ std::tuple<Tensor, Tensor> chan_stats(Tensor y, Tensor shift) {
   c10::DeviceGuard g(y.device());
   int64_t C = y.size(-1), M = y.numel() / C;
   check_vec(shift, C, "shift");
-  auto st = torch::zeros({2, C}, y.options().dtype(at::kFloat));
-  auto ps = st.narrow(0, 0, 1), pq = st.narrow(0, 1, 1);
+  // [2][R][C] replica-row partials: bn_finalize sums the R rows
+  auto st = torch::zeros({2, (int64_t)mipipe::kStatReplicas, C}, y.options().dtype(at::kFloat));
+  auto ps = st[0], pq = st[1];
+  // (the generic-C fallback kernel accumulates row 0 only; the other rows stay zero)
   mipipe::chan_stats(y.data_ptr(), shift.data_ptr<float>(), M, (int)C, ps.data_ptr<float>(),
                      pq.data_ptr<float>(), stream(), is_f32(y));
   return {ps, pq};
@@ -1289,11 +1291,16 @@ std::tuple<Tensor, Tensor> bn_generic_bwd_reduce(Tensor dz, optional<Tensor> z, 
   check_vec(invstd, C, "invstd");
   TORCH_CHECK(act >= 0 && act <= 2 && (act == 0 || z.has_value()), "activation backward needs z");
   const void* zp = act_mask_src(z, act, y);
-  auto st = torch::zeros({2, C}, y.options().dtype(at::kFloat));
-  auto sg = st[0], sgx = st[1];
+  const int R = mipipe::kStatReplicas;  // replica rows for the atomics, summed below
+  auto rep = torch::zeros({2, (int64_t)R, C}, y.options().dtype(at::kFloat));
   mipipe::bn_generic_bwd_reduce(dz.data_ptr(), zp, y.data_ptr(), mean.data_ptr<float>(),
                                 invstd.data_ptr<float>(), M, (int)C, (int)act,
-                                sg.data_ptr<float>(), sgx.data_ptr<float>(), stream(), is_f32(y));
+                                rep[0].data_ptr<float>(), rep[1].data_ptr<float>(), stream(),
+                                is_f32(y));
+  auto st = torch::empty({2, C}, y.options().dtype(at::kFloat));
+  auto sg = st[0], sgx = st[1];
+  mipipe::det_sum_rows(rep[0].data_ptr<float>(), rep[1].data_ptr<float>(), R, (int)C,
+                       sg.data_ptr<float>(), sgx.data_ptr<float>(), false, stream());
   return {sg, sgx};
 }
 

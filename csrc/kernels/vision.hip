@@ -507,8 +507,11 @@ __global__ __launch_bounds__(256) void bn_generic_bwd_apply_kernel(
 // strides over rows (tpr = C/8 threads per row, rpb = 256/tpr rows per block pass), so the
 // per-channel coefficients stay in registers; reductions go through LDS (stride 9: conflict-free
 // column reads), then one atomic per channel per block.
+// out: [R][C] replica rows (R = kStatReplicas); this block adds into row blockIdx % R, which
+// spreads the per-channel atomics of many blocks over R addresses (finalize sums the rows)
 __device__ __forceinline__ void lds_reduce_atomic8(float* sh, const float* v, int tpr, int rpb,
                                                    float* out) {
+  out += (long)(blockIdx.x % kStatReplicas) * (tpr * 8);
   const int t = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 8; ++k) sh[t * 9 + k] = v[k];
@@ -523,6 +526,14 @@ __device__ __forceinline__ void lds_reduce_atomic8(float* sh, const float* v, in
   }
   __syncthreads();
 }
+
+// v8 ("any C % 8") BN kernels: the statistics / backward reductions keep kV8RowU rows of loads
+// in flight per thread over up to 1024 blocks whose per-channel atomics go to kStatReplicas
+// replica rows (one [C] row took every block's atomics: on DenseNet's concatenated inputs that
+// serialised the reductions at ~2 TB/s, and more blocks made it slower); the apply passes walk
+// contiguous tiles of kV8ApplyU rows per thread with the loads issued first (as bn.hip's)
+constexpr int kV8RowU = 4;
+constexpr int kV8ApplyU = 2;
 
 template <class T>
 __global__ __launch_bounds__(256) void chan_stats_v8_kernel(const T* __restrict__ y,
@@ -539,14 +550,22 @@ __global__ __launch_bounds__(256) void chan_stats_v8_kernel(const T* __restrict_
     float sf[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) sf[k] = shift[cg * 8 + k];
-    for (long r = (long)blockIdx.x * rpb + rg; r < M; r += (long)gridDim.x * rpb) {
-      float v[8];
-      load8(y + r * C + cg * 8, v);
+    const long stride = (long)gridDim.x * rpb;
+    for (long r0 = (long)blockIdx.x * rpb + rg; r0 < M; r0 += kV8RowU * stride) {
+      Raw8<T> raw[kV8RowU];  // kV8RowU rows of loads in flight per thread
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float d = v[k] - sf[k];
-        s[k] += d;
-        q[k] += d * d;
+      for (int u = 0; u < kV8RowU; ++u) raw[u] = ld_raw8(y + min(r0 + u * stride, M - 1) * C + cg * 8);
+#pragma unroll
+      for (int u = 0; u < kV8RowU; ++u) {
+        if (r0 + u * stride >= M) break;
+        float v[8];
+        unpack_raw(raw[u], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float d = v[k] - sf[k];
+          s[k] += d;
+          q[k] += d * d;
+        }
       }
     }
   }
@@ -569,13 +588,21 @@ __global__ __launch_bounds__(256) void affine_act_v8_kernel(const T* __restrict_
     sc[k] = scale[cg * 8 + k];
     bi[k] = bias[cg * 8 + k];
   }
-  for (long r = (long)blockIdx.x * rpb + rg; r < M; r += (long)gridDim.x * rpb) {
-    const long off = r * C + cg * 8;
-    float v[8];
-    load8(y + off, v);
+  for (long r0 = (long)blockIdx.x * rpb * kV8ApplyU + rg; r0 < M;
+       r0 += (long)gridDim.x * rpb * kV8ApplyU) {
+    Raw8<T> raw[kV8ApplyU];  // a contiguous tile of kV8ApplyU*rpb rows per block iteration
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = act_apply(v[k] * sc[k] + bi[k], act);
-    store8(z + off, v);
+    for (int u = 0; u < kV8ApplyU; ++u) raw[u] = ld_raw8(y + min(r0 + u * rpb, M - 1) * C + cg * 8);
+#pragma unroll
+    for (int u = 0; u < kV8ApplyU; ++u) {
+      const long r = r0 + u * rpb;
+      if (r >= M) break;
+      float v[8];
+      unpack_raw(raw[u], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = act_apply(v[k] * sc[k] + bi[k], act);
+      store8(z + r * C + cg * 8, v);
+    }
   }
 }
 
@@ -596,16 +623,34 @@ __global__ __launch_bounds__(256) void bn_generic_bwd_reduce_v8_kernel(
       mu[k] = mean[cg * 8 + k];
       is[k] = invstd[cg * 8 + k];
     }
-    for (long r = (long)blockIdx.x * rpb + rg; r < M; r += (long)gridDim.x * rpb) {
-      const long off = r * C + cg * 8;
-      float g[8], v[8];
-      load8(dz + off, g);
-      if (act != 0) mask8(z + off, act, g);
-      load8(y + off, v);
+    const long stride = (long)gridDim.x * rpb;
+    for (long r0 = (long)blockIdx.x * rpb + rg; r0 < M; r0 += kV8RowU * stride) {
+      Raw8<T> rgv[kV8RowU], rz[kV8RowU], ry[kV8RowU];  // all loads of kV8RowU rows in flight
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        sg[k] += g[k];
-        sx[k] += g[k] * (v[k] - mu[k]) * is[k];
+      for (int u = 0; u < kV8RowU; ++u) {
+        const long off = min(r0 + u * stride, M - 1) * C + cg * 8;
+        rgv[u] = ld_raw8(dz + off);
+        if (act != 0) rz[u] = ld_raw8(z + off);
+        ry[u] = ld_raw8(y + off);
+      }
+#pragma unroll
+      for (int u = 0; u < kV8RowU; ++u) {
+        if (r0 + u * stride >= M) break;
+        float g[8], v[8];
+        unpack_raw(rgv[u], g);
+        if (act != 0) {
+          float zv[8];
+          unpack_raw(rz[u], zv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (!act_pass(zv[k], act)) g[k] = 0.f;
+        }
+        unpack_raw(ry[u], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          sg[k] += g[k];
+          sx[k] += g[k] * (v[k] - mu[k]) * is[k];
+        }
       }
     }
   }
@@ -633,15 +678,34 @@ __global__ __launch_bounds__(256) void bn_generic_bwd_apply_v8_kernel(
     Cc[k] = sum_g ? -A[k] * invstd[c] * sum_gx[c] * inv_count : 0.f;
     mu[k] = mean[c];
   }
-  for (long r = (long)blockIdx.x * rpb + rg; r < M; r += (long)gridDim.x * rpb) {
-    const long off = r * C + cg * 8;
-    float g[8], v[8];
-    load8(dz + off, g);
-    if (act != 0) mask8(z + off, act, g);
-    load8(y + off, v);
+  for (long r0 = (long)blockIdx.x * rpb * kV8ApplyU + rg; r0 < M;
+       r0 += (long)gridDim.x * rpb * kV8ApplyU) {
+    Raw8<T> rgv[kV8ApplyU], rz[kV8ApplyU], ry[kV8ApplyU];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) g[k] = A[k] * g[k] + B[k] + Cc[k] * (v[k] - mu[k]);
-    store8(dy + off, g);
+    for (int u = 0; u < kV8ApplyU; ++u) {
+      const long off = min(r0 + u * rpb, M - 1) * C + cg * 8;
+      rgv[u] = ld_raw8(dz + off);
+      if (act != 0) rz[u] = ld_raw8(z + off);
+      ry[u] = ld_raw8(y + off);
+    }
+#pragma unroll
+    for (int u = 0; u < kV8ApplyU; ++u) {
+      const long r = r0 + u * rpb;
+      if (r >= M) break;
+      float g[8], v[8];
+      unpack_raw(rgv[u], g);
+      if (act != 0) {
+        float zv[8];
+        unpack_raw(rz[u], zv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (!act_pass(zv[k], act)) g[k] = 0.f;
+      }
+      unpack_raw(ry[u], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = A[k] * g[k] + B[k] + Cc[k] * (v[k] - mu[k]);
+      store8(dy + r * C + cg * 8, g);
+    }
   }
 }
 
@@ -651,6 +715,12 @@ static int v8_grid(long M, int C, int cap) {
   const int rpb = 256 / (C / 8);
   long g = (M + rpb - 1) / rpb;
   return (int)std::max<long>(1, std::min<long>(g, cap));
+}
+
+// blocks for the apply passes: a block iteration covers kV8ApplyU * rpb rows
+static int v8_tiles(long M, int C, int U, int cap) {
+  const long rows = (long)(256 / (C / 8)) * U;
+  return (int)std::max<long>(1, std::min<long>((M + rows - 1) / rows, cap));
 }
 
 static dim3 chan_grid(long M, int C) {
@@ -664,7 +734,7 @@ void chan_stats(const void* y, const float* shift, long M, int C, float* psum, f
   auto run = [&](auto tag) {
     typedef decltype(tag) T;
     if (bn_v8(C)) {
-      hipLaunchKernelGGL((chan_stats_v8_kernel<T>), dim3(v8_grid(M, C, 512)), dim3(256), 0, st,
+      hipLaunchKernelGGL((chan_stats_v8_kernel<T>), dim3(v8_grid(M, C, 1024)), dim3(256), 0, st,
                          (const T*)y, shift, M, C, psum, psq);
       return;
     }
@@ -680,7 +750,7 @@ void affine_act(const void* y, const float* scale, const float* bias, void* z, l
   auto run = [&](auto tag) {
     typedef decltype(tag) T;
     if (bn_v8(C)) {
-      hipLaunchKernelGGL((affine_act_v8_kernel<T>), dim3(v8_grid(M, C, 4096)), dim3(256), 0, st,
+      hipLaunchKernelGGL((affine_act_v8_kernel<T>), dim3(v8_tiles(M, C, kV8ApplyU, 4096)), dim3(256), 0, st,
                          (const T*)y, scale, bias, (T*)z, M, C, act);
       return;
     }
@@ -698,7 +768,7 @@ void bn_generic_bwd_reduce(const void* dz, const void* z, const void* y, const f
   auto run = [&](auto tag) {
     typedef decltype(tag) T;
     if (bn_v8(C)) {
-      hipLaunchKernelGGL((bn_generic_bwd_reduce_v8_kernel<T>), dim3(v8_grid(M, C, 512)), dim3(256), 0,
+      hipLaunchKernelGGL((bn_generic_bwd_reduce_v8_kernel<T>), dim3(v8_grid(M, C, 1024)), dim3(256), 0,
                          st, (const T*)dz, (const T*)z, (const T*)y, mean, invstd, M,
                          C, act, out_g, out_gx);
       return;
@@ -718,7 +788,7 @@ void bn_generic_bwd_apply(const void* dz, const void* z, const void* y, const fl
   auto run = [&](auto tag) {
     typedef decltype(tag) T;
     if (bn_v8(C)) {
-      hipLaunchKernelGGL((bn_generic_bwd_apply_v8_kernel<T>), dim3(v8_grid(M, C, 4096)), dim3(256), 0,
+      hipLaunchKernelGGL((bn_generic_bwd_apply_v8_kernel<T>), dim3(v8_tiles(M, C, kV8ApplyU, 4096)), dim3(256), 0,
                          st, (const T*)dz, (const T*)z, (const T*)y, mean, invstd,
                          gamma, sum_g, sum_gx, 1.f / (float)count, M, C, act, (T*)dy);
       return;

@@ -279,7 +279,9 @@ def test_bn_generic_and_avgpool2d_fp32(C):
     y = f32(3, 7, 9, C) * 2 + 0.5
     shift = torch.randn(C, device=dev) * 0.1
     ps, pq = native().chan_stats(y, shift)
+    assert ps.shape[0] == native().STAT_REPLICAS  # replica rows, summed by bn_finalize
     psr, pqr = _ref.chan_stats(d(y), d(shift))
+    ps, pq = ps.sum(0).reshape(psr.shape), pq.sum(0).reshape(pqr.shape)
     assert rel_err(ps, psr) < TOL and rel_err(pq, pqr) < TOL
     scale, bias = torch.randn(C, device=dev), torch.randn(C, device=dev)
     z = native().affine_act(y, scale, bias, 1)

@@ -125,7 +125,9 @@ def test_bn_generic(C, act):
     y = bf(3, 7, 9, C, scale=2.0) + 0.5
     shift = torch.randn(C, device=dev) * 0.1
     ps, pq = native().chan_stats(y, shift)
+    assert ps.shape[0] == native().STAT_REPLICAS  # replica rows, summed by bn_finalize
     psr, pqr = _ref.chan_stats(y.float(), shift)
+    ps, pq = ps.sum(0).reshape(psr.shape), pq.sum(0).reshape(pqr.shape)
     assert rel_err(ps, psr) < 1e-3 and rel_err(pq, pqr) < 1e-3
     scale, bias = torch.randn(C, device=dev), torch.randn(C, device=dev)
     z = native().affine_act(y, scale, bias, ACT[act])
