@@ -68,7 +68,7 @@ class GraphedStep:
         with torch.cuda.stream(s):  # warm up on a side stream (allocator + lazy init)
             for i in range(max(1, warmup)):
                 x, y = self.static[i % len(self.static)]
-                self.fn(x, y).detach()
+                self.warmup_loss = self.fn(x, y).detach()  # loss of the last eager step
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
         _drain_collective_watchdog()

@@ -192,6 +192,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="allow float-atomic reductions (faster)")
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                    help="compute dtype on GPU (master weights stay fp32); CPU runs fp32")
+    p.add_argument("--hip-graph", action="store_true",
+                   help="replay full-size training steps (forward, backward with the DDP bucket "
+                        "all-reduces, SGD) from one captured hipGraph; partial batches run eagerly")
     p.add_argument("--steps", type=int, default=0, help="max training steps per epoch (0 = all)")
     p.add_argument("--eval-every", type=int, default=10, help="evaluate every N epochs (task.py:279)")
     p.add_argument("--log-every", type=int, default=20)
@@ -389,6 +392,25 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
     global_step = 0
     last_loss = float("nan")
     accuracy = None
+    # --hip-graph: the first full-size batch runs eagerly inside GraphedStep (a real training
+    # step: warmup=1), which then captures the step; later batches of that shape replay it
+    graphed, graph_shape = None, None
+    if args.hip_graph:
+        from mipipe.train.graph import GraphedStep, graph_safe
+        ok, why = graph_safe(_unwrap(model), optimizer) if use_gpu else (False, "no GPU")
+        if isinstance(model, DataParallel):
+            ok, why = False, "DataParallel runs replicas on host threads"
+        if not ok:
+            print(f"=> --hip-graph off: {why}", flush=True)
+            args.hip_graph = False
+
+    def _train_step(x, y):
+        optimizer.zero_grad()
+        loss_ = criterion(model(x), y)
+        loss_.backward()
+        optimizer.step()
+        return loss_
+
     for epoch in range(start_epoch, args.num_epochs):
         epoch_start = datetime.now().strftime("%Y_%m_%d_%H_%M_%S")
         print(f"Rank: {args.rank}, Epoch: {epoch}, Training start: {epoch_start}", flush=True)
@@ -414,15 +436,24 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
             inputs, labels = batch
             _fault_check(args.rank, global_step)
             meter.step_begin()
-            with trace.phase("zero_grad"):
-                optimizer.zero_grad()
-            with trace.phase("forward"):
-                outputs = model(inputs)
-                loss = criterion(outputs, labels)
-            with trace.phase("backward+allreduce"):
-                loss.backward()
-            with trace.phase("optimizer"):
-                optimizer.step()
+            if args.hip_graph and (graphed is None or tuple(inputs.shape) == graph_shape):
+                with trace.phase("graph_step"):
+                    if graphed is None:
+                        graphed = GraphedStep(_train_step, (inputs, labels), warmup=1)
+                        graph_shape = tuple(inputs.shape)
+                        loss = graphed.warmup_loss  # the eager warm-up step trained this batch
+                    else:
+                        loss = graphed.step(inputs, labels)
+            else:
+                with trace.phase("zero_grad"):
+                    optimizer.zero_grad()
+                with trace.phase("forward"):
+                    outputs = model(inputs)
+                    loss = criterion(outputs, labels)
+                with trace.phase("backward+allreduce"):
+                    loss.backward()
+                with trace.phase("optimizer"):
+                    optimizer.step()
             meter.step_end(inputs.shape[0])
             global_step += 1
             i += 1

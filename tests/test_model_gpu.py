@@ -253,3 +253,24 @@ def test_eager_training_memory_is_flat(arch, res):
     finally:
         gc.enable()
     assert grown <= 1 << 20, f"{grown / 2**20:.1f} MiB retained over 4 steps"
+
+
+def test_task_hip_graph_matches_eager(tmp_path, monkeypatch):
+    """task.py --hip-graph (full-size batches replayed from one captured step, the trailing
+    partial batch eager) trains to the same weights as the eager loop (deterministic kernels)."""
+    import mipipe.train.task as T
+    monkeypatch.delenv("AIP_MODEL_DIR", raising=False)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    sds = []
+    for extra in ([], ["--hip-graph"]):
+        out = tmp_path / ("g" if extra else "e")
+        rc = T.main(["--arch", "resnet18", "--num_classes", "10", "--dataset", "cifar10",
+                     "--batch_size", "64", "--train-samples", str(64 * 4 + 16),
+                     "--test-samples", "64", "--num_epochs", "1", "--local_training",
+                     "--model_dir", str(out), "--log-every", "0", "--gpu", "0"] + extra)
+        assert rc == 0
+        sds.append(torch.load(out / "resnet_distributed.pth", weights_only=True))
+    a = torch.cat([v.float().flatten() for k, v in sds[0].items() if v.is_floating_point()])
+    b = torch.cat([v.float().flatten() for k, v in sds[1].items() if v.is_floating_point()])
+    cos = float(torch.nn.functional.cosine_similarity(a, b, dim=0))
+    assert cos > 0.9999, cos
