@@ -74,7 +74,18 @@ def parse():
                     help="1: fixed-order reductions (no float atomics), bit-reproducible steps")
     ap.add_argument("--tune", type=int, default=1,
                     help="1: autotune conv tile configs per shape in the warm-up (cudnn.benchmark "
-                         "analogue); 0: heuristic tile choice")
+                         "analogue; in deterministic mode only a loaded / shipped table is used); "
+                         "0: heuristic tile choice; 2: time candidates even in deterministic mode "
+                         "(to build a shipped table with --save-tune)")
+    ap.add_argument("--emulate-ranks", type=int, default=1,
+                    help="world-1 reference for DDP equivalence tests: every step runs the R "
+                         "per-rank batches one after another (each BN sees its own chunk, rank 0's "
+                         "buffers are kept, as DDP's per-forward broadcast does) and averages "
+                         "their gradients before one optimizer step")
+    ap.add_argument("--dump-params", default=None,
+                    help="directory: each rank saves its final parameters and buffers there")
+    ap.add_argument("--save-tune", default=None,
+                    help="write the tuning table after the warm-up steps (JSON)")
     return ap.parse_args()
 
 
@@ -134,8 +145,8 @@ def main() -> int:
         # per-shape conv tile autotuning during the (untimed, eager) warm-up steps — the
         # analogue of the reference's cudnn.benchmark = True (task.py:244)
         from mipipe.ops import tuning
-        tuning.from_env()
-        tuning.set_benchmark(a.tune, verbose=False)
+        tuning.from_env(bool(a.deterministic))
+        tuning.set_benchmark(a.tune > 0, verbose=False, force=a.tune == 2)
         from mipipe.ops import determinism
         determinism.set_deterministic(bool(a.deterministic))
     if rank == 0:
@@ -155,21 +166,35 @@ def main() -> int:
         if rank == 0:  # progress for long first steps (kernel autotuning, graph capture)
             print(f"warmup step {i + 1}/{a.warmup}", file=sys.stderr, flush=True)
     _sync(dev)
+    if a.save_tune and rank == 0:
+        from mipipe.ops import tuning
+        tuning.save(a.save_tune)
     if distributed:
         dist.barrier()
     _sync(dev)
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        loss = step(*batches[i % 2])
-    _sync(dev)
-    if distributed:
-        dist.barrier()
-    _sync(dev)
-    dt = time.perf_counter() - t0
+    from mipipe.obs.clocks import ClockSampler
+    sampler = ClockSampler(local if not cpu else -1)
+    if cpu:
+        sampler.dir = None
+    with sampler:  # sysfs reads on a daemon thread: shader clock / power during the timed steps
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            loss = step(*batches[i % 2])
+        _sync(dev)
+        if distributed:
+            dist.barrier()
+        _sync(dev)
+        dt = time.perf_counter() - t0
     if distributed:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    if a.dump_params:
+        inner = getattr(model, "module", model)
+        os.makedirs(a.dump_params, exist_ok=True)
+        torch.save({"params": [p.detach().cpu() for p in inner.parameters()],
+                    "buffers": [b.detach().cpu() for b in inner.buffers()]},
+                   os.path.join(a.dump_params, f"rank{rank}.pt"))
     value = a.batch * world * a.steps / dt
     if is_bert:
         key = f"{a.model}_{a.seq}"
@@ -196,7 +221,7 @@ def main() -> int:
                        "hip_graph": bool(getattr(a, "graph_used", False)),
                        "deterministic": bool(a.deterministic),
                        "force_reduce": bool(a.force_reduce)},
-            "final_loss": loss_v}), flush=True)
+            "final_loss": loss_v, "gpu_clocks": sampler.summary()}), flush=True)
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
@@ -264,6 +289,17 @@ def build_cnn(a, world, local, dev, rank):
            for i in range(2)]
     in_ch = 1 if a.model == "mnist_cnn" else 3
     batches = [synthetic_batch(t, (in_ch, a.res, a.res), a.classes, seed=0) for t in idx]
+    R = a.emulate_ranks
+    if R > 1:
+        if world != 1 or a.impl != "mipipe":
+            raise SystemExit("--emulate-ranks is a world-1 mipipe reference run")
+        # step batch i = the R chunks ranks 0..R-1 would each draw for their step i
+        batches = []
+        for i in range(2):
+            parts = [synthetic_batch(torch.arange(i * a.batch, (i + 1) * a.batch, device=dev)
+                                     + r * 10_000_000, (in_ch, a.res, a.res), a.classes, seed=0)
+                     for r in range(R)]
+            batches.append((torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])))
 
     if a.impl == "mipipe":
         from mipipe.models import create_model
@@ -287,10 +323,31 @@ def build_cnn(a, world, local, dev, rank):
             opt.step()
             return loss
 
+        if R > 1:
+            def step(x, y):  # noqa: F811
+                opt.zero_grad()
+                bufs = list(model.buffers())
+                start = [b.detach().clone() for b in bufs]  # rank 0's broadcast buffers
+                after0, total = None, 0.0
+                for r, (xr, yr) in enumerate(zip(x.chunk(R), y.chunk(R))):
+                    for b, s0 in zip(bufs, start):
+                        b.copy_(s0)
+                    loss = cross_entropy(model(xr), yr) / R  # DDP: mean of per-rank gradients
+                    loss.backward()
+                    if r == 0:
+                        after0 = [b.detach().clone() for b in bufs]
+                    total = total + loss.detach()
+                for b, s1 in zip(bufs, after0):
+                    b.copy_(s1)
+                opt.step()
+                return total
+
         from mipipe.train.graph import GraphedStep, graph_safe
         ok, why = graph_safe(model, opt)
         if dev.type == "cpu":
             ok, why = False, "no hipGraph on the CPU"
+        if R > 1:
+            ok, why = False, "--emulate-ranks runs eagerly"
         if a.graph == "on" or (a.graph == "auto" and ok):
             if not ok:
                 raise SystemExit(f"--graph on is not possible here: {why}")

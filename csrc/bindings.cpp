@@ -90,6 +90,7 @@ mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int p
 // be exported / imported (mipipe.ops.tuning) so a job can ship a measured table.
 namespace tune {
 bool g_benchmark = false;
+bool g_force_tune = false;  // time candidates even in deterministic mode (table generation)
 bool g_verbose = false;
 int g_reps = 3;
 std::unordered_map<std::string, int> g_table;
@@ -122,6 +123,11 @@ int select_from(const std::string& k, const std::vector<int>& cands, F&& run) {
   auto it = g_table.find(k);
   if (it != g_table.end()) return it->second;
   if (!g_benchmark || capturing()) return -1;
+  // Deterministic mode: the tile plan fixes the reduction partition (BatchNorm partial rows per
+  // M tile, split-K slices), so a timing-based pick would make two runs sum in different
+  // orders.  Only a loaded table (MIPIPE_TUNE_TABLE / the shipped one) or the heuristic decide,
+  // unless tuning is forced (g_force_tune: building such a table).
+  if (mipipe::g_deterministic && !g_force_tune) return -1;
   hipStream_t st = stream();
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
@@ -1391,6 +1397,7 @@ PYBIND11_MODULE(_C, m) {
     tune::g_reps = std::max(1, reps);
   }, py::arg("on"), py::arg("verbose") = false, py::arg("reps") = 3);
   m.def("get_benchmark", []() { return tune::g_benchmark; });
+  m.def("set_force_tune", [](bool on) { tune::g_force_tune = on; });
   m.def("set_deterministic", [](bool on) { mipipe::g_deterministic = on ? 1 : 0; });
   m.def("get_deterministic", []() { return mipipe::g_deterministic != 0; });
   m.def("tune_table", []() { return tune::g_table; });

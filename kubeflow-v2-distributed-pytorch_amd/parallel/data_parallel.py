@@ -291,12 +291,18 @@ class DataParallel(tnn.Module):
         results: List[Any] = [None] * n
         errors: List[Optional[BaseException]] = [None] * n
         grad_on = torch.is_grad_enabled()
-        autocast = torch.is_autocast_enabled()
+        autocast = torch.is_autocast_enabled("cuda")
+        # autocast state is thread-local: hand the caller's dtype to every worker thread, or the
+        # replicas on other devices would fall back to autocast's default (fp16)
+        ac_dtype = torch.get_autocast_dtype("cuda")
+        # a backward that raised before its final callbacks ran left the flag set: every later
+        # backward would skip the replica-gradient reduction
+        self._reduce_queued = False
 
         def run(i: int) -> None:
             try:
                 with _device_ctx(devs[i]), torch.set_grad_enabled(grad_on), \
-                        torch.autocast("cuda", enabled=autocast) if devs[i].type == "cuda" else _nullctx():
+                        torch.autocast("cuda", dtype=ac_dtype, enabled=autocast) if devs[i].type == "cuda" else _nullctx():
                     a, kw = _to(pieces[i], devs[i])
                     results[i] = replicas[i](*a, **kw)
             except BaseException as e:  # re-raised on the caller's thread

@@ -14,7 +14,10 @@ Constraints of capture (checked or documented):
   NOT for AdamW's bias correction or per-step dropout seeds — :func:`graph_safe` refuses those;
 * under mipipe DDP the bucket all-reduces are captured too (RCCL on the process group's
   stream); capture runs in ``thread_local`` error mode so the RCCL watchdog thread can keep
-  querying its events.
+  querying its events, and capture starts only once every process group's watchdog tracks no
+  outstanding work (:func:`_drain_collective_watchdog`);
+* warm-up and capture run on one stream (:func:`step_stream`), so no parameter's AccumulateGrad
+  node is pinned to a stream outside the capture.
 """
 from __future__ import annotations
 
@@ -36,16 +39,51 @@ def graph_safe(model: torch.nn.Module, optimizer) -> Tuple[bool, str]:
     return True, ""
 
 
-def _drain_collective_watchdog(wait_s: float = 0.5) -> None:
-    """Let the process group's watchdog thread retire the (completed) work of the eager warm-up
-    collectives before capture starts: it polls every ~100 ms with event queries, and a query
-    that lands inside the capture window can fail and abort the process (seen once in ~10
-    world-1 RCCL captures, tests/test_ddp_gpu.py).  The device is idle here, so every pending
-    work object completes on its next poll."""
-    import time
+def _drain_collective_watchdog(timeout_s: float = 60.0) -> None:
+    """Block until every process group's watchdog has retired all of its enqueued work.
+
+    Why: ProcessGroupNCCL's watchdog thread polls the end events of every collective it still
+    tracks.  An event query that lands while this thread is capturing can fail the capture and
+    abort the process (observed once in ~10 world-1 RCCL captures in round 2).  The condition
+    that makes capture safe is "the watchdog tracks no work" — ``_wait_for_pending_works()``
+    waits for exactly that (the PG's work list and its completed-work list both empty).  The
+    device is synchronised before this is called, so every tracked work is complete and is
+    retired on the watchdog's next poll; nothing is enqueued during capture itself (captured
+    collectives are not handed to the watchdog)."""
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized():
-        time.sleep(wait_s)
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    from torch.distributed import distributed_c10d as c10d
+    pgs = list(getattr(c10d._world, "pg_map", {}).keys()) or [c10d._get_default_group()]
+    for pg in pgs:
+        try:
+            backend = dist.get_backend(pg)
+        except Exception:
+            backend = ""
+        if "nccl" not in str(backend):
+            continue  # gloo / other backends have no event-polling watchdog
+        wait = getattr(pg, "_wait_for_pending_works", None)
+        if wait is None:
+            raise RuntimeError("this torch build has no ProcessGroup._wait_for_pending_works: "
+                               "cannot prove the collective watchdog is idle before capture")
+        wait()
+
+
+_STEP_STREAMS = {}
+
+
+def step_stream(device: torch.device) -> "torch.cuda.Stream":
+    """The one side stream every eager warm-up step AND the capture of a device run on.
+
+    Autograd pins each parameter's AccumulateGrad node to the stream current when the node was
+    created; a node created on stream A and still alive when backward runs on stream B makes
+    the engine synchronise A with B ("AccumulateGrad node's stream does not match ...") — during
+    capture that is a cross-stream dependency on a stream outside the capture.  Warm-up and
+    capture on the same stream removes the mismatch at its cause."""
+    key = (device.type, device.index)
+    if key not in _STEP_STREAMS:
+        _STEP_STREAMS[key] = torch.cuda.Stream(device)
+    return _STEP_STREAMS[key]
 
 
 class GraphedStep:
@@ -63,7 +101,7 @@ class GraphedStep:
             list(inputs) if inputs is not None
             else [(example[0].clone(), example[1].clone())])
         self.copy_in = inputs is None
-        s = torch.cuda.Stream(dev)
+        s = step_stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):  # warm up on a side stream (allocator + lazy init)
             for i in range(max(1, warmup)):
@@ -79,7 +117,7 @@ class GraphedStep:
             g = torch.cuda.CUDAGraph()
             # thread_local: the process group's watchdog thread keeps polling its RCCL work
             # events while this thread captures; global mode would fail those queries
-            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+            with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode="thread_local"):
                 loss = self.fn(x, y).detach()  # drop the autograd graph: no stale grad nodes
             pool = g.pool()
             self.graphs.append(g)

@@ -67,12 +67,13 @@ def configure_kernels(use_gpu: bool, deterministic: bool = True) -> None:
     reductions, no float atomics: :mod:`mipipe.ops.determinism`); task.py:244
     ``cudnn.benchmark = True`` -> per-shape tile autotuning of the conv kernels
     (:mod:`mipipe.ops.tuning`; ``MIPIPE_BENCHMARK=0`` disables it, ``MIPIPE_TUNE_TABLE=path``
-    starts from a saved table)."""
+    starts from a saved table).  In deterministic mode nothing is picked by timing (the plan
+    fixes the reduction order): a loaded / shipped table or the heuristic decides."""
     if not use_gpu:
         return
     from mipipe.ops import determinism, tuning
     determinism.set_deterministic(deterministic)
-    tuning.from_env()
+    tuning.from_env(deterministic)  # deterministic: shipped measured tables replace timing
     tuning.set_benchmark(os.environ.get("MIPIPE_BENCHMARK", "1") != "0",
                          verbose=os.environ.get("MIPIPE_TUNE_VERBOSE", "0") == "1")
 

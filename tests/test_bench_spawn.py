@@ -83,3 +83,33 @@ def test_spawn_local_ranks_env_contract():
     assert all(e["WORLD_SIZE"] == "4" and e["MASTER_ADDR"] == "127.0.0.1"
                and e["MASTER_PORT"] == "12345" and e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
                for e in envs)
+
+
+def test_bench_world4_gloo_matches_global_batch(tmp_path):
+    """`bench.py --gpus 4` (4 gloo ranks, mipipe DDP) ends with bit-identical parameters on
+    every rank, equal (to fp32 reduction-order noise) to ONE process that runs the same four
+    per-rank batches and averages their gradients (--emulate-ranks 4): the DDP contract of the
+    reference's task.py:189 (average of per-rank gradients, rank 0's BN buffers broadcast before
+    every forward), rehearsed at world 4 before any 8-GPU run."""
+    import torch
+    args = ["--device", "cpu", "--model", "mnist_cnn", "--res", "28", "--classes", "10",
+            "--batch", "8", "--steps", "3", "--warmup", "1"]
+    d4, d1 = tmp_path / "w4", tmp_path / "w1"
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "4", "--dump-params", str(d4)] + args,
+                       env=_env(), capture_output=True, text=True, timeout=600, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--emulate-ranks", "4",
+                        "--dump-params", str(d1)] + args,
+                       env=_env(), capture_output=True, text=True, timeout=600, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    ranks = [torch.load(d4 / f"rank{i}.pt", weights_only=True) for i in range(4)]
+    ref = torch.load(d1 / "rank0.pt", weights_only=True)
+    for rk in ranks[1:]:
+        for a, b in zip(ranks[0]["params"], rk["params"]):
+            assert torch.equal(a, b)
+    moved = 0.0
+    for a, b in zip(ranks[0]["params"], ref["params"]):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5), (a - b).abs().max()
+        moved += float((a - b).abs().max())
+    for a, b in zip(ranks[0]["buffers"], ref["buffers"]):
+        assert torch.allclose(a.float(), b.float(), rtol=1e-4, atol=1e-5)

@@ -78,3 +78,24 @@ def test_det_reductions_match_atomic():
     rel = lambda a, b: ((a - b).abs().max() / b.abs().max()).item()  # noqa: E731
     assert rel(dw1, ref_dw) < 5e-3 and rel(dw1, dw3) < 1e-4
     assert rel(s1.sum(0), s3.sum(0)) < 1e-4 and rel(q1.sum(0), q3.sum(0)) < 1e-4
+
+
+def test_identical_runs_with_benchmark_mode_on():
+    """task.py's default is deterministic AND cudnn.benchmark-style tuning on (reference
+    task.py:25 + :244).  Timing-based plan selection would let two runs pick different reduction
+    partitions; in deterministic mode the plan must come from a table or the heuristic, so two
+    runs that each start from an empty tuning table still agree bit for bit."""
+    from mipipe.ops import tuning
+    determinism.set_deterministic(True)
+    try:
+        tuning.clear()
+        tuning.set_benchmark(True)
+        a, la = _train("resnet18", torch.bfloat16)
+        assert not tuning.table(), "deterministic mode must not time-tune"
+        tuning.clear()
+        b, lb = _train("resnet18", torch.bfloat16)
+    finally:
+        tuning.set_benchmark(False)
+        tuning.clear()
+    assert torch.equal(la, lb), (la, lb)
+    assert torch.equal(a, b), f"{(a != b).sum().item()} of {a.numel()} values differ"

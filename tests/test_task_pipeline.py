@@ -127,6 +127,24 @@ def test_reference_pipeline_end_to_end(gcs_root, tmp_path, monkeypatch):
     assert any(k.startswith("module.") for k in sd)  # DDP-wrapped, like the reference
 
 
+def test_find_pretrained_prefers_imagenet1k_v1(tmp_path, monkeypatch):
+    """With several torchvision weight versions cached, pretrained=True means IMAGENET1K_V1
+    (torchvision 0.8, the reference's container nb:137), independent of hash sort order."""
+    from mipipe.models import find_pretrained
+    ck = tmp_path / "hub" / "checkpoints"
+    ck.mkdir(parents=True)
+    for f in ("resnet50-11ad3fa6.pth", "resnet50-0676ba61.pth"):  # V2 sorts first
+        (ck / f).write_bytes(b"")
+    (ck / "inception_v3_google-0cc3c7bd.pth").write_bytes(b"")
+    monkeypatch.setenv("TORCH_HOME", str(tmp_path))
+    assert find_pretrained("resnet50") == str(ck / "resnet50-0676ba61.pth")
+    assert find_pretrained("inception_v3") == str(ck / "inception_v3_google-0cc3c7bd.pth")
+    (ck / "resnet18-aaaaaaaa.pth").write_bytes(b"")
+    (ck / "resnet18-bbbbbbbb.pth").write_bytes(b"")
+    with pytest.warns(UserWarning, match="IMAGENET1K_V1"):
+        assert find_pretrained("resnet18") == str(ck / "resnet18-aaaaaaaa.pth")
+
+
 def test_pretrained_from_local_torchvision_file(tmp_path, monkeypatch, capsys):
     """--pretrained (task.py:166-168) loads a torchvision-format state_dict from
     --pretrained-weights or the torchvision cache with a weights-only loader."""
