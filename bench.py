@@ -260,6 +260,23 @@ def build_bert(a, world, local, dev, rank):
             loss.backward()
             opt.step()
             return loss
+
+        # AdamW's step count and the dropout seeds' per-step part live on the device, so the
+        # whole step (dropout included) replays from one captured hipGraph
+        from mipipe.train.graph import GraphedStep, graph_safe
+        ok, why = graph_safe(model, opt)
+        if dev.type == "cpu":
+            ok, why = False, "no hipGraph on the CPU"
+        if a.graph == "on" or (a.graph == "auto" and ok):
+            if not ok:
+                raise SystemExit(f"--graph on is not possible here: {why}")
+            model.train()
+            gs = GraphedStep(step, batches[0], warmup=max(2, a.warmup), inputs=batches)
+            a.graph_used = True
+            ids_of = {id(b[0]): k for k, b in enumerate(batches)}
+
+            def step(ids, am, pos, labels):  # noqa: F811
+                return gs.replay(ids_of[id(ids)])
     else:
         from mipipe.models.reference import ref_bert
         model = ref_bert(a.model).to(dev)

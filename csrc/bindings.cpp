@@ -886,8 +886,16 @@ void sgd_step(Tensor p, Tensor g, Tensor m, optional<Tensor> shadow, double lr, 
                    (float)grad_scale, stream());
 }
 
+static const int* i32_dev(const optional<Tensor>& t, const char* name) {
+  if (!t.has_value()) return nullptr;
+  check_cuda(*t, name);
+  TORCH_CHECK(t->scalar_type() == at::kInt && t->numel() >= 1, name, " must be an int32 device counter");
+  return t->data_ptr<int>();
+}
+
 void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, optional<Tensor> shadow, double lr,
-                double b1, double b2, double eps, double wd, int64_t step, double grad_scale) {
+                double b1, double b2, double eps, double wd, int64_t step, double grad_scale,
+                optional<Tensor> step_dev) {
   int64_t n = p.numel();
   TORCH_CHECK(n % 4 == 0, "flat buffer size must be a multiple of 4");
   check_flat(p, n, "param");
@@ -903,7 +911,8 @@ void adamw_step(Tensor p, Tensor g, Tensor m, Tensor v, optional<Tensor> shadow,
   double bc1 = 1.0 - std::pow(b1, (double)step), bc2 = 1.0 - std::pow(b2, (double)step);
   mipipe::adamw_step(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(),
                      v.data_ptr<float>(), sh, n, (float)lr, (float)b1, (float)b2, (float)eps,
-                     (float)wd, (float)bc1, (float)bc2, (float)grad_scale, stream());
+                     (float)wd, (float)bc1, (float)bc2, (float)grad_scale, stream(),
+                     i32_dev(step_dev, "step_dev"));
 }
 
 Tensor nchw_to_nhwc(Tensor x, at::ScalarType dtype, int64_t pad_to) {
@@ -1086,7 +1095,7 @@ const float* mask_ptr(const optional<Tensor>& mask, int64_t B, int64_t S) {
 
 std::tuple<Tensor, Tensor> attention_fwd(Tensor qkv, int64_t B, int64_t S, int64_t H,
                                          optional<Tensor> mask, double scale, double p_drop,
-                                         int64_t seed) {
+                                         int64_t seed, optional<Tensor> seed_dev) {
   check_attn(qkv, B, S, H);
   c10::DeviceGuard g(qkv.device());
   TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "dropout p must be in [0, 1)");
@@ -1094,12 +1103,13 @@ std::tuple<Tensor, Tensor> attention_fwd(Tensor qkv, int64_t B, int64_t S, int64
   auto lse = torch::empty({B, H, S}, qkv.options().dtype(at::kFloat));
   mipipe::attention_fwd(qkv.data_ptr(), mask_ptr(mask, B, S), o.data_ptr(), lse.data_ptr<float>(),
                         (int)B, (int)S, (int)H, (float)scale, (float)p_drop, (uint32_t)seed,
-                        stream());
+                        stream(), (const uint32_t*)i32_dev(seed_dev, "seed_dev"));
   return {o, lse};
 }
 
 Tensor attention_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, int64_t B, int64_t S,
-                     int64_t H, optional<Tensor> mask, double scale, double p_drop, int64_t seed) {
+                     int64_t H, optional<Tensor> mask, double scale, double p_drop, int64_t seed,
+                     optional<Tensor> seed_dev) {
   check_attn(qkv, B, S, H);
   check_bf16(dout, "dout");
   check_bf16(o, "o");
@@ -1114,17 +1124,19 @@ Tensor attention_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, int64_t B, i
   mipipe::attention_bwd(dout.data_ptr(), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                         mask_ptr(mask, B, S), dqkv.data_ptr(), delta.data_ptr<float>(),
                         dq_acc.data_ptr<float>(), (int)B, (int)S, (int)H, (float)scale,
-                        (float)p_drop, (uint32_t)seed, stream());
+                        (float)p_drop, (uint32_t)seed, stream(),
+                        (const uint32_t*)i32_dev(seed_dev, "seed_dev"));
   return dqkv;
 }
 
-Tensor dropout_fwd(Tensor x, double p, int64_t seed) {
+Tensor dropout_fwd(Tensor x, double p, int64_t seed, optional<Tensor> seed_dev) {
   check_bf16(x, "x");
   c10::DeviceGuard g(x.device());
   TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
   TORCH_CHECK(x.numel() % 8 == 0, "dropout needs numel % 8 == 0");
   auto y = torch::empty_like(x);
-  mipipe::dropout_fwd(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (uint32_t)seed, stream());
+  mipipe::dropout_fwd(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (uint32_t)seed, stream(),
+                      (const uint32_t*)i32_dev(seed_dev, "seed_dev"));
   return y;
 }
 
@@ -1454,7 +1466,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd, py::arg("logits"), py::arg("labels"),
         py::arg("smoothing"), py::arg("ignore_index"), py::arg("valid_cols") = -1);
   m.def("sgd_step", &sgd_step);
-  m.def("adamw_step", &adamw_step);
+  m.def("adamw_step", &adamw_step, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"),
+        py::arg("shadow"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"),
+        py::arg("wd"), py::arg("step"), py::arg("grad_scale"), py::arg("step_dev") = py::none());
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("synthetic_batch", &synthetic_batch);
   m.def("gelu_fwd", &gelu_fwd);
@@ -1471,11 +1485,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_attn_waves", [](int v) { mipipe::g_attn_waves = v; });
   m.def("attention_fwd", &attention_fwd, py::arg("qkv"), py::arg("B"), py::arg("S"), py::arg("H"),
         py::arg("mask") = py::none(), py::arg("scale") = 0.125, py::arg("p_drop") = 0.0,
-        py::arg("seed") = 0);
+        py::arg("seed") = 0, py::arg("seed_dev") = py::none());
   m.def("attention_bwd", &attention_bwd, py::arg("dout"), py::arg("qkv"), py::arg("o"),
         py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("mask") = py::none(),
-        py::arg("scale") = 0.125, py::arg("p_drop") = 0.0, py::arg("seed") = 0);
-  m.def("dropout_fwd", &dropout_fwd);
+        py::arg("scale") = 0.125, py::arg("p_drop") = 0.0, py::arg("seed") = 0,
+        py::arg("seed_dev") = py::none());
+  m.def("dropout_fwd", &dropout_fwd, py::arg("x"), py::arg("p"), py::arg("seed"),
+        py::arg("seed_dev") = py::none());
   m.def("stem_pack", &stem_pack, py::arg("x"), py::arg("pad"), py::arg("Hp"), py::arg("Wsp"),
         py::arg("dtype") = at::kBFloat16);
   m.def("top1_correct", &top1_correct, py::arg("logits"), py::arg("labels"),

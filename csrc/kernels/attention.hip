@@ -110,7 +110,15 @@ struct FwdArgs {
   float p_drop;
   uint32_t drop_thr;
   uint32_t seed;
+  const uint32_t* seed_dev;  // device step counter mixed into the seed (hipGraph replays), or null
 };
+
+// effective dropout seed: host seed, or host seed mixed with the device step counter (read once
+// per wave through the scalar cache; the counter is advanced by a kernel before the forward)
+__device__ __forceinline__ uint32_t eff_seed(uint32_t seed, const uint32_t* dev) {
+  if (dev == nullptr) return seed;
+  return mix32(seed ^ (*dev * 0x9e3779b1u + 0x632be5abu));
+}
 
 constexpr int kFwdTile = 16384;  // K (8 KB) + V (8 KB) for 64 keys
 constexpr int kMaxS = 2048;
@@ -130,6 +138,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(FwdArgs a) {
   const __bf16* kb = qb + (long)H * D;
   const __bf16* vb = kb + (long)H * D;
   const int nkt = (S + 63) / 64;
+  const uint32_t dseed = a.p_drop > 0.f ? eff_seed(a.seed, a.seed_dev) : a.seed;
   float* maskl = reinterpret_cast<float*>(smem + 2 * kFwdTile);
   for (int i = tid; i < nkt * 64; i += 64 * NW)
     maskl[i] = i < S ? (a.mask ? a.mask[(long)b * S + i] * kLog2e : 0.f) : -INFINITY;
@@ -192,7 +201,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(FwdArgs a) {
         ls += p;
         if (a.p_drop > 0.f) {
           const uint32_t key = kt * 64 + sub * 32 + acc_row(i, hl);
-          p = keep_elem(a.seed, row_id, key, a.drop_thr) ? p * inv_keep : 0.f;
+          p = keep_elem(dseed, row_id, key, a.drop_thr) ? p * inv_keep : 0.f;
         }
         s[sub][i] = p;
       }
@@ -283,6 +292,7 @@ struct BwdArgs {
   float p_drop;
   uint32_t drop_thr;
   uint32_t seed;
+  const uint32_t* seed_dev;
 };
 
 // LDS: K tile (KB keys) | 2 x {Q 4 KB, dO 4 KB, lse 128 B, delta 128 B} | dSᵀ [KB][32] bf16
@@ -305,6 +315,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(BwdArgs a) {
   const __bf16* kb = qb + (long)H * D;
   const __bf16* vb = kb + (long)H * D;
   const __bf16* dob = a.dout + (long)b * S * ldq + h * D;
+  const uint32_t dseed = a.p_drop > 0.f ? eff_seed(a.seed, a.seed_dev) : a.seed;
   const float* lseb = a.lse + ((long)b * H + h) * S;
   const float* delb = a.delta + ((long)b * H + h) * S;
   const int key = kbk * KB + wave * 32 + r;
@@ -366,7 +377,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(BwdArgs a) {
       float pdrop = p, dpv = dp[i];
       if (a.p_drop > 0.f) {
         const uint32_t row_id = ((uint32_t)(b * H + h)) * (uint32_t)S + (uint32_t)min(it * 32 + qi, S - 1);
-        const bool kp = keep_elem(a.seed, row_id, (uint32_t)key, a.drop_thr);
+        const bool kp = keep_elem(dseed, row_id, (uint32_t)key, a.drop_thr);
         pdrop = kp ? p * inv_keep : 0.f;
         dpv = kp ? dpv * inv_keep : 0.f;
       }
@@ -488,9 +499,10 @@ static uint32_t drop_threshold(float p) {
 }
 
 void attention_fwd(const void* qkv, const float* mask, void* o, float* lse, int B, int S, int H,
-                   float scale, float p_drop, uint32_t seed, hipStream_t st) {
+                   float scale, float p_drop, uint32_t seed, hipStream_t st,
+                   const uint32_t* seed_dev) {
   attn::FwdArgs a{(const __bf16*)qkv, (__bf16*)o, lse, mask, B, S, H, scale * attn::kLog2e,
-                  p_drop, drop_threshold(p_drop), seed};
+                  p_drop, drop_threshold(p_drop), seed, seed_dev};
   if (attn_waves(B, S, H) == 2)
     hipLaunchKernelGGL(attn::attn_fwd_kernel<2>, dim3(B * H * ((S + 63) / 64)), dim3(128), 0, st, a);
   else
@@ -499,13 +511,14 @@ void attention_fwd(const void* qkv, const float* mask, void* o, float* lse, int 
 
 void attention_bwd(const void* dout, const void* qkv, const void* o, const float* lse,
                    const float* mask, void* dqkv, float* delta, float* dq_acc, int B, int S,
-                   int H, float scale, float p_drop, uint32_t seed, hipStream_t st) {
+                   int H, float scale, float p_drop, uint32_t seed, hipStream_t st,
+                   const uint32_t* seed_dev) {
   const long rows = (long)B * S * H;
   hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
                      (const __bf16*)dout, (const __bf16*)o, delta, dq_acc, B, S, H);
   attn::BwdArgs a{(const __bf16*)qkv, (const __bf16*)dout, lse, delta, mask, dq_acc,
                   (__bf16*)dqkv, B, S, H, scale, scale * attn::kLog2e, p_drop,
-                  drop_threshold(p_drop), seed};
+                  drop_threshold(p_drop), seed, seed_dev};
   if (attn_waves(B, S, H) == 2)
     hipLaunchKernelGGL(attn::attn_bwd_kernel<2>, dim3(B * H * ((S + 63) / 64)), dim3(128), 0, st, a);
   else

@@ -224,9 +224,10 @@ void top1_correct(const void* logits, const int64_t* labels, int R, int V, int* 
 void sgd_step(float* p, const float* g, float* m, void* shadow, long n, float lr, float momentum,
               float dampening, float wd, bool nesterov, bool first, float grad_scale,
               hipStream_t st);
+// t_dev (device step counter, may be null): bias corrections 1 - b^t computed in the kernel
 void adamw_step(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr,
                 float b1, float b2, float eps, float wd, float bc1, float bc2, float grad_scale,
-                hipStream_t st);
+                hipStream_t st, const int* t_dev = nullptr);
 void nchw_to_nhwc(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int Cp,
                   hipStream_t st, bool y_f32 = false);
 // Stem "super-pixel" packing (C <= 4): y[n][h'][j][p*4 + c] = x[n][c][h'-pad][2j+p-pad] (zero
@@ -253,14 +254,19 @@ void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st);
 // p_drop > 0 applies attention-probability dropout keyed by (seed, b, h, q, k).
 extern int g_attn_waves;  // attention block size override (0 auto, 2, 4)
 void attention_fwd(const void* qkv, const float* mask, void* o, float* lse, int B, int S, int H,
-                   float scale, float p_drop, uint32_t seed, hipStream_t st);
+                   float scale, float p_drop, uint32_t seed, hipStream_t st,
+                   const uint32_t* seed_dev = nullptr);
 // dqkv [B*S][3*H*64]; delta [B][H][S] and dq_acc [B*S][H*64] fp32 are scratch.
 void attention_bwd(const void* dout, const void* qkv, const void* o, const float* lse,
                    const float* mask, void* dqkv, float* delta, float* dq_acc, int B, int S,
-                   int H, float scale, float p_drop, uint32_t seed, hipStream_t st);
+                   int H, float scale, float p_drop, uint32_t seed, hipStream_t st,
+                   const uint32_t* seed_dev = nullptr);
 // Elementwise dropout keyed by (seed, element index): y = x * keep / (1 - p); the backward
 // recomputes the same keep mask from the seed (no mask tensor).
-void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStream_t st);
+// seed_dev (device step counter, may be null) is mixed into the seed inside the kernel, so a
+// replayed hipGraph draws a fresh mask every step.
+void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStream_t st,
+                 const uint32_t* seed_dev = nullptr);
 void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, int rows,
                    hipStream_t st);
 // work (deterministic mode, else null): [colsum_blocks(rows, cols)][cols] floats of partials

@@ -250,7 +250,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     __bf16* __restrict__ sh, long n4, float lr,
                                                     float b1, float b2, float eps, float wd,
-                                                    float bc1, float bc2, float gs) {
+                                                    float bc1, float bc2, float gs,
+                                                    const int* __restrict__ t_dev) {
+  if (t_dev != nullptr) {  // step count on the device: graph-replayable bias correction
+    const float t = (float)*t_dev;
+    bc1 = 1.f - exp2f(t * log2f(b1));
+    bc2 = 1.f - exp2f(t * log2f(b2));
+  }
   const float rbc2 = rsqrtf(bc2);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
@@ -279,10 +285,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 
 void adamw_step(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr,
                 float b1, float b2, float eps, float wd, float bc1, float bc2, float grad_scale,
-                hipStream_t st) {
+                hipStream_t st, const int* t_dev) {
   long n4 = n / 4;
   hipLaunchKernelGGL(adamw_kernel, dim3(grid1d(n4, 4)), dim3(256), 0, st, p, g, m, v,
-                     (__bf16*)shadow, n4, lr, b1, b2, eps, wd, bc1, bc2, grad_scale);
+                     (__bf16*)shadow, n4, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, t_dev);
 }
 
 // ------------------------------------------------------------------------------ layout / data
@@ -760,7 +766,9 @@ __device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
 
 __global__ __launch_bounds__(256) void dropout_kernel(const __bf16* __restrict__ x,
                                                       __bf16* __restrict__ y, long n8, float scale,
-                                                      uint32_t thr, uint32_t seed) {
+                                                      uint32_t thr, uint32_t seed,
+                                                      const uint32_t* __restrict__ seed_dev) {
+  if (seed_dev != nullptr) seed = drop_mix(seed ^ (*seed_dev * 0x9e3779b1u + 0x632be5abu));
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
        i += (long)gridDim.x * blockDim.x) {
     float f[8];
@@ -775,12 +783,13 @@ __global__ __launch_bounds__(256) void dropout_kernel(const __bf16* __restrict__
   }
 }
 
-void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStream_t st) {
+void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStream_t st,
+                 const uint32_t* seed_dev) {
   const long n8 = n / 8;
   double t = (double)p * 4294967296.0;
   uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
   hipLaunchKernelGGL(dropout_kernel, dim3(grid1d(n8)), dim3(256), 0, st, (const __bf16*)x,
-                     (__bf16*)y, n8, 1.f / (1.f - p), thr, seed);
+                     (__bf16*)y, n8, 1.f / (1.f - p), thr, seed, seed_dev);
 }
 
 // ------------------------------------------------------------------------------ stem packing

@@ -31,6 +31,7 @@ import torch.nn as tnn
 
 from mipipe import nn as mnn
 from mipipe.ops import functional as MF
+from mipipe.ops import kernels as K
 
 from . import register_model
 
@@ -152,6 +153,9 @@ class BertForMaskedLM(tnn.Module):
     -> MLM logits ``[B*P, V]`` for the masked positions (or ``[B*S, V]`` for all tokens).
     ``loss(logits, labels)`` = mean cross-entropy (labels -100 ignored)."""
 
+    # dropout seeds take their per-step part from a device counter on the GPU (graph-replayable)
+    device_seeds = True
+
     def __init__(self, config: Optional[BertConfig] = None, compute_dtype=None, seed: int = 0,
                  **kw):
         super().__init__()
@@ -162,6 +166,7 @@ class BertForMaskedLM(tnn.Module):
         self.cls = _Cls(c)
         self.seed = seed
         self._step = 0
+        self._step_dev: Optional[torch.Tensor] = None  # device step counter (dropout seeds)
         self._vpad = (-c.vocab_size) % 64  # decoder N padded to the GEMM's 64-wide tiles
         self._init_weights()
         # the tied decoder's weight-gradient GEMM runs before the embedding lookup's scatter in
@@ -209,18 +214,33 @@ class BertForMaskedLM(tnn.Module):
             self._step += 1
         rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
         base = (self.seed + 7919 * rank) & 0xFFFFFFFF
+        # On the GPU the per-step part of every dropout seed is a device counter advanced here by
+        # a device op, so a hipGraph-captured step draws fresh masks on every replay (the host
+        # counter self._step would be frozen at capture).
+        sdev = None
+        if self.training and input_ids.is_cuda:
+            if self._step_dev is None or self._step_dev.device != input_ids.device:
+                self._step_dev = torch.zeros(1, dtype=torch.int32, device=input_ids.device)
+            self._step_dev.add_(1)
+            sdev = self._step_dev
+
+        def seed_at(site: int):
+            if sdev is not None:
+                return K.DevSeed(_seed(base, 0, site), sdev)
+            return _seed(base, self._step, site)
+
         ids = input_ids.reshape(-1)
         pos = torch.arange(S, device=ids.device).repeat(B)
         tt = torch.zeros_like(ids) if token_type_ids is None else token_type_ids.reshape(-1)
         w = emb.word_embeddings(ids, dt)
         pt = emb.position_embeddings(pos, dt) + emb.token_type_embeddings(tt, dt)
         h = emb.LayerNorm(w, residual=pt)
-        h = MF.dropout(h, c.hidden_dropout_prob, _seed(base, self._step, 0), self.training)
+        h = MF.dropout(h, c.hidden_dropout_prob, seed_at(0), self.training)
         mask = None
         if attention_mask is not None:
             mask = (1.0 - attention_mask.float()) * -10000.0  # HF extended attention mask
         for i, layer in enumerate(self.bert.encoder.layer):
-            seeds = [_seed(base, self._step, 3 * i + j + 1) for j in range(3)]
+            seeds = [seed_at(3 * i + j + 1) for j in range(3)]
             h = layer(h, B, S, mask, seeds)
         if masked_positions is not None:
             P = masked_positions.shape[1]

@@ -928,8 +928,10 @@ def attention(qkv: Tensor, batch: int, seq: int, heads: int, mask: Optional[Tens
         scale = 1.0 / math.sqrt(D)
     if mask is not None:
         mask = mask.float().contiguous()
+    if not isinstance(seed, K.DevSeed):
+        seed = int(seed) & 0xFFFFFFFF
     return _AttentionFn.apply(qkv.contiguous(), batch, seq, heads, mask, float(scale),
-                              float(p_drop), int(seed) & 0xFFFFFFFF)
+                              float(p_drop), seed)
 
 
 class _DropoutFn(Function):
@@ -949,7 +951,9 @@ def dropout(x: Tensor, p: float, seed: int, training: bool = True) -> Tensor:
     regenerates it instead of storing it."""
     if not training or p <= 0.0:
         return x
-    return _DropoutFn.apply(x, float(p), int(seed) & 0xFFFFFFFF)
+    if not isinstance(seed, K.DevSeed):
+        seed = int(seed) & 0xFFFFFFFF
+    return _DropoutFn.apply(x, float(p), seed)
 
 
 class _EmbeddingFn(Function):

@@ -7,7 +7,7 @@ opted in with ``MIPIPE_ALLOW_REF_ON_GPU=1`` (debugging / numerics bisection only
 from __future__ import annotations
 
 import os
-from typing import Optional
+from typing import NamedTuple, Optional
 
 import torch
 
@@ -306,10 +306,14 @@ def sgd_step(param, grad, mom, shadow, lr, momentum, dampening, weight_decay, ne
 
 
 def adamw_step(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, weight_decay,
-               step, grad_scale=1.0):
+               step, grad_scale=1.0, step_dev=None):
+    """``step_dev``: int32 [1] device step count; the kernel then computes the bias corrections
+    itself (graph-replayable), ``step`` is ignored by the native path."""
     if use_native(param):
         return native().adamw_step(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2,
-                                   eps, weight_decay, step, grad_scale)
+                                   eps, weight_decay, step, grad_scale, step_dev)
+    if step_dev is not None:
+        step = int(step_dev.reshape(-1)[0].item())
     return _ref.adamw_step(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps,
                            weight_decay, step, grad_scale)
 
@@ -345,24 +349,50 @@ def colsum(x, out=None):
     return s
 
 
+class DevSeed(NamedTuple):
+    """A dropout seed whose per-step part lives on the device: ``base`` (host, per call site)
+    mixed inside the kernel with ``counter`` (int32 [1] device tensor advanced once per training
+    step by a device op).  A replayed hipGraph therefore draws a fresh mask every step."""
+    base: int
+    counter: torch.Tensor
+
+
+def _split_seed(seed):
+    """(host seed, device counter or None) for the native kernels."""
+    if isinstance(seed, DevSeed):
+        return seed.base & 0xFFFFFFFF, seed.counter
+    return int(seed) & 0xFFFFFFFF, None
+
+
+def _host_seed(seed) -> int:
+    """The plain-torch reference path: fold the counter value in on the host (no graphs there)."""
+    if isinstance(seed, DevSeed):
+        c = int(seed.counter.reshape(-1)[0].item())
+        return (seed.base ^ (c * 0x9E3779B1 + 0x632BE5AB)) & 0xFFFFFFFF
+    return int(seed)
+
+
 def attention_fwd(qkv, B, S, H, mask, scale, p_drop=0.0, seed=0):
     if use_native(qkv):
-        return native().attention_fwd(qkv, B, S, H, mask, scale, p_drop, seed)
-    return _ref.attention_fwd(qkv, B, S, H, mask, scale, p_drop, seed)
+        sd, dev = _split_seed(seed)
+        return native().attention_fwd(qkv, B, S, H, mask, scale, p_drop, sd, dev)
+    return _ref.attention_fwd(qkv, B, S, H, mask, scale, p_drop, _host_seed(seed))
 
 
 def attention_bwd(do, qkv, o, lse, B, S, H, mask, scale, p_drop=0.0, seed=0):
     if use_native(do):
-        return native().attention_bwd(do, qkv, o, lse, B, S, H, mask, scale, p_drop, seed)
-    return _ref.attention_bwd(do, qkv, o, lse, B, S, H, mask, scale, p_drop, seed)
+        sd, dev = _split_seed(seed)
+        return native().attention_bwd(do, qkv, o, lse, B, S, H, mask, scale, p_drop, sd, dev)
+    return _ref.attention_bwd(do, qkv, o, lse, B, S, H, mask, scale, p_drop, _host_seed(seed))
 
 
 def dropout_fwd(x, p, seed):
     """y = x·keep/(1-p) with keep hashed from (seed, element index); applying it to dy with the
-    same seed is the backward."""
+    same seed is the backward.  ``seed``: int or :class:`DevSeed`."""
     if use_native(x) and x.numel() % 8 == 0:
-        return native().dropout_fwd(x, p, seed & 0xFFFFFFFF)
-    return _ref.dropout_fwd(x, p, seed)
+        sd, dev = _split_seed(seed)
+        return native().dropout_fwd(x, p, sd, dev)
+    return _ref.dropout_fwd(x, p, _host_seed(seed))
 
 
 def embedding_bwd(dy, idx, num_rows, out=None):

@@ -121,6 +121,11 @@ class AdamW(_FlatOptimizer):
                         differentiable=False, fused=True)
         super().__init__(params, defaults, shadow_dtype)
         self._step = 0
+        # On the GPU the step count also lives on the device (int32 [1]): a device op advances it
+        # and the kernel derives the bias corrections 1 - beta^t from it, so a step captured
+        # into a hipGraph stays correct on every replay (train/graph.py graph_safe).
+        self._t_dev: Optional[torch.Tensor] = None
+        self.device_step = self.space.flat.is_cuda
 
     def _after_load(self) -> None:
         for p in self.params:
@@ -128,6 +133,19 @@ class AdamW(_FlatOptimizer):
             if s is not None:
                 self._step = int(s.item() if torch.is_tensor(s) else s)
                 break
+        self._t_dev = None  # re-seeded from the loaded count at the next step
+
+    def sync_step(self) -> int:
+        """Host view of the step count (after graph replays the device counter is ahead)."""
+        if self._t_dev is not None:
+            self._step = int(self._t_dev.item())
+            for p in self.params:
+                self.state[p]["step"] = torch.tensor(float(self._step))
+        return self._step
+
+    def state_dict(self):
+        self.sync_step()
+        return super().state_dict()
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0):
@@ -135,10 +153,17 @@ class AdamW(_FlatOptimizer):
         g = self.param_groups[0]
         self._step += 1
         b1, b2 = g["betas"]
+        tdev = None
+        if self.device_step:
+            if self._t_dev is None:
+                self._t_dev = torch.full((1,), self._step - 1, dtype=torch.int32,
+                                         device=self.space.flat.device)
+            self._t_dev.add_(1)
+            tdev = self._t_dev
         K.adamw_step(self.space.flat, self.space.flat_grad, self._flat_state("exp_avg"),
                      self._flat_state("exp_avg_sq"), self.space.shadow, float(g["lr"]),
                      float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]),
-                     self._step, float(grad_scale))
+                     self._step, float(grad_scale), step_dev=tdev)
         self.space.mark_synced()
         if self._step == 1:
             self._per_param_state(["exp_avg", "exp_avg_sq"])

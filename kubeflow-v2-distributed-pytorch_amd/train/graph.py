@@ -10,8 +10,9 @@ Constraints of capture (checked or documented):
   copy each batch into them (``GraphedStep.step(x, y)``) or capture one graph per resident
   batch buffer (``GraphedStep(..., inputs=[(x0, y0), (x1, y1)])``, zero copies);
 * no host synchronisation inside the step;
-* host-side scalars are frozen at capture: fine for SGD (momentum buffers are on the device),
-  NOT for AdamW's bias correction or per-step dropout seeds — :func:`graph_safe` refuses those;
+* host-side scalars are frozen at capture: SGD has none; AdamW keeps its step count on the
+  device and dropout seeds take their per-step part from a device counter (BERT), otherwise
+  :func:`graph_safe` refuses the step;
 * under mipipe DDP the bucket all-reduces are captured too (RCCL on the process group's
   stream); capture runs in ``thread_local`` error mode so the RCCL watchdog thread can keep
   querying its events, and capture starts only once every process group's watchdog tracks no
@@ -27,14 +28,23 @@ import torch
 
 
 def graph_safe(model: torch.nn.Module, optimizer) -> Tuple[bool, str]:
-    """Whether a step of ``model`` + ``optimizer`` can be replayed from one capture."""
-    from mipipe.optim import SGD
-    if not isinstance(optimizer, SGD):
+    """Whether a step of ``model`` + ``optimizer`` can be replayed from one capture.
+
+    Per-step values must live on the device: SGD has none; AdamW's step count / bias corrections
+    are a device counter (``device_step``); mipipe dropout seeds take their per-step part from a
+    device counter when the model declares ``device_seeds`` (BERT on the GPU)."""
+    from mipipe.optim import SGD, AdamW
+    if isinstance(optimizer, AdamW):
+        if not getattr(optimizer, "device_step", False):
+            return False, "AdamW without a device step counter (CPU) uses host-side bias corrections"
+    elif not isinstance(optimizer, SGD):
         return False, f"{type(optimizer).__name__} uses host-side per-step scalars"
+    root = getattr(model, "module", model)
+    dev_seeds = bool(getattr(root, "device_seeds", False))
     for m in model.modules():
         if isinstance(m, torch.nn.Dropout) and m.p > 0 and m.training:
-            return False, "dropout seeds are host-side per-step values"
-        if getattr(m, "p_hidden", 0) or getattr(m, "p_attn", 0):
+            return False, "torch.nn.Dropout draws its mask from the host generator state"
+        if (getattr(m, "p_hidden", 0) or getattr(m, "p_attn", 0)) and not dev_seeds:
             return False, "dropout seeds are host-side per-step values"
     return True, ""
 
@@ -87,38 +97,38 @@ def step_stream(device: torch.device) -> "torch.cuda.Stream":
 
 
 class GraphedStep:
-    """Capture ``step_fn(x, y) -> loss`` into hipGraph(s) after ``warmup`` eager steps.
+    """Capture ``step_fn(*batch) -> loss`` into hipGraph(s) after ``warmup`` eager steps.
 
-    ``inputs``: the resident batch buffers to capture against (one graph each); when omitted,
-    one graph is captured against internal static buffers and :meth:`step` copies in."""
+    ``inputs``: the resident batch buffers (tuples of tensors) to capture against, one graph
+    each; when omitted, one graph is captured against internal static copies of ``example`` and
+    :meth:`step` copies each batch in."""
 
-    def __init__(self, step_fn: Callable[[torch.Tensor, torch.Tensor], torch.Tensor],
-                 example: Tuple[torch.Tensor, torch.Tensor], warmup: int = 3,
-                 inputs: Optional[Sequence[Tuple[torch.Tensor, torch.Tensor]]] = None):
+    def __init__(self, step_fn: Callable[..., torch.Tensor], example: Sequence[torch.Tensor],
+                 warmup: int = 3, inputs: Optional[Sequence[Sequence[torch.Tensor]]] = None):
         self.fn = step_fn
         dev = example[0].device
-        self.static: List[Tuple[torch.Tensor, torch.Tensor]] = (
-            list(inputs) if inputs is not None
-            else [(example[0].clone(), example[1].clone())])
+        self.static: List[Tuple[torch.Tensor, ...]] = (
+            [tuple(b) for b in inputs] if inputs is not None
+            else [tuple(t.clone() for t in example)])
         self.copy_in = inputs is None
         s = step_stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):  # warm up on a side stream (allocator + lazy init)
+        with torch.cuda.stream(s):  # warm up on the capture stream (allocator + lazy init)
             for i in range(max(1, warmup)):
-                x, y = self.static[i % len(self.static)]
-                self.warmup_loss = self.fn(x, y).detach()  # loss of the last eager step
+                batch = self.static[i % len(self.static)]
+                self.warmup_loss = self.fn(*batch).detach()  # loss of the last eager step
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
         _drain_collective_watchdog()
         self.graphs: List[torch.cuda.CUDAGraph] = []
         self.losses: List[torch.Tensor] = []
         pool = None
-        for x, y in self.static:
+        for batch in self.static:
             g = torch.cuda.CUDAGraph()
-            # thread_local: the process group's watchdog thread keeps polling its RCCL work
-            # events while this thread captures; global mode would fail those queries
+            # thread_local: the process group's watchdog thread may still poll its (retired)
+            # work events while this thread captures; global mode would fail those queries
             with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode="thread_local"):
-                loss = self.fn(x, y).detach()  # drop the autograd graph: no stale grad nodes
+                loss = self.fn(*batch).detach()  # drop the autograd graph: no stale grad nodes
             pool = g.pool()
             self.graphs.append(g)
             self.losses.append(loss)
@@ -130,11 +140,10 @@ class GraphedStep:
         self.graphs[k].replay()
         return self.losses[k]
 
-    def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    def step(self, *batch: torch.Tensor) -> torch.Tensor:
         """Copy a batch into the static buffers and run one step."""
         if not self.copy_in:
             raise RuntimeError("captured against resident buffers: use replay(i)")
-        sx, sy = self.static[0]
-        sx.copy_(x, non_blocking=True)
-        sy.copy_(y, non_blocking=True)
+        for dst, src in zip(self.static[0], batch):
+            dst.copy_(src, non_blocking=True)
         return self.replay(0)

@@ -207,3 +207,82 @@ def test_tied_embedding_reported_ready_only_when_complete():
     assert len(seen) == 1
     assert torch.equal(seen[0], w.grad)
     del opt
+
+
+def _bert_step_fn(m, opt):
+    def step(ids, am, pos, labels):
+        opt.zero_grad()
+        loss = m(ids, am, masked_positions=pos, labels=labels)
+        loss.backward()
+        opt.step()
+        return loss
+    return step
+
+
+def test_device_seeded_dropout_changes_per_step_and_replays():
+    """The per-step part of a dropout seed is a device counter: a graph-captured dropout draws a
+    new mask on every replay, the mask equals the eager one at the same counter value, and the
+    backward regenerates the forward's mask."""
+    from mipipe.ops import kernels as K
+    x = torch.randn(4096, 64, device="cuda").to(torch.bfloat16)
+    ctr = torch.zeros(1, dtype=torch.int32, device="cuda")
+    seed = K.DevSeed(1234, ctr)
+    eager = []
+    for _ in range(3):
+        ctr.add_(1)
+        eager.append(K.dropout_fwd(x, 0.1, seed))
+    assert not torch.equal(eager[0], eager[1]) and not torch.equal(eager[1], eager[2])
+    keep = (eager[0] != 0).float().mean().item()
+    assert 0.88 < keep < 0.92, keep
+    ctr.zero_()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        ctr.add_(1)
+        y = K.dropout_fwd(x, 0.1, seed)
+    ctr.zero_()
+    for i in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y, eager[i]), i
+    assert int(ctr.item()) == 3
+
+
+def test_bert_graphed_step_matches_eager():
+    """BERT MLM + AdamW + dropout replayed from one captured hipGraph follows the eager steps:
+    AdamW's step count and the dropout seeds are device counters (graph_safe accepts the step).
+    BERT's backward keeps float atomics (attention dQ, embedding scatter), so the comparison is
+    against the run-to-run noise of a second eager model."""
+    import copy
+    from mipipe.models import create_model
+    from mipipe.optim import AdamW
+    from mipipe.train.graph import GraphedStep, graph_safe
+    torch.manual_seed(0)
+    a = create_model("bert_tiny").cuda()
+    b, c = copy.deepcopy(a), copy.deepcopy(a)
+    opts = [AdamW(m.parameters(), lr=1e-3, weight_decay=0.01) for m in (a, b, c)]
+    ok, why = graph_safe(b, opts[1])
+    assert ok, why
+    B, S, P, V = 8, 128, 20, a.config.vocab_size
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    ids = torch.randint(0, V, (B, S), device="cuda", generator=g)
+    am = torch.ones(B, S, device="cuda", dtype=torch.int64)
+    pos = torch.stack([torch.randperm(S, device="cuda", generator=g)[:P] for _ in range(B)])
+    labels = torch.randint(0, V, (B, P), device="cuda", generator=g)
+    batch = (ids, am, pos, labels)
+    la = [_bert_step_fn(a, opts[0])(*batch).item() for _ in range(4)]
+    lc = [_bert_step_fn(c, opts[2])(*batch).item() for _ in range(4)]
+    gs = GraphedStep(_bert_step_fn(b, opts[1]), batch, warmup=1, inputs=[batch])
+    lb = [gs.warmup_loss.item()] + [gs.replay(0).item() for _ in range(3)]
+    torch.cuda.synchronize()
+    assert int(b._step_dev.item()) == 4 and opts[1].sync_step() == 4
+    assert lb[0] == la[0]  # the eager warm-up step is the eager step
+    noise = max(abs(x - y) for x, y in zip(la, lc)) + 1e-3 * abs(la[0])
+    assert max(abs(x - y) for x, y in zip(la, lb)) < 3 * noise + 1e-3, (la, lb, lc)
+    for (n, p), (_, q), (_, r) in zip(a.named_parameters(), b.named_parameters(),
+                                       c.named_parameters()):
+        d_pq = (p - q).abs().max().item()
+        d_pr = (p - r).abs().max().item()
+        assert d_pq <= 3 * d_pr + 1e-5, (n, d_pq, d_pr)

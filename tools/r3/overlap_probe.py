@@ -23,6 +23,8 @@ import time
 import torch
 import torch.distributed as dist
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
 
 def timeit(fn, reps=5):
     torch.cuda.synchronize()
