@@ -131,6 +131,8 @@ def main() -> int:
         dev = torch.device("cuda", local)
     distributed = world > 1 or a.force_reduce
     if distributed:
+        from mipipe.parallel.dist_utils import configure_rccl_env
+        configure_rccl_env()  # high-priority RCCL stream: bucket all-reduces overlap backward
         if cpu:
             dist.init_process_group("gloo")
         else:

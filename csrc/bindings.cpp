@@ -440,6 +440,15 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
     col.dbeta2 = fptr(col_dbeta2, C);
     colp = &col;
   }
+  // 3x3 / stride-1 convolutions: the patch-resident kernel (input patch in LDS shared by the
+  // 9 taps, partial tiles summed in a fixed order: deterministic in both modes)
+  if (cfg < 0 && mipipe::g_wgrad3x3 && mipipe::conv_wgrad3x3_supported(s)) {
+    const int S = mipipe::conv_wgrad3x3_splits(s);
+    auto ws = torch::empty({S, (int64_t)s.Co * 9 * s.Ci}, dy.options().dtype(at::kFloat));
+    mipipe::conv_wgrad3x3(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(),
+                          ws.data_ptr<float>(), S, colp);
+    return dw;
+  }
   // plan = tile id + 16 * split count (0: heuristic split)
   int plan = cfg;
   if (plan < 0) {
@@ -1410,6 +1419,8 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("on"), py::arg("verbose") = false, py::arg("reps") = 3);
   m.def("get_benchmark", []() { return tune::g_benchmark; });
   m.def("set_force_tune", [](bool on) { tune::g_force_tune = on; });
+  m.def("set_wgrad3x3", [](bool on) { mipipe::g_wgrad3x3 = on; });
+  m.def("get_wgrad3x3", []() { return mipipe::g_wgrad3x3; });
   m.def("set_deterministic", [](bool on) { mipipe::g_deterministic = on ? 1 : 0; });
   m.def("get_deterministic", []() { return mipipe::g_deterministic != 0; });
   m.def("tune_table", []() { return tune::g_table; });

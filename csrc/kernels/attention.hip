@@ -117,7 +117,10 @@ struct FwdArgs {
 // per wave through the scalar cache; the counter is advanced by a kernel before the forward)
 __device__ __forceinline__ uint32_t eff_seed(uint32_t seed, const uint32_t* dev) {
   if (dev == nullptr) return seed;
-  return mix32(seed ^ (*dev * 0x9e3779b1u + 0x632be5abu));
+  // agent-scope relaxed load: served by L2 (sc1), never by a scalar / L1 line that kernels
+  // replayed back to back from a hipGraph might not have invalidated since the counter was bumped
+  const uint32_t c = __hip_atomic_load(dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return mix32(seed ^ (c * 0x9e3779b1u + 0x632be5abu));
 }
 
 constexpr int kFwdTile = 16384;  // K (8 KB) + V (8 KB) for 64 keys

@@ -78,10 +78,52 @@ __global__ void splitk_sum_tail_kernel(const float* __restrict__ ws, int splits,
   out[i] += a;
 }
 
+// Many splits over a small output (the patch-resident 3x3 weight-grad: 256 slices of a 36 K-float
+// tile): one thread per float4 column would serialise 256 dependent loads.  P threads per column
+// each sum a fixed strided subset of the slices, then the P partials are added in a fixed order
+// through LDS — deterministic for a given (splits, P).
+template <int P>
+__global__ __launch_bounds__(256) void splitk_sum_wide_kernel(const float* __restrict__ ws,
+                                                              int splits, long n4,
+                                                              float* __restrict__ out) {
+  constexpr int C = 256 / P;  // float4 columns per block
+  __shared__ float4 part[P][C];
+  const int c = threadIdx.x % C, w = threadIdx.x / C;
+  const long col = (long)blockIdx.x * C + c;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < n4) {
+    for (int s = w; s < splits; s += P) {
+      const float4 b = reinterpret_cast<const float4*>(ws + (long)s * n4 * 4)[col];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+  }
+  part[w][c] = a;
+  __syncthreads();
+  if (w == 0 && col < n4) {
+    float4 t = part[0][c];
+#pragma unroll
+    for (int q = 1; q < P; ++q) {
+      const float4 b = part[q][c];
+      t.x += b.x; t.y += b.y; t.z += b.z; t.w += b.w;
+    }
+    float4 o = reinterpret_cast<float4*>(out)[col];
+    o.x += t.x; o.y += t.y; o.z += t.z; o.w += t.w;
+    reinterpret_cast<float4*>(out)[col] = o;
+  }
+}
+
 void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st) {
   // the vector path needs n % 4 == 0 and 16-B aligned rows of ws / out
   const bool vec = (n % 4) == 0 && (reinterpret_cast<uintptr_t>(out) % 16) == 0;
-  if (vec) {
+  if (vec && splits >= 32) {
+    const long n4 = n / 4;
+    hipLaunchKernelGGL(splitk_sum_wide_kernel<16>, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0,
+                       st, ws, splits, n4, out);
+  } else if (vec && splits >= 8) {
+    const long n4 = n / 4;
+    hipLaunchKernelGGL(splitk_sum_wide_kernel<4>, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0,
+                       st, ws, splits, n4, out);
+  } else if (vec) {
     const long n4 = n / 4;
     const long g = std::min<long>(4096, (n4 + 255) / 256);
     hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)std::max<long>(1, g)), dim3(256), 0, st,

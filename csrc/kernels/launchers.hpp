@@ -99,6 +99,13 @@ struct BnCollect {
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
                 int cfg = -1, float* ws = nullptr, int splits = -1, const BnCollect* col = nullptr);
 int conv_wgrad_splits(const ConvShape& s, int cfg, int splits = -1);
+// 3x3 / stride 1 / pad 1 bf16 weight-grad with the input patch resident in LDS (wgrad3x3.hip):
+// partial tiles per split go to ws [splits][Co*9*Ci] and are added to dw in a fixed order
+bool conv_wgrad3x3_supported(const ConvShape& s);
+int conv_wgrad3x3_splits(const ConvShape& s, int splits_req = -1);
+void conv_wgrad3x3(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
+                   float* ws, int splits, const BnCollect* col = nullptr);
+extern bool g_wgrad3x3;  // route supported shapes to conv_wgrad3x3 (default on)
 
 // ---- direct convolution, BatchNorm for any C, k x k average pool (vision.hip) ----------------
 struct GConvShape {

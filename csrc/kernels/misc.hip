@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
                                                     float bc1, float bc2, float gs,
                                                     const int* __restrict__ t_dev) {
   if (t_dev != nullptr) {  // step count on the device: graph-replayable bias correction
-    const float t = (float)*t_dev;
+    const float t = (float)__hip_atomic_load(t_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bc1 = 1.f - exp2f(t * log2f(b1));
     bc2 = 1.f - exp2f(t * log2f(b2));
   }
@@ -768,7 +768,10 @@ __global__ __launch_bounds__(256) void dropout_kernel(const __bf16* __restrict__
                                                       __bf16* __restrict__ y, long n8, float scale,
                                                       uint32_t thr, uint32_t seed,
                                                       const uint32_t* __restrict__ seed_dev) {
-  if (seed_dev != nullptr) seed = drop_mix(seed ^ (*seed_dev * 0x9e3779b1u + 0x632be5abu));
+  if (seed_dev != nullptr) {  // L2-served agent-scope load (see attention.hip eff_seed)
+    const uint32_t c = __hip_atomic_load(seed_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    seed = drop_mix(seed ^ (c * 0x9e3779b1u + 0x632be5abu));
+  }
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
        i += (long)gridDim.x * blockDim.x) {
     float f[8];

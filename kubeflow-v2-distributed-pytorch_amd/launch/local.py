@@ -37,6 +37,9 @@ def rank_envs(nprocs: int, port: Optional[int] = None,
         e = dict(os.environ)
         if extra:
             e.update(extra)
+        from mipipe.parallel.dist_utils import RCCL_ENV_DEFAULTS
+        for k, v in RCCL_ENV_DEFAULTS.items():
+            e.setdefault(k, v)
         e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nprocs),
                   "LOCAL_WORLD_SIZE": str(nprocs), "GROUP_RANK": "0",
                   "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),

@@ -476,7 +476,9 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
                "batch_per_process": args.batch_size, "global_batch": args.batch_size * world,
                "samples_per_sec_per_rank": meter.samples_per_sec(),
                "samples_per_sec_job": meter.samples_per_sec() * world,
-               "dtype": str(compute_dtype).replace("torch.", ""), "device": str(device)}
+               "dtype": str(compute_dtype).replace("torch.", ""), "device": str(device),
+               "backend": (torch.distributed.get_backend() if args.distributed else "none"),
+               "hip_graph": bool(args.hip_graph), "deterministic": bool(args.deterministic)}
     if args.rank == 0:
         ckpt.export_model(model, args, args.num_epochs, accuracy)
         ckpt.save_checkpoint(model, optimizer, args, args.num_epochs, best_acc1)
