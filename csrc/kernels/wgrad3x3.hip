@@ -32,7 +32,6 @@ using gk::mc_off;
 using gk::mc_swz;
 using gk::wait_vmcnt;
 
-constexpr int kThreads = 256;
 constexpr int TM = 64;           // co per block
 constexpr int TC = 64;           // ci per block
 constexpr int kSlots = 64;       // MFMA k-slots (pixels) per k-step
@@ -40,8 +39,6 @@ constexpr int kDyBytes = kSlots * TM * 2;            // 8 KB
 constexpr int kPatchPix = 192;                       // >= (R+2)*(W+2) for every supported shape
 constexpr int kPatchBytes = kPatchPix * TC * 2;      // 24 KB
 constexpr int kStage = kDyBytes + kPatchBytes;       // 32 KB
-constexpr int kPatchInstr = kPatchPix / (4 * 8);     // glds per wave for the patch (8 px each)
-constexpr int kLoads = 2 + kPatchInstr;              // glds per wave per stage
 // 3 LDS stages, two k-steps of loads in flight (counted vmcnt): with the 36 accumulator tiles
 // the kernel runs one wave per SIMD, so the prefetch depth, not other waves, hides HBM latency
 constexpr int kStages = 3;
@@ -86,43 +83,55 @@ __device__ __forceinline__ bf16x8 join(s16x4 lo, s16x4 hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// The 18 (ks, tap) units of one k-step, software-pipelined kLook units deep: both k halves' A
-// fragments are requested first, then B(0..kLook-1); unit u requests B(u+kLook) and waits until
+// The 18 (ks, tap) units of one k-step, software-pipelined LOOK units deep: both k halves' A
+// fragments are requested first, then B(0..LOOK-1); unit u requests B(u+LOOK) and waits until
 // only the reads issued after B(u) are outstanding (LDS returns in order), so its MFMAs overlap
-// the next kLook units' reads.  All counts are compile-time immediates (lgkmcnt <= 15).
-constexpr int kLook = 5;
+// the next LOOK units' reads.  All counts are compile-time immediates (lgkmcnt <= 15).
+template <int CB>
 struct Frags {
-  s16x4 a_lo[2][4], a_hi[2][4];
+  s16x4 a_lo[2][CB], a_hi[2][CB];
   s16x4 b_lo[18], b_hi[18];
 };
+template <int LOOK>
 __device__ constexpr int unit_allowed(int u) {
-  return 2 * ((u + kLook < 18 ? u + kLook : 17) - u);
+  return 2 * ((u + LOOK < 18 ? u + LOOK : 17) - u);
 }
 
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
-template <int U, class FA, class FB>
-__device__ __forceinline__ void unit(Frags& f, f32x4 (&acc)[9][4], FA& issueA, FB& issueB) {
+template <int LOOK, int U, int CB, class FB>
+__device__ __forceinline__ void unit(Frags<CB>& f, f32x4 (&acc)[9][CB], FB& issueB) {
   constexpr int ks = U / 9, t = U % 9;
-  if constexpr (U + kLook <= 17) issueB(U + kLook);
-  wait_lgkm<unit_allowed(U)>();
+  if constexpr (U + LOOK <= 17) issueB(U + LOOK);
+  wait_lgkm<unit_allowed<LOOK>(U)>();
   const bf16x8 bf = join(f.b_lo[U], f.b_hi[U]);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < CB; ++i)
     acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, join(f.a_lo[ks][i], f.a_hi[ks][i]),
                                                         acc[t][i], 0, 0, 0);
 }
-template <class FA, class FB, int... U>
-__device__ __forceinline__ void units(Frags& f, f32x4 (&acc)[9][4], FA& issueA, FB& issueB,
+template <int LOOK, int CB, class FB, int... U>
+__device__ __forceinline__ void units(Frags<CB>& f, f32x4 (&acc)[9][CB], FB& issueB,
                                       std::integer_sequence<int, U...>) {
-  (unit<U>(f, acc, issueA, issueB), ...);
+  (unit<LOOK, U, CB>(f, acc, issueB), ...);
 }
 
-__global__ __launch_bounds__(kThreads, 1) void wgrad3x3_kernel(
+// NW = 4: wave w owns ci [16w, 16w+16) x all 64 co (4 co blocks, 36 accumulator tiles, one wave
+//         per SIMD — the register file holds the tiles, the 3-stage prefetch hides latency);
+// NW = 8: wave w owns ci [16(w&3), +16) x co [32(w>>2), +32) (2 co blocks, 18 tiles): two waves
+//         per SIMD hide each other's LDS / barrier latency at 2x the A-fragment reads.
+template <int NW>
+__global__ __launch_bounds__(64 * NW, NW / 4) void wgrad3x3_kernel(
     const __bf16* __restrict__ dy, const __bf16* __restrict__ x, float* __restrict__ ws, Geo g,
     BnCollect col) {
+  constexpr int CB = 16 / NW;                  // co blocks (16 co) per wave
+  constexpr int DYI = 8 / NW;                  // dy-image glds per wave per stage
+  constexpr int PTI = kPatchPix / (NW * 8);    // patch glds per wave per stage
+  constexpr int LOADS = DYI + PTI;
+  constexpr int LOOK = NW == 8 ? 6 : 5;
+  static_assert(PTI * NW * 8 == kPatchPix && DYI * NW == 8, "staging split");
   // one __shared__ array per stage, indexed statically (the k-loop is unrolled by kStages): the
   // compiler can then prove that the LDS-DMA into stage s+2 does not alias the ds_reads of stage
   // s and keeps the counted vmcnt (one runtime-indexed array makes it wait vmcnt(0) before the
@@ -132,7 +141,7 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad3x3_kernel(
   __shared__ __attribute__((aligned(16))) char smem2[kStage];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (col.rep != nullptr && blockIdx.x == 0 && blockIdx.y == 0) gk::bn_collect_block<kThreads>(col);
+  if (col.rep != nullptr && blockIdx.x == 0 && blockIdx.y == 0) gk::bn_collect_block<64 * NW>(col);
   const int tilesC = g.Ci / TC;
   const int tile = blockIdx.x;
   const int co0 = (tile / tilesC) * TM, ci0 = (tile % tilesC) * TC;
@@ -140,27 +149,26 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad3x3_kernel(
   const int s1 = min(g.steps, s0 + g.per);
   const int W = g.W, H = g.H, PW = g.PW, RW = g.R * g.W;
   const __bf16* zero = reinterpret_cast<const __bf16*>(gk::g_conv_zero);
+  const int wci = wave & 3;                       // this wave's 16-ci quarter
+  const int wco = NW == 8 ? (wave >> 2) * 32 : 0;  // this wave's first co
 
-  // ---- staging: dy image MC [64 slots][64 co] (2 glds per wave: slot = (wave*2+i)*8 + lane/8);
-  // x patch [pix][64 ci] with the same chunk swizzle, 8 px per wave-instruction.  Per-lane
-  // geometry is recomputed per stage (a FastDiv by the patch width) to keep registers for the
-  // 36 accumulator tiles.
-  // Staging offsets: a lane's patch pixel (row r_i, col c_i) per glds is loop-invariant, only the
-  // image / row-group base moves, so the element offsets are precomputed (32-bit: the host checks
-  // numel < 2^31) and each k-step adds one base and selects the zero page for halo / out-of-image
-  // rows — a few VALU ops per glds instead of a division and a 64-bit multiply.
-  int dy_rel[2], dy_slot[2];
+  // ---- staging: dy image MC [64 slots][64 co] (8 px per wave-instruction); x patch [pix][64 ci]
+  // with the same chunk swizzle.  A lane's pixel per glds is loop-invariant, only the image /
+  // row-group base moves, so the element offsets are precomputed (32-bit: the host checks
+  // numel < 2^31) and each k-step adds one base and selects the zero page for halo /
+  // out-of-image rows — a few VALU ops per glds instead of a division and a 64-bit multiply.
+  int dy_rel[DYI], dy_slot[DYI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    dy_slot[i] = (wave * 2 + i) * 8 + (lane >> 3);
+  for (int i = 0; i < DYI; ++i) {
+    dy_slot[i] = (wave * DYI + i) * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ (int)mc_swz<64>((uint32_t)dy_slot[i]);
     dy_rel[i] = dy_slot[i] * g.Co + co0 + ch * 8;
   }
-  int pt_rel[kPatchInstr], pt_r[kPatchInstr];
+  int pt_rel[PTI], pt_r[PTI];
   uint32_t wi_ok = 0;
 #pragma unroll
-  for (int i = 0; i < kPatchInstr; ++i) {
-    const int p = (wave * kPatchInstr + i) * 8 + (lane >> 3);
+  for (int i = 0; i < PTI; ++i) {
+    const int p = (wave * PTI + i) * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ (int)mc_swz<64>((uint32_t)p);
     const int r = p / PW;
     const int wi = p - r * PW - 1;
@@ -175,60 +183,52 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad3x3_kernel(
     const int P = rows * W;
     const int dy0 = (n * H + ho0) * W * g.Co;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < DYI; ++i) {
       const void* src = dy_slot[i] < P ? (const void*)(dy + dy0 + dy_rel[i]) : (const void*)zero;
-      glds16(src, buf + (wave * 2 + i) * 1024);
+      glds16(src, buf + (wave * DYI + i) * 1024);
     }
     char* pb = buf + kDyBytes;
     const int x0 = (n * H + ho0 - 1) * W * g.Ci;  // patch row 0 = image row ho0 - 1
     const int rlo = ho0 == 0 ? 1 : 0;                // patch rows that exist in the image
     const int rhi = min(rows + 2, H - ho0 + 1);
 #pragma unroll
-    for (int i = 0; i < kPatchInstr; ++i) {
+    for (int i = 0; i < PTI; ++i) {
       const bool ok = ((wi_ok >> i) & 1u) & (pt_r[i] >= rlo) & (pt_r[i] < rhi);
       const void* src = ok ? (const void*)(x + x0 + pt_rel[i]) : (const void*)zero;
-      glds16(src, pb + (wave * kPatchInstr + i) * 1024);
+      glds16(src, pb + (wave * PTI + i) * 1024);
     }
   };
 
   // ---- fragment geometry: slots this lane's transposed reads start at (k0 and k0 + 4)
   const int grp16 = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
-  int pp[2][2];  // [ks][half] patch pixel for tap (0,0)
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const int k0 = ks * 32 + 8 * grp16 + q;
-    pp[ks][0] = slot_pix(k0, W, RW, PW);
-    pp[ks][1] = slot_pix(k0 + 4, W, RW, PW);
-  }
-  const int bchunk = (wave * 16) / 8 + (pq >> 1);  // this wave's ci block: 16 cols = 2 chunks
+  const int bchunk = wci * 2 + (pq >> 1);  // this wave's ci block: 16 cols = 2 chunks
   const int bhalf = pq & 1;
   // LDS byte offsets (from a stage's base) of every transposed read of a k-step: A (dy image,
   // the MC loader's lane map) per [ks][co block][half], B (patch) per [unit][half]
-  uint32_t aoff[2][4][2], boff[18][2];
+  uint32_t aoff[2][CB][2], boff[18][2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
+    const int k0 = ks * 32 + 8 * grp16 + q;
+    const int pp0 = slot_pix(k0, W, RW, PW), pp1 = slot_pix(k0 + 4, W, RW, PW);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t c = (uint32_t)(i * 2 + (pq >> 1));
-      const uint32_t k0 = (uint32_t)(ks * 32 + 8 * grp16 + q);
-      aoff[ks][i][0] = mc_off<64>(k0, c) + 8 * bhalf;
-      aoff[ks][i][1] = mc_off<64>(k0 + 4, c) + 8 * bhalf;
+    for (int i = 0; i < CB; ++i) {
+      const uint32_t c = (uint32_t)((wco >> 3) + i * 2 + (pq >> 1));
+      aoff[ks][i][0] = mc_off<64>((uint32_t)k0, c) + 8 * bhalf;
+      aoff[ks][i][1] = mc_off<64>((uint32_t)k0 + 4, c) + 8 * bhalf;
     }
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int toff = (t / 3) * PW + (t % 3);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        boff[ks * 9 + t][h] = kDyBytes + mc_off<64>((uint32_t)(pp[ks][h] + toff), (uint32_t)bchunk) +
-                              8 * bhalf;
+      boff[ks * 9 + t][0] = kDyBytes + mc_off<64>((uint32_t)(pp0 + toff), (uint32_t)bchunk) + 8 * bhalf;
+      boff[ks * 9 + t][1] = kDyBytes + mc_off<64>((uint32_t)(pp1 + toff), (uint32_t)bchunk) + 8 * bhalf;
     }
   }
 
-  f32x4 acc[9][4];
+  f32x4 acc[9][CB];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < CB; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // one k-step reading stage buffer `cur` (while step+2 is staged into `nxt`)
   auto kstep = [&](const char* cur, char* nxt, int step) {
@@ -236,30 +236,28 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad3x3_kernel(
     // drain vmcnt(0) before the next ds_read): the stage two k-steps ahead is always issued,
     // past the end it re-stages the last k-step into a buffer nobody reads again, so exactly one
     // younger stage is in flight at every wait.
-    wait_vmcnt<kLoads>();  // this wave's loads of `step` landed
+    wait_vmcnt<LOADS>();  // this wave's loads of `step` landed
     // every wave's loads of `step` landed, and every wave finished reading step-1's buffer
     __builtin_amdgcn_s_waitcnt((7 << 4) | (0 << 8) | 15 | (3 << 14));  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
     stage(nxt, min(step + 2, s1 - 1));
     const uint32_t base = lds_u32(cur);
-    Frags f;
-    auto issueA = [&](int ks) {
+    Frags<CB> f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < CB; ++i) {
         f.a_lo[ks][i] = tr_read(base + aoff[ks][i][0]);
         f.a_hi[ks][i] = tr_read(base + aoff[ks][i][1]);
       }
-    };
     auto issueB = [&](int u) {
       f.b_lo[u] = tr_read(base + boff[u][0]);
       f.b_hi[u] = tr_read(base + boff[u][1]);
     };
-    issueA(0);
-    issueA(1);
 #pragma unroll
-    for (int u = 0; u < kLook; ++u) issueB(u);
+    for (int u = 0; u < LOOK; ++u) issueB(u);
     __builtin_amdgcn_s_setprio(1);
-    units(f, acc, issueA, issueB, std::make_integer_sequence<int, 18>{});
+    units<LOOK>(f, acc, issueB, std::make_integer_sequence<int, 18>{});
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -275,12 +273,12 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad3x3_kernel(
   }
   // ---- partial tile -> workspace slice blockIdx.y: lane holds C[co][ci..ci+3] per (tap, i)
   float* out = ws + (long)blockIdx.y * g.ws_stride;
-  const int ci = ci0 + wave * 16 + 4 * (lane >> 4);
+  const int ci = ci0 + wci * 16 + 4 * (lane >> 4);
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = co0 + i * 16 + (lane & 15);
+    for (int i = 0; i < CB; ++i) {
+      const int co = co0 + wco + i * 16 + (lane & 15);
       *reinterpret_cast<float4*>(out + ((long)co * 9 + t) * g.Ci + ci) =
           make_float4(acc[t][i][0], acc[t][i][1], acc[t][i][2], acc[t][i][3]);
     }
@@ -291,6 +289,11 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad3x3_kernel(
 bool g_wgrad3x3 = [] {
   const char* v = getenv("MIPIPE_WGRAD3");
   return v == nullptr || atoi(v) != 0;
+}();
+
+int g_wgrad3x3_waves = [] {
+  const char* v = getenv("MIPIPE_WGRAD3_WAVES");
+  return v != nullptr && atoi(v) == 4 ? 4 : 8;
 }();
 
 bool conv_wgrad3x3_supported(const ConvShape& s) {
@@ -328,8 +331,12 @@ void conv_wgrad3x3(const void* dy, const void* x, float* dw, const ConvShape& s,
   const int tiles = (s.Co / w3::TM) * (s.Ci / w3::TC);
   BnCollect c{};
   if (col != nullptr) c = *col;
-  hipLaunchKernelGGL(w3::wgrad3x3_kernel, dim3(tiles, S), dim3(w3::kThreads), 0, st,
-                     (const __bf16*)dy, (const __bf16*)x, ws, g, c);
+  if (g_wgrad3x3_waves == 4)
+    hipLaunchKernelGGL(w3::wgrad3x3_kernel<4>, dim3(tiles, S), dim3(256), 0, st,
+                       (const __bf16*)dy, (const __bf16*)x, ws, g, c);
+  else
+    hipLaunchKernelGGL(w3::wgrad3x3_kernel<8>, dim3(tiles, S), dim3(512), 0, st,
+                       (const __bf16*)dy, (const __bf16*)x, ws, g, c);
   splitk_sum(ws, S, g.ws_stride, dw, st);
 }
 

@@ -177,6 +177,31 @@ class DistributedDataParallel(tnn.Module):
         for flat in self._flat_bufs:
             self._broadcast(flat)
 
+    def _broadcast_buffers_async(self) -> None:
+        """C4 off the critical path: the per-forward buffer broadcast (BN running stats, ~38 KB
+        for ResNet-18) is issued asynchronously and the compute stream waits on it only right
+        before the first module that owns buffers runs (a one-shot forward pre-hook) — the
+        training forward does not read running stats, so the latency-bound collective overlaps
+        the stem instead of stalling the step's first kernel."""
+        if getattr(self, "_flat_bufs", None) is None:
+            self._flatten_buffers()
+            self._buffer_owners = [m for m in self.module.modules()
+                                   if any(b is not None for b in m._buffers.values())]
+            for m in self._buffer_owners:
+                m.register_forward_pre_hook(self._wait_buffer_sync)
+        works = []
+        for flat in self._flat_bufs:
+            self._clog.record("broadcast", flat)
+            works.append(dist.broadcast(flat, 0, group=self.process_group, async_op=True))
+        self._pending_buffer_work = works
+
+    def _wait_buffer_sync(self, module, args) -> None:
+        works = getattr(self, "_pending_buffer_work", None)
+        if works:
+            self._pending_buffer_work = None
+            for w in works:
+                w.wait()  # stream semantics on RCCL: the compute stream waits, the host does not
+
     def _build_buckets(self, cap_bytes: float, first_bytes: float,
                        last_bytes: float = 0.0) -> List[Bucket]:
         """Contiguous flat-gradient slices in gradient-ready order: a small FIRST bucket (the
@@ -229,13 +254,15 @@ class DistributedDataParallel(tnn.Module):
     def forward(self, *args, **kwargs):
         if self._comm and torch.is_grad_enabled() and self.broadcast_buffers \
                 and self.require_forward_param_sync:
-            self._broadcast_buffers_now()
+            self._broadcast_buffers_async()
         if torch.is_grad_enabled() and self.module.training:
             self._prepare_backward()
             self.require_forward_param_sync = True
         else:
             self.require_forward_param_sync = False
-        return self.module(*args, **kwargs)
+        out = self.module(*args, **kwargs)
+        self._wait_buffer_sync(None, None)  # a module without buffer owners: settle it here
+        return out
 
     @contextlib.contextmanager
     def no_sync(self):
