@@ -726,6 +726,130 @@ std::tuple<Tensor, Tensor, Tensor> pool_bn_bwd(Tensor dp, Tensor idx, Tensor pou
   return {dy, sg, sgx};
 }
 
+// ---- recompute-fused ResNet stem (stem.hip): packed input xp [N][Hp][115][8] bf16, packed
+// weights [64][7][4][8] bf16; the 7x7/2 conv output is never stored.
+struct StemGeo {
+  int N, Ho, Hp;
+};
+static bool stem_geo_ok(const Tensor& xp, const Tensor& w, StemGeo* g) {
+  if (xp.dim() != 4 || xp.size(3) != 8 || w.dim() != 4 || w.size(0) != 64 || w.size(1) != 7 ||
+      w.size(2) != 4 || w.size(3) != 8)
+    return false;
+  const int N = (int)xp.size(0), Hp = (int)xp.size(1), Wsp = (int)xp.size(2);
+  const int Ho = (Hp - 7) / 2 + 1, Wo = Wsp - 3;
+  if (g != nullptr) *g = StemGeo{N, Ho, Hp};
+  return (Hp - 7) % 2 == 0 && mipipe::stem_fused_supported(N, Ho, Wo, Hp, Wsp, 64, Ho / 2, Wo / 2);
+}
+static StemGeo stem_check(const Tensor& xp, const Tensor& w) {
+  check_bf16(xp, "xp");
+  check_bf16(w, "w");
+  StemGeo g;
+  TORCH_CHECK(stem_geo_ok(xp, w, &g), "fused stem: needs xp [N][2*Ho+5][115][8] (112 output "
+              "columns, Ho % 4 == 0) and w [64][7][4][8]");
+  return g;
+}
+
+bool stem_fused_supported(Tensor xp, Tensor w) {
+  return xp.is_cuda() && xp.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+         stem_geo_ok(xp, w, nullptr);
+}
+
+// Σ(y-shift), Σ(y-shift)² into the zeroed fwd replica slabs [R][64] (re-zeroed by bn_finalize).
+std::tuple<Tensor, Tensor> stem_fwd_stats(Tensor xp, Tensor w, Tensor shift, Tensor slab_sum,
+                                          Tensor slab_sq) {
+  const StemGeo g = stem_check(xp, w);
+  c10::DeviceGuard dg(xp.device());
+  check_vec(shift, 64, "shift");
+  const int R = mipipe::kStatReplicas;
+  check_f32(slab_sum, "slab_sum");
+  check_f32(slab_sq, "slab_sq");
+  TORCH_CHECK(slab_sum.numel() == R * 64 && slab_sq.numel() == R * 64, "stat slabs must be [R, 64]");
+  float *s0 = slab_sum.data_ptr<float>(), *s1 = slab_sq.data_ptr<float>();
+  if (mipipe::g_deterministic) {
+    const int G = mipipe::stem_stats_blocks(g.N, g.Ho);
+    auto part = torch::empty({2, G, 64}, xp.options().dtype(at::kFloat));
+    float* p0 = part.data_ptr<float>();
+    mipipe::stem_fwd_stats(xp.data_ptr(), w.data_ptr(), g.N, g.Ho, g.Hp, shift.data_ptr<float>(), p0,
+                           p0 + (long)G * 64, R, G, stream());
+    mipipe::det_sum_rows(p0, p0 + (long)G * 64, G, 64, s0, s1, false, stream());
+  } else {
+    mipipe::stem_fwd_stats(xp.data_ptr(), w.data_ptr(), g.N, g.Ho, g.Hp, shift.data_ptr<float>(), s0,
+                           s1, R, 0, stream());
+  }
+  return {slab_sum, slab_sq};
+}
+
+// (maxpool_3x3/2/1(relu(bn(conv(xp)))), window tap (0xFF where the output is not > 0), y)
+std::tuple<Tensor, Tensor, optional<Tensor>> stem_fwd_pool(Tensor xp, Tensor w, Tensor scale,
+                                                           Tensor bias, bool want_y) {
+  const StemGeo g = stem_check(xp, w);
+  c10::DeviceGuard dg(xp.device());
+  check_vec(scale, 64, "scale");
+  check_vec(bias, 64, "bias");
+  auto out = torch::empty({g.N, g.Ho / 2, 56, 64}, xp.options());
+  auto idx = torch::empty({g.N, g.Ho / 2, 56, 64}, xp.options().dtype(at::kByte));
+  optional<Tensor> y;
+  if (want_y) y = torch::empty({g.N, g.Ho, 112, 64}, xp.options());
+  mipipe::stem_fwd_pool(xp.data_ptr(), w.data_ptr(), g.N, g.Ho, g.Hp, scale.data_ptr<float>(),
+                        bias.data_ptr<float>(), out.data_ptr(), idx.data_ptr<uint8_t>(),
+                        want_y ? y->data_ptr() : nullptr, stream());
+  return {out, idx, y};
+}
+
+// Backward of the fused stem: Σg, Σg·x̂ (bwd slab `rep` [3][R][64], re-zeroed; + dγ / dβ
+// accumulators) -> packed dW [64][7][4][8] fp32 with the BN-apply folded into the weight-grad.
+// Returns (dW, Σg, Σg·x̂).
+std::tuple<Tensor, Tensor, Tensor> stem_bwd(Tensor xp, Tensor y, Tensor dp, Tensor idx, Tensor pout,
+                                            Tensor mean, Tensor invstd, Tensor gamma, Tensor rep,
+                                            int64_t count, optional<Tensor> dgamma,
+                                            optional<Tensor> dbeta) {
+  check_bf16(xp, "xp");
+  c10::DeviceGuard dg(xp.device());
+  const int N = (int)xp.size(0), Hp = (int)xp.size(1), Ho = (Hp - 7) / 2 + 1;
+  TORCH_CHECK(xp.dim() == 4 && xp.size(2) == 115 && xp.size(3) == 8 && (Hp - 7) % 2 == 0 &&
+                  mipipe::stem_fused_supported(N, Ho, 112, Hp, 115, 64, Ho / 2, 56),
+              "stem_bwd: xp must be the packed 224-px stem input");
+  check_bf16(y, "y");
+  check_bf16(dp, "dp");
+  check_bf16(pout, "pout");
+  check_cuda(idx, "idx");
+  const std::vector<int64_t> ps = {N, Ho / 2, 56, 64}, ys = {N, Ho, 112, 64};
+  TORCH_CHECK(dp.sizes() == ps && idx.sizes() == ps && pout.sizes() == ps && y.sizes() == ys &&
+                  idx.scalar_type() == at::kByte, "stem_bwd: shape mismatch");
+  for (const Tensor* t : {&mean, &invstd, &gamma}) check_vec(*t, 64, "BN vector");
+  check_f32(rep, "rep");
+  const int R = mipipe::kStatReplicas;
+  TORCH_CHECK(rep.numel() == 3ll * R * 64, "rep must be [3,R,64]");
+  TORCH_CHECK(dgamma.has_value() == dbeta.has_value(), "pass both accumulators or none");
+  float* r = rep.data_ptr<float>();
+  const long pixels = (long)N * Ho * 112;
+  if (mipipe::g_deterministic) {
+    const int G = mipipe::pool_bn_bwd_reduce_blocks(pixels, 64);
+    auto part = torch::empty({2, G, 64}, dp.options().dtype(at::kFloat));
+    float* p0 = part.data_ptr<float>();
+    mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), pout.data_ptr(), y.data_ptr(),
+                               mean.data_ptr<float>(), invstd.data_ptr<float>(), N, Ho, 112, 64,
+                               Ho / 2, 56, 3, 2, 1, p0, G, stream(), false);
+    mipipe::det_sum_rows(p0, p0 + (long)G * 64, G, 64, r, r + (long)R * 64, false, stream());
+  } else {
+    mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), pout.data_ptr(), y.data_ptr(),
+                               mean.data_ptr<float>(), invstd.data_ptr<float>(), N, Ho, 112, 64,
+                               Ho / 2, 56, 3, 2, 1, r, 0, stream(), false);
+  }
+  auto o = rep.options();
+  auto sg = torch::empty({64}, o), sgx = torch::empty({64}, o);
+  mipipe::bn_bwd_collect(r, 64, sg.data_ptr<float>(), sgx.data_ptr<float>(), fptr(dgamma, 64),
+                         fptr(dbeta, 64), stream());
+  const int G2 = mipipe::stem_wgrad_blocks(N, Ho);
+  auto ws = torch::empty({(int64_t)G2 * 64 * 224}, o);
+  auto dw = torch::zeros({64, 7, 4, 8}, o);
+  mipipe::stem_bwd_wgrad(xp.data_ptr(), y.data_ptr(), N, Ho, Hp, dp.data_ptr(),
+                         idx.data_ptr<uint8_t>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                         gamma.data_ptr<float>(), sg.data_ptr<float>(), sgx.data_ptr<float>(), count,
+                         ws.data_ptr<float>(), dw.data_ptr<float>(), stream());
+  return {dw, sg, sgx};
+}
+
 Tensor maxpool_bwd(Tensor dy, Tensor idx, std::vector<int64_t> xs, int k, int s, int p) {
   check_act(dy, "dy");
   check_cuda(idx, "idx");
@@ -1469,6 +1593,13 @@ PYBIND11_MODULE(_C, m) {
         py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("rep"), py::arg("count"),
         py::arg("k"), py::arg("s"), py::arg("p"), py::arg("dgamma") = py::none(),
         py::arg("dbeta") = py::none());
+  m.def("stem_fused_supported", &stem_fused_supported);
+  m.def("stem_fwd_stats", &stem_fwd_stats);
+  m.def("stem_fwd_pool", &stem_fwd_pool, py::arg("xp"), py::arg("w"), py::arg("scale"),
+        py::arg("bias"), py::arg("want_y") = true);
+  m.def("stem_bwd", &stem_bwd, py::arg("xp"), py::arg("y"), py::arg("dp"), py::arg("idx"),
+        py::arg("pout"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("rep"),
+        py::arg("count"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("trans_a"), py::arg("trans_b"),

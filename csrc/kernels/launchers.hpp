@@ -245,6 +245,26 @@ void stem_pack(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int 
                int Hp, int Wsp, hipStream_t st, bool y_f32 = false);
 void synthetic_batch(const int64_t* idx, int n, int C, int H, int W, int classes, int seed,
                      void* x, bool bf16_out, int64_t* labels, hipStream_t st);
+// Fused ResNet stem on the packed input (stem.hip): conv 7x7/2 (packed K = 224, 64 channels,
+// 112 output columns) -> BN -> ReLU -> max-pool 3x3/2/1.
+//   stem_fwd_stats : shifted Σ, Σ² of bf16(y) per channel (conv recomputed, y not stored) ->
+//                    replica rows (atomics) or, with det_rows = stem_stats_blocks(), one partial
+//                    row per block (plain stores)
+//   stem_fwd_pool  : y (bf16, for the backward), out = maxpool(bf16(relu(y*scale + bias))),
+//                    idx = window tap (0xFF where out is not > 0)
+//   stem_bwd_wgrad : dW[64][224] += Σ dy ⊗ x with dy = A·g + B·y + C formed in LDS (g routed from
+//                    dp / idx; Σg, Σg·x̂ from pool_bn_bwd_reduce); ws: [stem_wgrad_blocks][64*224]
+bool stem_fused_supported(int N, int Ho, int Wo, int Hp, int Wsp, int Co, int Hpool, int Wpool);
+int stem_stats_blocks(int N, int Ho);
+int stem_wgrad_blocks(int N, int Ho);
+void stem_fwd_stats(const void* xp, const void* w, int N, int Ho, int Hp, const float* shift,
+                    float* ssum, float* ssq, int R, int det_rows, hipStream_t st);
+void stem_fwd_pool(const void* xp, const void* w, int N, int Ho, int Hp, const float* scale,
+                   const float* bias, void* out, uint8_t* idx, void* y, hipStream_t st);
+void stem_bwd_wgrad(const void* xp, const void* y, int N, int Ho, int Hp, const void* dp,
+                    const uint8_t* idx, const float* mean, const float* invstd, const float* gamma,
+                    const float* sum_g, const float* sum_gx, long count, float* ws, float* dw,
+                    hipStream_t st);
 
 // ---- transformer ops ------------------------------------------------------------------------
 void layernorm_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y,

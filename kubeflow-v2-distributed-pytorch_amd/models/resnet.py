@@ -129,9 +129,7 @@ class _StemConv(mnn.Conv2d):
         # super-tap j holds kw = 2j + p at channels p*4 + c
         return wp.reshape(Co, k, kw2, 8).to(dtype).contiguous()
 
-    def forward(self, x, stats_shift=None, slabs=None, prev=None, res_take=None, res_give=None):
-        """x: packed super-pixels from :meth:`pack_input`."""
-        w_c = self.compute_weight(x.dtype)
+    def _ensure_wgrad_map(self):
         if getattr(self.weight, "_mipipe_wgrad_map", None) is None:
             k, C = self.kernel_size[0], self.in_channels
 
@@ -140,9 +138,27 @@ class _StemConv(mnn.Conv2d):
                 d = dw.reshape(Co, k, -1, 4)[:, :, :k, :C]
                 return d.permute(0, 3, 1, 2).contiguous()
             self.weight._mipipe_wgrad_map = unpack
+
+    def forward(self, x, stats_shift=None, slabs=None, prev=None, res_take=None, res_give=None):
+        """x: packed super-pixels from :meth:`pack_input`."""
+        w_c = self.compute_weight(x.dtype)
+        self._ensure_wgrad_map()
         y, ps, pss = MF.conv2d(x, self.weight, w_c, (self.stride[0], 1), 0, stats_shift, slabs,
                                prev, res_take, res_give)
         return y if stats_shift is None else (y, ps, pss)
+
+    def fused_bn_relu_maxpool(self, xp, bn, k: int, s: int, p: int):
+        """maxpool(relu(bn(conv(xp)))) on the recompute-fused stem kernels (stem.hip), or None
+        when they do not apply (other geometry / dtype / pool, eval with autograd on)."""
+        if (k, s, p) != (3, 2, 1) or self.bias is not None or self.kernel_size[0] != 7:
+            return None
+        if not bn.training and torch.is_grad_enabled():
+            return None
+        w_c = self.compute_weight(xp.dtype)
+        if not MF.stem_fused_ok(xp, w_c, bn):
+            return None
+        self._ensure_wgrad_map()
+        return MF.stem_conv_bn_relu_maxpool(xp, self.weight, w_c, bn)
 
 
 class _PaddedStemConv(mnn.Conv2d):

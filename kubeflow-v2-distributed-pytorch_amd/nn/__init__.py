@@ -249,6 +249,11 @@ def conv_bn_relu_maxpool(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d,
     kernel (the normalised activation is never stored) and a gather-based fused backward."""
     if pool.ceil_mode or pool.dilation not in (1, (1, 1)):
         return pool(conv_bn_act(x, conv, bn, relu=True))
+    fused = getattr(conv, "fused_bn_relu_maxpool", None)
+    if fused is not None:  # packed stem: recompute-fused kernels, conv output never stored
+        out = fused(x, bn, *pool.geometry())
+        if out is not None:
+            return out
     use_batch = bn.training
     if use_batch:
         ws = MF.bn_workspace(bn, "fwd", x.device)

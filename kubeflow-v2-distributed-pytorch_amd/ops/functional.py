@@ -707,6 +707,76 @@ def bn_relu_maxpool(y: Tensor, st: BNStats, bn, k: int, stride: int, pad: int) -
     return max_pool2d(batchnorm_act(y, st, bn, relu=True), k, stride, pad)
 
 
+_STEM_FUSED = os.environ.get("MIPIPE_STEM_FUSED", "1") != "0"
+
+
+def set_stem_fused(on: bool) -> None:
+    """Route the packed ResNet stem to the recompute-fused kernels (default on)."""
+    global _STEM_FUSED
+    _STEM_FUSED = bool(on)
+
+
+def stem_fused_ok(xp: Tensor, w_c: Tensor, bn) -> bool:
+    """The recompute-fused stem applies: bf16 packed input that needs no gradient, the 224 px
+    geometry (112 output columns), a BatchNorm with affine parameters and running statistics."""
+    return (_STEM_FUSED and K.use_native(xp) and xp.dtype == torch.bfloat16
+            and not xp.requires_grad and bn.affine and bn.running_mean is not None
+            and bn.weight.dtype == torch.float32 and K.stem_fused_supported(xp, w_c))
+
+
+class _StemFusedFn(Function):
+    """maxpool_3x3/2/1(relu(bn(conv7x7/2(x)))) for the packed stem (stem.hip).  Forward: a
+    statistics pass that recomputes the conv instead of storing y, then one pass that computes
+    the conv again and writes y, the pooled output and argmax (BN-apply + ReLU + pool in
+    registers / LDS).  Backward: the BN reduction over (y, dp, argmax) (pool.hip), then ONE pass
+    that routes the pooled gradient, forms dy = A·g + B·y + C in LDS and accumulates the weight
+    gradient from it — dy never reaches HBM.  Numerics follow the unfused conv -> pool_bn path."""
+
+    @staticmethod
+    def forward(ctx, xp, weight, w_c, gamma, beta, bn):
+        ws = bn_workspace(bn, "fwd", xp.device)
+        ps, pss = K.stem_fwd_stats(xp, w_c, bn.running_mean, ws[0], ws[1])
+        count = xp.shape[0] * ((xp.shape[1] - 7) // 2 + 1) * (xp.shape[2] - 3)
+        st = bn_stats_from_partials(ps, pss, count, bn, True)
+        out, idx, y = K.stem_fwd_pool(xp, w_c, st.scale, st.bias)
+        ctx.save_for_backward(xp, y, out, idx, gamma)
+        ctx.st, ctx.bn, ctx.weight, ctx.beta = st, bn, weight, beta
+        return out
+
+    @staticmethod
+    def backward(ctx, dp):
+        xp, y, out, idx, gamma = ctx.saved_tensors
+        st, bn = ctx.st, ctx.bn
+        rep = bn_workspace(bn, "bwd", dp.device)
+        direct = None
+        if ctx.needs_input_grad[3] and ctx.needs_input_grad[4]:
+            tg, tb = _direct_grad_target(gamma), _direct_grad_target(ctx.beta)
+            if tg is not None and tb is not None:
+                direct = (tg[1], tb[1])
+        dwp, sg, sgx = K.stem_bwd(xp, y, dp.contiguous(), idx, out, st.mean, st.invstd,
+                                  gamma.detach(), rep, st.count, acc=direct)
+        _ws_done(bn, "bwd")
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = ctx.weight._mipipe_wgrad_map(dwp).to(ctx.weight.dtype)
+        if direct is not None:
+            fs = _direct_grad_target(gamma)[0]
+            fs.grad_ready(gamma)
+            fs.grad_ready(ctx.beta)
+            return None, dw, None, None, None, None
+        return (None, dw, None, sgx.to(gamma.dtype) if ctx.needs_input_grad[3] else None,
+                sg.to(gamma.dtype) if ctx.needs_input_grad[4] else None, None)
+
+
+def stem_conv_bn_relu_maxpool(xp: Tensor, weight: Tensor, w_c: Tensor, bn) -> Tensor:
+    """Fused stem on packed input ``xp`` (see :func:`stem_fused_ok`).  Training: batch statistics
+    (recompute-fused forward and backward); eval: running statistics, one BN + ReLU + pool pass."""
+    if bn.training:
+        return _StemFusedFn.apply(xp, weight, w_c, bn.weight, bn.bias, bn)
+    st = bn_stats_from_partials(None, None, 0, bn, False)
+    return K.stem_fwd_pool(xp, w_c, st.scale, st.bias, want_y=False)[0]
+
+
 def max_pool2d(x: Tensor, k: int, stride: int, pad: int, ceil_mode: bool = False) -> Tensor:
     return _MaxPoolFn.apply(x, k, stride, pad, bool(ceil_mode))
 

@@ -17,7 +17,8 @@ from ._native import native, native_available
 
 __all__ = ["conv_fwd", "conv_dgrad", "conv_wgrad", "bn_finalize", "bn_act_fwd",
            "bn_act_bwd_reduce", "bn_act_bwd_apply", "maxpool_fwd", "maxpool_bwd",
-           "avgpool_fwd", "avgpool_bwd", "pool_bn_fwd", "pool_bn_bwd", "pool_bn_supported", "gemm", "cross_entropy_fwd_bwd", "top1_correct", "sgd_step",
+           "avgpool_fwd", "avgpool_bwd", "pool_bn_fwd", "pool_bn_bwd", "pool_bn_supported", "stem_fused_supported", "stem_fwd_stats",
+           "stem_fwd_pool", "stem_bwd", "gemm", "cross_entropy_fwd_bwd", "top1_correct", "sgd_step",
            "adamw_step", "layernorm_fwd", "layernorm_bwd", "attention_fwd", "attention_bwd", "dropout_fwd", "colsum", "bn_bwd_collect", "stem_pack",
            "embedding_bwd", "gelu_fwd", "gelu_bwd", "nchw_to_nhwc", "use_native",
            "gconv_fwd", "gconv_dgrad", "gconv_wgrad", "chan_stats", "affine_act",
@@ -203,6 +204,32 @@ def pool_bn_bwd(dp, idx, pout, y, mean, invstd, gamma, rep, count, k, stride, pa
     a = acc if acc is not None else (None, None)
     return native().pool_bn_bwd(dp, idx, pout, y, mean, invstd, gamma, rep, count, k, stride, pad,
                                 *a)
+
+
+def stem_fused_supported(xp, w) -> bool:
+    """The recompute-fused stem kernels (stem.hip) take this packed input / weight."""
+    return use_native(xp) and bool(native().stem_fused_supported(xp, w))
+
+
+def stem_fwd_stats(xp, w, shift, slab_sum, slab_sq):
+    """Shifted Σ, Σ² of the packed stem conv's bf16 output into zeroed replica slabs [R, 64]
+    (native; the conv output is recomputed, not stored)."""
+    return native().stem_fwd_stats(xp, w, shift, slab_sum, slab_sq)
+
+
+def stem_fwd_pool(xp, w, scale, bias, want_y=True):
+    """(maxpool_3x3/2/1(relu(conv(xp)*scale + bias)), window tap, conv output y or None)
+    (native); the tap is 0xFF where the output is not > 0."""
+    return native().stem_fwd_pool(xp, w, scale.contiguous(), bias.contiguous(), bool(want_y))
+
+
+def stem_bwd(xp, y, dp, idx, pout, mean, invstd, gamma, rep, count, acc=None):
+    """Backward of the fused stem: (packed dW [64,7,4,8] fp32, Σg, Σg·x̂) — the BN reduction over
+    (y, dp, argmax), then the BN-apply folded into the weight-grad; ``acc`` = (dγ, dβ)
+    accumulators or None; ``rep``: zeroed bwd replica slab (native)."""
+    a = acc if acc is not None else (None, None)
+    return native().stem_bwd(xp, y, dp, idx, pout, mean, invstd, gamma.float().contiguous(), rep,
+                             int(count), *a)
 
 
 def pool_bn_supported(y) -> bool:
