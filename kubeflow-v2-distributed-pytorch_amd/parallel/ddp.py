@@ -178,24 +178,22 @@ class DistributedDataParallel(tnn.Module):
             self._broadcast(flat)
 
     def _broadcast_buffers_async(self) -> None:
-        """C4 off the critical path: the per-forward buffer broadcast (BN running stats, ~38 KB
-        for ResNet-18) is issued asynchronously and the compute stream waits on it only right
-        before the first module that owns buffers runs (a one-shot forward pre-hook) — the
-        training forward does not read running stats, so the latency-bound collective overlaps
-        the stem instead of stalling the step's first kernel."""
+        """C4: the per-forward buffer broadcast (BN running stats, ~38 KB for ResNet-18) as one
+        collective per dtype on the comm stream; :meth:`_wait_buffer_sync` makes the compute
+        stream wait for it (the host does not block on RCCL).  The wait comes before the module
+        runs: the fused conv -> BN paths read ``running_mean`` (the statistics shift) and update
+        the running statistics in place without calling the BatchNorm module, so no per-module
+        hook can place the wait later without racing the broadcast (measured: a hook on the
+        buffer owners left the 4-rank gloo run nondeterministic)."""
         if getattr(self, "_flat_bufs", None) is None:
             self._flatten_buffers()
-            self._buffer_owners = [m for m in self.module.modules()
-                                   if any(b is not None for b in m._buffers.values())]
-            for m in self._buffer_owners:
-                m.register_forward_pre_hook(self._wait_buffer_sync)
         works = []
         for flat in self._flat_bufs:
             self._clog.record("broadcast", flat)
             works.append(dist.broadcast(flat, 0, group=self.process_group, async_op=True))
         self._pending_buffer_work = works
 
-    def _wait_buffer_sync(self, module, args) -> None:
+    def _wait_buffer_sync(self, module=None, args=None) -> None:
         works = getattr(self, "_pending_buffer_work", None)
         if works:
             self._pending_buffer_work = None
@@ -255,14 +253,13 @@ class DistributedDataParallel(tnn.Module):
         if self._comm and torch.is_grad_enabled() and self.broadcast_buffers \
                 and self.require_forward_param_sync:
             self._broadcast_buffers_async()
+            self._wait_buffer_sync()
         if torch.is_grad_enabled() and self.module.training:
             self._prepare_backward()
             self.require_forward_param_sync = True
         else:
             self.require_forward_param_sync = False
-        out = self.module(*args, **kwargs)
-        self._wait_buffer_sync(None, None)  # a module without buffer owners: settle it here
-        return out
+        return self.module(*args, **kwargs)
 
     @contextlib.contextmanager
     def no_sync(self):

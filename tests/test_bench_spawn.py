@@ -18,7 +18,7 @@ def _env(**kw):
     e = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         e.pop(k, None)
-    e["OMP_NUM_THREADS"] = "2"
+    e["OMP_NUM_THREADS"] = "1"  # single-threaded CPU kernels: run-to-run identical sums
     e.update(kw)
     return e
 
@@ -109,7 +109,9 @@ def test_bench_world4_gloo_matches_global_batch(tmp_path):
             assert torch.equal(a, b)
     moved = 0.0
     for a, b in zip(ranks[0]["params"], ref["params"]):
-        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5), (a - b).abs().max()
+        # fp32 reduction-order noise only (~3e-8): a race between the per-forward buffer
+        # broadcast and the BN statistics shift showed up here as 1e-5..2e-4 run-to-run noise
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a - b).abs().max()
         moved += float((a - b).abs().max())
     for a, b in zip(ranks[0]["buffers"], ref["buffers"]):
         assert torch.allclose(a.float(), b.float(), rtol=1e-4, atol=1e-5)
