@@ -110,8 +110,14 @@ bool capturing() {
 
 std::vector<int> candidates(bool f32, bool wgrad) {
   if (f32) return {0, 2, 8};
+  // MIPIPE_CONV_TILES=n: tune over the first n tile configs only (A/B of added tiles)
+  static const int ntiles = [] {
+    const char* v = getenv("MIPIPE_CONV_TILES");
+    const int n = v == nullptr ? mipipe::kConvTileConfigs : atoi(v);
+    return n > 0 && n <= mipipe::kConvTileConfigs ? n : mipipe::kConvTileConfigs;
+  }();
   std::vector<int> c;
-  for (int i = 0; i < mipipe::kConvTileConfigs; ++i)
+  for (int i = 0; i < ntiles; ++i)
     if (!(wgrad && i == 6)) c.push_back(i);
   return c;
 }
