@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--res", type=int, default=224)
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--bucket-cap-mb", type=float, default=32.0)
+    ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="DDP gradient wire format (bf16: packed pre-scaled by 1/world, half the "
+                         "all-reduce bytes; fp32 = the reference's)")
     ap.add_argument("--impl", default="mipipe", choices=["mipipe", "stock"],
                     help="stock = torch DDP + MIOpen comparator")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
@@ -222,7 +225,8 @@ def main() -> int:
                        "parallelism": f"dp{world}", "impl": a.impl, "optimizer": opt_s,
                        "hip_graph": bool(getattr(a, "graph_used", False)),
                        "deterministic": bool(a.deterministic),
-                       "force_reduce": bool(a.force_reduce)},
+                       "force_reduce": bool(a.force_reduce),
+                       "comm_dtype": a.comm_dtype},
             "final_loss": loss_v, "gpu_clocks": sampler.summary()}), flush=True)
     if distributed:
         dist.barrier()
@@ -253,7 +257,8 @@ def build_bert(a, world, local, dev, rank):
         model.compute_dtype = _compute_dtype(a)
         if a.distributed:
             model = DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=a.bucket_cap_mb,
-                                            force_reduce=a.force_reduce)
+                                            force_reduce=a.force_reduce,
+                                            comm_dtype=_comm_dtype(a))
         opt = AdamW(model.parameters(), lr=1e-4, weight_decay=0.01)
 
         def step(ids, am, pos, labels):
@@ -298,6 +303,10 @@ def build_bert(a, world, local, dev, rank):
     return step, model, batches
 
 
+def _comm_dtype(a):
+    return torch.bfloat16 if a.comm_dtype == "bf16" else None
+
+
 def _compute_dtype(a):
     return torch.float32 if (a.device == "cpu" or a.dtype == "fp32") else torch.bfloat16
 
@@ -330,7 +339,8 @@ def build_cnn(a, world, local, dev, rank):
         model.compute_dtype = _compute_dtype(a)
         if a.distributed:
             model = DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=a.bucket_cap_mb,
-                                            force_reduce=a.force_reduce)
+                                            force_reduce=a.force_reduce,
+                                            comm_dtype=_comm_dtype(a))
         # fp32 compute reads the fp32 master weights directly: no bf16 shadow to refresh
         opt = SGD(model.parameters(), 0.1, momentum=0.9, weight_decay=1e-4,
                   shadow_dtype=None if _compute_dtype(a) == torch.float32 else "auto")

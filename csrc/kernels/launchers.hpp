@@ -231,6 +231,9 @@ void top1_correct(const void* logits, const int64_t* labels, int R, int V, int* 
 void sgd_step(float* p, const float* g, float* m, void* shadow, long n, float lr, float momentum,
               float dampening, float wd, bool nesterov, bool first, float grad_scale,
               hipStream_t st);
+// DDP bf16 wire: wire = bf16(g * scale), g = fp32(wire); n % 8 == 0, 16-B aligned pointers
+void grad_pack_bf16(const float* g, void* wire, long n, float scale, hipStream_t st);
+void grad_unpack_bf16(const void* wire, float* g, long n, hipStream_t st);
 // t_dev (device step counter, may be null): bias corrections 1 - b^t computed in the kernel
 void adamw_step(float* p, const float* g, float* m, float* v, void* shadow, long n, float lr,
                 float b1, float b2, float eps, float wd, float bc1, float bc2, float grad_scale,

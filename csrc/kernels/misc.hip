@@ -246,6 +246,50 @@ void sgd_step(float* p, const float* g, float* m, void* shadow, long n, float lr
                      n4, lr, momentum, dampening, wd, nesterov, first, grad_scale);
 }
 
+// ------------------------------------------------------------------------------ DDP wire format
+// bf16 gradient wire (DistributedDataParallel(comm_dtype=bf16)): one pass turns a
+// bucket of the flat fp32 gradient into bf16 already multiplied by 1/world, so RCCL's SUM is the
+// average (no post-divide pass); one pass widens the reduced bucket back into the fp32 gradient.
+// Buckets are 64-element aligned slices of the flat buffer: n % 8 == 0, 16-B aligned.
+__global__ __launch_bounds__(256) void grad_pack_bf16_kernel(const float* __restrict__ g,
+                                                             uint4* __restrict__ w, long n8,
+                                                             float scale) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    load8(g + i * 8, f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) f[q] *= scale;
+    w[i] = pack8(f);
+  }
+}
+
+__global__ __launch_bounds__(256) void grad_unpack_bf16_kernel(const uint4* __restrict__ w,
+                                                               float* __restrict__ g, long n8) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(w[i], f);
+    float4* o = reinterpret_cast<float4*>(g + i * 8);
+    o[0] = make_float4(f[0], f[1], f[2], f[3]);
+    o[1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+}
+
+void grad_pack_bf16(const float* g, void* wire, long n, float scale, hipStream_t st) {
+  const long n8 = n / 8;
+  if (n8 == 0) return;
+  hipLaunchKernelGGL(grad_pack_bf16_kernel, dim3(grid1d(n8, 4)), dim3(256), 0, st, g,
+                     (uint4*)wire, n8, scale);
+}
+
+void grad_unpack_bf16(const void* wire, float* g, long n, hipStream_t st) {
+  const long n8 = n / 8;
+  if (n8 == 0) return;
+  hipLaunchKernelGGL(grad_unpack_bf16_kernel, dim3(grid1d(n8, 4)), dim3(256), 0, st,
+                     (const uint4*)wire, g, n8);
+}
+
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     __bf16* __restrict__ sh, long n4, float lr,

@@ -21,6 +21,15 @@ the 8-GPU xGMI mesh) with a small first bucket so communication starts early and
 bucket so little is left to all-reduce after the final backward kernel; the optional
 ``comm_dtype=torch.bfloat16`` halves the bytes on the wire.
 
+Reducer: the native C++ reducer (``mipipe._C.Reducer``, csrc/comm/reducer.cpp) counts bucket
+readiness from post hooks on the AccumulateGrad nodes and from the HIP kernels that write
+gradients straight into the flat buffer, launches each bucket's all-reduce through the c10d
+process group, and makes the compute stream wait on them at the end of backward — no Python
+frame per parameter.  With ``comm_dtype=torch.bfloat16`` one HIP pass packs a bucket into a bf16
+wire buffer pre-scaled by 1/world and one pass widens the reduced bucket back.  The pure-Python
+reducer below is the fallback when ``_C`` is not built (``MIPIPE_NATIVE_REDUCER=0`` forces it);
+both issue the identical collective sequence.
+
 Debug aid (SURVEY §5.2 hazard): ``check_collectives=True`` (or ``MIPIPE_CHECK_COLLECTIVES=1``)
 hashes every collective this wrapper issues and compares the digests across ranks every
 ``check_every`` steps, turning a mismatched collective sequence into an immediate error.
@@ -69,7 +78,10 @@ class _CollectiveLog:
         self.count = 0
 
     def record(self, op: str, t: torch.Tensor) -> None:
-        self.h.update(f"{op}:{t.numel()}:{t.dtype};".encode())
+        self.record_shape(op, t.numel(), t.dtype)
+
+    def record_shape(self, op: str, numel: int, dtype) -> None:
+        self.h.update(f"{op}:{numel}:{dtype};".encode())
         self.count += 1
 
     def digest(self) -> bytes:
@@ -128,9 +140,42 @@ class DistributedDataParallel(tnn.Module):
         self._next_bucket = 0
         self._callback_queued = False
         self._reported = set()
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_ready) for p in params]
-        # kernels that accumulate weight gradients straight into the flat buffer report here
-        self.space.add_ready_listener(self._on_ready)
+        self._reducer = self._make_native_reducer() if self._comm else None
+        if self._reducer is not None:
+            self._slot_of = {id(p): i for i, (_, _, p) in enumerate(self.space.ranges())}
+            self._reducer.register_hooks([r[2] for r in self.space.ranges()])
+            self._hooks = []
+            # kernels that write weight gradients straight into the flat buffer report here
+            self.space.add_ready_listener(self._native_ready)
+        else:
+            self._hooks = [p.register_post_accumulate_grad_hook(self._on_ready) for p in params]
+            self.space.add_ready_listener(self._on_ready)
+
+    def _make_native_reducer(self):
+        if os.environ.get("MIPIPE_NATIVE_REDUCER", "1") == "0":
+            return None
+        from mipipe.ops._native import native, native_available
+        if not native_available():
+            return None
+        if self.comm_dtype not in (None, torch.float32, torch.bfloat16):
+            return None
+        pg = self.process_group if self.process_group is not None else dist.group.WORLD
+        slot_bucket = []
+        for b in self.buckets:
+            slot_bucket += [b.index] * len(b.params)
+        return native().Reducer(pg.group_name, self.space.flat_grad,
+                                [(b.start, b.end) for b in self.buckets], slot_bucket,
+                                self.world, self._avg_supported,
+                                self.comm_dtype == torch.bfloat16)
+
+    @property
+    def native_reducer(self) -> bool:
+        return self._reducer is not None
+
+    def _native_ready(self, param) -> None:
+        slot = self._slot_of.get(id(param))
+        if slot is not None:
+            self._reducer.mark_ready(slot)
 
     # ------------------------------------------------------------------ construction
     def _verify_shapes(self, params) -> None:
@@ -265,6 +310,8 @@ class DistributedDataParallel(tnn.Module):
     def no_sync(self):
         old = self._sync_enabled
         self._sync_enabled = False
+        if self._reducer is not None:
+            self._reducer.prepare(False)
         try:
             yield
         finally:
@@ -272,6 +319,19 @@ class DistributedDataParallel(tnn.Module):
 
     # ------------------------------------------------------------------ backward / comm
     def _prepare_backward(self) -> None:
+        if self._reducer is not None:
+            on = self._comm and self._sync_enabled
+            self._reducer.prepare(on)
+            self.space.ensure_grad_views()
+            if on:
+                # the native reducer issues exactly this sequence during the coming backward
+                wdt = torch.bfloat16 if self._reducer.wire_bf16 else torch.float32
+                for b in self.buckets:
+                    self._clog.record_shape("all_reduce", b.end - b.start, wdt)
+                self._steps += 1
+                if self.check_collectives and self._steps % self.check_every == 0:
+                    self.verify_collective_sequence()
+            return
         self._reported = set()
         for b in self.buckets:
             b.pending = len(b.params)

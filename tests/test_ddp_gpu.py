@@ -37,11 +37,15 @@ def nccl_pg():
     dist.destroy_process_group()
 
 
-def test_rccl_ddp_graphed_matches_eager(nccl_pg):
+@pytest.mark.parametrize("reducer", ["native", "python"])
+def test_rccl_ddp_graphed_matches_eager(nccl_pg, reducer, monkeypatch):
     """DDP (RCCL, world 1, every bucket forced through the collective) replayed from a hipGraph
-    == the same steps run eagerly.  Deterministic kernels: without them a batch-32 bf16
-    BatchNorm net amplifies atomic-order noise to ~0.98 cosine between two EAGER runs within
-    four SGD steps, which is no basis for comparing graph against eager."""
+    == the same steps run eagerly, with the native C++ reducer (mipipe._C.Reducer: hooks on the
+    AccumulateGrad nodes, collectives issued from C++) and with the Python fallback.
+    Deterministic kernels: without them a batch-32 bf16 BatchNorm net amplifies atomic-order
+    noise to ~0.98 cosine between two EAGER runs within four SGD steps, which is no basis for
+    comparing graph against eager."""
+    monkeypatch.setenv("MIPIPE_NATIVE_REDUCER", "1" if reducer == "native" else "0")
     from mipipe.models import create_model
     from mipipe.ops.determinism import deterministic
     from mipipe.ops.functional import cross_entropy
@@ -55,6 +59,7 @@ def test_rccl_ddp_graphed_matches_eager(nccl_pg):
             for m in mods]
     for d in ddps:
         assert d._comm and len(d.buckets) >= 2
+        assert d.native_reducer == (reducer == "native")
     opts = [SGD(d.parameters(), 0.05, momentum=0.9, weight_decay=1e-4) for d in ddps]
     assert graph_safe(ddps[1], opts[1])[0]
     x = torch.randn(32, 3, 32, 32, device="cuda")
@@ -86,23 +91,53 @@ def test_rccl_ddp_graphed_matches_eager(nccl_pg):
         if b.is_floating_point():
             torch.testing.assert_close(b, c, rtol=1e-4, atol=1e-5, msg=n)
 
-def test_rccl_bf16_comm_dtype(nccl_pg):
-    """comm_dtype=bf16 halves the bytes on the wire; the averaged gradient equals the fp32
-    gradient to bf16 rounding."""
+@pytest.mark.parametrize("reducer", ["native", "python"])
+def test_rccl_bf16_comm_dtype(nccl_pg, reducer, monkeypatch):
+    """comm_dtype=bf16 halves the bytes on the wire.  At world 1 the RCCL sum of one rank's
+    packed bucket is that bucket, so the reduced gradient must equal the local fp32 gradient
+    rounded to bf16 (round-to-nearest-even) EXACTLY — the pack (scale 1/world, rounding), the
+    collective and the unpack are all checked, bucket by bucket."""
     from mipipe.models import create_model
+    from mipipe.ops.determinism import deterministic
     from mipipe.ops.functional import cross_entropy
     from mipipe.parallel import DistributedDataParallel
+    monkeypatch.setenv("MIPIPE_NATIVE_REDUCER", "1" if reducer == "native" else "0")
     torch.manual_seed(1)
     m = create_model("resnet18", num_classes=10).cuda()
+    ref = copy.deepcopy(m)
     d = DistributedDataParallel(m, device_ids=[0], force_reduce=True, comm_dtype=torch.bfloat16)
+    assert d.native_reducer == (reducer == "native")
     x = torch.randn(16, 3, 32, 32, device="cuda")
     y = torch.randint(0, 10, (16,), device="cuda")
-    d.space.zero_grad()
-    cross_entropy(d(x), y).backward()
-    g = d.space.flat_grad.clone()
+    from mipipe.optim.flat import get_flat_space
+    rs = get_flat_space(list(ref.parameters()), torch.bfloat16, ref)
+    with deterministic(True):
+        d.space.zero_grad()
+        cross_entropy(d(x), y).backward()
+        rs.zero_grad()
+        cross_entropy(ref(x), y).backward()
+    torch.cuda.synchronize()
+    g, gl = d.space.flat_grad, rs.flat_grad
     assert torch.isfinite(g).all() and g.abs().sum() > 0
-    # every bucket went through a bf16 temporary: values are bf16-representable
-    assert torch.equal(g, g.to(torch.bfloat16).float())
+    assert torch.equal(g, gl.to(torch.bfloat16).float()), float((g - gl).abs().max())
+    assert not torch.equal(g, gl)  # the wire really was bf16
+
+
+def test_grad_wire_pack_unpack_kernels():
+    """The HIP wire passes against torch: pack = bf16(g * scale) (RNE), unpack = widening."""
+    from mipipe.ops._native import native
+    torch.manual_seed(0)
+    for n in (8, 4096 + 8, 1 << 20):
+        g = torch.randn(n, device="cuda") * 3
+        w = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+        native().grad_pack_bf16(g, w, 0.125)
+        assert torch.equal(w, (g * 0.125).to(torch.bfloat16))
+        out = torch.empty(n, device="cuda")
+        native().grad_unpack_bf16(w, out)
+        assert torch.equal(out, w.float())
+    with pytest.raises(RuntimeError):
+        native().grad_pack_bf16(torch.zeros(12, device="cuda"),
+                                torch.zeros(12, dtype=torch.bfloat16, device="cuda"), 1.0)
 
 
 def test_bench_force_reduce_graph_gpu():

@@ -130,10 +130,16 @@ def test_ddp_gloo_matches_single_process(double_report):
     assert torch.allclose(f0, ref, atol=1e-5)
 
 
-def test_ddp_check_tool_cpu():
-    """tools/ddp_gpu_check.py on the CPU path (2 gloo ranks): bucket all-reduces intercepted --
-    no gradient lands after its bucket launched, reduced == sum of local gradients -- and the
-    ranks stay bit-identical."""
+@pytest.mark.parametrize("reducer", ["python", "native"])
+def test_ddp_check_tool_cpu(reducer):
+    """tools/ddp_gpu_check.py on the CPU path (2 gloo ranks).  Python reducer: bucket all-reduces
+    intercepted -- no gradient lands after its bucket launched, reduced == sum of local gradients.
+    Native reducer (mipipe._C.Reducer): the collectives are issued from C++; the all-reduced
+    gradient is checked against single-process replicas.  Both: the ranks stay bit-identical."""
+    if reducer == "native":
+        from mipipe.ops._native import native_available
+        if not native_available():
+            pytest.skip("mipipe._C not built")
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -142,10 +148,12 @@ def test_ddp_check_tool_cpu():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", port,
                         os.path.join(root, "tools", "ddp_gpu_check.py"), "--device", "cpu",
-                        "--arch", "resnet18"], capture_output=True, text=True, timeout=600,
-                       env=env, cwd=root)
+                        "--arch", "resnet18", "--reducer", reducer], capture_output=True,
+                       text=True, timeout=600, env=env, cwd=root)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    assert "step0 bucket check OK" in r.stdout and "DDP gpu check OK" in r.stdout
+    first = "step0 bucket check OK" if reducer == "python" else "step0 native reducer"
+    assert first in r.stdout and "DDP gpu check OK" in r.stdout
+    assert "step0 gradient vs truth" in r.stdout
 
 
 def test_data_parallel_passthrough_and_unwrap():

@@ -71,7 +71,7 @@ def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True) -> s
     hip_flags = common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + tflags
     cpp_flags = common + tflags
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    cpps = [os.path.join(CSRC, "bindings.cpp")]
+    cpps = [os.path.join(CSRC, "bindings.cpp")] + sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
     hdr = _newest_header()
     jobs_list = []
     for s in srcs:

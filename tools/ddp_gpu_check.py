@@ -86,7 +86,12 @@ def main():
     ap.add_argument("--arch", default="resnet18")
     ap.add_argument("--res", type=int, default=32)
     ap.add_argument("--device", default="cuda", help="cpu: the same check on the CPU path")
+    ap.add_argument("--reducer", default="python", choices=["python", "native"],
+                    help="python: the interceptable reducer (checks (1)/(2) per bucket); native: "
+                         "mipipe._C.Reducer (collectives issued from C++: checks (1)/(2) are "
+                         "replaced by the replica comparison and check (3))")
     a = ap.parse_args()
+    os.environ["MIPIPE_NATIVE_REDUCER"] = "1" if a.reducer == "native" else "0"
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = torch.device(a.device, 0) if a.device == "cuda" else torch.device("cpu")
@@ -123,6 +128,12 @@ def main():
         finally:
             dist.all_reduce = _DeferredAllReduce.real
         if step == 0:
+            assert model.native_reducer == (a.reducer == "native")
+        if step == 0 and a.reducer == "native":
+            assert not _DeferredAllReduce.log  # nothing went through the Python collective API
+            if rank == 0:
+                print(f"step0 native reducer: {len(model.buckets)} buckets issued from C++", flush=True)
+        if step == 0 and a.reducer == "python":
             log = _DeferredAllReduce.log
             assert len(log) == len(model.buckets), (len(log), len(model.buckets))
             late = [i for i, (lt, _, _) in enumerate(log) if lt]
@@ -132,6 +143,7 @@ def main():
             if rank == 0:
                 print(f"step0 bucket check OK: {len(log)} buckets, no late writes, reduced == "
                       f"sum of local gradients (max rel err {worst_err:.1e})", flush=True)
+        if step == 0:
             # replicas (and the fp64 truth): average of the per-rank gradients
             for r in [ro[0] for ro in refs] + [truth]:
                 rd = next(r.parameters()).device
