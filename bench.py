@@ -226,7 +226,9 @@ def main() -> int:
                        "hip_graph": bool(getattr(a, "graph_used", False)),
                        "deterministic": bool(a.deterministic),
                        "force_reduce": bool(a.force_reduce),
-                       "comm_dtype": a.comm_dtype},
+                       "comm_dtype": a.comm_dtype,
+                       "native_reducer": bool(getattr(model, "native_reducer", False)),
+                       "rccl": _rccl_settings() if distributed else None},
             "final_loss": loss_v, "gpu_clocks": sampler.summary()}), flush=True)
     if distributed:
         dist.barrier()
@@ -301,6 +303,11 @@ def build_bert(a, world, local, dev, rank):
             opt.step()
             return loss
     return step, model, batches
+
+
+def _rccl_settings():
+    from mipipe.parallel.dist_utils import rccl_settings
+    return rccl_settings()
 
 
 def _comm_dtype(a):

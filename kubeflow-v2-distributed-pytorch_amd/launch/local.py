@@ -37,9 +37,8 @@ def rank_envs(nprocs: int, port: Optional[int] = None,
         e = dict(os.environ)
         if extra:
             e.update(extra)
-        from mipipe.parallel.dist_utils import RCCL_ENV_DEFAULTS
-        for k, v in RCCL_ENV_DEFAULTS.items():
-            e.setdefault(k, v)
+        from mipipe.parallel.dist_utils import configure_rccl_env
+        configure_rccl_env(e)  # high-priority comm stream + MIPIPE_RCCL_PROFILE channels
         e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nprocs),
                   "LOCAL_WORLD_SIZE": str(nprocs), "GROUP_RANK": "0",
                   "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),

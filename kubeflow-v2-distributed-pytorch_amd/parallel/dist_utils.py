@@ -60,14 +60,49 @@ RCCL_ENV_DEFAULTS = {
     "HSA_ENABLE_IPC_MODE_LEGACY": "0",
 }
 
+# Channel profiles for the 8-GPU xGMI mesh (``MIPIPE_RCCL_PROFILE``; the environment still wins).
+# One RCCL channel is one workgroup on one CU, moving its slice over one ring / tree edge, so the
+# channel count trades link parallelism against CUs taken from the kernels it overlaps:
+#  * "auto" (default): RCCL's own topology search — it reads the xGMI full mesh (7 links per
+#    MI355X) and picks rings and channel counts per message size.  DDP buckets overlap backward
+#    here (94.5 % concurrent, profiles/r3_ddp_rccl_overlap_eager_highprio.txt), so the CUs a
+#    bigger channel count would take cost more than the link time they would save.
+#  * "overlap": at most 8 channels — for steps whose collectives are fully hidden under compute:
+#    RCCL takes <= 8 of the 256 CUs from the overlapped kernels.
+#  * "bandwidth": at least 32 channels — for exposed collectives (parameter broadcast at start,
+#    gradient tails of compute-light models): every xGMI link carries several rings' slices.
+RCCL_PROFILES = {
+    "auto": {},
+    "overlap": {"NCCL_MAX_NCHANNELS": "8"},
+    "bandwidth": {"NCCL_MIN_NCHANNELS": "32"},
+}
 
-def configure_rccl_env(env: Optional[dict] = None) -> dict:
-    """Apply :data:`RCCL_ENV_DEFAULTS` to ``env`` (``os.environ`` by default) without
-    overriding values already set; returns the target mapping."""
+
+def rccl_profile_env(profile: Optional[str] = None) -> dict:
+    """The RCCL variables of ``profile`` (default: ``$MIPIPE_RCCL_PROFILE`` or "auto")."""
+    name = profile if profile is not None else os.environ.get("MIPIPE_RCCL_PROFILE", "auto")
+    if name not in RCCL_PROFILES:
+        raise ValueError(f"MIPIPE_RCCL_PROFILE={name!r}: expected one of {sorted(RCCL_PROFILES)}")
+    return dict(RCCL_PROFILES[name])
+
+
+def configure_rccl_env(env: Optional[dict] = None, profile: Optional[str] = None) -> dict:
+    """Apply :data:`RCCL_ENV_DEFAULTS` and the channel profile to ``env`` (``os.environ`` by
+    default) without overriding values already set; returns the target mapping.  Must run before
+    the first process group / communicator exists (RCCL reads its variables at comm init)."""
     target = os.environ if env is None else env
-    for k, v in RCCL_ENV_DEFAULTS.items():
+    prof = rccl_profile_env(profile if profile is not None else target.get("MIPIPE_RCCL_PROFILE"))
+    for k, v in list(RCCL_ENV_DEFAULTS.items()) + list(prof.items()):
         target.setdefault(k, v)
     return target
+
+
+def rccl_settings(env: Optional[dict] = None) -> dict:
+    """The RCCL / ProcessGroupNCCL variables in effect (recorded with every bench line)."""
+    src = os.environ if env is None else env
+    keys = sorted(k for k in src if k.startswith(("NCCL_", "RCCL_", "TORCH_NCCL_")) or
+                  k == "MIPIPE_RCCL_PROFILE")
+    return {k: src[k] for k in keys}
 
 
 def init_distributed(backend: str, init_method: str, world_size: int, rank: int,

@@ -38,6 +38,10 @@ def test_bench_self_spawn_gloo(n):
     assert j["n_gpus"] == n and j["config"]["parallelism"] == f"dp{n}"
     assert j["config"]["global_batch"] == 8 * n
     assert j["steps"] == 2 and j["warmup"] == 1 and j["value"] > 0
+    if n > 1:
+        from mipipe.ops._native import native_available
+        assert j["config"]["native_reducer"] == native_available()
+        assert j["config"]["rccl"]["TORCH_NCCL_HIGH_PRIORITY"] == "1"
 
 
 def test_bench_force_reduce_world1_gloo():
@@ -121,3 +125,19 @@ def test_bench_world4_gloo_matches_global_batch(tmp_path, comm):
     for a, b in zip(ranks[0]["buffers"], ref["buffers"]):
         btol = dict(rtol=1e-4, atol=1e-5) if comm == "fp32" else dict(rtol=1e-2, atol=1e-3)
         assert torch.allclose(a.float(), b.float(), **btol)
+
+
+def test_rccl_profiles_env():
+    """MIPIPE_RCCL_PROFILE channel profiles: applied as defaults (the environment wins), the
+    high-priority comm stream always, unknown names rejected; the settings report lists them."""
+    from mipipe.parallel.dist_utils import configure_rccl_env, rccl_settings
+    e = configure_rccl_env({})
+    assert e["TORCH_NCCL_HIGH_PRIORITY"] == "1" and "NCCL_MAX_NCHANNELS" not in e
+    e = configure_rccl_env({"MIPIPE_RCCL_PROFILE": "overlap"})
+    assert e["NCCL_MAX_NCHANNELS"] == "8"
+    e = configure_rccl_env({"NCCL_MIN_NCHANNELS": "4"}, profile="bandwidth")
+    assert e["NCCL_MIN_NCHANNELS"] == "4"  # explicit setting kept
+    with pytest.raises(ValueError):
+        configure_rccl_env({}, profile="fastest")
+    rep = rccl_settings({"NCCL_MIN_NCHANNELS": "32", "PATH": "/bin", "TORCH_NCCL_HIGH_PRIORITY": "1"})
+    assert rep == {"NCCL_MIN_NCHANNELS": "32", "TORCH_NCCL_HIGH_PRIORITY": "1"}
