@@ -1520,11 +1520,13 @@ Tensor avgpool2d_bwd(Tensor dy, std::vector<int64_t> xs, int64_t k, int64_t s, i
 
 namespace mipipe_comm {
 void init_comm(py::module& m);  // csrc/comm/reducer.cpp: native DDP reducer, bf16 wire passes
+void init_oneshot(py::module& m);  // csrc/comm/oneshot.cpp: one-shot IPC collectives
 }
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "mipipe gfx950 (MI355X) HIP kernels";
   mipipe_comm::init_comm(m);
+  mipipe_comm::init_oneshot(m);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("shift") = py::none(), py::arg("slab_sum") = py::none(),
         py::arg("slab_sq") = py::none(), py::arg("bias") = py::none(), py::arg("relu") = false,

@@ -231,6 +231,11 @@ void top1_correct(const void* logits, const int64_t* labels, int R, int V, int* 
 void sgd_step(float* p, const float* g, float* m, void* shadow, long n, float lr, float momentum,
               float dampening, float wd, bool nesterov, bool first, float grad_scale,
               hipStream_t st);
+// One-shot collective over peer workspaces (csrc/kernels/oneshot.hip): fp32 sum * scale
+// (reduce) or a byte broadcast from `src`; nbytes % 16 == 0, nbytes <= cap.
+constexpr long kOneShotHeaderBytes = 4096;
+void oneshot_launch(char* const* bases, int rank, int world, const void* in, void* out,
+                    long nbytes, bool reduce, int src, float scale, long cap, hipStream_t st);
 // DDP bf16 wire: wire = bf16(g * scale), g = fp32(wire); n % 8 == 0, 16-B aligned pointers
 void grad_pack_bf16(const float* g, void* wire, long n, float scale, hipStream_t st);
 void grad_unpack_bf16(const void* wire, float* g, long n, hipStream_t st);

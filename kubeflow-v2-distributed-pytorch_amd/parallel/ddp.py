@@ -128,6 +128,13 @@ class DistributedDataParallel(tnn.Module):
         self.space: FlatParamSpace = get_flat_space(params, shadow, module)
         backend = dist.get_backend(process_group) if dist.is_initialized() else "none"
         self._avg_supported = backend == "nccl"
+        # latency path for the per-forward buffer broadcast (C4): one-shot over IPC peer
+        # pointers (parallel/oneshot.py) when MIPIPE_ONESHOT=1 on a single-node GPU job
+        self._oneshot = None
+        if self._comm and dev.type == "cuda":
+            from mipipe.parallel.oneshot import OneShotComm, oneshot_enabled
+            if oneshot_enabled():
+                self._oneshot = OneShotComm(process_group, device=dev)
         if self._comm:
             self._verify_shapes(params)
             self._sync_module_states()
@@ -208,7 +215,12 @@ class DistributedDataParallel(tnn.Module):
                 if b is not None:
                     by_dtype.setdefault(b.dtype, []).append((mod, name, b))
         for dt, lst in by_dtype.items():
-            flat = torch.cat([b.detach().reshape(-1) for _, _, b in lst])
+            parts = [b.detach().reshape(-1) for _, _, b in lst]
+            esz = parts[0].element_size()
+            pad = (-sum(p.numel() for p in parts) * esz) % 16 // esz  # 16-B multiple (one-shot)
+            if pad:
+                parts.append(torch.zeros(pad, dtype=dt, device=parts[0].device))
+            flat = torch.cat(parts)
             off = 0
             for mod, name, b in lst:
                 n = b.numel()
@@ -235,7 +247,10 @@ class DistributedDataParallel(tnn.Module):
         works = []
         for flat in self._flat_bufs:
             self._clog.record("broadcast", flat)
-            works.append(dist.broadcast(flat, 0, group=self.process_group, async_op=True))
+            if self._oneshot is not None and self._oneshot.fits(flat):
+                self._oneshot.broadcast(flat, 0)  # one IPC hop, ordered on the compute stream
+            else:
+                works.append(dist.broadcast(flat, 0, group=self.process_group, async_op=True))
         self._pending_buffer_work = works
 
     def _wait_buffer_sync(self, module=None, args=None) -> None:

@@ -191,7 +191,8 @@ def main():
     assert all(torch.equal(gathered[0], t) for t in gathered), "ranks diverged"
     if rank == 0:
         print(f"DDP gpu check OK ({a.arch}): world={world}, parameters bit-identical across ranks after 3 "
-              f"steps, collectives={model._clog.count}", flush=True)
+              f"steps, collectives={model._clog.count} oneshot={model._oneshot is not None}",
+              flush=True)
     dist.destroy_process_group()
 
 
