@@ -34,6 +34,34 @@ Tensor = torch.Tensor
 # block-output ReLU masks kept as bits for the fused backward (MIPIPE_RELU_BITMASK=0: read z)
 _RELU_BITMASK = os.environ.get("MIPIPE_RELU_BITMASK", "1") != "0"
 
+# Weight-grads on a side stream (MIPIPE_SIDE_WGRAD=1): a conv's weight-grad is off the backward
+# critical path (dgrad -> BN apply -> next dgrad), so it can run beside the chain; the side
+# stream joins the compute stream at the end of backward (engine callback).
+_SIDE_WGRAD = os.environ.get("MIPIPE_SIDE_WGRAD", "0") == "1"
+_SIDE_STREAMS = {}
+_SIDE_JOIN_PENDING = set()
+
+
+def _side_stream(t: Tensor):
+    key = t.device.index
+    s = _SIDE_STREAMS.get(key)
+    if s is None:
+        s = torch.cuda.Stream(t.device)
+        _SIDE_STREAMS[key] = s
+    return s
+
+
+def _queue_side_join(main, side) -> None:
+    key = id(side)
+    if key in _SIDE_JOIN_PENDING:
+        return
+    _SIDE_JOIN_PENDING.add(key)
+
+    def join():
+        _SIDE_JOIN_PENDING.discard(key)
+        main.wait_stream(side)
+    torch.autograd.Variable._execution_engine.queue_callback(join)
+
 
 # ----------------------------------------------------------------------------- conv
 def _direct_grad_target(p: Tensor, rows: Optional[int] = None):
@@ -170,7 +198,13 @@ class _ConvFn(Function):
         if ctx.needs_input_grad[1]:
             weight = ctx.weight
             collect = None
-            if bnr is not None:
+            tgt = (_direct_grad_target(weight)
+                   if x.shape[-1] == ci and ctx.wmap is None and K.use_native(dy) else None)
+            side = None
+            if (_SIDE_WGRAD and tgt is not None and dy.is_cuda and not tgt[0]._ready_listeners
+                    and not (bnr is not None and tok.y2 is not None)):
+                side = _side_stream(dy)
+            if bnr is not None and side is None:
                 # the weight-grad launch also collects the slab the fused dgrad just filled
                 # (one of its blocks; no separate bn_bwd_collect launch)
                 two = tok.y2 is not None
@@ -188,9 +222,18 @@ class _ConvFn(Function):
                 t2 = targets(tok.bn2) if two else (None, None)
                 collect = (bnr[5], out2) + t1 + ((True,) + t2 if two else ())
                 tok.collected = (out2, t1[0] is not None, t2[0] is not None)
-            tgt = (_direct_grad_target(weight)
-                   if x.shape[-1] == ci and ctx.wmap is None and K.use_native(dy) else None)
-            if tgt is not None:
+            if side is not None:
+                # the BN backward collects its own slab (bn_bwd_collect) on the compute stream
+                fs, g = tgt
+                main = torch.cuda.current_stream(dy.device)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    K.conv_wgrad(dy, x, kh, kw, stride, pad, out=g.permute(0, 2, 3, 1))
+                dy.record_stream(side)
+                x.record_stream(side)
+                _queue_side_join(main, side)
+                fs.grad_ready(weight)
+            elif tgt is not None:
                 # gradient accumulates straight into the flat DDP bucket: no zero-fill, no
                 # autograd AccumulateGrad add; tell the reducer the gradient is ready.
                 fs, g = tgt
