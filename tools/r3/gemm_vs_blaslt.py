@@ -1,0 +1,50 @@
+"""mipipe's MFMA GEMM (tuned per shape) vs torch.matmul (hipBLASLt) on the BERT-base 32x128
+shapes: forward (x @ W^T), data-grad (dy @ W), weight-grad (dy^T @ x, fp32 out)."""
+import time
+
+import torch
+
+from mipipe.ops import kernels as K
+from mipipe.ops._native import native
+
+
+def t_ms(fn, reps=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / reps * 1e3
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    native().set_benchmark(True, False, 5)
+    M = 4096
+    rows = []
+    for (N, Kd, name) in [(2304, 768, "qkv"), (768, 768, "proj"), (3072, 768, "ffn1"),
+                          (768, 3072, "ffn2"), (30528, 768, "mlm")]:
+        x = torch.randn(M, Kd, device=dev, dtype=torch.bfloat16)
+        w = torch.randn(N, Kd, device=dev, dtype=torch.bfloat16) * 0.02
+        dy = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
+        g = torch.zeros(N, Kd, device=dev)
+        fl = 2.0 * M * N * Kd
+        for kind, f_mi, f_bl in [
+            ("fwd", lambda: K.gemm(x, w, False, True, None, "none", torch.bfloat16),
+             lambda: torch.mm(x, w.t())),
+            ("dgrad", lambda: K.gemm(dy, w, False, False, None, "none", torch.bfloat16),
+             lambda: torch.mm(dy, w)),
+            ("wgrad", lambda: K.gemm(dy, x, True, False, None, "none", torch.float32, g, 1.0),
+             lambda: torch.mm(dy.t(), x)),
+        ]:
+            a, b = t_ms(f_mi), t_ms(f_bl)
+            rows.append((name, kind, a, b))
+            print(f"{name:5s} {kind:5s} M={M} N={N} K={Kd}: mipipe {a*1e3:7.1f} us ({fl/a/1e9:6.0f} TF)"
+                  f"  hipBLASLt {b*1e3:7.1f} us ({fl/b/1e9:6.0f} TF)", flush=True)
+    print(f"sum: mipipe {sum(r[2] for r in rows)*1e3:.0f} us, hipBLASLt {sum(r[3] for r in rows)*1e3:.0f} us")
+
+
+if __name__ == "__main__":
+    main()
