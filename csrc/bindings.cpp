@@ -942,15 +942,34 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
                 addend->is_contiguous(), "addend must be a contiguous [M, N] tensor");
     add_p = addend->data_ptr();
   }
+  // Split-K for activation-dtype outputs without an epilogue (e.g. the MLM decoder's data-grad:
+  // K = 30528, only 192 output tiles of 128 x 128 for 256 CUs): the splits accumulate into a
+  // zeroed fp32 workspace, one pass rounds it into the bf16 output.  Not in deterministic mode
+  // (float atomics); the tuner times these plans against the unsplit ones.
+  const bool splittable = mode == 0 && bias_p == nullptr && act_i == 0 && add_p == nullptr &&
+                          !f32 && mipipe::g_deterministic == 0;
   auto launch = [&](void* C, int p) {
     const int cfg = p < 0 ? -1 : p % tune::kPlanSplit;
     const int sp = p < 0 ? -1 : (p / tune::kPlanSplit > 0 ? p / tune::kPlanSplit : -1);
+    if (splittable && sp > 1) {
+      Tensor ws = torch::zeros({M, N}, a.options().dtype(at::kFloat));
+      mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b,
+                   ws.data_ptr(), N, (int)M, (int)N, (int)K, nullptr, 0, 2, stream(), f32, cfg,
+                   sp, nullptr);
+      torch::from_blob(C, {M, N}, a.options()).copy_(ws);
+      return;
+    }
     mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b, C, N,
                  (int)M, (int)N, (int)K, bias_p, act_i, mode, stream(), f32, cfg, sp, add_p);
   };
   if (plan < 0) {
+    std::vector<int> cands = tune::gemm_candidates(f32, mode == 2);
+    if (splittable && K >= 4096) {
+      for (int t : tune::candidates(f32, false))
+        for (int sp : {2, 4, 8}) cands.push_back(t + tune::kPlanSplit * sp);
+    }
     plan = tune::select_from(tune::gemm_key(M, N, K, !trans_a, trans_b, add_p != nullptr ? 3 : mode, f32),
-                             tune::gemm_candidates(f32, mode == 2), [&](int p) {
+                             cands, [&](int p) {
                                auto scratch = mode == 2 ? torch::zeros_like(out)
                                                         : torch::empty_like(out);
                                launch(scratch.data_ptr(), p);

@@ -1,8 +1,12 @@
 """mipipe's MFMA GEMM (tuned per shape) vs torch.matmul (hipBLASLt) on the BERT-base 32x128
 shapes: forward (x @ W^T), data-grad (dy @ W), weight-grad (dy^T @ x, fp32 out)."""
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from mipipe.ops import kernels as K
 from mipipe.ops._native import native
