@@ -946,8 +946,12 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
   // K = 30528, only 192 output tiles of 128 x 128 for 256 CUs): the splits accumulate into a
   // zeroed fp32 workspace, one pass rounds it into the bf16 output.  Not in deterministic mode
   // (float atomics); the tuner times these plans against the unsplit ones.
-  const bool splittable = mode == 0 && bias_p == nullptr && act_i == 0 && add_p == nullptr &&
-                          !f32 && mipipe::g_deterministic == 0;
+  static const bool splitk_on = [] {
+    const char* v = getenv("MIPIPE_GEMM_SPLITK");
+    return v == nullptr || atoi(v) != 0;
+  }();
+  const bool splittable = splitk_on && mode == 0 && bias_p == nullptr && act_i == 0 &&
+                          add_p == nullptr && !f32 && mipipe::g_deterministic == 0;
   auto launch = [&](void* C, int p) {
     const int cfg = p < 0 ? -1 : p % tune::kPlanSplit;
     const int sp = p < 0 ? -1 : (p / tune::kPlanSplit > 0 ? p / tune::kPlanSplit : -1);

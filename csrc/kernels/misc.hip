@@ -333,7 +333,11 @@ void adamw_step(float* p, const float* g, float* m, float* v, void* shadow, long
   long n4 = n / 4;
   // 32768 blocks: 5.10 TB/s at BERT-base size vs 4.63 with the default 8192 cap (more waves in
   // flight per SIMD; tools/r3/adamw_lab.hip, profiles/r3_bert_gemm_splitk_adamw.txt)
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid1d(n4, 1, 32768)), dim3(256), 0, st, p, g, m, v,
+  static const int cap = [] {
+    const char* e = getenv("MIPIPE_ADAMW_BLOCKS");
+    return e == nullptr ? 32768 : atoi(e);
+  }();
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid1d(n4, 1, cap)), dim3(256), 0, st, p, g, m, v,
                      (__bf16*)shadow, n4, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, t_dev);
 }
 

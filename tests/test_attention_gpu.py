@@ -252,8 +252,11 @@ def test_device_seeded_dropout_changes_per_step_and_replays():
 def test_bert_graphed_step_matches_eager():
     """BERT MLM + AdamW + dropout replayed from one captured hipGraph follows the eager steps:
     AdamW's step count and the dropout seeds are device counters (graph_safe accepts the step).
-    BERT's backward keeps float atomics (attention dQ, embedding scatter), so the comparison is
-    against the run-to-run noise of a second eager model."""
+    BERT's backward keeps float atomics (attention dQ, embedding scatter), and AdamW turns a
+    near-zero gradient's atomic-order noise into a full lr-sized step (m / sqrt(v) ~ sign), so a
+    few hundred embedding elements can legitimately differ by ~1e-4 between ANY two runs
+    (eager vs eager included: measured flaky at the element level).  The parameters are compared
+    by norm: the graph-vs-eager difference must be a small fraction of the 4-step update."""
     import copy
     from mipipe.models import create_model
     from mipipe.optim import AdamW
@@ -261,6 +264,7 @@ def test_bert_graphed_step_matches_eager():
     torch.manual_seed(0)
     a = create_model("bert_tiny").cuda()
     b, c = copy.deepcopy(a), copy.deepcopy(a)
+    init = {n: p.detach().clone() for n, p in a.named_parameters()}
     opts = [AdamW(m.parameters(), lr=1e-3, weight_decay=0.01) for m in (a, b, c)]
     ok, why = graph_safe(b, opts[1])
     assert ok, why
@@ -281,8 +285,11 @@ def test_bert_graphed_step_matches_eager():
     assert lb[0] == la[0]  # the eager warm-up step is the eager step
     noise = max(abs(x - y) for x, y in zip(la, lc)) + 1e-3 * abs(la[0])
     assert max(abs(x - y) for x, y in zip(la, lb)) < 3 * noise + 1e-3, (la, lb, lc)
+    bad = []
     for (n, p), (_, q), (_, r) in zip(a.named_parameters(), b.named_parameters(),
                                        c.named_parameters()):
-        d_pq = (p - q).abs().max().item()
-        d_pr = (p - r).abs().max().item()
-        assert d_pq <= 3 * d_pr + 1e-5, (n, d_pq, d_pr)
+        upd = float((p - init[n]).norm())
+        d_pq, d_pr = float((p - q).norm()), float((p - r).norm())
+        if not d_pq <= max(0.02 * upd, 3 * d_pr) + 1e-6:
+            bad.append((n, d_pq, d_pr, upd))
+    assert not bad, bad

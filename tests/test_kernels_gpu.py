@@ -148,6 +148,22 @@ def test_gemm_every_plan(M, N, K, ta, tb):
             assert rel_err(acc - acc0, ref32) < 2e-3, (cfg, sp)
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 768, 8192), (200, 136, 4104)])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False)])
+def test_gemm_splitk_bf16_output(M, N, K, ta, tb):
+    """Split-K plans of a plain bf16-output GEMM (no epilogue; e.g. the MLM decoder data-grad,
+    K = 30528): the splits accumulate into an fp32 workspace and one pass rounds it to bf16 —
+    every tile config at 2/4/8 splits against the fp32 product."""
+    a = bf(M, K)
+    b = bf(N, K) if tb else bf(K, N)
+    ref = _ref.gemm(a.float(), b.float(), ta, tb, None, "none", torch.float32)
+    for cfg in range(native().CONV_TILE_CONFIGS):
+        for sp in (2, 4, 8):
+            out = native().gemm(a, b, ta, tb, None, "none", torch.bfloat16, None, 0.0, cfg + 16 * sp)
+            assert out.dtype == torch.bfloat16 and out.shape == (M, N)
+            assert rel_err(out, ref) < 1e-2, (cfg, sp)
+
+
 @pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (4096, 768, 3072), (200, 64, 136)])
 def test_gemm_addend_epilogue(M, N, K):
     """dx = dy @ W + addend in one GEMM (the residual-stream gradient fused into the data-grad
