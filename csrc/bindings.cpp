@@ -171,6 +171,7 @@ int select(const std::string& k, bool f32, bool wgrad, F&& run) {
 
 // GEMM plans: tile id + 16 * split-K count (0 = heuristic split; accumulating GEMMs only)
 constexpr int kPlanSplit = 16;
+constexpr int kPlanWs = 1024;  // gemm plans: split-K through per-split workspace slices
 std::vector<int> gemm_candidates(bool f32, bool accumulate) {
   std::vector<int> c;
   for (int t : candidates(f32, accumulate)) {
@@ -952,9 +953,24 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
   }();
   const bool splittable = splitk_on && mode == 0 && bias_p == nullptr && act_i == 0 &&
                           add_p == nullptr && !f32 && mipipe::g_deterministic == 0;
+  // Workspace split-K for accumulating GEMMs (weight-grads into the flat fp32 gradient): each
+  // split stores its partial tile into its own slice, splitk_sum adds the slices in order.
+  // Plans with kPlanWs set; chosen by the tuner where the output is small against the CU count
+  // (BERT's 768 x 768 / 768 x 3072 weight-grads: 36-144 tiles) and atomics would cost more.
   auto launch = [&](void* C, int p) {
+    const bool ws_plan = p >= 0 && (p & tune::kPlanWs) != 0;
+    if (ws_plan) p &= ~tune::kPlanWs;
     const int cfg = p < 0 ? -1 : p % tune::kPlanSplit;
     const int sp = p < 0 ? -1 : (p / tune::kPlanSplit > 0 ? p / tune::kPlanSplit : -1);
+    if (ws_plan && mode == 2 && sp > 1) {
+      const int ns = mipipe::gemm_ws_splits((int)K, sp);
+      Tensor ws = torch::empty({(int64_t)ns, M, N}, a.options().dtype(at::kFloat));
+      mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b,
+                   ws.data_ptr(), N, (int)M, (int)N, (int)K, nullptr, 0, 2, stream(), f32, cfg,
+                   sp, nullptr, true);
+      mipipe::splitk_sum(ws.data_ptr<float>(), ns, M * N, static_cast<float*>(C), stream());
+      return;
+    }
     if (splittable && sp > 1) {
       Tensor ws = torch::zeros({M, N}, a.options().dtype(at::kFloat));
       mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b,
@@ -968,6 +984,10 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
   };
   if (plan < 0) {
     std::vector<int> cands = tune::gemm_candidates(f32, mode == 2);
+    if (mode == 2 && K >= 1024) {
+      for (int t : tune::candidates(f32, true))
+        for (int sp : {2, 4, 8}) cands.push_back((t + tune::kPlanSplit * sp) | tune::kPlanWs);
+    }
     if (splittable && K >= 4096) {
       for (int t : tune::candidates(f32, false))
         for (int sp : {2, 4, 8}) cands.push_back(t + tune::kPlanSplit * sp);

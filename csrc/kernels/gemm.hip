@@ -94,14 +94,24 @@ static int plan_splits(uint32_t tiles, int nk, int splits) {
   return std::max(1, std::min(s, 4));
 }
 
+int gemm_ws_splits(int K, int splits) {
+  const int nk = (int)cdiv_u(K, 64);
+  const int per = (int)cdiv_u(nk, std::max(1, std::min(splits, nk)));
+  return (int)cdiv_u(nk, per);
+}
+
 template <class C, class T>
 static void launch_tile(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc,
                         int M, int N, int K, int out, EpiParams e, int splits_req,
-                        hipStream_t st) {
+                        hipStream_t st, bool ws_split) {
   uint32_t tN = cdiv_u(N, C::BN), tiles = cdiv_u(M, C::BM) * tN;
   int nk = (int)cdiv_u(K, 64);
   int splits = 1, per = nk;
-  if (out == 2) {
+  if (out == 2 && ws_split) {  // per-split workspace slices (epilogue_f32's det_rows path)
+    splits = gemm_ws_splits(K, splits_req);
+    per = (int)cdiv_u(nk, splits);
+    e.det_rows = 1;
+  } else if (out == 2) {
     splits = plan_splits(tiles, nk, splits_req);
     per = (int)cdiv_u(nk, splits);
     splits = (int)cdiv_u(nk, per);
@@ -127,11 +137,11 @@ int default_gemm_cfg(int M, int N, bool f32) {
 template <class T>
 static void gemm_t(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, int M,
                    int N, int K, int out, const EpiParams& e, int cfg, int splits,
-                   hipStream_t st) {
+                   hipStream_t st, bool ws_split) {
   if (cfg < 0 || !tile_ok_for<T>(cfg)) cfg = default_gemm_cfg(M, N, std::is_same<T, float>::value);
   auto go = [&](auto tile) {
     typedef decltype(tile) C;
-    launch_tile<C, T>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, splits, st);
+    launch_tile<C, T>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, splits, st, ws_split);
   };
   // fp32-output modes stage BM x BN fp32 in LDS: no 256 x 256 tile there
   if (out == 0 || out == 3) with_tile<T, false>(cfg, go);
@@ -140,15 +150,16 @@ static void gemm_t(const void* A, long lda, bool a_kc, const void* B, long ldb, 
 
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
           long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
-          bool f32, int cfg, int splits, const void* addend) {
+          bool f32, int cfg, int splits, const void* addend, bool ws_split) {
   EpiParams e{};
   e.C = C; e.ldc = ldc; e.M = (uint32_t)M; e.N = (uint32_t)N; e.bias = bias; e.act = act;
   if (addend != nullptr && out == 0 && a_kc && !b_kc) {
     e.addend = addend;
     out = 3;
   }
-  if (f32) gemm_t<float>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st);
-  else gemm_t<__bf16>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st);
+  ws_split = ws_split && out == 2 && splits > 1 && bias == nullptr;
+  if (f32) gemm_t<float>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st, ws_split);
+  else gemm_t<__bf16>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st, ws_split);
 }
 
 }  // namespace mipipe

@@ -155,9 +155,15 @@ void avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho,
 //  cfg: tile config id (conv_common.hpp table; -1 = heuristic); splits (out 2): > 0 forces the
 //  split-K count (1 = no split), -1 = heuristic.  addend (out 0, A [M][K], B [K][N] only): a
 //  [M][ldc] tensor of the output dtype added to the product in the epilogue.
+//  ws_split (out 2, splits > 1): C is a [splits][M][ldc] fp32 WORKSPACE; split s stores its
+//  partial tile into slice s with plain stores (no atomics; the caller sums the slices in order
+//  with splitk_sum) — deterministic, and for small outputs faster than atomics (~1.3 TB/s).
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
           long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
-          bool f32 = false, int cfg = -1, int splits = -1, const void* addend = nullptr);
+          bool f32 = false, int cfg = -1, int splits = -1, const void* addend = nullptr,
+          bool ws_split = false);
+// the split count a ws_split gemm of this K actually uses for `splits` requested
+int gemm_ws_splits(int K, int splits);
 int default_gemm_cfg(int M, int N, bool f32);
 
 // ---- BatchNorm ------------------------------------------------------------------------------

@@ -146,6 +146,16 @@ def test_gemm_every_plan(M, N, K, ta, tb):
             acc0 = acc.clone()
             native().gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0, cfg + 16 * sp)
             assert rel_err(acc - acc0, ref32) < 2e-3, (cfg, sp)
+        for sp in (2, 4, 8):  # workspace split-K (kPlanWs): per-split slices + ordered sum
+            acc = torch.randn(M, N, device=dev)
+            acc0 = acc.clone()
+            native().gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0,
+                          (cfg + 16 * sp) | 1024)
+            assert rel_err(acc - acc0, ref32) < 2e-3, (cfg, sp, "ws")
+            acc2 = acc0.clone()
+            native().gemm(a, b, ta, tb, None, "none", torch.float32, acc2, 1.0,
+                          (cfg + 16 * sp) | 1024)
+            assert torch.equal(acc, acc2), (cfg, sp, "ws split-K must be deterministic")
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 768, 8192), (200, 136, 4104)])
