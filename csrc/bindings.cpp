@@ -1150,7 +1150,9 @@ Tensor gelu_bwd(Tensor dy, Tensor x) {
 
 std::tuple<Tensor, Tensor, Tensor, optional<Tensor>> layernorm_fwd(Tensor x, Tensor gamma,
                                                                    Tensor beta, double eps,
-                                                                   optional<Tensor> res) {
+                                                                   optional<Tensor> res,
+                                                                   double drop_p, int64_t drop_seed,
+                                                                   optional<Tensor> drop_seed_dev) {
   check_bf16(x, "x");
   c10::DeviceGuard g(x.device());
   int64_t H = x.size(-1), rows = x.numel() / H;
@@ -1168,16 +1170,21 @@ std::tuple<Tensor, Tensor, Tensor, optional<Tensor>> layernorm_fwd(Tensor x, Ten
   auto shp = x.sizes().vec();
   shp.pop_back();
   auto mean = torch::empty(shp, o), rstd = torch::empty(shp, o);
+  TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "dropout p must be in [0, 1)");
+  TORCH_CHECK(drop_p == 0.0 || res.has_value(), "fused dropout needs the residual (xsum is saved)");
+  const mipipe::DropSpec ds{(float)drop_p, (uint32_t)drop_seed,
+                            (const uint32_t*)i32_dev(drop_seed_dev, "drop_seed_dev")};
   mipipe::layernorm_fwd(x.data_ptr(), ptr_or_null(res), gamma.data_ptr<float>(),
                         beta.data_ptr<float>(), y.data_ptr(), xs.has_value() ? xs->data_ptr() : nullptr,
                         mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, (int)H, (float)eps,
-                        stream());
+                        stream(), drop_p > 0.0 ? &ds : nullptr);
   return {y, mean, rstd, xs};
 }
 
-std::tuple<Tensor, optional<Tensor>, optional<Tensor>> layernorm_bwd(
+std::tuple<Tensor, optional<Tensor>, optional<Tensor>, optional<Tensor>> layernorm_bwd(
     Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, optional<Tensor> dgamma_acc,
-    optional<Tensor> dbeta_acc) {
+    optional<Tensor> dbeta_acc, double drop_p, int64_t drop_seed,
+    optional<Tensor> drop_seed_dev) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   c10::DeviceGuard g(x.device());
@@ -1200,10 +1207,16 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> layernorm_bwd(
     pb = db->data_ptr<float>();
   }
   auto work = torch::empty({2 * (int64_t)mipipe::layernorm_bwd_blocks(rows), H}, o);
+  TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "dropout p must be in [0, 1)");
+  optional<Tensor> dxd;
+  const mipipe::DropSpec ds{(float)drop_p, (uint32_t)drop_seed,
+                            (const uint32_t*)i32_dev(drop_seed_dev, "drop_seed_dev")};
+  if (drop_p > 0.0) dxd = torch::empty_like(x);
   mipipe::layernorm_bwd(dy.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                         gamma.data_ptr<float>(), dx.data_ptr(), pg, pb, work.data_ptr<float>(),
-                        rows, (int)H, stream());
-  return {dx, dg, db};
+                        rows, (int)H, stream(), dxd.has_value() ? dxd->data_ptr() : nullptr,
+                        drop_p > 0.0 ? &ds : nullptr);
+  return {dx, dg, db, dxd};
 }
 
 Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows, optional<Tensor> out) {
@@ -1671,10 +1684,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("synthetic_batch", &synthetic_batch);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
-  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"),
+        py::arg("eps"), py::arg("res") = py::none(), py::arg("drop_p") = 0.0,
+        py::arg("drop_seed") = 0, py::arg("drop_seed_dev") = py::none());
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("mean"),
         py::arg("rstd"), py::arg("gamma"), py::arg("dgamma") = py::none(),
-        py::arg("dbeta") = py::none());
+        py::arg("dbeta") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,
+        py::arg("drop_seed_dev") = py::none());
   m.def("embedding_bwd", &embedding_bwd, py::arg("dy"), py::arg("idx"), py::arg("num_rows"),
         py::arg("out") = py::none());
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(),

@@ -281,12 +281,21 @@ void stem_bwd_wgrad(const void* xp, const void* y, int N, int Ho, int Hp, const 
                     hipStream_t st);
 
 // ---- transformer ops ------------------------------------------------------------------------
+// Hash dropout of an operand (the mask of dropout_fwd with the same seed / element index).
+struct DropSpec {
+  float p;
+  uint32_t seed;
+  const uint32_t* seed_dev;  // device step counter mixed into the seed (may be null)
+};
+// drop (may be null): y = LN(dropout(x) + res) — BERT's post-LN residual branch in one pass
 void layernorm_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y,
                    void* xsum, float* mean, float* rstd, long rows, int H, float eps,
-                   hipStream_t st);
+                   hipStream_t st, const DropSpec* drop = nullptr);
+// drop + dxd: also writes dxd = dropout'(dx), the dropped branch's gradient
 void layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd,
                    const float* gamma, void* dx, float* dgamma, float* dbeta, float* work,
-                   long rows, int H, hipStream_t st);
+                   long rows, int H, hipStream_t st, void* dxd = nullptr,
+                   const DropSpec* drop = nullptr);
 int layernorm_bwd_blocks(long rows);  // partial rows of layernorm_bwd's work
 void gelu_fwd(const void* x, void* y, long n, hipStream_t st);
 void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st);

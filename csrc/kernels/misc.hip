@@ -599,10 +599,52 @@ void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H
                      (const __bf16*)dy, idx, out, n, H);
 }
 
+// ------------------------------------------------------------------------------ dropout hash
+// keep(element i) = hash(seed, i) >= p * 2^32; the per-step part of a device seed (graph replay)
+// is mixed in from seed_dev.  Shared by the standalone dropout kernel and the LayerNorm kernels
+// that fuse the residual branch's dropout (identical masks: same element index, same hash).
+__device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
+  x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t drop_base(uint32_t seed, const uint32_t* seed_dev) {
+  if (seed_dev != nullptr) {  // L2-served agent-scope load (see attention.hip eff_seed)
+    const uint32_t c = __hip_atomic_load(seed_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    seed = drop_mix(seed ^ (c * 0x9e3779b1u + 0x632be5abu));
+  }
+  return drop_mix(seed * 0x9e3779b1u + 0x7f4a7c15u);
+}
+
+__device__ __forceinline__ bool drop_keep(uint32_t base, long idx, uint32_t thr) {
+  return drop_mix(base ^ (uint32_t)idx * 0x85ebca77u) >= thr;
+}
+
+struct DropArgs {  // by value into the kernels; thr == 0 and scale == 1 when p == 0
+  float scale;
+  uint32_t thr, seed;
+  const uint32_t* seed_dev;
+};
+
+static DropArgs drop_args(const DropSpec* d) {
+  DropArgs a{1.f, 0u, 0u, nullptr};
+  if (d != nullptr && d->p > 0.f) {
+    const double t = (double)d->p * 4294967296.0;
+    a.thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+    a.scale = 1.f / (1.f - d->p);
+    a.seed = d->seed;
+    a.seed_dev = d->seed_dev;
+  }
+  return a;
+}
+
 // ------------------------------------------------------------------------------ LayerNorm
 // One wave per row, up to 4 x 8 elements per lane (H <= 2048), H % 8 == 0.
+// DROP: y = LN(dropout(x) + res) — the post-LN residual branch's dropout applied on the load of x
+// (the dropped tensor is never stored; the stored sum is what the backward normalises).
 constexpr int LN_MAXC = 4;
 
+template <bool DROP>
 __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const __bf16* __restrict__ x,
                                                             const __bf16* __restrict__ res,
                                                             const float* __restrict__ gamma,
@@ -611,11 +653,12 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const __bf16* __rest
                                                             __bf16* __restrict__ xsum,
                                                             float* __restrict__ mean,
                                                             float* __restrict__ rstd, long rows,
-                                                            int H, float eps) {
+                                                            int H, float eps, DropArgs dr) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int nc = H / 8;
+  const uint32_t dbase = DROP ? drop_base(dr.seed, dr.seed_dev) : 0u;
   float v[LN_MAXC][8];
   float s = 0.f;
 #pragma unroll
@@ -623,6 +666,14 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const __bf16* __rest
     int c = lane + k * 64;
     if (c < nc) {
       unpack8(*reinterpret_cast<const uint4*>(x + row * H + c * 8), v[k]);
+      if constexpr (DROP) {
+        // the standalone kernel rounds the dropped value to bf16: same here, same sums
+        float t[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          t[q] = drop_keep(dbase, row * H + c * 8 + q, dr.thr) ? v[k][q] * dr.scale : 0.f;
+        unpack8(pack8(t), v[k]);
+      }
       if (res != nullptr) {
         float r[8];
         unpack8(*reinterpret_cast<const uint4*>(res + row * H + c * 8), r);
@@ -667,17 +718,24 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const __bf16* __rest
 
 void layernorm_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y,
                    void* xsum, float* mean, float* rstd, long rows, int H, float eps,
-                   hipStream_t st) {
-  hipLaunchKernelGGL(layernorm_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, st,
-                     (const __bf16*)x, (const __bf16*)res, gamma, beta, (__bf16*)y,
-                     (__bf16*)xsum, mean, rstd, rows, H, eps);
+                   hipStream_t st, const DropSpec* drop) {
+  const DropArgs dr = drop_args(drop);
+  if (dr.thr != 0u)
+    hipLaunchKernelGGL(layernorm_fwd_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, st,
+                       (const __bf16*)x, (const __bf16*)res, gamma, beta, (__bf16*)y,
+                       (__bf16*)xsum, mean, rstd, rows, H, eps, dr);
+  else
+    hipLaunchKernelGGL(layernorm_fwd_kernel<false>, dim3((rows + 3) / 4), dim3(256), 0, st,
+                       (const __bf16*)x, (const __bf16*)res, gamma, beta, (__bf16*)y,
+                       (__bf16*)xsum, mean, rstd, rows, H, eps, dr);
 }
 
 // dx = rstd*(g*γ - mean(g*γ) - x̂*mean(g*γ*x̂)); per-block partials of Σg·x̂ and Σg for dγ, dβ.
 // Each wave walks rows w, w+4, ... of its block with the NEXT row's dy / x loads in flight while
 // it reduces the current one (the kernel is latency-bound otherwise: two dependent wave sums
 // per row); γ is held in registers for the whole block.
-template <int NCH>
+// DROP: also dxd = dropout'(dx) — the gradient of the dropped branch (the residual keeps dx).
+template <int NCH, bool DROP>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __restrict__ dy,
                                                             const __bf16* __restrict__ x,
                                                             const float* __restrict__ mean,
@@ -686,8 +744,10 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
                                                             __bf16* __restrict__ dx,
                                                             float* __restrict__ pg,
                                                             float* __restrict__ pb, long rows,
-                                                            int H, int rows_per_block) {
+                                                            int H, int rows_per_block,
+                                                            __bf16* __restrict__ dxd, DropArgs dr) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t dbase = DROP ? drop_base(dr.seed, dr.seed_dev) : 0u;
   const int nc = H / 8;
   float accg[NCH][8], accb[NCH][8], gam[NCH][8];
 #pragma unroll
@@ -751,7 +811,16 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
         float o[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) o[q] = rs * (g[k][q] * gam[k][q] - s1 - xh[k][q] * s2);
-        *reinterpret_cast<uint4*>(dx + row * H + c * 8) = pack8(o);
+        const uint4 ob = pack8(o);
+        *reinterpret_cast<uint4*>(dx + row * H + c * 8) = ob;
+        if constexpr (DROP) {  // from the bf16-rounded dx, as the standalone kernel would see it
+          float od[8];
+          unpack8(ob, od);
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            od[q] = drop_keep(dbase, row * H + c * 8 + q, dr.thr) ? od[q] * dr.scale : 0.f;
+          *reinterpret_cast<uint4*>(dxd + row * H + c * 8) = pack8(od);
+        }
       }
     }
   }
@@ -790,7 +859,7 @@ int layernorm_bwd_blocks(long rows) {
 
 void layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd,
                    const float* gamma, void* dx, float* dgamma, float* dbeta, float* work,
-                   long rows, int H, hipStream_t st) {
+                   long rows, int H, hipStream_t st, void* dxd, const DropSpec* drop) {
   // dgamma / dbeta are ACCUMULATED into (zeroed buffers or the flat gradient views) from the
   // per-block partial rows in work ([2][layernorm_bwd_blocks(rows)][H])
   int G, rpb;
@@ -798,40 +867,38 @@ void layernorm_bwd(const void* dy, const void* x, const float* mean, const float
   float* wg = work;
   float* wb = work + (long)G * H;
   // register arrays sized for H: 2 chunks of 8 per lane up to H = 1024 (BERT-base), else 4
-  if (H <= 1024)
-    hipLaunchKernelGGL(layernorm_bwd_kernel<2>, dim3(G), dim3(256), 0, st, (const __bf16*)dy,
-                       (const __bf16*)x, mean, rstd, gamma, (__bf16*)dx, wg, wb, rows, H, rpb);
-  else
-    hipLaunchKernelGGL(layernorm_bwd_kernel<LN_MAXC>, dim3(G), dim3(256), 0, st,
+  const DropArgs dr = drop_args(drop);
+  const bool dp = dr.thr != 0u && dxd != nullptr;
+  auto go = [&](auto nch, auto drop_c) {
+    constexpr int NCH = decltype(nch)::value;
+    constexpr bool DROP = decltype(drop_c)::value;
+    hipLaunchKernelGGL((layernorm_bwd_kernel<NCH, DROP>), dim3(G), dim3(256), 0, st,
                        (const __bf16*)dy, (const __bf16*)x, mean, rstd, gamma, (__bf16*)dx, wg,
-                       wb, rows, H, rpb);
+                       wb, rows, H, rpb, (__bf16*)dxd, dr);
+  };
+  if (H <= 1024) {
+    if (dp) go(std::integral_constant<int, 2>(), std::true_type());
+    else go(std::integral_constant<int, 2>(), std::false_type());
+  } else {
+    if (dp) go(std::integral_constant<int, LN_MAXC>(), std::true_type());
+    else go(std::integral_constant<int, LN_MAXC>(), std::false_type());
+  }
   det_sum_rows(wg, wb, G, H, dgamma, dbeta, true, st);
 }
 
 // ------------------------------------------------------------------------------ dropout
-__device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
-  x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16;
-  return x;
-}
 
 __global__ __launch_bounds__(256) void dropout_kernel(const __bf16* __restrict__ x,
                                                       __bf16* __restrict__ y, long n8, float scale,
                                                       uint32_t thr, uint32_t seed,
                                                       const uint32_t* __restrict__ seed_dev) {
-  if (seed_dev != nullptr) {  // L2-served agent-scope load (see attention.hip eff_seed)
-    const uint32_t c = __hip_atomic_load(seed_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    seed = drop_mix(seed ^ (c * 0x9e3779b1u + 0x632be5abu));
-  }
+  const uint32_t base = drop_base(seed, seed_dev);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
        i += (long)gridDim.x * blockDim.x) {
     float f[8];
     unpack8(reinterpret_cast<const uint4*>(x)[i], f);
-    const uint32_t base = drop_mix(seed * 0x9e3779b1u + 0x7f4a7c15u);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint32_t hsh = drop_mix(base ^ (uint32_t)(i * 8 + e) * 0x85ebca77u);
-      f[e] = hsh >= thr ? f[e] * scale : 0.f;
-    }
+    for (int e = 0; e < 8; ++e) f[e] = drop_keep(base, i * 8 + e, thr) ? f[e] * scale : 0.f;
     reinterpret_cast<uint4*>(y)[i] = pack8(f);
   }
 }

@@ -107,12 +107,14 @@ class BertLayer(tnn.Module):
         ctx = MF.attention(qkv, B, S, self.heads, mask, p_drop=self.p_attn if train else 0.0,
                            seed=seeds[0])
         a = self.attention.output.dense(ctx)
-        a = MF.dropout(a, self.p_hidden, seeds[1], train)
-        h1 = self.attention.output.LayerNorm(a, residual=h, res_give=s_h)
+        # hidden dropout fused into the post-LN residual kernels (same mask as MF.dropout)
+        p = self.p_hidden if train else 0.0
+        h1 = self.attention.output.LayerNorm(a, residual=h, res_give=s_h, dropout_p=p,
+                                             dropout_seed=seeds[1])
         f = self.intermediate.dense(h1, act="gelu", res_take=s_h1)
         f2 = self.output.dense(f)
-        f2 = MF.dropout(f2, self.p_hidden, seeds[2], train)
-        return self.output.LayerNorm(f2, residual=h1, res_give=s_h1)
+        return self.output.LayerNorm(f2, residual=h1, res_give=s_h1, dropout_p=p,
+                                     dropout_seed=seeds[2])
 
 
 class _Encoder(tnn.Module):

@@ -297,8 +297,10 @@ class Embedding(ShadowMixin, tnn.Embedding):
 
 class LayerNorm(tnn.LayerNorm):
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                res_give=None) -> torch.Tensor:
-        return MF.layer_norm(x, self.weight, self.bias, self.eps, residual, res_give)
+                res_give=None, dropout_p: float = 0.0, dropout_seed=None) -> torch.Tensor:
+        """LN(dropout(x) [+ residual]); the dropout is fused into the LayerNorm kernels."""
+        return MF.layer_norm(x, self.weight, self.bias, self.eps, residual, res_give,
+                             dropout_p, dropout_seed)
 
 
 class Dropout(tnn.Dropout):

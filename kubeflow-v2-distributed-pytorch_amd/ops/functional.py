@@ -959,12 +959,13 @@ def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0,
 # ----------------------------------------------------------------------------- transformer ops
 class _LayerNormFn(Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps, residual, res_give):
-        y, mean, rstd, xs = K.layernorm_fwd(x, gamma, beta, eps, residual)
+    def forward(ctx, x, gamma, beta, eps, residual, res_give, drop):
+        y, mean, rstd, xs = K.layernorm_fwd(x, gamma, beta, eps, residual, drop)
         ctx.save_for_backward(x if xs is None else xs, mean, rstd, gamma)
         ctx.beta = beta
         ctx.has_res = residual is not None
         ctx.res_give = res_give
+        ctx.drop = drop
         return y
 
     @staticmethod
@@ -975,26 +976,39 @@ class _LayerNormFn(Function):
             tg, tb = _direct_grad_target(gamma), _direct_grad_target(ctx.beta)
             if tg is not None and tb is not None:
                 acc = (tg[1], tb[1])
-        dx, dgamma, dbeta = K.layernorm_bwd(dy.contiguous(), x, mean, rstd, gamma, acc)
+        dx, dgamma, dbeta, dxd = K.layernorm_bwd(dy.contiguous(), x, mean, rstd, gamma, acc,
+                                                 ctx.drop)
         dres = None
         if ctx.has_res:
             # d/d residual = d/dx; handed to the residual's other consumer when it fuses the add
             dres = ctx.res_give.produce(dx) if ctx.res_give is not None else dx
+        dxin = dxd if dxd is not None else dx  # fused dropout: the dropped branch's gradient
         if acc is not None:
             fs = _direct_grad_target(gamma)[0]
             fs.grad_ready(gamma)
             fs.grad_ready(ctx.beta)
-            return dx, None, None, None, dres, None
-        return dx, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), None, dres, None
+            return dxin, None, None, None, dres, None, None
+        return dxin, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), None, dres, None, None
 
 
 def layer_norm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float = 1e-12,
                residual: Optional[Tensor] = None,
-               res_give: Optional["ResidualSlot"] = None) -> Tensor:
-    """LN(x [+ residual]) — the BERT post-LN residual add fused into the norm.  ``res_give``:
-    the residual's gradient goes to the slot (for the residual's other consumer to add in its
-    own kernel) instead of through autograd."""
-    return _LayerNormFn.apply(x, gamma, beta, eps, residual, res_give)
+               res_give: Optional["ResidualSlot"] = None, dropout_p: float = 0.0,
+               dropout_seed=None) -> Tensor:
+    """LN(dropout(x) [+ residual]) — BERT's post-LN residual branch (dropout, add, norm) in one
+    kernel each way.  ``res_give``: the residual's gradient goes to the slot (for the residual's
+    other consumer to add in its own kernel) instead of through autograd.  ``dropout_p`` > 0
+    (with ``residual``): the branch's dropout, mask identical to :func:`dropout` with that
+    seed."""
+    drop = None
+    if dropout_p > 0.0:
+        if residual is None:
+            x = dropout(x, dropout_p, dropout_seed)
+        else:
+            seed = dropout_seed if isinstance(dropout_seed, K.DevSeed) \
+                else int(dropout_seed) & 0xFFFFFFFF
+            drop = (float(dropout_p), seed)
+    return _LayerNormFn.apply(x, gamma, beta, eps, residual, res_give, drop)
 
 
 class _GeluFn(Function):

@@ -345,24 +345,36 @@ def adamw_step(param, grad, exp_avg, exp_avg_sq, shadow, lr, beta1, beta2, eps, 
                            weight_decay, step, grad_scale)
 
 
-def layernorm_fwd(x, gamma, beta, eps, residual=None):
+def layernorm_fwd(x, gamma, beta, eps, residual=None, drop=None):
+    """-> (y, mean, rstd, xsum).  ``drop=(p, seed)`` (needs ``residual``): y = LN(dropout(x) +
+    residual), the dropout mask being :func:`dropout_fwd`'s for that seed."""
     if use_native(x):
+        if drop is not None and drop[0] > 0.0:
+            sd, dev = _split_seed(drop[1])
+            return native().layernorm_fwd(x, gamma, beta, eps, residual, drop[0], sd, dev)
         return native().layernorm_fwd(x, gamma, beta, eps, residual)
+    if drop is not None and drop[0] > 0.0:
+        x = dropout_fwd(x, drop[0], drop[1])
     return _ref.layernorm_fwd(x, gamma, beta, eps, residual)
 
 
-def layernorm_bwd(dy, x, mean, rstd, gamma, acc=None):
-    """-> (dx, dgamma, dbeta); with ``acc=(dgamma_buf, dbeta_buf)`` the parameter grads are
-    accumulated into those buffers and returned as None."""
+def layernorm_bwd(dy, x, mean, rstd, gamma, acc=None, drop=None):
+    """-> (dx, dgamma, dbeta, dxd); with ``acc=(dgamma_buf, dbeta_buf)`` the parameter grads are
+    accumulated into those buffers and returned as None.  ``drop=(p, seed)``: dxd = dropout'(dx),
+    the gradient of the dropped branch (else None)."""
     if use_native(dy):
         a = acc if acc is not None else (None, None)
+        if drop is not None and drop[0] > 0.0:
+            sd, dev = _split_seed(drop[1])
+            return native().layernorm_bwd(dy, x, mean, rstd, gamma, *a, drop[0], sd, dev)
         return native().layernorm_bwd(dy, x, mean, rstd, gamma, *a)
     dx, dg, db = _ref.layernorm_bwd(dy, x, mean, rstd, gamma)
+    dxd = dropout_fwd(dx, drop[0], drop[1]) if drop is not None and drop[0] > 0.0 else None
     if acc is not None:
         acc[0].add_(dg.to(acc[0].dtype))
         acc[1].add_(db.to(acc[1].dtype))
-        return dx, None, None
-    return dx, dg, db
+        return dx, None, None, dxd
+    return dx, dg, db, dxd
 
 
 def colsum(x, out=None):

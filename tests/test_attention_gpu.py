@@ -293,3 +293,29 @@ def test_bert_graphed_step_matches_eager():
         if not d_pq <= max(0.02 * upd, 3 * d_pr) + 1e-6:
             bad.append((n, d_pq, d_pr, upd))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("dev_seed", [False, True])
+def test_layernorm_fused_dropout_matches_unfused(dev_seed):
+    """LN(dropout(x) + res) in one kernel == dropout kernel then LN kernel, bit for bit, forward
+    (y, mean, rstd, the saved sum) and backward (dx for the residual, dropout'(dx) for x), with a
+    host seed and with a device-counter seed (graph replay)."""
+    from mipipe.ops import kernels as K
+    torch.manual_seed(3)
+    x = torch.randn(512, 768, device="cuda").to(torch.bfloat16)
+    res = torch.randn(512, 768, device="cuda").to(torch.bfloat16)
+    gamma = torch.rand(768, device="cuda") + 0.5
+    beta = torch.randn(768, device="cuda")
+    seed = K.DevSeed(77, torch.full((1,), 5, dtype=torch.int32, device="cuda")) if dev_seed else 77
+    y0, m0, r0, s0 = K.layernorm_fwd(K.dropout_fwd(x, 0.1, seed), gamma, beta, 1e-12, res)
+    y1, m1, r1, s1 = K.layernorm_fwd(x, gamma, beta, 1e-12, res, (0.1, seed))
+    for a, b in ((y0, y1), (m0, m1), (r0, r1), (s0, s1)):
+        assert torch.equal(a, b)
+    dy = torch.randn(512, 768, device="cuda").to(torch.bfloat16)
+    dx0, g0, b0, _ = K.layernorm_bwd(dy, s0, m0, r0, gamma)
+    dxd0 = K.dropout_fwd(dx0, 0.1, seed)
+    dx1, g1, b1, dxd1 = K.layernorm_bwd(dy, s1, m1, r1, gamma, None, (0.1, seed))
+    for a, b in ((dx0, dx1), (g0, g1), (b0, b1), (dxd0, dxd1)):
+        assert torch.equal(a, b)
+    keep = (dxd1 != 0).float().mean().item()
+    assert 0.88 < keep < 0.92
