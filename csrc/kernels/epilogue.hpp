@@ -125,6 +125,13 @@ constexpr int kEpiLdsBytes() { return kStatsLdsOffset<BM, BN, T>() + 2 * WM * BN
 // (Priming it before a short main loop was measured slower in round 2: the seven ResNet-50
 // layer-1 1x1 data-grads went from ~1.9 ms to 3.4 ms per step — the early loads stretch the main
 // loop's vmcnt waits and the registers' lifetime.)
+// The loads are UNCONDITIONAL: an absent stream reads a 16-B zero line (g_epi_zero, L1/L2
+// resident) instead of sitting behind `if (ptr != nullptr)`.  A load behind a runtime branch
+// made hipcc close every ring slot with `s_waitcnt vmcnt(0)` right after issuing it (round 3,
+// .s of the two-branch data-grad: 126 full drains), serialising the prefetch ring into one
+// memory latency per 16-B chunk.
+__device__ __attribute__((aligned(64))) uint4 g_epi_zero[4];
+
 template <int BM, int BN, bool FUSE, class T, int WM, int WN, bool TWO = false>
 struct EpiOps {
   static constexpr int kThreads = 64 * WM * WN;
@@ -133,6 +140,27 @@ struct EpiOps {
   static constexpr int PF = FUSE ? (ITER < 4 ? ITER : 4) : 1;
   Raw8<T> ad[PF], y[PF], z[PF], y2[TWO ? PF : 1];
   uint32_t mk[PF];
+  // stream bases (the zero line when absent) and row strides (0 when absent): wave-uniform
+  const T *p_ad, *p_y, *p_z, *p_y2;
+  const uint8_t* p_mk;
+  long s_ad, s_y, s_z, s_y2, s_mk;
+  __device__ __forceinline__ void setup(const EpiParams& e) {
+    const T* zt = reinterpret_cast<const T*>(g_epi_zero);
+    const bool bnr = e.bnr_rep != nullptr;
+    p_ad = e.addend != nullptr ? reinterpret_cast<const T*>(e.addend) : zt;
+    s_ad = e.addend != nullptr ? e.ldc : 0;
+    p_y = bnr ? reinterpret_cast<const T*>(e.bnr_y) : zt;
+    s_y = bnr ? e.ldc : 0;
+    const bool zl = bnr && e.bnr_mask == nullptr && e.bnr_z != nullptr;
+    p_z = zl ? reinterpret_cast<const T*>(e.bnr_z) : zt;
+    s_z = zl ? e.ldc : 0;
+    const bool y2l = TWO && bnr && e.bnr_y2 != nullptr;
+    p_y2 = y2l ? reinterpret_cast<const T*>(e.bnr_y2) : zt;
+    s_y2 = y2l ? e.ldc : 0;
+    const bool ml = bnr && e.bnr_mask != nullptr;
+    p_mk = ml ? e.bnr_mask : reinterpret_cast<const uint8_t*>(g_epi_zero);
+    s_mk = ml ? e.ldc / 8 : 0;
+  }
   __device__ __forceinline__ void issue(const EpiParams& e, uint32_t m0, uint32_t n0, int it,
                                         int slot) {
     const uint32_t my_n = n0 + (threadIdx.x % CPR) * 8;
@@ -140,18 +168,15 @@ struct EpiOps {
     const uint32_t r = (threadIdx.x + it * kThreads) / CPR;
     const uint32_t m = min(m0 + r, e.M - 1);
     const long orow = out_row(e, m);
-    if (e.addend != nullptr) ad[slot] = ld_raw8(reinterpret_cast<const T*>(e.addend) + orow * e.ldc + ld_n);
-    if (e.bnr_rep != nullptr) {
-      y[slot] = ld_raw8(reinterpret_cast<const T*>(e.bnr_y) + orow * e.ldc + ld_n);
-      if constexpr (TWO)
-        y2[slot] = ld_raw8(reinterpret_cast<const T*>(e.bnr_y2) + orow * e.ldc + ld_n);
-      if (e.bnr_mask != nullptr)
-        mk[slot] = e.bnr_mask[orow * (e.ldc / 8) + ld_n / 8];
-      else if (e.bnr_z != nullptr)
-        z[slot] = ld_raw8(reinterpret_cast<const T*>(e.bnr_z) + orow * e.ldc + ld_n);
-    }
+    const long col_ad = s_ad != 0 ? (long)ld_n : 0, col_y = s_y != 0 ? (long)ld_n : 0;
+    ad[slot] = ld_raw8(p_ad + orow * s_ad + col_ad);
+    y[slot] = ld_raw8(p_y + orow * s_y + col_y);
+    z[slot] = ld_raw8(p_z + orow * s_z + (s_z != 0 ? (long)ld_n : 0));
+    if constexpr (TWO) y2[slot] = ld_raw8(p_y2 + orow * s_y2 + (s_y2 != 0 ? (long)ld_n : 0));
+    mk[slot] = p_mk[orow * s_mk + (s_mk != 0 ? (long)(ld_n / 8) : 0)];
   }
   __device__ __forceinline__ void prime(const EpiParams& e, uint32_t m0, uint32_t n0) {
+    setup(e);
     if (FUSE && (e.addend != nullptr || e.bnr_rep != nullptr)) {
 #pragma unroll
       for (int it = 0; it < PF; ++it) issue(e, m0, n0, it, it);
@@ -322,55 +347,63 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
   float sg[8], sgx[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) sg[q] = sgx[q] = 0.f;
+  if (FUSE && (has_add || bnr)) {
+    // fused loop: the ring's next loads are issued unconditionally (absent streams read the
+    // zero line), so hipcc keeps PF iterations of loads in flight with counted waits
 #pragma unroll
-  for (int it = 0; it < ITER; ++it) {
-    const int c = threadIdx.x + it * kThreads;
-    const uint32_t r = c / CPR, cc = c % CPR;
-    const uint32_t m = m0 + r, n = n0 + cc * 8;
-    if (m < e.M && n < e.N) {
+    for (int it = 0; it < ITER; ++it) {
+      const int c = threadIdx.x + it * kThreads;
+      const uint32_t r = c / CPR, cc = c % CPR;
+      const uint32_t m = m0 + r, n = n0 + cc * 8;
       Raw8<T> v;
 #pragma unroll
       for (int h = 0; h < (int)(sizeof(T) / 2); ++h)
         v.v[h] = *reinterpret_cast<const uint4*>(smem + r * P + cc * 8 * sizeof(T) + 16 * h);
-      const long orow = out_row(e, m);
-      if (FUSE && (has_add || bnr)) {
-        float f[8];
-        unpack_raw(v, f);
-        if (has_add) {
-          float a[8];
-          unpack_raw(ops.ad[it % PF], a);
+      float f[8], a[8];
+      unpack_raw(v, f);
+      unpack_raw(ops.ad[it % PF], a);  // zeros when there is no addend
 #pragma unroll
-          for (int q = 0; q < 8; ++q) f[q] += a[q];
+      for (int q = 0; q < 8; ++q) f[q] += a[q];
+      const bool ok = m < e.M && n < e.N;
+      if (bnr) {
+        float yv[8], zv[8];
+        unpack_raw(ops.y[it % PF], yv);
+        unpack_raw(ops.z[it % PF], zv);
+        const uint32_t bits = ops.mk[it % PF];
+        const float w = ok ? 1.f : 0.f;  // rows past M add nothing to the sums
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float zq = bmask ? (float)((bits >> q) & 1u)
+                                 : (zmask ? zv[q] : yv[q] * b_sc[q] + b_bi[q]);
+          const float gq = zq > 0.f ? as_stored<T>(f[q]) : 0.f;  // stats of the stored g
+          f[q] = gq;
+          sg[q] += w * gq;
+          sgx[q] += w * gq * (yv[q] - b_mu[q]) * b_is[q];
         }
-        if (bnr) {
-          float yv[8], zv[8];
-          unpack_raw(ops.y[it % PF], yv);
-          if (zmask) unpack_raw(ops.z[it % PF], zv);
-          const uint32_t bits = bmask ? ops.mk[it % PF] : 0u;
+        if constexpr (TWO) {
+          float y2v[8];
+          unpack_raw(ops.y2[it % PF], y2v);
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const float zq = bmask ? (float)((bits >> q) & 1u)
-                                   : (zmask ? zv[q] : yv[q] * b_sc[q] + b_bi[q]);
-            const float gq = zq > 0.f ? as_stored<T>(f[q]) : 0.f;  // stats of the stored g
-            f[q] = gq;
-            sg[q] += gq;
-            sgx[q] += gq * (yv[q] - b_mu[q]) * b_is[q];
-          }
-          if constexpr (TWO) {
-            float y2v[8];
-            unpack_raw(ops.y2[it % PF], y2v);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) sgx2[q] += f[q] * (y2v[q] - b_mu2[q]) * b_is2[q];
-          }
+          for (int q = 0; q < 8; ++q) sgx2[q] += w * f[q] * (y2v[q] - b_mu2[q]) * b_is2[q];
         }
-        store8(C + orow * e.ldc + n, f);
-      } else {
+      }
+      if (ok) store8(C + out_row(e, m) * e.ldc + n, f);
+      if (it + PF < ITER) ops.issue(e, m0, n0, it + PF, it % PF);
+    }
+  } else {
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int c = threadIdx.x + it * kThreads;
+      const uint32_t r = c / CPR, cc = c % CPR;
+      const uint32_t m = m0 + r, n = n0 + cc * 8;
+      if (m < e.M && n < e.N) {
+        const long orow = out_row(e, m);
 #pragma unroll
         for (int h = 0; h < (int)(sizeof(T) / 2); ++h)
-          reinterpret_cast<uint4*>(C + orow * e.ldc + n)[h] = v.v[h];
+          reinterpret_cast<uint4*>(C + orow * e.ldc + n)[h] =
+              *reinterpret_cast<const uint4*>(smem + r * P + cc * 8 * sizeof(T) + 16 * h);
       }
     }
-    if (FUSE && (has_add || bnr) && it + PF < ITER) ops.issue(e, m0, n0, it + PF, it % PF);
   }
   if (FUSE && bnr) {
     // threads t, t+CPR, ... share a column chunk: reduce them through LDS, then one atomic
