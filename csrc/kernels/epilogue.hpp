@@ -252,8 +252,11 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
       uint32_t n = n0 + nl0 + j * 16;
       float b[4] = {0.f, 0.f, 0.f, 0.f};
       if (e.bias != nullptr) {
+        // unconditional loads at a clamped column (N % 4 == 0: a quad is all in or all out);
+        // a load behind a per-element branch costs a vmcnt(0) drain each (see EpiOps)
+        const uint32_t nc = n < e.N ? n : 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) b[q] = (n + q < e.N) ? e.bias[n + q] : 0.f;
+        for (int q = 0; q < 4; ++q) b[q] = n < e.N ? e.bias[nc + q] : 0.f;
       }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
@@ -273,8 +276,9 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
     for (int j = 0; j < NT; ++j) {
       uint32_t n = n0 + nl0 + j * 16;
       float sh[4];
+      const uint32_t nc = n < e.N ? n : 0;  // clamped: unconditional loads (see the bias above)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) sh[q] = (n + q < e.N) ? e.st_shift[n + q] : 0.f;
+      for (int q = 0; q < 4; ++q) sh[q] = e.st_shift[nc + q];
       float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < MT; ++i) {

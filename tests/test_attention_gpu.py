@@ -288,7 +288,15 @@ def test_bert_graphed_step_matches_eager():
     bad = []
     for (n, p), (_, q), (_, r) in zip(a.named_parameters(), b.named_parameters(),
                                        c.named_parameters()):
-        upd = float((p - init[n]).norm())
+        if n.endswith("qkv.bias"):
+            # the KEY bias has an exactly-zero gradient (softmax is shift-invariant per query):
+            # its AdamW updates are pure rounding noise amplified to ±lr steps — compare Q and V
+            H = p.shape[0] // 3
+            keep = torch.cat([torch.arange(0, H), torch.arange(2 * H, 3 * H)]).to(p.device)
+            p, q, r, i0 = p[keep], q[keep], r[keep], init[n][keep]
+        else:
+            i0 = init[n]
+        upd = float((p - i0).norm())
         d_pq, d_pr = float((p - q).norm()), float((p - r).norm())
         if not d_pq <= max(0.02 * upd, 3 * d_pr) + 1e-6:
             bad.append((n, d_pq, d_pr, upd))
