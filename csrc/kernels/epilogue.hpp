@@ -247,17 +247,24 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
   }
   // bias / activation
   if (e.bias != nullptr || e.act) {
+    // every bias quad loaded before use, at a clamped column (N % 4 == 0: a quad is all in or
+    // all out; the zero line when there is no bias): loads behind per-element branches cost a
+    // vmcnt(0) drain each (see EpiOps)
+    float bv[NT][4];
+    const float* bp = e.bias != nullptr ? e.bias : reinterpret_cast<const float*>(g_epi_zero);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const uint32_t n = n0 + nl0 + j * 16;
+      const uint32_t nc = (e.bias != nullptr && n < e.N) ? n : 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[j][q] = bp[nc + q];
+    }
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       uint32_t n = n0 + nl0 + j * 16;
-      float b[4] = {0.f, 0.f, 0.f, 0.f};
-      if (e.bias != nullptr) {
-        // unconditional loads at a clamped column (N % 4 == 0: a quad is all in or all out);
-        // a load behind a per-element branch costs a vmcnt(0) drain each (see EpiOps)
-        const uint32_t nc = n < e.N ? n : 0;
+      float b[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) b[q] = n < e.N ? e.bias[nc + q] : 0.f;
-      }
+      for (int q = 0; q < 4; ++q) b[q] = n < e.N ? bv[j][q] : 0.f;
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -272,13 +279,20 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
   // wave-instructions, no per-block partial rows to reduce later.
   if (e.st_sum != nullptr) {
     float* lst = reinterpret_cast<float*>(smem + kStatsLdsOffset<BM, BN, T>());  // [2][WM][BN]
+    // every column's shift requested before any is used (clamped column: unconditional loads),
+    // so the block waits one memory latency here, not one per 16-column group
+    float shv[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const uint32_t n = n0 + nl0 + j * 16;
+      const uint32_t nc = n < e.N ? n : 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) shv[j][q] = e.st_shift[nc + q];
+    }
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       uint32_t n = n0 + nl0 + j * 16;
-      float sh[4];
-      const uint32_t nc = n < e.N ? n : 0;  // clamped: unconditional loads (see the bias above)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sh[q] = e.st_shift[nc + q];
+      const float* sh = shv[j];
       float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
