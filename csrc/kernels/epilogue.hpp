@@ -140,26 +140,23 @@ struct EpiOps {
   static constexpr int PF = FUSE ? (ITER < 4 ? ITER : 4) : 1;
   Raw8<T> ad[PF], y[PF], z[PF], y2[TWO ? PF : 1];
   uint32_t mk[PF];
-  // stream bases (the zero line when absent) and row strides (0 when absent): wave-uniform
+  // stream bases (the zero line when absent) and presence flags: wave-uniform
   const T *p_ad, *p_y, *p_z, *p_y2;
   const uint8_t* p_mk;
-  long s_ad, s_y, s_z, s_y2, s_mk;
+  bool h_ad, h_y, h_z, h_y2, h_mk;
   __device__ __forceinline__ void setup(const EpiParams& e) {
     const T* zt = reinterpret_cast<const T*>(g_epi_zero);
     const bool bnr = e.bnr_rep != nullptr;
-    p_ad = e.addend != nullptr ? reinterpret_cast<const T*>(e.addend) : zt;
-    s_ad = e.addend != nullptr ? e.ldc : 0;
-    p_y = bnr ? reinterpret_cast<const T*>(e.bnr_y) : zt;
-    s_y = bnr ? e.ldc : 0;
-    const bool zl = bnr && e.bnr_mask == nullptr && e.bnr_z != nullptr;
-    p_z = zl ? reinterpret_cast<const T*>(e.bnr_z) : zt;
-    s_z = zl ? e.ldc : 0;
-    const bool y2l = TWO && bnr && e.bnr_y2 != nullptr;
-    p_y2 = y2l ? reinterpret_cast<const T*>(e.bnr_y2) : zt;
-    s_y2 = y2l ? e.ldc : 0;
-    const bool ml = bnr && e.bnr_mask != nullptr;
-    p_mk = ml ? e.bnr_mask : reinterpret_cast<const uint8_t*>(g_epi_zero);
-    s_mk = ml ? e.ldc / 8 : 0;
+    h_ad = e.addend != nullptr;
+    h_y = bnr;
+    h_z = bnr && e.bnr_mask == nullptr && e.bnr_z != nullptr;
+    h_y2 = TWO && bnr && e.bnr_y2 != nullptr;
+    h_mk = bnr && e.bnr_mask != nullptr;
+    p_ad = h_ad ? reinterpret_cast<const T*>(e.addend) : zt;
+    p_y = h_y ? reinterpret_cast<const T*>(e.bnr_y) : zt;
+    p_z = h_z ? reinterpret_cast<const T*>(e.bnr_z) : zt;
+    p_y2 = h_y2 ? reinterpret_cast<const T*>(e.bnr_y2) : zt;
+    p_mk = h_mk ? e.bnr_mask : reinterpret_cast<const uint8_t*>(g_epi_zero);
   }
   __device__ __forceinline__ void issue(const EpiParams& e, uint32_t m0, uint32_t n0, int it,
                                         int slot) {
@@ -168,12 +165,12 @@ struct EpiOps {
     const uint32_t r = (threadIdx.x + it * kThreads) / CPR;
     const uint32_t m = min(m0 + r, e.M - 1);
     const long orow = out_row(e, m);
-    const long col_ad = s_ad != 0 ? (long)ld_n : 0, col_y = s_y != 0 ? (long)ld_n : 0;
-    ad[slot] = ld_raw8(p_ad + orow * s_ad + col_ad);
-    y[slot] = ld_raw8(p_y + orow * s_y + col_y);
-    z[slot] = ld_raw8(p_z + orow * s_z + (s_z != 0 ? (long)ld_n : 0));
-    if constexpr (TWO) y2[slot] = ld_raw8(p_y2 + orow * s_y2 + (s_y2 != 0 ? (long)ld_n : 0));
-    mk[slot] = p_mk[orow * s_mk + (s_mk != 0 ? (long)(ld_n / 8) : 0)];
+    const long off = orow * e.ldc + ld_n;  // one element offset shared by every present stream
+    ad[slot] = ld_raw8(p_ad + (h_ad ? off : 0));
+    y[slot] = ld_raw8(p_y + (h_y ? off : 0));
+    z[slot] = ld_raw8(p_z + (h_z ? off : 0));
+    if constexpr (TWO) y2[slot] = ld_raw8(p_y2 + (h_y2 ? off : 0));
+    mk[slot] = p_mk[h_mk ? off / 8 : 0];  // ldc % 8 == 0: the mask byte of columns ld_n..+7
   }
   __device__ __forceinline__ void prime(const EpiParams& e, uint32_t m0, uint32_t n0) {
     setup(e);
@@ -217,7 +214,9 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
   constexpr int PF = Ops::PF;
   Ops local;
   Ops& ops = early != nullptr ? *early : local;
-  if (early == nullptr) ops.prime(e, m0, n0);
+  // the ring is primed after the accumulators went to LDS (below): priming it here kept the
+  // 64 accumulator registers and the ring live together — 168 VGPRs and ~100 spilled to scratch
+  // in the fused 128x128 data-grads (round 3 .s) — for an overlap of one short LDS staging
   (void)ld_n;
   // BN-backward coefficients of this thread's 8 columns, requested now (16-B vector loads; the
   // host checks N % 8 == 0 and 16-B alignment) so their latency hides under the staging below:
@@ -340,6 +339,7 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
         *reinterpret_cast<uint2*>(smem + ml * P + nl * 2) = v;
       }
     }
+  if (early == nullptr) ops.prime(e, m0, n0);  // accumulators are dead now
   lds_barrier();
   if (e.st_sum != nullptr) {
     // one fp32 atomic per column per block into replica row blockIdx % st_R (fire and forget:
@@ -516,20 +516,41 @@ __device__ void epilogue_f32(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
       }
     }
   } else {
+    // the C quads of a group of iterations (read-modify-write) are requested before any is
+    // used, unconditionally at clamped addresses: a load behind `if (e.rmw)` / a bounds branch
+    // was closed by a vmcnt(0) each — one memory latency per 16-B chunk, ITER per block
     constexpr int CPR = BN / 4;
-    for (int c = threadIdx.x; c < BM * CPR; c += kThreads) {
-      uint32_t r = c / CPR, cc = c % CPR;
-      uint32_t m = m0 + r, n = n0 + cc * 4;
-      if (m < e.M && n < e.N) {
-        float4 v = *reinterpret_cast<const float4*>(smem + r * P + cc * 16);
-        if (e.rmw) {
-          const float4 o = *reinterpret_cast<const float4*>(C + (long)m * e.ldc + n);
-          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+    constexpr int ITER = (BM * CPR + kThreads - 1) / kThreads;
+    constexpr int G = ITER < 8 ? ITER : 8;  // 8 quads in flight: 32 VGPRs
+    static_assert(ITER % G == 0, "epilogue_f32 groups");
+    const bool rmw = e.rmw != 0, has_b = e.bias != nullptr;
+    const float* bp = has_b ? e.bias : reinterpret_cast<const float*>(g_epi_zero);
+#pragma unroll
+    for (int g0 = 0; g0 < ITER; g0 += G) {
+      float4 old[G];
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        const int c = threadIdx.x + (g0 + k) * kThreads;
+        const uint32_t r = c / CPR, cc = c % CPR;
+        const uint32_t m = min(m0 + r, e.M - 1), n = n0 + cc * 4;
+        const float* src = rmw ? C + (long)m * e.ldc + (n < e.N ? n : 0)
+                               : reinterpret_cast<const float*>(g_epi_zero);
+        old[k] = *reinterpret_cast<const float4*>(src);
+      }
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        const int c = threadIdx.x + (g0 + k) * kThreads;
+        const uint32_t r = c / CPR, cc = c % CPR;
+        const uint32_t m = m0 + r, n = n0 + cc * 4;
+        if (c < BM * CPR && m < e.M && n < e.N) {
+          float4 v = *reinterpret_cast<const float4*>(smem + r * P + cc * 16);
+          v.x += old[k].x; v.y += old[k].y; v.z += old[k].z; v.w += old[k].w;  // 0 unless rmw
+          if (has_b) {
+            const float4 b = *reinterpret_cast<const float4*>(bp + n);
+            v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+          }
+          *reinterpret_cast<float4*>(C + (long)m * e.ldc + n) = v;
         }
-        if (e.bias != nullptr) {
-          v.x += e.bias[n]; v.y += e.bias[n + 1]; v.z += e.bias[n + 2]; v.w += e.bias[n + 3];
-        }
-        *reinterpret_cast<float4*>(C + (long)m * e.ldc + n) = v;
       }
     }
   }

@@ -355,15 +355,12 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const void* __restric
     for (int c0 = 0; c0 < Cp; c0 += 8) {
       float v[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        int c = c0 + q;
-        if (c < C) {
-          long src = (n * C + c) * hw + pix;
-          v[q] = BF16IN ? (float)reinterpret_cast<const __bf16*>(xin)[src]
-                        : reinterpret_cast<const float*>(xin)[src];
-        } else {
-          v[q] = 0.f;
-        }
+      for (int q = 0; q < 8; ++q) {  // unconditional loads (clamped channel), padding selected
+        const int c = c0 + q;
+        const long src = (n * C + (c < C ? c : C - 1)) * hw + pix;
+        const float x = BF16IN ? (float)reinterpret_cast<const __bf16*>(xin)[src]
+                               : reinterpret_cast<const float*>(xin)[src];
+        v[q] = c < C ? x : 0.f;
       }
       store8(y + t * Cp + c0, v);
     }
@@ -926,22 +923,26 @@ __global__ __launch_bounds__(256) void stem_pack_kernel(const void* __restrict__
     const int hp = (int)(r % Hp);
     const int n = (int)(r / Hp);
     const int h = hp - pad;
+    // all 8 loads issued unconditionally at clamped (in-image) addresses, then the padding
+    // zeroed by selects: a load behind its bounds branch was closed by a vmcnt(0) each
     float v[8];
+    bool inb[8];
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       const int w = 2 * j + p - pad;
       const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const int hc = min(max(h, 0), H - 1), wc = min(max(w, 0), W - 1);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        float x = 0.f;
-        if (in && c < C) {
-          const long idx = (((long)n * C + c) * H + h) * W + w;
-          x = IN_BF16 ? (float)reinterpret_cast<const __bf16*>(xin)[idx]
-                      : reinterpret_cast<const float*>(xin)[idx];
-        }
-        v[p * 4 + c] = x;
+        const int cc = c < C ? c : C - 1;
+        const long idx = (((long)n * C + cc) * H + hc) * W + wc;
+        v[p * 4 + c] = IN_BF16 ? (float)reinterpret_cast<const __bf16*>(xin)[idx]
+                               : reinterpret_cast<const float*>(xin)[idx];
+        inb[p * 4 + c] = in && c < C;
       }
     }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = inb[q] ? v[q] : 0.f;
     store8(y + t * 8, v);
   }
 }
