@@ -36,8 +36,9 @@ extern int g_ns1_max_k_gather;  // same for the gathered (im2col / strided dgrad
 // Deterministic mode (reference task.py:25-26 cudnn.deterministic): every float reduction runs
 // in a fixed order — no float atomics (det.hip); set from Python (mipipe.ops.set_deterministic).
 extern int g_deterministic;
-// out[c] (+)= sum over P rows of in[p][c] (and in1 -> out1), fixed order.
-void det_sum_rows(const float* in0, const float* in1, int P, int C, float* out0, float* out1,
+// out[c] (+)= sum over P rows of in[p][c] (and in1 -> out1), fixed order.  The partial rows are
+// SCRATCH: long sums (P > 256) are done in two levels, the first writing chunk sums in place.
+void det_sum_rows(float* in0, float* in1, int P, int C, float* out0, float* out1,
                   bool accumulate, hipStream_t st);
 // out[i] += sum_s ws[s][i] over splits in order.
 void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st);
