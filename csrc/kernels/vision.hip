@@ -207,6 +207,50 @@ __global__ __launch_bounds__(256) void dwconv_fwd_v8_kernel(
   }
 }
 
+// 3x3 depthwise forward with every tap's loads issued unconditionally (clamped in-image
+// coordinates, out-of-image taps zeroed by a select): the generic kernel's `continue` on the
+// bounds made hipcc branch around each tap's loads and drain vmcnt(0) per tap.
+template <class T>
+__global__ __launch_bounds__(256) void dwconv3_fwd_v8_kernel(
+    const T* __restrict__ x, const T* __restrict__ wt, const float* __restrict__ bias,
+    T* __restrict__ y, GConvShape s, int act) {
+  const int C = s.Co, cg = C / 8;
+  const long total = (long)s.N * s.Ho * s.Wo * cg;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(t % cg);
+    const long pix = t / cg;
+    const int wo = (int)(pix % s.Wo);
+    const long r = pix / s.Wo;
+    const int ho = (int)(r % s.Ho);
+    const int n = (int)(r / s.Ho);
+    float xv[9][8];
+    bool ok[9];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int hi = ho * s.sh - s.ph + kh, wi = wo * s.sw - s.pw + kw;
+        ok[kh * 3 + kw] = (unsigned)hi < (unsigned)s.H && (unsigned)wi < (unsigned)s.W;
+        const int hc = min(max(hi, 0), s.H - 1), wc = min(max(wi, 0), s.W - 1);
+        load8(x + (((long)n * s.H + hc) * s.W + wc) * C + c8 * 8, xv[kh * 3 + kw]);
+      }
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = bias ? bias[c8 * 8 + q] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      float wv[8];
+      load8(wt + (long)k * C + c8 * 8, wv);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += ok[k] ? xv[k][q] * wv[q] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = act_apply(acc[q], act);
+    store8(y + pix * C + c8 * 8, acc);
+  }
+}
+
 template <class T>
 __global__ __launch_bounds__(256) void dwconv_dgrad_v8_kernel(
     const T* __restrict__ dy, const T* __restrict__ wt, const T* __restrict__ z,
@@ -365,8 +409,12 @@ void dwconv_fwd(const void* x, const void* wt, const float* bias, void* y, const
   auto run = [&](auto tag) {
     typedef decltype(tag) T;
     long work = (long)s.N * s.Ho * s.Wo * (s.Co / 8);
-    hipLaunchKernelGGL((dwconv_fwd_v8_kernel<T>), dim3(grid_for(work)), dim3(256), 0, st,
-                       (const T*)x, (const T*)wt, bias, (T*)y, s, act);
+    if (s.KH == 3 && s.KW == 3)
+      hipLaunchKernelGGL((dwconv3_fwd_v8_kernel<T>), dim3(grid_for(work)), dim3(256), 0, st,
+                         (const T*)x, (const T*)wt, bias, (T*)y, s, act);
+    else
+      hipLaunchKernelGGL((dwconv_fwd_v8_kernel<T>), dim3(grid_for(work)), dim3(256), 0, st,
+                         (const T*)x, (const T*)wt, bias, (T*)y, s, act);
   };
   if (f32) run(float{});
   else run(__bf16{});
