@@ -172,6 +172,7 @@ int select(const std::string& k, bool f32, bool wgrad, F&& run) {
 // GEMM plans: tile id + 16 * split-K count (0 = heuristic split; accumulating GEMMs only)
 constexpr int kPlanSplit = 16;
 constexpr int kPlanWs = 1024;  // gemm plans: split-K through per-split workspace slices
+constexpr int kPlanLib = 4096;  // gemm plans: the library GEMM (hipBLASLt via at::mm / at::addmm)
 std::vector<int> gemm_candidates(bool f32, bool accumulate) {
   std::vector<int> c;
   for (int t : candidates(f32, accumulate)) {
@@ -957,7 +958,32 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
   // split stores its partial tile into its own slice, splitk_sum adds the slices in order.
   // Plans with kPlanWs set; chosen by the tuner where the output is small against the CU count
   // (BERT's 768 x 768 / 768 x 3072 weight-grads: 36-144 tiles) and atomics would cost more.
+  // Library plan (kPlanLib): the same product through hipBLASLt (at::mm / at::addmm) for GEMMs
+  // without a ReLU epilogue, where the library's kernels time faster (BERT's weight-grads with
+  // K = 4096 tokens, the MLM decoder: profiles/r3_gemm_vs_blaslt_graph.txt).  The tuner times it
+  // against the MFMA plans; a bias is rounded to the operand dtype first (the library's bias
+  // epilogue).  Never in deterministic mode: the library's algorithm choice is not ours to pin.
+  static const bool lib_on = [] {
+    const char* v = getenv("MIPIPE_GEMM_LIB");
+    return v == nullptr || atoi(v) != 0;
+  }();
+  const bool lib_ok = lib_on && !f32 && act_i == 0 && mipipe::g_deterministic == 0 &&
+                      (bias_p == nullptr || mode == 0);
   auto launch = [&](void* C, int p) {
+    if (p >= 0 && (p & tune::kPlanLib) != 0) {
+      if (lib_ok) {
+        const Tensor A = trans_a ? a.t() : a;
+        const Tensor B = trans_b ? b.t() : b;
+        Tensor Ct = torch::from_blob(C, {M, N}, out.options());
+        if (mode == 2) at::addmm_out(Ct, Ct, A, B, at::kFloat, 1, 1);
+        else if (mode == 1) at::mm_out(Ct, A, B, at::kFloat);
+        else if (add_p != nullptr) at::addmm_out(Ct, *addend, A, B);
+        else if (bias_p != nullptr) at::addmm_out(Ct, bias->to(a.scalar_type()), A, B);
+        else at::mm_out(Ct, A, B);
+        return;
+      }
+      p = -1;  // a table entry from a non-deterministic run: the heuristic MFMA plan
+    }
     const bool ws_plan = p >= 0 && (p & tune::kPlanWs) != 0;
     if (ws_plan) p &= ~tune::kPlanWs;
     const int cfg = p < 0 ? -1 : p % tune::kPlanSplit;
@@ -992,6 +1018,7 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
       for (int t : tune::candidates(f32, false))
         for (int sp : {2, 4, 8}) cands.push_back(t + tune::kPlanSplit * sp);
     }
+    if (lib_ok) cands.push_back(tune::kPlanLib);
     plan = tune::select_from(tune::gemm_key(M, N, K, !trans_a, trans_b, add_p != nullptr ? 3 : mode, f32),
                              cands, [&](int p) {
                                auto scratch = mode == 2 ? torch::zeros_like(out)

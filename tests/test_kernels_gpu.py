@@ -185,6 +185,46 @@ def test_gemm_addend_epilogue(M, N, K):
         assert rel_err(out, ref) < 1e-2, cfg
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (768, 3072, 4096), (200, 136, 72)])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
+def test_gemm_library_plan(M, N, K, ta, tb):
+    """The library plan (hipBLASLt through at::mm / at::addmm, plan flag 4096) computes the same
+    products as the MFMA plans: bf16 output (plain, with a bias, with an addend), fp32 output and
+    fp32 accumulation into C (beta = 1, the weight-grad contract)."""
+    LIB = 4096
+    a = bf(K, M) if ta else bf(M, K)
+    b = bf(N, K) if tb else bf(K, N)
+    ref32 = _ref.gemm(a.float(), b.float(), ta, tb, None, "none", torch.float32)
+    out = native().gemm(a, b, ta, tb, None, "none", torch.bfloat16, None, 0.0, LIB)
+    assert out.dtype == torch.bfloat16 and rel_err(out, ref32) < 1e-2
+    bias = torch.randn(N, device=dev)
+    out = native().gemm(a, b, ta, tb, bias, "none", torch.bfloat16, None, 0.0, LIB)
+    assert rel_err(out, ref32 + bias) < 1e-2
+    out32 = native().gemm(a, b, ta, tb, None, "none", torch.float32, None, 0.0, LIB)
+    assert out32.dtype == torch.float32 and rel_err(out32, ref32) < 2e-3
+    acc = torch.randn(M, N, device=dev)
+    acc0 = acc.clone()
+    native().gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0, LIB)
+    assert rel_err(acc - acc0, ref32) < 2e-3
+    if not ta and not tb:
+        add = bf(M, N)
+        out = native().gemm(a, b, False, False, None, "none", torch.bfloat16, None, 0.0, LIB, add)
+        assert rel_err(out, ref32 + add.float()) < 1e-2
+
+
+def test_gemm_library_plan_not_in_deterministic_mode():
+    """A library plan from a table built without determinism falls back to the MFMA heuristic
+    plan in deterministic mode: the result is bit-identical to the default plan's."""
+    a, b = bf(512, 768), bf(1024, 768)
+    native().set_deterministic(True)
+    try:
+        ref = native().gemm(a, b, False, True, None, "none", torch.float32, None, 0.0, -1)
+        out = native().gemm(a, b, False, True, None, "none", torch.float32, None, 0.0, 4096)
+    finally:
+        native().set_deterministic(False)
+    assert torch.equal(out, ref)
+
+
 def test_gemm_identity_asymmetric():
     # A = I with asymmetric B catches transposed C writes (cdna guide §3)
     M = 64
