@@ -835,12 +835,13 @@ std::tuple<Tensor, Tensor, Tensor> stem_bwd(Tensor xp, Tensor y, Tensor dp, Tens
     const int G = mipipe::pool_bn_bwd_reduce_blocks(pixels, 64);
     auto part = torch::empty({2, G, 64}, dp.options().dtype(at::kFloat));
     float* p0 = part.data_ptr<float>();
-    mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), pout.data_ptr(), y.data_ptr(),
+    // pout = nullptr: the stem's argmax carries the ReLU mask, the pooled output is not read
+    mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), nullptr, y.data_ptr(),
                                mean.data_ptr<float>(), invstd.data_ptr<float>(), N, Ho, 112, 64,
                                Ho / 2, 56, 3, 2, 1, p0, G, stream(), false);
     mipipe::det_sum_rows(p0, p0 + (long)G * 64, G, 64, r, r + (long)R * 64, false, stream());
   } else {
-    mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), pout.data_ptr(), y.data_ptr(),
+    mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), nullptr, y.data_ptr(),
                                mean.data_ptr<float>(), invstd.data_ptr<float>(), N, Ho, 112, 64,
                                Ho / 2, 56, 3, 2, 1, r, 0, stream(), false);
   }

@@ -1,6 +1,8 @@
 // NHWC pooling: max-pool with 1-byte window-argmax (fwd/bwd) and global average pool.
 // Backward max-pool is a gather over the windows covering each input pixel (deterministic,
 // no atomics).  Each thread moves 8 channels (one 16-B bf16 vector or two fp32 vectors).
+#include <stdexcept>
+
 #include "common.hpp"
 #include "launchers.hpp"
 
@@ -229,7 +231,9 @@ __device__ __forceinline__ void pool_grad8(const T* __restrict__ dp, const uint8
 // a thread loads those four windows once (dp, argmax, output) instead of 1 + 2 + 2 + 4 window
 // visits, with no data-dependent loop.  Pixel (2a+i, 2b+j) is tap (1+i-2di)*3 + (1+j-2dj) of
 // window (a+di, b+dj).  g[i*2+j][q]; windows outside the output grid contribute nothing.
-template <class T>
+// MASKED: the argmax already carries the ReLU mask (255 where the output is not > 0: the fused
+// stem's stem_pool_kernel), so the pooled output is not read.
+template <bool MASKED, class T>
 __device__ __forceinline__ void pool_grad_quad(const T* __restrict__ dp,
                                                const uint8_t* __restrict__ idx,
                                                const T* __restrict__ pout, int n, int a, int b,
@@ -247,7 +251,7 @@ __device__ __forceinline__ void pool_grad_quad(const T* __restrict__ dp,
       const bool ok = a + di < Ho && b + dj < Wo;
       const long o = (((long)n * Ho + min(a + di, Ho - 1)) * Wo + min(b + dj, Wo - 1)) * C + c0;
       load8(dp + o, d[di][dj]);
-      load8(pout + o, pv[di][dj]);
+      if constexpr (!MASKED) load8(pout + o, pv[di][dj]);
       ai[di][dj] = *reinterpret_cast<const uint2*>(idx + o);
       if (!ok) ai[di][dj] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);  // no tap matches 255
     }
@@ -266,12 +270,12 @@ __device__ __forceinline__ void pool_grad_quad(const T* __restrict__ dp,
           for (int q = 0; q < 8; ++q) {
             const uint32_t word = q < 4 ? ai[di][dj].x : ai[di][dj].y;
             const uint8_t at = (uint8_t)(word >> ((q & 3) * 8));
-            if (at == tap && pv[di][dj][q] > 0.f) g[i * 2 + j][q] += d[di][dj][q];
+            if (at == tap && (MASKED || pv[di][dj][q] > 0.f)) g[i * 2 + j][q] += d[di][dj][q];
           }
         }
 }
 
-template <bool QUAD, class T>
+template <bool QUAD, bool MASKED, class T>
 __global__ __launch_bounds__(256) void pool_bn_bwd_reduce_kernel(
     const T* __restrict__ dp, const uint8_t* __restrict__ idx, const T* __restrict__ pout,
     const T* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -305,14 +309,27 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_reduce_kernel(
       const long r = qd / QW;
       const int a = (int)(r % QH);
       const int n = (int)(r / QH);
-      float g[4][8];
-      pool_grad_quad(dp, idx, pout, n, a, b, c8 * 8, C, Ho, Wo, g);
+      float g[4][8], yv[4][8];
+      bool in[4];
+      pool_grad_quad<MASKED>(dp, idx, pout, n, a, b, c8 * 8, C, Ho, Wo, g);
+      // the quad's y loads are issued unconditionally (clamped pixel; a pixel past an odd edge
+      // adds nothing): behind the bounds branch each was closed with a full vmcnt drain
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          if (2 * a + i < H && 2 * b + j < W)
-            acc(g[i * 2 + j], ((long)n * H + 2 * a + i) * W + 2 * b + j);
+        for (int j = 0; j < 2; ++j) {
+          in[i * 2 + j] = 2 * a + i < H && 2 * b + j < W;
+          const long pix = ((long)n * H + min(2 * a + i, H - 1)) * W + min(2 * b + j, W - 1);
+          load8(y + pix * C + c8 * 8, yv[i * 2 + j]);
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float gq = in[u] ? as_stored<T>(g[u][q]) : 0.f;
+          sg[q] += gq;
+          sx[q] += gq * (yv[u][q] - mu[q]) * is[q];
+        }
     }
   } else {
     const long total = (long)N * H * W * cg;
@@ -381,14 +398,27 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_apply_kernel(
       const long r = qd / QW;
       const int a = (int)(r % QH);
       const int n = (int)(r / QH);
-      float g[4][8];
-      pool_grad_quad(dp, idx, pout, n, a, b, c8 * 8, C, Ho, Wo, g);
+      float g[4][8], yv[4][8];
+      pool_grad_quad<false>(dp, idx, pout, n, a, b, c8 * 8, C, Ho, Wo, g);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {  // unconditional y loads, as in the reduction
+          const long pix = ((long)n * H + min(2 * a + i, H - 1)) * W + min(2 * b + j, W - 1);
+          load8(y + pix * C + c8 * 8, yv[i * 2 + j]);
+        }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          if (2 * a + i < H && 2 * b + j < W)
-            emit(g[i * 2 + j], ((long)n * H + 2 * a + i) * W + 2 * b + j);
+          if (2 * a + i < H && 2 * b + j < W) {
+            const long pix = ((long)n * H + 2 * a + i) * W + 2 * b + j;
+            float o[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              o[q] = A[q] * as_stored<T>(g[i * 2 + j][q]) + Bc[q] * yv[i * 2 + j][q] + Cc[q];
+            store8(dy + pix * C + c8 * 8, o);
+          }
     }
   } else {
     const long total = (long)N * H * W * cg;
@@ -471,11 +501,18 @@ void pool_bn_bwd_reduce(const void* dp, const uint8_t* idx, const void* pout, co
   const int G = det_rows > 0 ? det_rows : pool_bn_bwd_reduce_blocks((long)N * H * W, C);
   auto launch = [&](auto tag, auto quad) {
     typedef decltype(tag) T;
-    hipLaunchKernelGGL((pool_bn_bwd_reduce_kernel<decltype(quad)::value, T>), dim3(G), dim3(256),
-                       0, st, (const T*)dp, idx, (const T*)pout, (const T*)y, mean, invstd, N, H,
-                       W, C, Ho, Wo, k, stride, pad, rep, det_rows);
+    hipLaunchKernelGGL((pool_bn_bwd_reduce_kernel<decltype(quad)::value, false, T>), dim3(G),
+                       dim3(256), 0, st, (const T*)dp, idx, (const T*)pout, (const T*)y, mean,
+                       invstd, N, H, W, C, Ho, Wo, k, stride, pad, rep, det_rows);
   };
   const bool quad = pool_quad_ok(H, W, Ho, Wo, k, stride, pad);
+  if (pout == nullptr) {  // argmax carries the ReLU mask (fused stem): quad gather, bf16 only
+    if (f32 || !quad) throw std::invalid_argument("pool_bn_bwd_reduce: masked argmax needs the bf16 quad path");
+    hipLaunchKernelGGL((pool_bn_bwd_reduce_kernel<true, true, __bf16>), dim3(G), dim3(256), 0, st,
+                       (const __bf16*)dp, idx, (const __bf16*)nullptr, (const __bf16*)y, mean,
+                       invstd, N, H, W, C, Ho, Wo, k, stride, pad, rep, det_rows);
+    return;
+  }
   if (f32) {
     if (quad) launch(float{}, std::true_type{});
     else launch(float{}, std::false_type{});
