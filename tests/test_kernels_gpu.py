@@ -371,6 +371,29 @@ def test_layernorm_gelu_embedding():
     assert rel_err(cs, dy.float().sum(0)) < 1e-3
 
 
+@pytest.mark.parametrize("H", [64, 512, 768, 1032, 2048])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_layernorm_fwd_widths(H, with_res):
+    """LayerNorm forward at every chunk count per lane (1..4 x 8 elements, partial last chunk at
+    H = 1032), with and without the residual, γ / β given as views off a 16-byte boundary
+    (the parameter views of a flat buffer need not be vector-aligned)."""
+    R = 37
+    x = bf(R, H)
+    res = bf(R, H) if with_res else None
+    gbuf = torch.rand(H + 1, device=dev) + 0.5
+    bbuf = torch.randn(H + 1, device=dev)
+    gma, bta = gbuf[1:], bbuf[1:]
+    y, mean, rstd, xs = native().layernorm_fwd(x, gma, bta, 1e-5, res)
+    # the kernel normalises the bf16-rounded sum (what the backward sees)
+    xin = x if res is None else (x.float() + res.float()).to(torch.bfloat16)
+    yr, mr, rr, _ = _ref.layernorm_fwd(xin.float(), gma, bta, 1e-5)
+    assert rel_err(y, yr) < 1e-2
+    assert rel_err(mean, mr) < 1e-3 and rel_err(rstd, rr) < 1e-3
+    assert (xs is None) == (res is None)
+    if res is not None:
+        assert rel_err(xs, x.float() + res.float()) < 1e-2
+
+
 @pytest.mark.parametrize("M,N,K", [(64, 10, 2048), (30, 100, 512), (64, 16, 27)])
 def test_gemm_odd_sizes_padded(M, N, K):
     """Odd sizes (10/100-class heads) go through the zero-padded path of ops.kernels.gemm."""
