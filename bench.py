@@ -105,6 +105,16 @@ def _heartbeat(every_s: float = 30.0) -> None:
     threading.Thread(target=beat, daemon=True).start()
 
 
+def _transports(path):
+    if path is None:
+        return None
+    from mipipe.parallel.dist_utils import rccl_transports
+    try:
+        return rccl_transports(path)
+    except OSError:
+        return None
+
+
 def _sync(dev) -> None:
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
@@ -130,12 +140,17 @@ def main() -> int:
     if cpu:
         dev = torch.device("cpu")
     else:
+        from mipipe.launch.env import device_offset
+        local += device_offset()  # all GPUs visible, the launcher names this rank's (launch/env.py)
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     distributed = world > 1 or a.force_reduce
+    rccl_log = None
     if distributed:
-        from mipipe.parallel.dist_utils import configure_rccl_env
+        from mipipe.parallel.dist_utils import configure_rccl_env, enable_rccl_transport_log
         configure_rccl_env()  # high-priority RCCL stream: bucket all-reduces overlap backward
+        if not cpu and world > 1:
+            rccl_log = enable_rccl_transport_log()  # which transport each peer pair gets
         if cpu:
             dist.init_process_group("gloo")
         else:
@@ -194,6 +209,8 @@ def main() -> int:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        if hasattr(model, "check_comm_errors"):
+            model.check_comm_errors(final=True)  # a one-shot wait that gave up fails the run
     if a.dump_params:
         inner = getattr(model, "module", model)
         os.makedirs(a.dump_params, exist_ok=True)
@@ -228,7 +245,8 @@ def main() -> int:
                        "force_reduce": bool(a.force_reduce),
                        "comm_dtype": a.comm_dtype,
                        "native_reducer": bool(getattr(model, "native_reducer", False)),
-                       "rccl": _rccl_settings() if distributed else None},
+                       "rccl": _rccl_settings() if distributed else None,
+                       "rccl_transports": _transports(rccl_log)},
             "final_loss": loss_v, "gpu_clocks": sampler.summary()}), flush=True)
     if distributed:
         dist.barrier()

@@ -27,14 +27,21 @@ namespace mipipe_comm {
 
 class OneShot {
  public:
-  OneShot(int rank, int world, int64_t cap_bytes, int device)
-      : rank_(rank), world_(world), cap_((cap_bytes + 4095) / 4096 * 4096), device_(device) {
+  OneShot(int rank, int world, int64_t cap_bytes, int device, double timeout_s)
+      : rank_(rank), world_(world), cap_((cap_bytes + 4095) / 4096 * 4096), device_(device),
+        timeout_s_(timeout_s) {
     TORCH_CHECK(world >= 1 && world <= 8, "OneShot: 1..8 ranks (one xGMI node), got ", world);
     TORCH_CHECK(rank >= 0 && rank < world, "OneShot: bad rank ", rank);
     TORCH_CHECK(cap_bytes > 0 && cap_bytes <= (64ll << 20), "OneShot: cap must be in (0, 64 MiB]");
+    TORCH_CHECK(timeout_s > 0.0 && timeout_s < 1e5, "OneShot: timeout_s must be in (0, 1e5)");
+    nblocks_ = mipipe::oneshot_blocks(cap_);
     OS_CHECK(hipSetDevice(device_));
     OS_CHECK(hipMalloc(&own_, mipipe::kOneShotHeaderBytes + 2 * cap_));
-    OS_CHECK(hipMemset(own_, 0, mipipe::kOneShotHeaderBytes));  // flags, error word, counters
+    OS_CHECK(hipMemset(own_, 0, mipipe::kOneShotHeaderBytes));  // flags, error words, counters
+    OS_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 2 * sizeof(unsigned int),
+                           hipHostMallocDefault));
+    err_host_[0] = err_host_[1] = 0;
+    OS_CHECK(hipEventCreateWithFlags(&err_ev_, hipEventDisableTiming));
     OS_CHECK(hipDeviceSynchronize());
     bases_.assign(world_, nullptr);
     bases_[rank_] = own_;
@@ -44,6 +51,8 @@ class OneShot {
     hipSetDevice(device_);
     for (int r = 0; r < world_; ++r)
       if (r != rank_ && bases_[r] != nullptr) hipIpcCloseMemHandle(bases_[r]);
+    if (err_ev_ != nullptr) hipEventDestroy(err_ev_);
+    if (err_host_ != nullptr) hipHostFree(err_host_);
     if (own_ != nullptr) hipFree(own_);
   }
 
@@ -73,7 +82,8 @@ class OneShot {
   void all_reduce(at::Tensor t, bool avg) {
     check(t, true);
     mipipe::oneshot_launch(bases_.data(), rank_, world_, t.data_ptr(), t.data_ptr(),
-                           t.numel() * 4, true, 0, avg ? 1.0f / world_ : 1.0f, cap_, stream());
+                           t.numel() * 4, true, 0, avg ? 1.0f / world_ : 1.0f, cap_, nblocks_,
+                           timeout_s_, stream());
   }
 
   // In place: t = rank src's t (any dtype; byte size a multiple of 16).
@@ -81,18 +91,40 @@ class OneShot {
     check(t, false);
     TORCH_CHECK(src >= 0 && src < world_, "OneShot: bad src ", src);
     mipipe::oneshot_launch(bases_.data(), rank_, world_, t.data_ptr(), t.data_ptr(),
-                           t.numel() * t.element_size(), false, src, 1.0f, cap_, stream());
+                           t.numel() * t.element_size(), false, src, 1.0f, cap_, nblocks_,
+                           timeout_s_, stream());
   }
 
-  // Host read of the error word (synchronises the device): nonzero = a wait gave up.
-  int error() const {
-    unsigned int v = 0;
+  // Host read of the error words (synchronises the device): {1 + peer, epoch}; peer word 0 =
+  // no wait ever gave up.
+  std::pair<int, int64_t> error_info() const {
+    unsigned int v[2] = {0, 0};
     OS_CHECK(hipDeviceSynchronize());
-    OS_CHECK(hipMemcpy(&v, own_ + 2048, 4, hipMemcpyDeviceToHost));
-    return (int)v;
+    OS_CHECK(hipMemcpy(v, own_ + mipipe::kOneShotErrOffset, 8, hipMemcpyDeviceToHost));
+    return {(int)v[0], (int64_t)v[1]};
+  }
+  int error() const { return error_info().first; }
+
+  // Asynchronous error check without a host sync: request_error() enqueues a copy of the error
+  // words into pinned host memory on the current stream; poll_error() returns the words of the
+  // last request once that copy has completed, else {-1, -1} (not known yet).
+  void request_error() {
+    OS_CHECK(hipMemcpyAsync(err_host_, own_ + mipipe::kOneShotErrOffset, 8,
+                            hipMemcpyDeviceToHost, stream()));
+    OS_CHECK(hipEventRecord(err_ev_, stream()));
+    requested_ = true;
+  }
+  std::pair<int, int64_t> poll_error() const {
+    if (!requested_) return {-1, -1};
+    const hipError_t q = hipEventQuery(err_ev_);
+    if (q == hipErrorNotReady) return {-1, -1};
+    OS_CHECK(q);
+    return {(int)err_host_[0], (int64_t)err_host_[1]};
   }
 
   int64_t cap() const { return cap_; }
+  int nblocks() const { return nblocks_; }
+  double timeout_s() const { return timeout_s_; }
 
  private:
   static hipStream_t stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
@@ -112,21 +144,31 @@ class OneShot {
   int rank_, world_;
   int64_t cap_;
   int device_;
+  double timeout_s_;
+  int nblocks_ = 1;
   char* own_ = nullptr;
+  unsigned int* err_host_ = nullptr;  // pinned
+  hipEvent_t err_ev_ = nullptr;
+  bool requested_ = false;
   std::vector<char*> bases_;
   bool opened_ = false;
 };
 
 void init_oneshot(py::module& m) {
   py::class_<OneShot>(m, "OneShot")
-      .def(py::init<int, int, int64_t, int>(), py::arg("rank"), py::arg("world"),
-           py::arg("cap_bytes"), py::arg("device"))
+      .def(py::init<int, int, int64_t, int, double>(), py::arg("rank"), py::arg("world"),
+           py::arg("cap_bytes"), py::arg("device"), py::arg("timeout_s") = 120.0)
       .def("handle", &OneShot::handle)
       .def("open", &OneShot::open)
       .def("all_reduce", &OneShot::all_reduce, py::arg("t"), py::arg("avg") = false)
       .def("broadcast", &OneShot::broadcast, py::arg("t"), py::arg("src") = 0)
       .def("error", &OneShot::error)
-      .def_property_readonly("cap", &OneShot::cap);
+      .def("error_info", &OneShot::error_info)
+      .def("request_error", &OneShot::request_error)
+      .def("poll_error", &OneShot::poll_error)
+      .def_property_readonly("cap", &OneShot::cap)
+      .def_property_readonly("nblocks", &OneShot::nblocks)
+      .def_property_readonly("timeout_s", &OneShot::timeout_s);
 }
 
 }  // namespace mipipe_comm

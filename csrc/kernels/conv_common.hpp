@@ -14,6 +14,7 @@
 // ops live in separate translation units (conv_fwd.hip / conv_dgrad.hip / conv_wgrad.hip).
 #pragma once
 #include "epilogue.hpp"
+#include "gemm_pp.hpp"
 #include "launchers.hpp"
 
 namespace mipipe {
@@ -23,11 +24,14 @@ namespace gk {
 static __device__ __attribute__((aligned(64))) uint4 g_conv_zero[8];
 
 // Block tile BM x BN, NS LDS stages, WM x WN waves (wave tile (BM/WM) x (BN/WN)).
-template <int BM_, int BN_, int NS_, int WM_, int WN_>
+// PP: the ping-pong 8-wave main loop of gemm_pp.hpp (2 LDS stages of half tiles; accumulators
+// in its half-tile row/column map, which the epilogues take as HALVES).
+template <int BM_, int BN_, int NS_, int WM_, int WN_, bool PP_ = false>
 struct Tile {
   static constexpr int BM = BM_, BN = BN_, NS = NS_, WM = WM_, WN = WN_;
   static constexpr int NW = WM * WN;
   static constexpr int THREADS = 64 * NW;
+  static constexpr bool PP = PP_;
 };
 
 // The config table.  Ids are stable (they key the tuning table).
@@ -43,6 +47,10 @@ struct Tile {
 //  9: 128x64,  1 stage               — short-K streaming convs (one or two k-steps, large M):
 //     24.6 KB of LDS -> 6 blocks per CU to keep more epilogue traffic in flight
 // 10: 64x128,  1 stage               — same for narrow M
+// 11: 256x256, ping-pong 2x4 waves    — large GEMMs: 1.38 PF on 4096^3 vs 1.22 PF for config 6
+//     (tools/gemm_lab/pp_lab.hip, profiles/r4_pp_lab_v1.jsonl)
+// 12: 256x128, ping-pong 2x4 waves    — large M, medium N
+// 13: 128x256, ping-pong 2x4 waves    — medium M, large N
 typedef Tile<128, 128, 2, 2, 2> T0;
 typedef Tile<128, 128, 1, 2, 2> T1;
 typedef Tile<128, 64, 2, 2, 2> T2;
@@ -54,7 +62,11 @@ typedef Tile<256, 64, 2, 4, 1> T7;
 typedef Tile<64, 128, 2, 2, 2> T8;
 typedef Tile<128, 64, 1, 2, 2> T9;
 typedef Tile<64, 128, 1, 2, 2> T10;
-constexpr int kNumTiles = 11;
+typedef Tile<256, 256, 2, 2, 4, true> T11;
+typedef Tile<256, 128, 2, 2, 4, true> T12;
+typedef Tile<128, 256, 2, 2, 4, true> T13;
+constexpr int kNumTiles = 14;
+static_assert(kNumTiles == kConvTileConfigs, "launchers.hpp tile count");
 
 // fp32 operands run the split-bf16x3 loop (3 LDS images): 4-wave tiles only.
 template <class T>
@@ -63,17 +75,67 @@ constexpr bool tile_ok_for(int cfg) {
                                        : (cfg >= 0 && cfg < kNumTiles);
 }
 
-template <class T, class C, class OpA, class OpB>
+template <class T, class C>
+constexpr int main_lds_bytes() {
+  return std::is_same<T, float>::value ? 3 * (C::BM + C::BN) * BK * 2  // split-bf16x3 images
+                                       : C::NS * (C::BM + C::BN) * BK * 2;
+}
+template <class T, class C>
 constexpr int lds_bytes_out() {
-  constexpr int a = MainLoopFor<T, C::BM, C::BN, OpA, OpB, C::NS, C::WM, C::WN>::LDS_BYTES;
+  constexpr int a = main_lds_bytes<T, C>();
   constexpr int b = kEpiLdsBytes<C::BM, C::BN, T, C::WM>();
   return a > b ? a : b;
 }
-template <class T, class C, class OpA, class OpB>
+template <class T, class C>
 constexpr int lds_bytes_f32out() {
-  constexpr int a = MainLoopFor<T, C::BM, C::BN, OpA, OpB, C::NS, C::WM, C::WN>::LDS_BYTES;
-  constexpr int b = C::BM * (C::BN * 4 + 16);
+  constexpr int a = main_lds_bytes<T, C>();
+  constexpr int b = kEpiF32Rows<C::BM, C::BN, C::PP>() * (C::BN * 4 + 16);
   return a > b ? a : b;
+}
+
+// Operand-policy families: template <int R, int NW> using type = <policy over R rows, NW waves>.
+template <class T> struct PolKCDense { template <int R, int NW> using type = KCDense<R, T, NW>; };
+template <class T> struct PolMCDense { template <int R, int NW> using type = MCDense<R, T, NW>; };
+template <bool AL, class T> struct PolKCIm2col {
+  template <int R, int NW> using type = KCIm2col<R, AL, T, NW>;
+};
+template <bool AL, class T> struct PolKCDgrad {
+  template <int R, int NW> using type = KCDgrad<R, AL, T, NW>;
+};
+template <class T> struct PolMCDgradW { template <int R, int NW> using type = MCDgradW<R, T, NW>; };
+template <class T> struct PolMCIm2colT {
+  template <int R, int NW> using type = MCIm2colT<R, T, NW>;
+};
+
+// The main loop of tile config C over k-steps [kt0, kt1).  Operand policies come from the
+// families PA / PB; ia(op, row_origin) / ib(op, col_origin) initialise one policy instance.
+// Ping-pong tiles stage half tiles: two instances per operand (origins +0 and +BM/2 / +BN/2).
+template <class T, class C, class PA, class PB, int V = kLoopDefault, class IA, class IB>
+__device__ __forceinline__ void run_main_loop(char* smem, IA&& ia, IB&& ib, uint32_t m0,
+                                              uint32_t n0, int kt0, int kt1,
+                                              f32x4 (&acc)[C::BM / C::WM / 16][C::BN / C::WN / 16],
+                                              int wave, int lane) {
+  if constexpr (C::PP) {
+    static_assert(!std::is_same<T, float>::value, "ping-pong tiles are bf16-only");
+    typedef typename PA::template type<C::BM / 2, C::NW> OA;
+    typedef typename PB::template type<C::BN / 2, C::NW> OB;
+    OA a[2];
+    OB b[2];
+    ia(a[0], m0);
+    ia(a[1], m0 + C::BM / 2);
+    ib(b[0], n0);
+    ib(b[1], n0 + C::BN / 2);
+    MainLoopPP<C::BM, C::BN, OA, OB, C::WM, C::WN>::run(smem, a, b, kt0, kt1, acc, wave, lane);
+  } else {
+    typedef typename PA::template type<C::BM, C::NW> OA;
+    typedef typename PB::template type<C::BN, C::NW> OB;
+    OA a;
+    OB b;
+    ia(a, m0);
+    ib(b, n0);
+    MainLoopFor<T, C::BM, C::BN, OA, OB, C::NS, C::WM, C::WN, V>::type::run(smem, a, b, kt0, kt1,
+                                                                            acc, wave, lane);
+  }
 }
 // Minimum resident blocks per CU promised to the register allocator.
 template <class T, class C>
@@ -88,11 +150,9 @@ template <class C, bool DENSE, bool ALIGNED, class T, bool DGRAD_EPI = false>
 __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_fwd_kernel(
     const T* __restrict__ x, const T* __restrict__ w, ConvGeom g, uint32_t M,
     uint32_t tilesN, EpiParams e) {
-  constexpr int BM = C::BM, BN = C::BN, NW = C::NW;
-  typedef typename std::conditional<DENSE, KCDense<BM, T, NW>,
-                                    KCIm2col<BM, ALIGNED, T, NW>>::type OpA;
-  typedef KCDense<BN, T, NW> OpB;
-  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_out<T, C, OpA, OpB>()];
+  constexpr int BM = C::BM, BN = C::BN;
+  typedef typename std::conditional<DENSE, PolKCDense<T>, PolKCIm2col<ALIGNED, T>>::type PA;
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_out<T, C>()];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
@@ -100,15 +160,15 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_fwd_kerne
   const uint32_t m0 = tm * BM, n0 = tn * BN;
   const uint32_t K = (uint32_t)(g.KH * g.KW * g.C);
   const int nk = (int)((K + BK - 1) / BK);
-  OpA a;
-  if constexpr (DENSE) a.init(x, g.C, M, K, m0, wave, lane, g_conv_zero);
-  else a.init(x, g, M, m0, wave, lane, g_conv_zero);
-  OpB b;
-  b.init(w, K, e.N, K, n0, wave, lane, g_conv_zero);
+  auto ia = [&](auto& a, uint32_t origin) {
+    if constexpr (DENSE) a.init(x, g.C, M, K, origin, wave, lane, g_conv_zero);
+    else a.init(x, g, M, origin, wave, lane, g_conv_zero);
+  };
+  auto ib = [&](auto& b, uint32_t origin) { b.init(w, K, e.N, K, origin, wave, lane, g_conv_zero); };
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
-  MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN>::type::run(smem, a, b, 0, nk, acc, wave,
-                                                                    lane);
-  epilogue_out<BM, BN, DGRAD_EPI, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
+  run_main_loop<T, C, PA, PolKCDense<T>>(smem, ia, ib, m0, n0, 0, nk, acc, wave, lane);
+  epilogue_out<BM, BN, DGRAD_EPI, T, C::WM, C::WN, false, C::PP>(smem, acc, e, m0, n0, 0, wave,
+                                                                 lane);
 }
 
 // TWO: BN-backward fusion of a two-branch block output (dense bf16 data-grads only)
@@ -116,11 +176,10 @@ template <class C, bool DENSE, bool ALIGNED, class T, bool TWO = false>
 __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_dgrad_kernel(
     const T* __restrict__ dy, const T* __restrict__ w, int Ho, int Wo, int Co, int taps,
     FastDiv fCo, DgradClass cls, uint32_t M, uint32_t tilesN, EpiParams e) {
-  constexpr int BM = C::BM, BN = C::BN, NW = C::NW;
-  typedef typename std::conditional<DENSE, KCDense<BM, T, NW>,
-                                    KCDgrad<BM, ALIGNED, T, NW>>::type OpA;
-  typedef typename std::conditional<DENSE, MCDense<BN, T, NW>, MCDgradW<BN, T, NW>>::type OpB;
-  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_out<T, C, OpA, OpB>()];
+  constexpr int BM = C::BM, BN = C::BN;
+  typedef typename std::conditional<DENSE, PolKCDense<T>, PolKCDgrad<ALIGNED, T>>::type PA;
+  typedef typename std::conditional<DENSE, PolMCDense<T>, PolMCDgradW<T>>::type PB;
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_out<T, C>()];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
@@ -129,19 +188,17 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_dgrad_ker
   const uint32_t Ci = e.N;
   const uint32_t K = (uint32_t)(cls.ntaps * Co);
   const int nk = (int)((K + BK - 1) / BK);
-  OpA a;
-  OpB b;
-  if constexpr (DENSE) {
-    a.init(dy, Co, M, K, m0, wave, lane, g_conv_zero);
-    b.init(w, Ci, Ci, K, n0, wave, lane, g_conv_zero);
-  } else {
-    a.init(dy, Ho, Wo, Co, fCo, cls, M, m0, wave, lane, g_conv_zero);
-    b.init(w, (uint32_t)Co, (uint32_t)taps, Ci, fCo, cls, n0, wave, lane, g_conv_zero);
-  }
+  auto ia = [&](auto& a, uint32_t origin) {
+    if constexpr (DENSE) a.init(dy, Co, M, K, origin, wave, lane, g_conv_zero);
+    else a.init(dy, Ho, Wo, Co, fCo, cls, M, origin, wave, lane, g_conv_zero);
+  };
+  auto ib = [&](auto& b, uint32_t origin) {
+    if constexpr (DENSE) b.init(w, Ci, Ci, K, origin, wave, lane, g_conv_zero);
+    else b.init(w, (uint32_t)Co, (uint32_t)taps, Ci, fCo, cls, origin, wave, lane, g_conv_zero);
+  };
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
-  MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN>::type::run(smem, a, b, 0, nk, acc, wave,
-                                                                    lane);
-  epilogue_out<BM, BN, true, T, C::WM, C::WN, TWO>(smem, acc, e, m0, n0, 0, wave, lane);
+  run_main_loop<T, C, PA, PB>(smem, ia, ib, m0, n0, 0, nk, acc, wave, lane);
+  epilogue_out<BM, BN, true, T, C::WM, C::WN, TWO, C::PP>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
 // ATOMIC: split-K partial tiles added with fp32 atomics; else the block owns its output tile
@@ -150,10 +207,9 @@ template <class C, bool DENSE, class T, bool ATOMIC = true>
 __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_wgrad_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, ConvGeom g, uint32_t tilesN,
     int kt_per_split, EpiParams e) {
-  constexpr int BM = C::BM, BN = C::BN, NW = C::NW;
-  typedef MCDense<BM, T, NW> OpA;
-  typedef typename std::conditional<DENSE, MCDense<BN, T, NW>, MCIm2colT<BN, T, NW>>::type OpB;
-  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_f32out<T, C, OpA, OpB>()];
+  constexpr int BM = C::BM, BN = C::BN;
+  typedef typename std::conditional<DENSE, PolMCDense<T>, PolMCIm2colT<T>>::type PB;
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_f32out<T, C>()];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
@@ -165,15 +221,14 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_wgrad_ker
   const int kt0 = blockIdx.y * kt_per_split;
   const int kt1 = min(nk, kt0 + kt_per_split);
   if (e.col.rep != nullptr && blockIdx.x == 0 && blockIdx.y == 0) bn_collect_block<C::THREADS>(e.col);
-  OpA a;
-  a.init(dy, Co, Co, K, m0, wave, lane, g_conv_zero);
-  OpB b;
-  if constexpr (DENSE) b.init(x, g.C, g.C, K, n0, wave, lane, g_conv_zero);
-  else b.init(x, g, n0, wave, lane, g_conv_zero);
+  auto ia = [&](auto& a, uint32_t origin) { a.init(dy, Co, Co, K, origin, wave, lane, g_conv_zero); };
+  auto ib = [&](auto& b, uint32_t origin) {
+    if constexpr (DENSE) b.init(x, g.C, g.C, K, origin, wave, lane, g_conv_zero);
+    else b.init(x, g, origin, wave, lane, g_conv_zero);
+  };
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
-  MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN>::type::run(smem, a, b, kt0, kt1, acc,
-                                                                    wave, lane);
-  epilogue_f32<BM, BN, ATOMIC, C::WM, C::WN>(smem, acc, e, m0, n0, wave, lane);
+  run_main_loop<T, C, PolMCDense<T>, PB>(smem, ia, ib, m0, n0, kt0, kt1, acc, wave, lane);
+  epilogue_f32<BM, BN, ATOMIC, C::WM, C::WN, C::PP>(smem, acc, e, m0, n0, wave, lane);
 }
 
 }  // namespace gk
@@ -223,6 +278,9 @@ inline void with_tile(int cfg, F&& f) {
       case 8: f(T8{}); break;
       case 9: f(T9{}); break;
       case 10: f(T10{}); break;
+      case 11: f(T11{}); break;
+      case 12: f(T12{}); break;
+      case 13: f(T13{}); break;
       default: f(T0{}); break;
     }
   }

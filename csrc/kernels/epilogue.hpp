@@ -103,6 +103,33 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Tile-local row / column of accumulator tile (i, j) of wave (wr, wc) (before the lane offset
+// (lane & 15) / (lane >> 4) * 4): contiguous wave tiles, or the ping-pong loop's half-tile map
+// (gemm_pp.hpp MainLoopPP::row / col).
+template <int BM, int BN, int WM, int WN, bool HALVES>
+struct AccMap {
+  static constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
+  __device__ static uint32_t row(int wr, int i) {
+    if constexpr (HALVES)
+      return (uint32_t)((i / (MT / 2)) * (BM / 2) + wr * (MT / 2) * 16 + (i % (MT / 2)) * 16);
+    else
+      return (uint32_t)(wr * (BM / WM) + i * 16);
+  }
+  __device__ static uint32_t col(int wc, int j) {
+    if constexpr (HALVES)
+      return (uint32_t)((j / (NT / 2)) * (BN / 2) + wc * (NT / 2) * 16 + (j % (NT / 2)) * 16);
+    else
+      return (uint32_t)(wc * (BN / WN) + j * 16);
+  }
+};
+
+// Rows of the fp32 output tile staged in LDS at once: all of them, or one m-half at a time for
+// the ping-pong 256-row tiles (a 256 x 256 fp32 tile would need 260 KB).
+template <int BM, int BN, bool HALVES>
+constexpr int kEpiF32Rows() {
+  return (HALVES && BM * (BN * 4 + 16) > 160 * 1024) ? BM / 2 : BM;
+}
+
 __device__ __forceinline__ long out_row(const EpiParams& e, uint32_t m) {
   if (e.rm_s == 0) return (long)m;
   uint32_t img = fdiv(e.rm_fHcWc, m);
@@ -187,7 +214,7 @@ struct EpiOps {
 // them keep their register budget.  early: an operand ring the kernel already primed.
 // TWO: the BN-backward fusion of a two-branch block output (e.bnr_y2 set, FUSE only).
 template <int BM, int BN, bool FUSE = false, class T = __bf16, int WM = 2, int WN = 2,
-          bool TWO = false>
+          bool TWO = false, bool HALVES = false>
 __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                              const EpiParams& e, uint32_t m0, uint32_t n0, uint32_t prow_base,
                              int wave, int lane,
@@ -195,8 +222,8 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
   constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
   constexpr int kThreads = 64 * WM * WN;
   const int wr = wave / WN, wc = wave % WN;
-  const uint32_t ml0 = wr * (BM / WM) + (lane & 15);
-  const uint32_t nl0 = wc * (BN / WN) + (lane >> 4) * 4;
+  typedef AccMap<BM, BN, WM, WN, HALVES> Map;
+  const uint32_t lr = lane & 15, lc = (lane >> 4) * 4;
   // dgrad fusions: issue this thread's addend / y loads now so their latency overlaps the
   // accumulator staging below (a thread always owns the same 8-column chunk)
   constexpr int CPR = BN / 8;  // 8-element chunks per row
@@ -253,14 +280,14 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
     const float* bp = e.bias != nullptr ? e.bias : reinterpret_cast<const float*>(g_epi_zero);
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      const uint32_t n = n0 + nl0 + j * 16;
+      const uint32_t n = n0 + Map::col(wc, j) + lc;
       const uint32_t nc = (e.bias != nullptr && n < e.N) ? n : 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) bv[j][q] = bp[nc + q];
     }
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      uint32_t n = n0 + nl0 + j * 16;
+      uint32_t n = n0 + Map::col(wc, j) + lc;
       float b[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) b[q] = n < e.N ? bv[j][q] : 0.f;
@@ -283,19 +310,18 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
     float shv[NT][4];
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      const uint32_t n = n0 + nl0 + j * 16;
+      const uint32_t n = n0 + Map::col(wc, j) + lc;
       const uint32_t nc = n < e.N ? n : 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) shv[j][q] = e.st_shift[nc + q];
     }
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      uint32_t n = n0 + nl0 + j * 16;
       const float* sh = shv[j];
       float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        uint32_t m = m0 + ml0 + i * 16;
+        uint32_t m = m0 + Map::row(wr, i) + lr;
         if (m < e.M) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -311,7 +337,7 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
         ss[q] = row16_sum(ss[q]);
       }
       if ((lane & 15) == 0) {
-        uint32_t nl = nl0 + j * 16;
+        uint32_t nl = Map::col(wc, j) + lc;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           lst[(0 * WM + wr) * BN + nl + q] = s[q];
@@ -330,7 +356,7 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      uint32_t ml = ml0 + i * 16, nl = nl0 + j * 16;
+      uint32_t ml = Map::row(wr, i) + lr, nl = Map::col(wc, j) + lc;
       if constexpr (F32) {
         *reinterpret_cast<float4*>(smem + ml * P + nl * 4) =
             make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
@@ -476,80 +502,91 @@ __device__ void epilogue_bf16(char* smem, f32x4 (&acc)[BM / 32][BN / 32], const 
 }
 
 // fp32 output; ATOMIC accumulates into C (split-K), otherwise plain store (beta = 0) or, with
-// e.rmw, a non-atomic accumulate (beta = 1, one block per element).
-template <int BM, int BN, bool ATOMIC, int WM = 2, int WN = 2>
+// e.rmw, a non-atomic accumulate (beta = 1, one block per element).  The tile is staged through
+// LDS in passes of kEpiF32Rows rows (two m-halves for the ping-pong 256 x 256 tile).
+template <int BM, int BN, bool ATOMIC, int WM = 2, int WN = 2, bool HALVES = false>
 __device__ void epilogue_f32(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16],
                              const EpiParams& e, uint32_t m0, uint32_t n0, int wave, int lane) {
   constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
   constexpr int kThreads = 64 * WM * WN;
+  constexpr int RP = kEpiF32Rows<BM, BN, HALVES>();  // rows per pass
+  constexpr int PASSES = BM / RP;
+  static_assert(PASSES == 1 || HALVES, "multi-pass fp32 staging needs the half-tile map");
   const int wr = wave / WN, wc = wave % WN;
-  const uint32_t ml0 = wr * (BM / WM) + (lane & 15);
-  const uint32_t nl0 = wc * (BN / WN) + (lane >> 4) * 4;
-  // stage fp32 tile: pitch BN*4 + 16 bytes (BM*(BN*4+16) <= LDS of the main loop)
+  typedef AccMap<BM, BN, WM, WN, HALVES> Map;
+  const uint32_t lr = lane & 15, lc = (lane >> 4) * 4;
+  // stage fp32 tile: pitch BN*4 + 16 bytes (RP*(BN*4+16) <= LDS of the kernel)
   constexpr int P = BN * 4 + 16;
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      uint32_t ml = ml0 + i * 16, nl = nl0 + j * 16;
-      *reinterpret_cast<float4*>(smem + ml * P + nl * 4) =
-          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-    }
-  __syncthreads();
   float* C = reinterpret_cast<float*>(e.C);
-  if (ATOMIC && e.det_rows > 0) {
-    // deterministic split-K: this split's partial tile goes to its own workspace slice
-    C += (long)blockIdx.y * e.M * e.ldc;
-    for (int c = threadIdx.x; c < BM * BN; c += kThreads) {
-      uint32_t r = c / BN, cc = c % BN;
-      uint32_t m = m0 + r, n = n0 + cc;
-      if (m < e.M && n < e.N) C[(long)m * e.ldc + n] = *reinterpret_cast<const float*>(smem + r * P + cc * 4);
-    }
-  } else if constexpr (ATOMIC) {
-    // each wave-instruction: 64 lanes x 4 B = 256 contiguous bytes of one row
-    for (int c = threadIdx.x; c < BM * BN; c += kThreads) {
-      uint32_t r = c / BN, cc = c % BN;
-      uint32_t m = m0 + r, n = n0 + cc;
-      if (m < e.M && n < e.N) {
-        float v = *reinterpret_cast<const float*>(smem + r * P + cc * 4);
-        atomicAdd(C + (long)m * e.ldc + n, v);
+  if (ATOMIC && e.det_rows > 0) C += (long)blockIdx.y * e.M * e.ldc;
+#pragma unroll
+  for (int pass = 0; pass < PASSES; ++pass) {
+    if (pass > 0) __syncthreads();  // the previous pass's staging reads are done
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      if (PASSES > 1 && i / (MT / 2) != pass) continue;  // compile-time after unrolling
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        uint32_t ml = Map::row(wr, i) + lr - pass * RP, nl = Map::col(wc, j) + lc;
+        *reinterpret_cast<float4*>(smem + ml * P + nl * 4) =
+            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       }
     }
-  } else {
-    // the C quads of a group of iterations (read-modify-write) are requested before any is
-    // used, unconditionally at clamped addresses: a load behind `if (e.rmw)` / a bounds branch
-    // was closed by a vmcnt(0) each — one memory latency per 16-B chunk, ITER per block
-    constexpr int CPR = BN / 4;
-    constexpr int ITER = (BM * CPR + kThreads - 1) / kThreads;
-    constexpr int G = ITER < 8 ? ITER : 8;  // 8 quads in flight: 32 VGPRs
-    static_assert(ITER % G == 0, "epilogue_f32 groups");
-    const bool rmw = e.rmw != 0, has_b = e.bias != nullptr;
-    const float* bp = has_b ? e.bias : reinterpret_cast<const float*>(g_epi_zero);
-#pragma unroll
-    for (int g0 = 0; g0 < ITER; g0 += G) {
-      float4 old[G];
-#pragma unroll
-      for (int k = 0; k < G; ++k) {
-        const int c = threadIdx.x + (g0 + k) * kThreads;
-        const uint32_t r = c / CPR, cc = c % CPR;
-        const uint32_t m = min(m0 + r, e.M - 1), n = n0 + cc * 4;
-        const float* src = rmw ? C + (long)m * e.ldc + (n < e.N ? n : 0)
-                               : reinterpret_cast<const float*>(g_epi_zero);
-        old[k] = *reinterpret_cast<const float4*>(src);
+    __syncthreads();
+    const uint32_t pm0 = m0 + pass * RP;  // first output row of this pass
+    if (ATOMIC && e.det_rows > 0) {
+      // deterministic split-K: this split's partial tile goes to its own workspace slice
+      for (int c = threadIdx.x; c < RP * BN; c += kThreads) {
+        uint32_t r = c / BN, cc = c % BN;
+        uint32_t m = pm0 + r, n = n0 + cc;
+        if (m < e.M && n < e.N) C[(long)m * e.ldc + n] = *reinterpret_cast<const float*>(smem + r * P + cc * 4);
       }
+    } else if constexpr (ATOMIC) {
+      // each wave-instruction: 64 lanes x 4 B = 256 contiguous bytes of one row
+      for (int c = threadIdx.x; c < RP * BN; c += kThreads) {
+        uint32_t r = c / BN, cc = c % BN;
+        uint32_t m = pm0 + r, n = n0 + cc;
+        if (m < e.M && n < e.N) {
+          float v = *reinterpret_cast<const float*>(smem + r * P + cc * 4);
+          atomicAdd(C + (long)m * e.ldc + n, v);
+        }
+      }
+    } else {
+      // the C quads of a group of iterations (read-modify-write) are requested before any is
+      // used, unconditionally at clamped addresses: a load behind `if (e.rmw)` / a bounds branch
+      // was closed by a vmcnt(0) each — one memory latency per 16-B chunk, ITER per block
+      constexpr int CPR = BN / 4;
+      constexpr int ITER = (RP * CPR + kThreads - 1) / kThreads;
+      constexpr int G = ITER < 8 ? ITER : 8;  // 8 quads in flight: 32 VGPRs
+      static_assert(ITER % G == 0, "epilogue_f32 groups");
+      const bool rmw = e.rmw != 0, has_b = e.bias != nullptr;
+      const float* bp = has_b ? e.bias : reinterpret_cast<const float*>(g_epi_zero);
 #pragma unroll
-      for (int k = 0; k < G; ++k) {
-        const int c = threadIdx.x + (g0 + k) * kThreads;
-        const uint32_t r = c / CPR, cc = c % CPR;
-        const uint32_t m = m0 + r, n = n0 + cc * 4;
-        if (c < BM * CPR && m < e.M && n < e.N) {
-          float4 v = *reinterpret_cast<const float4*>(smem + r * P + cc * 16);
-          v.x += old[k].x; v.y += old[k].y; v.z += old[k].z; v.w += old[k].w;  // 0 unless rmw
-          if (has_b) {
-            const float4 b = *reinterpret_cast<const float4*>(bp + n);
-            v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+      for (int g0 = 0; g0 < ITER; g0 += G) {
+        float4 old[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+          const int c = threadIdx.x + (g0 + k) * kThreads;
+          const uint32_t r = c / CPR, cc = c % CPR;
+          const uint32_t m = min(pm0 + r, e.M - 1), n = n0 + cc * 4;
+          const float* src = rmw ? C + (long)m * e.ldc + (n < e.N ? n : 0)
+                                 : reinterpret_cast<const float*>(g_epi_zero);
+          old[k] = *reinterpret_cast<const float4*>(src);
+        }
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+          const int c = threadIdx.x + (g0 + k) * kThreads;
+          const uint32_t r = c / CPR, cc = c % CPR;
+          const uint32_t m = pm0 + r, n = n0 + cc * 4;
+          if (c < RP * CPR && m < e.M && n < e.N) {
+            float4 v = *reinterpret_cast<const float4*>(smem + r * P + cc * 16);
+            v.x += old[k].x; v.y += old[k].y; v.z += old[k].z; v.w += old[k].w;  // 0 unless rmw
+            if (has_b) {
+              const float4 b = *reinterpret_cast<const float4*>(bp + n);
+              v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+            }
+            *reinterpret_cast<float4*>(C + (long)m * e.ldc + n) = v;
           }
-          *reinterpret_cast<float4*>(C + (long)m * e.ldc + n) = v;
         }
       }
     }

@@ -28,13 +28,12 @@ template <class C, bool A_KC, bool B_KC, int OUT, class T>
 __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void gemm_dense_kernel(
     const T* __restrict__ A, long lda, const T* __restrict__ B, long ldb, uint32_t K,
     uint32_t tilesN, int kt_per_split, EpiParams e) {
-  constexpr int BM = C::BM, BN = C::BN, NW = C::NW;
-  typedef typename std::conditional<A_KC, KCDense<BM, T, NW>, MCDense<BM, T, NW>>::type OpA;
-  typedef typename std::conditional<B_KC, KCDense<BN, T, NW>, MCDense<BN, T, NW>>::type OpB;
-  typedef MainLoopFor<T, BM, BN, OpA, OpB, C::NS, C::WM, C::WN, kGemmLoop> ML;
-  constexpr int main_lds = ML::LDS_BYTES;
-  constexpr int epi_lds =
-      (OUT == 0 || OUT == 3) ? kEpiLdsBytes<BM, BN, T, C::WM>() : BM * (BN * 4 + 16);
+  constexpr int BM = C::BM, BN = C::BN;
+  typedef typename std::conditional<A_KC, PolKCDense<T>, PolMCDense<T>>::type PA;
+  typedef typename std::conditional<B_KC, PolKCDense<T>, PolMCDense<T>>::type PB;
+  constexpr int main_lds = main_lds_bytes<T, C>();
+  constexpr int epi_lds = (OUT == 0 || OUT == 3) ? kEpiLdsBytes<BM, BN, T, C::WM>()
+                                                 : kEpiF32Rows<BM, BN, C::PP>() * (BN * 4 + 16);
   __shared__ __attribute__((aligned(16))) char smem[main_lds > epi_lds ? main_lds : epi_lds];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -44,15 +43,16 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void gemm_dense_ker
   const int nk = (int)((K + BK - 1) / BK);
   const int kt0 = blockIdx.y * kt_per_split;
   const int kt1 = min(nk, kt0 + kt_per_split);
-  OpA a;
-  a.init(A, lda, e.M, K, m0, wave, lane, g_gemm_zero);
-  OpB b;
-  b.init(B, ldb, e.N, K, n0, wave, lane, g_gemm_zero);
+  auto ia = [&](auto& a, uint32_t origin) { a.init(A, lda, e.M, K, origin, wave, lane, g_gemm_zero); };
+  auto ib = [&](auto& b, uint32_t origin) { b.init(B, ldb, e.N, K, origin, wave, lane, g_gemm_zero); };
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
-  ML::type::run(smem, a, b, kt0, kt1, acc, wave, lane);
-  if constexpr (OUT == 0) epilogue_out<BM, BN, false, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
-  else if constexpr (OUT == 3) epilogue_out<BM, BN, true, T, C::WM, C::WN>(smem, acc, e, m0, n0, 0, wave, lane);
-  else epilogue_f32<BM, BN, OUT == 2, C::WM, C::WN>(smem, acc, e, m0, n0, wave, lane);
+  run_main_loop<T, C, PA, PB, kGemmLoop>(smem, ia, ib, m0, n0, kt0, kt1, acc, wave, lane);
+  if constexpr (OUT == 0)
+    epilogue_out<BM, BN, false, T, C::WM, C::WN, false, C::PP>(smem, acc, e, m0, n0, 0, wave, lane);
+  else if constexpr (OUT == 3)
+    epilogue_out<BM, BN, true, T, C::WM, C::WN, false, C::PP>(smem, acc, e, m0, n0, 0, wave, lane);
+  else
+    epilogue_f32<BM, BN, OUT == 2, C::WM, C::WN, C::PP>(smem, acc, e, m0, n0, wave, lane);
 }
 
 }  // namespace gk
@@ -68,9 +68,9 @@ static void launch_out(const void* A, long lda, const void* B, long ldb, int K, 
   dim3 grid(tiles, splits);
   const T* a = (const T*)A;
   const T* b = (const T*)B;
-  // a 256 x 256 fp32 tile does not fit the LDS: those tiles only serve out 0 (with_tile maps
-  // the fp32-output modes to 256 x 128)
-  constexpr bool kWide = C::BM * C::BN > 256 * 128;
+  // a 256 x 256 fp32 tile does not fit the LDS: the 2-phase loop's 256 x 256 tile only serves
+  // out 0 (with_tile maps the fp32-output modes to 256 x 128); the ping-pong one stages halves
+  constexpr bool kWide = C::BM * C::BN > 256 * 128 && !C::PP;
   if (out == 3) {  // addend epilogue: instantiated for the data-grad layout (A [M][K], B [K][N])
     if constexpr (AK && !BK_)
       hipLaunchKernelGGL((gemm_dense_kernel<C, AK, BK_, 3, T>), grid, dim3(C::THREADS), 0, st, a, lda, b, ldb, (uint32_t)K, tN, per, e);

@@ -46,7 +46,7 @@ int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 // bias / relu: optional per-channel bias and ReLU in the epilogue (convs without BN: VGG, AlexNet)
 // cfg: tile config id (conv_common.hpp table; < 0 = heuristic default)
-constexpr int kConvTileConfigs = 11;
+constexpr int kConvTileConfigs = 14;
 //  det_rows > 0 (deterministic mode): st_sum / st_sq are [det_rows][Co] partial slabs, one row
 //  per M-tile (det_rows = conv_fwd_tiles_m(s, cfg)), written without atomics.
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
@@ -239,10 +239,14 @@ void sgd_step(float* p, const float* g, float* m, void* shadow, long n, float lr
               float dampening, float wd, bool nesterov, bool first, float grad_scale,
               hipStream_t st);
 // One-shot collective over peer workspaces (csrc/kernels/oneshot.hip): fp32 sum * scale
-// (reduce) or a byte broadcast from `src`; nbytes % 16 == 0, nbytes <= cap.
+// (reduce) or a byte broadcast from `src`; nbytes % 16 == 0, nbytes <= cap.  nblocks: the
+// communicator's fixed grid (oneshot_blocks(cap)); timeout_s: the bounded wait for a peer.
 constexpr long kOneShotHeaderBytes = 4096;
+constexpr long kOneShotErrOffset = 2048;  // two words: {1 + peer, epoch} of a wait that gave up
+int oneshot_blocks(long cap);
 void oneshot_launch(char* const* bases, int rank, int world, const void* in, void* out,
-                    long nbytes, bool reduce, int src, float scale, long cap, hipStream_t st);
+                    long nbytes, bool reduce, int src, float scale, long cap, int nblocks,
+                    double timeout_s, hipStream_t st);
 // DDP bf16 wire: wire = bf16(g * scale), g = fp32(wire); n % 8 == 0, 16-B aligned pointers
 void grad_pack_bf16(const float* g, void* wire, long n, float scale, hipStream_t st);
 void grad_unpack_bf16(const void* wire, float* g, long n, hipStream_t st);

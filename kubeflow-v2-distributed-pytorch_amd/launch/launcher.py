@@ -7,9 +7,12 @@ every replica with the rendezvous env contract task.py consumes — ``WORLD_SIZE
 (task.py:61, 80, 98, 141, 289) — and, in ``nproc_per_node`` mode, the torchrun contract
 (``RANK``/``LOCAL_RANK``/``WORLD_SIZE``/``LOCAL_WORLD_SIZE`` per GPU rank).
 
-MI355X specifics: each replica is pinned to a disjoint slice of the node's GPUs through
-``HIP_VISIBLE_DEVICES`` (one process per GPU is the RCCL/xGMI sweet spot);
-``HSA_ENABLE_IPC_MODE_LEGACY=0`` is forced so RCCL's dmabuf IPC works.
+MI355X specifics: each replica OWNS a disjoint slice of the node's GPUs (one process per GPU is
+the RCCL/xGMI sweet spot) but every process still SEES all of them: RCCL's xGMI P2P/IPC
+transport needs the peers visible.  The slice is passed as ``MIPIPE_DEVICE_OFFSET`` /
+``MIPIPE_LOCAL_GPUS`` and the rank picks ``cuda:(offset + local index)`` — the one policy of
+:mod:`mipipe.launch.env`, shared with ``bench.py``'s launcher.  ``HSA_ENABLE_IPC_MODE_LEGACY=0``
+is forced so RCCL's dmabuf IPC works.
 
 Failure semantics: fail-fast — the first replica that exits non-zero causes
 every other replica's process group to get SIGTERM, then SIGKILL after a grace period; the
@@ -27,6 +30,8 @@ import threading
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
+
+from .env import rank_env
 
 __all__ = ["LaunchSpec", "launch", "free_port", "visible_gpu_ids", "ReplicaResult"]
 
@@ -127,34 +132,17 @@ def build_envs(spec: LaunchSpec) -> List[Dict[str, str]]:
     procs_per_replica = nproc or 1
     world = spec.replica_count * procs_per_replica
     for r in range(spec.replica_count):
-        slice_ = gpus[r * per_replica:(r + 1) * per_replica] if per_replica else []
         for lr in range(procs_per_replica):
-            e = dict(os.environ)
-            e.update(spec.env)
-            e["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
-            e["MASTER_ADDR"] = spec.master_addr
-            e["MASTER_PORT"] = str(port)
             if nproc:
-                e["WORLD_SIZE"] = str(world)
-                e["RANK"] = str(r * procs_per_replica + lr)
-                e["LOCAL_RANK"] = str(lr)
-                e["LOCAL_WORLD_SIZE"] = str(procs_per_replica)
-                e["GROUP_RANK"] = str(r)
-                dev = slice_[lr:lr + 1] if per_replica else []
-                if per_replica and not dev:
+                if per_replica and lr >= per_replica:
                     raise RuntimeError(f"nproc_per_node={nproc} exceeds accelerator_count={per_replica}")
-                vis = ",".join(dev)
-            else:
-                e["WORLD_SIZE"] = str(spec.replica_count)
-                e["RANK"] = str(r)
-                vis = ",".join(slice_)
-            if per_replica:
-                e["HIP_VISIBLE_DEVICES"] = vis
-                e.pop("CUDA_VISIBLE_DEVICES", None)
-                e.pop("ROCR_VISIBLE_DEVICES", None)
-            else:
-                e["HIP_VISIBLE_DEVICES"] = ""
-                e["MIPIPE_FORCE_CPU"] = "1"
+                ids = dict(world=world, rank=r * procs_per_replica + lr, local_rank=lr,
+                           local_world=procs_per_replica, group_rank=r)
+            else:  # one process per replica that spawns its GPU workers (task.py:117-124)
+                ids = dict(world=spec.replica_count, rank=r)
+            e = rank_env(os.environ, master_addr=spec.master_addr, master_port=port,
+                         gpu_offset=r * per_replica, replica_gpus=per_replica, extra=spec.env,
+                         **ids)
             if spec.model_dir:
                 e["AIP_MODEL_DIR"] = spec.model_dir
             if spec.checkpoint_dir:

@@ -8,7 +8,8 @@ builds environments and starts ``N`` brand-new interpreters with ``subprocess`` 
 imports a HIP-initialising API.  Each child gets ``RANK = LOCAL_RANK = i``,
 ``WORLD_SIZE = LOCAL_WORLD_SIZE = N``, ``MASTER_ADDR = 127.0.0.1`` and a free
 ``MASTER_PORT``; all GPUs stay visible to every rank (RCCL needs the peers for xGMI P2P), the
-rank selects ``cuda:LOCAL_RANK`` itself.
+rank selects ``cuda:LOCAL_RANK`` itself — the policy of :mod:`mipipe.launch.env`, whose
+:func:`~mipipe.launch.env.rank_env` builds these environments for every launcher.
 
 Output: rank 0's stdout passes through unchanged (``bench.py`` prints its JSON line there);
 the other ranks' stdout is redirected to the parent's stderr so the driver still sees exactly
@@ -24,6 +25,7 @@ import sys
 import time
 from typing import Dict, List, Optional, Sequence
 
+from .env import rank_env
 from .launcher import free_port
 
 __all__ = ["spawn_local_ranks", "rank_envs"]
@@ -32,19 +34,9 @@ __all__ = ["spawn_local_ranks", "rank_envs"]
 def rank_envs(nprocs: int, port: Optional[int] = None,
               extra: Optional[Dict[str, str]] = None) -> List[Dict[str, str]]:
     port = port or free_port()
-    envs = []
-    for r in range(nprocs):
-        e = dict(os.environ)
-        if extra:
-            e.update(extra)
-        from mipipe.parallel.dist_utils import configure_rccl_env
-        configure_rccl_env(e)  # high-priority comm stream + MIPIPE_RCCL_PROFILE channels
-        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nprocs),
-                  "LOCAL_WORLD_SIZE": str(nprocs), "GROUP_RANK": "0",
-                  "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
-                  "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
-        envs.append(e)
-    return envs
+    return [rank_env(os.environ, master_addr="127.0.0.1", master_port=port, world=nprocs,
+                     rank=r, local_rank=r, local_world=nprocs, group_rank=0, extra=extra)
+            for r in range(nprocs)]
 
 
 def _terminate(procs: Sequence[subprocess.Popen], grace: float) -> None:

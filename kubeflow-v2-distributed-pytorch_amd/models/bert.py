@@ -219,12 +219,17 @@ class BertForMaskedLM(tnn.Module):
         # On the GPU the per-step part of every dropout seed is a device counter advanced here by
         # a device op, so a hipGraph-captured step draws fresh masks on every replay (the host
         # counter self._step would be frozen at capture).
+        # The counter starts at the host step (so a resumed run, whose _step the checkpoint
+        # restores, continues the mask sequence), and each forward hands its kernels a SNAPSHOT
+        # of it: the backward regenerates its masks from the value this forward used even if
+        # another training forward advances the counter before this backward runs.
         sdev = None
         if self.training and input_ids.is_cuda:
             if self._step_dev is None or self._step_dev.device != input_ids.device:
-                self._step_dev = torch.zeros(1, dtype=torch.int32, device=input_ids.device)
+                self._step_dev = torch.full((1,), self._step - 1, dtype=torch.int32,
+                                            device=input_ids.device)
             self._step_dev.add_(1)
-            sdev = self._step_dev
+            sdev = self._step_dev.clone()
 
         def seed_at(site: int):
             if sdev is not None:

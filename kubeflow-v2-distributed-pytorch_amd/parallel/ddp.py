@@ -345,7 +345,7 @@ class DistributedDataParallel(tnn.Module):
                     self._clog.record_shape("all_reduce", b.end - b.start, wdt)
                 self._steps += 1
                 if self.check_collectives and self._steps % self.check_every == 0:
-                    self.verify_collective_sequence()
+                    self._verify_when_safe()
             return
         self._reported = set()
         for b in self.buckets:
@@ -421,9 +421,25 @@ class DistributedDataParallel(tnn.Module):
                 b.tmp = None
         self._steps += 1
         if self.check_collectives and self._steps % self.check_every == 0:
-            self.verify_collective_sequence()
+            self._verify_when_safe()
 
     # ------------------------------------------------------------------ debugging
+    def check_comm_errors(self, final: bool = False) -> None:
+        """Raise :class:`CollectiveSequenceError` if a one-shot collective gave up waiting for a
+        peer.  Cheap (no host sync) unless ``final``; the trainer calls it at every
+        log interval and once at the end.  RCCL collectives fail through the process group's
+        own timeout instead."""
+        if self._oneshot is not None:
+            self._oneshot.check(final=final)
+
+    def _verify_when_safe(self) -> None:
+        """The digest exchange synchronises the host with every rank: never inside a hipGraph
+        capture (warm-up / capture of a graphed step); that check is skipped, the next one covers it
+        (the digest accumulates every collective)."""
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return
+        self.verify_collective_sequence()
+
     def verify_collective_sequence(self) -> None:
         """All-gather the per-rank digest of collectives issued so far; raise on mismatch."""
         d = (self._clog.digest().hex(), self._clog.count)

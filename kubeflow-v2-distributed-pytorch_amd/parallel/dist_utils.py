@@ -97,6 +97,53 @@ def configure_rccl_env(env: Optional[dict] = None, profile: Optional[str] = None
     return target
 
 
+def enable_rccl_transport_log(env: Optional[dict] = None) -> Optional[str]:
+    """Send RCCL's INFO log of communicator setup (not per-collective lines) to a per-process file
+    so :func:`rccl_transports` can report which transport each peer pair got — the evidence that
+    an 8-GPU run used xGMI P2P rather than host shared memory.  Must run before the first
+    communicator exists.  Returns the log path, or None when the caller already routes NCCL_DEBUG
+    elsewhere (or ``MIPIPE_RCCL_TRANSPORT_LOG=0``)."""
+    import tempfile
+    target = os.environ if env is None else env
+    if target.get("MIPIPE_RCCL_TRANSPORT_LOG", "1") == "0":
+        return None
+    if "NCCL_DEBUG" in target and "NCCL_DEBUG_FILE" not in target:
+        return None
+    d = target.get("MIPIPE_RCCL_LOG_DIR") or tempfile.gettempdir()
+    target.setdefault("NCCL_DEBUG", "INFO")
+    target.setdefault("NCCL_DEBUG_SUBSYS", "INIT,P2P,SHM,NET,GRAPH")
+    target.setdefault("NCCL_DEBUG_FILE", os.path.join(d, f"mipipe_rccl.{os.getpid()}.log"))
+    return target["NCCL_DEBUG_FILE"]
+
+
+_VIA = None
+
+
+def rccl_transports(path: Optional[str]) -> Optional[dict]:
+    """Parse RCCL channel-setup lines (``Channel 00/0 : 0[0] -> 1[1] via P2P/IPC``) from an INFO
+    log: ``{"transports": {"P2P/IPC": n, ...}, "pairs": {"0->1": "P2P/IPC", ...}}``, or None
+    when the log is missing or has no such lines."""
+    global _VIA
+    import re
+    if not path or not os.path.exists(path):
+        return None
+    if _VIA is None:
+        _VIA = re.compile(r"(\d+)\[[^\]]*\]\s*->\s*(\d+)\[[^\]]*\].*?\bvia\s+([A-Za-z0-9_]+(?:/[A-Za-z0-9_]+)?)")
+    counts: dict = {}
+    pairs: dict = {}
+    with open(path, errors="replace") as f:
+        for line in f:
+            m = _VIA.search(line)
+            if not m:
+                continue
+            t = m.group(3)
+            counts[t] = counts.get(t, 0) + 1
+            pairs.setdefault(f"{m.group(1)}->{m.group(2)}", t)
+    if not counts:
+        return None
+    return {"transports": counts, "pairs": dict(sorted(pairs.items()))}
+
+
 def rccl_settings(env: Optional[dict] = None) -> dict:
     """The RCCL / ProcessGroupNCCL variables in effect (recorded with every bench line)."""
     src = os.environ if env is None else env

@@ -12,6 +12,13 @@ Scope: the ranks of one node (all peers reachable over xGMI; at most 8), every r
 same sequence of calls with the same sizes.  DDP uses it for C4 when ``MIPIPE_ONESHOT=1``;
 RCCL stays the default (the one-shot path is checked on one GPU with two processes sharing it
 — ``tests/test_oneshot_gpu.py`` — not yet on an 8-GPU mesh).
+
+Failure ("a hang becomes an error"): a kernel that waits longer than ``timeout_s``
+(``MIPIPE_ONESHOT_TIMEOUT_S``, default 120 s) for a peer records {peer, epoch} in its error words
+and leaves the output untouched instead of reading a slot the peer never filled.  :meth:`check`
+turns the error words into a :class:`~mipipe.parallel.ddp.CollectiveSequenceError`; it reads
+them through an asynchronous copy into pinned memory (no host sync), so DDP can poll it at every
+log interval and once, synchronously, at the end of training.
 """
 from __future__ import annotations
 
@@ -42,7 +49,8 @@ class OneShotComm:
     """One workspace per rank with ``cap_bytes`` per message; ``all_reduce`` (fp32, in place,
     sum or average) and ``broadcast`` (any dtype, in place)."""
 
-    def __init__(self, group=None, cap_bytes: int = 1 << 20, device: Optional[torch.device] = None):
+    def __init__(self, group=None, cap_bytes: int = 1 << 20, device: Optional[torch.device] = None,
+                 timeout_s: Optional[float] = None):
         from mipipe.ops._native import native
         self.group = group
         self.rank = dist.get_rank(group)
@@ -53,7 +61,11 @@ class OneShotComm:
             raise ValueError("one-shot collectives need every rank on this node")
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.device = dev
-        self._c = native().OneShot(self.rank, self.world, int(cap_bytes), dev.index)
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("MIPIPE_ONESHOT_TIMEOUT_S", "120"))
+        self.timeout_s = float(timeout_s)
+        self._c = native().OneShot(self.rank, self.world, int(cap_bytes), dev.index,
+                                   self.timeout_s)
         hs = [None] * self.world
         dist.all_gather_object(hs, bytes(self._c.handle()), group=group)
         self._c.open(hs)
@@ -76,5 +88,25 @@ class OneShotComm:
         return t
 
     def error(self) -> int:
-        """Nonzero when a wait for a peer gave up (5 s); synchronises the device."""
+        """1 + the peer a wait gave up on (0: none); synchronises the device."""
         return self._c.error()
+
+    def check(self, final: bool = False) -> None:
+        """Raise if any one-shot call so far gave up waiting for a peer.
+
+        ``final=False`` (the per-log-interval poll): reads the error words copied by the previous
+        poll if that copy has landed, then requests a new copy — no host synchronisation, so the
+        answer lags by one interval.  ``final=True``: synchronous read (end of training)."""
+        from mipipe.parallel.ddp import CollectiveSequenceError
+        if final:
+            peer, epoch = self._c.error_info()
+        else:
+            if torch.cuda.is_current_stream_capturing():
+                return
+            peer, epoch = self._c.poll_error()
+            self._c.request_error()
+        if peer > 0:
+            raise CollectiveSequenceError(
+                f"one-shot collective: rank {self.rank} waited more than {self.timeout_s:g} s for "
+                f"rank {peer - 1} at call epoch {epoch} (that rank skipped or stalled a collective "
+                "this rank issued); the result of that call was not written")

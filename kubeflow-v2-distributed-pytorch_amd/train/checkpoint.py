@@ -65,12 +65,26 @@ def _ckpt_dir(args) -> str:
     return uri_to_local_path(base)
 
 
+def _inner(model):
+    return getattr(model, "module", model)
+
+
 def save_checkpoint(model, optimizer, args, epoch: int, best_acc1: float) -> str:
     state = {"epoch": epoch, "arch": args.arch, "best_acc1": float(best_acc1),
              "state_dict": _cpu_state_dict(model), "optimizer": optimizer.state_dict()}
+    step = getattr(_inner(model), "_step", None)
+    if isinstance(step, int):
+        # the model's dropout-seed step (BERT): a resumed run continues the mask sequence
+        # instead of replaying it from step 1
+        state["model_step"] = step
     path = os.path.join(_ckpt_dir(args), CHECKPOINT_NAME)
     _atomic_save(state, path)
     return path
+
+
+def restore_model_step(model, state: Dict[str, Any]) -> None:
+    if "model_step" in state and hasattr(_inner(model), "_step"):
+        _inner(model)._step = int(state["model_step"])
 
 
 def resolve_resume_path(resume: str, model_dir: str) -> str:

@@ -42,6 +42,7 @@ import torch.multiprocessing as mp
 from mipipe.models import create_model, model_names
 from mipipe.obs import trace
 from mipipe.obs.log import JsonlLogger
+from mipipe.launch.env import device_offset, local_gpus
 from mipipe.parallel import DataParallel, DistributedDataParallel, DistributedSampler
 from mipipe.parallel import dist_utils
 from mipipe.data.synthetic import DATASET_SHAPES, DeviceBatchLoader, SyntheticImageDataset
@@ -216,9 +217,12 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def _ngpus() -> int:
+    """GPUs of this node (replica): the launcher's MIPIPE_LOCAL_GPUS when it set one (every GPU
+    of the node stays visible, launch/env.py), else every visible device."""
     if os.environ.get("MIPIPE_FORCE_CPU") == "1":
         return 0
-    return torch.cuda.device_count()
+    n = local_gpus()
+    return n if n is not None else torch.cuda.device_count()
 
 
 def main(argv=None) -> int:
@@ -282,6 +286,7 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
     use_gpu = _ngpus() > 0
     if use_gpu:
         local = args.gpu if args.gpu is not None else int(os.environ.get("LOCAL_RANK", 0))
+        local += device_offset()  # this replica's first GPU (launch/env.py)
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
@@ -344,6 +349,7 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
             start_epoch = int(state["epoch"])
             best_acc1 = float(state.get("best_acc1", 0.0))
             ckpt.load_model_state(model, state["state_dict"])
+            ckpt.restore_model_step(model, state)
             optimizer.load_state_dict(state["optimizer"])
             print(f"=> loaded checkpoint '{path}' (epoch {start_epoch})")
         else:
@@ -459,6 +465,8 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
             global_step += 1
             i += 1
             if args.log_every and global_step % args.log_every == 0:
+                if isinstance(model, DistributedDataParallel):
+                    model.check_comm_errors()  # a one-shot wait that gave up -> error, no sync
                 last_loss = float(loss.detach().float().item())
                 jlog.log("step", epoch=epoch, step=global_step, loss=last_loss,
                          samples_per_sec=meter.samples_per_sec())
@@ -467,6 +475,8 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
                           f"{meter.samples_per_sec() * world:.1f} samples/s (job)", flush=True)
         if args.rank == 0:
             ckpt.save_checkpoint(model, optimizer, args, epoch + 1, best_acc1)
+    if isinstance(model, DistributedDataParallel):
+        model.check_comm_errors(final=True)
     # fixed quirk: evaluate and save the *trained* model at the end as well
     accuracy = evaluate(model, device, test_loader)
     best_acc1 = max(best_acc1, accuracy)

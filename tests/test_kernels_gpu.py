@@ -535,7 +535,7 @@ TILE_CASES = [
 ]
 
 
-@pytest.mark.parametrize("cfg", list(range(11)))
+@pytest.mark.parametrize("cfg", list(range(14)))
 @pytest.mark.parametrize("case", TILE_CASES)
 def test_conv_every_tile_config(cfg, case):
     """Every tile config of the tuning table (block tile / LDS stages / 4- or 8-wave grid) gives

@@ -86,3 +86,97 @@ def test_ddp_native_reducer_two_ranks_one_gpu(oneshot):
     assert "step0 native reducer" in r.stdout and "DDP gpu check OK" in r.stdout
     if oneshot == "1":
         assert "oneshot=True" in r.stdout
+
+
+def _run_two(target, timeout=150):
+    out = mp.Manager().dict()
+    ctx = mp.get_context("spawn")
+    port = 29100 + os.getpid() % 250 + (hash(target.__name__) % 50)
+    ps = [ctx.Process(target=target, args=(r, 2, port, out)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=timeout)
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    return out
+
+
+def _worker_no_sync(rank, world, port, out):
+    """Back-to-back calls whose sizes straddle the old per-message grid boundary (1000 / 1025
+    16-byte vectors), no host sync between them: the fixed grid keeps every block's epoch in
+    lock-step (advisor finding, round 3)."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from mipipe.parallel.oneshot import OneShotComm
+    c = OneShotComm(cap_bytes=1 << 20, device=torch.device("cuda", 0))
+    res = {"ok": True, "msg": "", "nblocks": c._c.nblocks}
+    ts, exps = [], []
+    for it in range(48):
+        n = (1000 if it % 2 == 0 else 1025) * 4  # floats
+        parts = [torch.randn(n, generator=torch.Generator().manual_seed(77 * it + r))
+                 for r in range(world)]
+        t = parts[rank].cuda()
+        c.all_reduce(t)
+        ts.append(t)
+        exps.append(parts[0] + parts[1])
+    torch.cuda.synchronize()
+    for it, (t, e) in enumerate(zip(ts, exps)):
+        if not torch.equal(t.cpu(), e):
+            res = {"ok": False, "msg": f"call {it}: {(t.cpu() - e).abs().max()}"}
+            break
+    res["err"] = c.error()
+    out[rank] = res
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_oneshot_alternating_sizes_without_host_sync():
+    out = _run_two(_worker_no_sync)
+    for r in range(2):
+        assert out[r]["ok"], out[r]["msg"]
+        assert out[r]["err"] == 0 and out[r]["nblocks"] == 16, out[r]
+
+
+def _worker_skip(rank, world, port, out):
+    """Rank 1 skips one broadcast: rank 0's kernel gives up after its 2 s deadline, leaves its
+    output untouched and check() raises CollectiveSequenceError naming rank 1."""
+    import time
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from mipipe.parallel.ddp import CollectiveSequenceError
+    from mipipe.parallel.oneshot import OneShotComm
+    c = OneShotComm(cap_bytes=1 << 20, device=torch.device("cuda", 0), timeout_s=2.0)
+    b = torch.full((4096,), float(rank + 1), device="cuda")
+    c.broadcast(b, src=1)  # both ranks: fine
+    torch.cuda.synchronize()
+    res = {"first": float(b[0]), "raised": "", "untouched": None, "dt": 0.0}
+    if rank == 0:
+        c.check()  # poll: requests the first async copy, nothing known yet
+        b2 = torch.full((4096,), 5.0, device="cuda")
+        t0 = time.time()
+        c.broadcast(b2, src=1)  # rank 1 never issues this one
+        torch.cuda.synchronize()
+        res["dt"] = time.time() - t0
+        res["untouched"] = bool(torch.all(b2 == 5.0))
+        try:
+            c.check(final=True)
+        except CollectiveSequenceError as e:
+            res["raised"] = str(e)
+    out[rank] = res
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_oneshot_skipped_call_raises():
+    out = _run_two(_worker_skip)
+    assert out[0]["first"] == 2.0 and out[1]["first"] == 2.0
+    r0 = out[0]
+    assert "rank 1" in r0["raised"] and "one-shot" in r0["raised"], r0
+    assert r0["untouched"] is True and 1.5 < r0["dt"] < 30, r0

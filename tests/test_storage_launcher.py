@@ -41,7 +41,10 @@ def test_env_contract(monkeypatch):
                                  model_dir="gs://b/m/"))
     assert [e["RANK"] for e in envs] == ["0", "1", "2"]
     assert all(e["WORLD_SIZE"] == "3" for e in envs)
-    assert [e["HIP_VISIBLE_DEVICES"] for e in envs] == ["0,1", "2,3", "4,5"]
+    # every replica sees the whole node (RCCL xGMI P2P) and owns a slice of it
+    assert all(e["HIP_VISIBLE_DEVICES"] == "0,1,2,3,4,5,6,7" for e in envs)
+    assert [(e["MIPIPE_DEVICE_OFFSET"], e["MIPIPE_LOCAL_GPUS"]) for e in envs] == \
+        [("0", "2"), ("2", "2"), ("4", "2")]
     assert all(e["AIP_MODEL_DIR"] == "gs://b/m/" for e in envs)
     assert all(e["MASTER_ADDR"] == "127.0.0.1" for e in envs)
     assert len({e["MASTER_PORT"] for e in envs}) == 1
@@ -49,7 +52,28 @@ def test_env_contract(monkeypatch):
                                  nproc_per_node=4))
     assert [e["RANK"] for e in envs] == [str(i) for i in range(8)]
     assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"] * 2
-    assert envs[5]["HIP_VISIBLE_DEVICES"] == "5"
+    assert envs[5]["HIP_VISIBLE_DEVICES"] == "0,1,2,3,4,5,6,7"
+    assert envs[5]["MIPIPE_DEVICE_OFFSET"] == "4" and envs[5]["LOCAL_RANK"] == "1"  # -> cuda:5
+    cpu = build_envs(LaunchSpec(command=["x"], replica_count=2, accelerator_count=0))
+    assert all(e["MIPIPE_FORCE_CPU"] == "1" and e["HIP_VISIBLE_DEVICES"] == "" for e in cpu)
+
+
+def test_launchers_share_one_env_builder(monkeypatch):
+    """bench.py's launcher (launch.local.rank_envs) and the job launcher (launch.build_envs) build
+    rank environments with the same function: same RCCL settings, same visibility policy."""
+    from mipipe.launch.local import rank_envs
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3")
+    monkeypatch.setenv("MIPIPE_RCCL_PROFILE", "overlap")
+    a = rank_envs(4, port=23456)
+    b = build_envs(LaunchSpec(command=["x"], replica_count=1, accelerator_count=4,
+                              nproc_per_node=4, master_port=23456))
+    for ea, eb in zip(a, b):
+        for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_PORT",
+                  "HIP_VISIBLE_DEVICES", "HSA_ENABLE_IPC_MODE_LEGACY", "TORCH_NCCL_HIGH_PRIORITY",
+                  "NCCL_MAX_NCHANNELS"):
+            assert ea.get(k) == eb.get(k), k
+    from mipipe.launch.env import device_offset
+    assert [int(e["LOCAL_RANK"]) + device_offset(e) for e in b] == [0, 1, 2, 3]
     with pytest.raises(RuntimeError):
         build_envs(LaunchSpec(command=["x"], replica_count=5, accelerator_count=2))
 
