@@ -1247,12 +1247,17 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>, optional<Tensor>> layerno
   return {dx, dg, db, dxd};
 }
 
-Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows, optional<Tensor> out) {
+// ordered (or deterministic mode): no float atomics — large tables through a stable sort of the
+// ids and one writer per row (embedding_bwd_sorted), small tables through per-block partial
+// tables summed in block order.  scale multiplies the scattered rows (ordered path only).
+Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows, optional<Tensor> out, bool ordered,
+                     double scale) {
   check_bf16(dy, "dy");
   check_cuda(idx, "idx");
   c10::DeviceGuard g(dy.device());
   int64_t H = dy.size(-1), n = dy.numel() / H;
   TORCH_CHECK(idx.numel() == n && idx.scalar_type() == at::kLong, "embedding_bwd idx mismatch");
+  TORCH_CHECK(H % 8 == 0 && H <= 2048, "embedding_bwd needs H % 8 == 0, H <= 2048");
   Tensor o;
   if (out.has_value()) {  // accumulate into (e.g. the flat-gradient view of the table)
     check_f32(*out, "out");
@@ -1260,6 +1265,26 @@ Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows, optional<Tensor> o
     o = *out;
   } else {
     o = torch::zeros({num_rows, H}, dy.options().dtype(at::kFloat));
+  }
+  const bool det = ordered || mipipe::g_deterministic;
+  TORCH_CHECK(scale == 1.0 || det, "embedding_bwd: scale needs the ordered path");
+  if (det && n > 0) {
+    auto dyc = dy.contiguous();
+    if (num_rows <= 8) {
+      auto part = torch::empty({mipipe::embedding_bwd_small_blocks(n), num_rows * H},
+                               dy.options().dtype(at::kFloat));
+      if (scale != 1.0) dyc = (dyc.to(at::kFloat) * scale).to(at::kBFloat16);
+      mipipe::embedding_bwd(dyc.data_ptr(), idx.data_ptr<int64_t>(), o.data_ptr<float>(), n,
+                            (int)H, (int)num_rows, stream(), part.data_ptr<float>());
+    } else {
+      auto srt = at::sort(idx.reshape({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
+      auto sid = std::get<0>(srt).contiguous();
+      auto perm = std::get<1>(srt).contiguous();
+      mipipe::embedding_bwd_sorted(dyc.data_ptr(), sid.data_ptr<int64_t>(),
+                                   perm.data_ptr<int64_t>(), o.data_ptr<float>(), n, (int)H,
+                                   (float)scale, stream());
+    }
+    return o;
   }
   mipipe::embedding_bwd(dy.data_ptr(), idx.data_ptr<int64_t>(), o.data_ptr<float>(), n, (int)H,
                         (int)num_rows, stream());
@@ -1343,7 +1368,7 @@ Tensor attention_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, int64_t B, i
   auto dqkv = torch::empty_like(qkv);
   auto f = qkv.options().dtype(at::kFloat);
   auto delta = torch::empty({B, H, S}, f);
-  auto dq_acc = torch::empty({B * S, H * 64}, f);
+  auto dq_acc = torch::empty({mipipe::attention_dq_slabs((int)S), B * S, H * 64}, f);
   mipipe::attention_bwd(dout.data_ptr(), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                         mask_ptr(mask, B, S), dqkv.data_ptr(), delta.data_ptr<float>(),
                         dq_acc.data_ptr<float>(), (int)B, (int)S, (int)H, (float)scale,
@@ -1720,7 +1745,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dbeta") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,
         py::arg("drop_seed_dev") = py::none());
   m.def("embedding_bwd", &embedding_bwd, py::arg("dy"), py::arg("idx"), py::arg("num_rows"),
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("ordered") = false, py::arg("scale") = 1.0);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(),
         py::arg("two_pass") = false);
   m.def("set_colsum_row_blocks", [](int v) { mipipe::g_colsum_row_blocks = v; });

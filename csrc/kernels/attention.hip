@@ -26,6 +26,7 @@
 // Replaces torch.nn.MultiheadAttention / HF BertSelfAttention's matmul-softmax-matmul chain
 // (SURVEY.md §2.5 "BASELINE config 4": softmax-attention flash-style fwd/bwd, head_dim 64).
 #include "common.hpp"
+#include "launchers.hpp"
 
 namespace mipipe {
 namespace attn {
@@ -288,8 +289,9 @@ struct BwdArgs {
   const float* lse;    // [B][H][S]
   const float* delta;  // [B][H][S]
   const float* mask;
-  float* dq_acc;       // [B*S][H*64] fp32, zeroed
+  float* dq_acc;       // [B*S][H*64] fp32, zeroed; det: [nkb][B*S][H*64] slabs, written
   __bf16* dqkv;
+  int det;             // deterministic mode: each key block STORES its dQ part in its own slab
   int B, S, H;
   float scale, scale_log2;
   float p_drop;
@@ -444,8 +446,16 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(BwdArgs a) {
         const int qg = it * 32 + qr0 + 4 * g + i;
         if (qg < S) {
           float* dst = a.dq_acc + ((long)b * S + qg) * ldq + h * D + dc0 + li;
+          if (a.det) {
+            // deterministic: this key block's slab; every (q, d) of it is written exactly once
+            // (one q tile per iteration), and attn_dq_store_kernel sums the slabs in key order
+            dst += (long)kbk * a.B * S * ldq;
 #pragma unroll
-          for (int dt = 0; dt < DT; ++dt) atomicAdd(dst + 16 * dt, cacc[dt][i]);
+            for (int dt = 0; dt < DT; ++dt) dst[16 * dt] = cacc[dt][i];
+          } else {
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) atomicAdd(dst + 16 * dt, cacc[dt][i]);
+          }
         }
       }
     }
@@ -469,17 +479,22 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(BwdArgs a) {
   }
 }
 
-// dq (fp32 accumulator) -> bf16 q columns of dqkv
+// dq (fp32 accumulator, or `slabs` per-key-block slabs summed in key-block order) -> bf16 q
+// columns of dqkv
 __global__ __launch_bounds__(256) void attn_dq_store_kernel(const float* __restrict__ acc,
                                                             __bf16* __restrict__ dqkv, long T,
-                                                            int HD) {
+                                                            int HD, int slabs) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-element chunk each
   const long per_row = HD / 8;
   if (i >= T * per_row) return;
   const long t = i / per_row, c = i % per_row;
-  const float4* src = reinterpret_cast<const float4*>(acc + t * HD + c * 8);
-  float4 x = src[0], y = src[1];
-  float f[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+  float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int sl = 0; sl < slabs; ++sl) {
+    const float4* src = reinterpret_cast<const float4*>(acc + ((long)sl * T + t) * HD + c * 8);
+    const float4 x = src[0], y = src[1];
+    f[0] += x.x; f[1] += x.y; f[2] += x.z; f[3] += x.w;
+    f[4] += y.x; f[5] += y.y; f[6] += y.z; f[7] += y.w;
+  }
   *reinterpret_cast<uint4*>(dqkv + t * 3l * HD + c * 8) = pack8(f);
 }
 
@@ -512,15 +527,25 @@ void attention_fwd(const void* qkv, const float* mask, void* o, float* lse, int 
     hipLaunchKernelGGL(attn::attn_fwd_kernel<4>, dim3(B * H * ((S + 127) / 128)), dim3(256), 0, st, a);
 }
 
+int attention_dq_slabs(int S) {
+  if (!g_deterministic) return 1;
+  const int kb = attn_waves(1, S, 1) == 2 ? 64 : 128;  // keys per backward block
+  return (S + kb - 1) / kb;
+}
+
 void attention_bwd(const void* dout, const void* qkv, const void* o, const float* lse,
                    const float* mask, void* dqkv, float* delta, float* dq_acc, int B, int S,
                    int H, float scale, float p_drop, uint32_t seed, hipStream_t st,
                    const uint32_t* seed_dev) {
   const long rows = (long)B * S * H;
+  // deterministic mode with several key blocks per (b, h): per-key-block dQ slabs summed in a
+  // fixed order instead of fp32 atomics (one key block: its single add is already exact)
+  const int slabs = attention_dq_slabs(S);
+  const int det = slabs > 1 ? 1 : 0;
   hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
                      (const __bf16*)dout, (const __bf16*)o, delta, dq_acc, B, S, H);
   attn::BwdArgs a{(const __bf16*)qkv, (const __bf16*)dout, lse, delta, mask, dq_acc,
-                  (__bf16*)dqkv, B, S, H, scale, scale * attn::kLog2e, p_drop,
+                  (__bf16*)dqkv, det, B, S, H, scale, scale * attn::kLog2e, p_drop,
                   drop_threshold(p_drop), seed, seed_dev};
   if (attn_waves(B, S, H) == 2)
     hipLaunchKernelGGL(attn::attn_bwd_kernel<2>, dim3(B * H * ((S + 63) / 64)), dim3(128), 0, st, a);
@@ -528,7 +553,7 @@ void attention_bwd(const void* dout, const void* qkv, const void* o, const float
     hipLaunchKernelGGL(attn::attn_bwd_kernel<4>, dim3(B * H * ((S + 127) / 128)), dim3(256), 0, st, a);
   const long chunks = (long)B * S * H * attn::D / 8;
   hipLaunchKernelGGL(attn::attn_dq_store_kernel, dim3((chunks + 255) / 256), dim3(256), 0, st,
-                     dq_acc, (__bf16*)dqkv, (long)B * S, H * attn::D);
+                     dq_acc, (__bf16*)dqkv, (long)B * S, H * attn::D, det ? slabs : 1);
 }
 
 }  // namespace mipipe

@@ -311,7 +311,9 @@ extern int g_attn_waves;  // attention block size override (0 auto, 2, 4)
 void attention_fwd(const void* qkv, const float* mask, void* o, float* lse, int B, int S, int H,
                    float scale, float p_drop, uint32_t seed, hipStream_t st,
                    const uint32_t* seed_dev = nullptr);
-// dqkv [B*S][3*H*64]; delta [B][H][S] and dq_acc [B*S][H*64] fp32 are scratch.
+// dqkv [B*S][3*H*64]; delta [B][H][S] and dq_acc [attention_dq_slabs(S)][B*S][H*64] fp32 are
+// scratch (deterministic mode: one dQ slab per key block, summed in order; else 1 slab + atomics).
+int attention_dq_slabs(int S);
 void attention_bwd(const void* dout, const void* qkv, const void* o, const float* lse,
                    const float* mask, void* dqkv, float* delta, float* dq_acc, int B, int S,
                    int H, float scale, float p_drop, uint32_t seed, hipStream_t st,
@@ -322,8 +324,16 @@ void attention_bwd(const void* dout, const void* qkv, const void* o, const float
 // replayed hipGraph draws a fresh mask every step.
 void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStream_t st,
                  const uint32_t* seed_dev = nullptr);
+// partial (tables of <= 8 rows, deterministic mode): [embedding_bwd_small_blocks(n)][rows*H]
+// scratch — per-block tables summed in block order instead of float atomics
 void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, int rows,
-                   hipStream_t st);
+                   hipStream_t st, float* partial = nullptr);
+int embedding_bwd_small_blocks(long n);
+// Deterministic scatter-add: out[sorted_ids[i]] += scale * dy[perm[i]], tokens stably sorted by
+// id (perm: their positions); one writer per output row, rows summed in position order.
+// H % 8 == 0, H <= 2048.
+void embedding_bwd_sorted(const void* dy, const int64_t* sorted_ids, const int64_t* perm,
+                          float* out, long n, int H, float scale, hipStream_t st);
 // work (deterministic mode, else null): [colsum_blocks(rows, cols)][cols] floats of partials
 void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
                 hipStream_t st);

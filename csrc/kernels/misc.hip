@@ -567,9 +567,13 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const __bf16* __rest
 
 constexpr int kEmbSmallRows = 8;
 
+// (Column c of the LDS table is only ever touched by thread c % 256, in token order, so the
+// block's table is deterministic; with `partial` set each block WRITES its table to row
+// blockIdx.x of a [blocks][rows*H] slab — summed in block order by det_sum_rows — instead of
+// adding it to out with float atomics.)
 __global__ __launch_bounds__(256) void embedding_bwd_small_kernel(
     const __bf16* __restrict__ dy, const int64_t* __restrict__ idx, float* __restrict__ out,
-    long n, int H, int rows, long tok_per_block) {
+    long n, int H, int rows, long tok_per_block, float* __restrict__ partial) {
   extern __shared__ float tab[];  // [rows][H]
   for (int i = threadIdx.x; i < rows * H; i += 256) tab[i] = 0.f;
   __syncthreads();
@@ -579,21 +583,116 @@ __global__ __launch_bounds__(256) void embedding_bwd_small_kernel(
     for (int c = threadIdx.x; c < H; c += 256) atomicAdd(&tab[r * H + c], (float)dy[t * H + c]);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < rows * H; i += 256) atomicAdd(out + i, tab[i]);
+  if (partial != nullptr) {
+    float* dst = partial + (long)blockIdx.x * rows * H;
+    for (int i = threadIdx.x; i < rows * H; i += 256) dst[i] = tab[i];
+  } else {
+    for (int i = threadIdx.x; i < rows * H; i += 256) atomicAdd(out + i, tab[i]);
+  }
+}
+
+// Deterministic scatter-add over tokens SORTED by row id (stable sort: position order inside a
+// run of equal ids).  One wave per sorted index; the wave that starts a run sums the run's dy
+// rows in that order (8 bf16 columns per 16-B chunk, NC chunks per lane, four rows of loads in
+// flight) and adds scale * sum to its output row — exactly one writer per row, no atomics, so
+// the result is bit-identical run to run and on every rank that scatters the same tokens.
+template <int NC>
+__global__ __launch_bounds__(256) void embedding_bwd_sorted_kernel(
+    const __bf16* __restrict__ dy, const int64_t* __restrict__ sid,
+    const int64_t* __restrict__ perm, float* __restrict__ out, long n, int H, float scale) {
+  const long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const int64_t id = sid[i];
+  if (i > 0 && sid[i - 1] == id) return;  // not the start of a run
+  const int nch = H / 8;
+  float acc[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[c][e] = 0.f;
+  long j = i;
+  while (j < n && sid[j] == id) {
+    // up to four rows of this run per iteration, all loads issued before the adds (in order)
+    long p[4];
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool in = j + u < n && sid[j + u] == id;
+      p[u] = in ? perm[j + u] : perm[j];
+      cnt += in ? 1 : 0;
+    }
+    uint4 v[4][NC];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ch = lane + 64 * c;
+        v[u][c] = ch < nch ? *reinterpret_cast<const uint4*>(dy + p[u] * H + ch * 8)
+                           : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u < cnt) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          float f[8];
+          unpack8(v[u][c], f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[c][e] += f[e];
+        }
+      }
+    }
+    j += cnt;
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      float* o = out + id * H + ch * 8;
+      const float4 a = reinterpret_cast<float4*>(o)[0], b = reinterpret_cast<float4*>(o)[1];
+      reinterpret_cast<float4*>(o)[0] = make_float4(a.x + scale * acc[c][0], a.y + scale * acc[c][1],
+                                                    a.z + scale * acc[c][2], a.w + scale * acc[c][3]);
+      reinterpret_cast<float4*>(o)[1] = make_float4(b.x + scale * acc[c][4], b.y + scale * acc[c][5],
+                                                    b.z + scale * acc[c][6], b.w + scale * acc[c][7]);
+    }
+  }
+}
+
+int embedding_bwd_small_blocks(long n) {
+  const long G = std::max<long>(1, std::min<long>(256, (n + 31) / 32));
+  const long per = (n + G - 1) / G;
+  return (int)((n + per - 1) / per);
 }
 
 void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H, int rows,
-                   hipStream_t st) {
+                   hipStream_t st, float* partial) {
   if (rows > 0 && rows <= kEmbSmallRows) {
-    const long G = std::max<long>(1, std::min<long>(256, (n + 31) / 32));
+    const int G = embedding_bwd_small_blocks(n);
     const long per = (n + G - 1) / G;
-    hipLaunchKernelGGL(embedding_bwd_small_kernel, dim3((unsigned)((n + per - 1) / per)),
-                       dim3(256), (size_t)rows * H * 4, st, (const __bf16*)dy, idx, out, n, H,
-                       rows, per);
+    hipLaunchKernelGGL(embedding_bwd_small_kernel, dim3((unsigned)G), dim3(256),
+                       (size_t)rows * H * 4, st, (const __bf16*)dy, idx, out, n, H, rows, per,
+                       partial);
+    if (partial != nullptr) det_sum_rows(partial, nullptr, G, rows * H, out, nullptr, true, st);
     return;
   }
   hipLaunchKernelGGL(embedding_bwd_kernel, dim3(grid1d(n * H)), dim3(256), 0, st,
                      (const __bf16*)dy, idx, out, n, H);
+}
+
+void embedding_bwd_sorted(const void* dy, const int64_t* sorted_ids, const int64_t* perm,
+                          float* out, long n, int H, float scale, hipStream_t st) {
+  const unsigned g = (unsigned)((n + 3) / 4);
+  const int nc = (H / 8 + 63) / 64;
+  if (nc <= 1)
+    hipLaunchKernelGGL(embedding_bwd_sorted_kernel<1>, dim3(g), dim3(256), 0, st,
+                       (const __bf16*)dy, sorted_ids, perm, out, n, H, scale);
+  else if (nc == 2)
+    hipLaunchKernelGGL(embedding_bwd_sorted_kernel<2>, dim3(g), dim3(256), 0, st,
+                       (const __bf16*)dy, sorted_ids, perm, out, n, H, scale);
+  else
+    hipLaunchKernelGGL(embedding_bwd_sorted_kernel<4>, dim3(g), dim3(256), 0, st,
+                       (const __bf16*)dy, sorted_ids, perm, out, n, H, scale);
 }
 
 // ------------------------------------------------------------------------------ dropout hash

@@ -434,12 +434,16 @@ def dropout_fwd(x, p, seed):
     return _ref.dropout_fwd(x, p, _host_seed(seed))
 
 
-def embedding_bwd(dy, idx, num_rows, out=None):
-    """Scatter-add of dy rows into a [num_rows, H] fp32 table gradient (``out``: accumulate into
-    it, e.g. the parameter's flat-gradient view; else a fresh zeroed tensor)."""
+def embedding_bwd(dy, idx, num_rows, out=None, ordered: bool = False, scale: float = 1.0):
+    """Scatter-add of ``scale`` * dy rows into a [num_rows, H] fp32 table gradient (``out``:
+    accumulate into it, e.g. the parameter's flat-gradient view; else a fresh zeroed tensor).
+    ``ordered`` (implied in deterministic mode): no float atomics — rows are summed per table row
+    in token order (stable sort of the ids), so the result is bit-reproducible."""
     if use_native(dy):
-        return native().embedding_bwd(dy, idx, num_rows, out)
+        return native().embedding_bwd(dy, idx, num_rows, out, bool(ordered), float(scale))
     g = _ref.embedding_bwd(dy, idx, num_rows)
+    if scale != 1.0:
+        g = g * scale
     if out is not None:
         out.add_(g.to(out.dtype))
         return out

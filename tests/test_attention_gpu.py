@@ -303,6 +303,43 @@ def test_bert_graphed_step_matches_eager():
     assert not bad, bad
 
 
+def test_bert_deterministic_mode_bit_identical_graphed_and_eager():
+    """In deterministic mode (the reference's cudnn.deterministic, task.py:25) BERT's backward has
+    no float atomics left — attention dQ in per-key-block slabs summed in order, the embedding
+    scatters through a stable id sort — so two eager runs and a hipGraph-replayed run of 4 MLM +
+    AdamW steps end with bit-identical parameters, element by element (S = 512: four key blocks
+    per head, the case whose dQ used to be atomic)."""
+    import copy
+    from mipipe.models import create_model
+    from mipipe.ops.determinism import deterministic
+    from mipipe.optim import AdamW
+    from mipipe.train.graph import GraphedStep
+    with deterministic(True):
+        torch.manual_seed(0)
+        a = create_model("bert_tiny").cuda()
+        b, c = copy.deepcopy(a), copy.deepcopy(a)
+        opts = [AdamW(m.parameters(), lr=1e-3, weight_decay=0.01) for m in (a, b, c)]
+        B, S, P, V = 2, 512, 40, a.config.vocab_size
+        g = torch.Generator(device="cuda")
+        g.manual_seed(11)
+        ids = torch.randint(0, V, (B, S), device="cuda", generator=g)
+        ids[:, :64] = 101  # a frequent token: long runs in the embedding scatter
+        am = torch.ones(B, S, device="cuda", dtype=torch.int64)
+        pos = torch.stack([torch.randperm(S, device="cuda", generator=g)[:P] for _ in range(B)])
+        labels = torch.randint(0, V, (B, P), device="cuda", generator=g)
+        batch = (ids, am, pos, labels)
+        la = [_bert_step_fn(a, opts[0])(*batch).item() for _ in range(4)]
+        lc = [_bert_step_fn(c, opts[2])(*batch).item() for _ in range(4)]
+        gs = GraphedStep(_bert_step_fn(b, opts[1]), batch, warmup=1, inputs=[batch])
+        lb = [gs.warmup_loss.item()] + [gs.replay(0).item() for _ in range(3)]
+        torch.cuda.synchronize()
+    assert la == lc and la == lb, (la, lb, lc)
+    for (n, p), (_, q), (_, r) in zip(a.named_parameters(), b.named_parameters(),
+                                       c.named_parameters()):
+        assert torch.equal(p, r), n  # eager vs eager
+        assert torch.equal(p, q), n  # eager vs graph replay
+
+
 @pytest.mark.parametrize("dev_seed", [False, True])
 def test_layernorm_fused_dropout_matches_unfused(dev_seed):
     """LN(dropout(x) + res) in one kernel == dropout kernel then LN kernel, bit for bit, forward

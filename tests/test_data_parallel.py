@@ -97,8 +97,8 @@ def test_dp_gpu_replicas_match_per_chunk_copies():
     replica reads its own flat bf16 shadow, writes its own flat gradients, and the reduction sums
     them into the master's.  (A single module looped over both chunks is not the oracle in bf16:
     its second chunk normalises around the running mean the first chunk just moved, and batch-8
-    bf16 BatchNorm gradients are sensitive to that at the 10 % level — fp32 agrees to 1e-5,
-    tools/r2/dp_debug.py.)"""
+    bf16 BatchNorm gradients are sensitive to that at the 10 % level — fp32 agrees to 1e-5;
+    measured in round 2.)"""
     from mipipe.ops.determinism import deterministic
     torch.manual_seed(0)
     dev = torch.device("cuda", 0)

@@ -717,3 +717,23 @@ def test_conv_dgrad_two_branch_bn_fusion(case, det):
     assert rel_err(dg, sgx) < 1e-3 and rel_err(db, sg) < 1e-3
     assert rel_err(dg2, sgx2) < 1e-3 and rel_err(db2, sg) < 1e-3
     assert float(rep.abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("rows,H,n", [(30528, 768, 4096), (512, 768, 4096), (2, 768, 4096),
+                                      (50, 64, 300), (1000, 1032, 777)])
+def test_embedding_bwd_ordered(rows, H, n):
+    """Ordered (deterministic) embedding backward: stable sort of the ids and one writer per
+    table row (or per-block tables summed in order for <= 8 rows) — equals the fp32 reference,
+    is bit-identical run to run, accumulates into `out` and applies `scale`."""
+    dy = bf(n, H)
+    idx = torch.randint(0, rows, (n,), device=dev)
+    idx[: n // 4] = idx[0]  # one long run of equal ids (a frequent token)
+    ref = _ref.embedding_bwd(dy.float(), idx, rows)
+    a = native().embedding_bwd(dy, idx, rows, None, True)
+    b = native().embedding_bwd(dy, idx, rows, None, True)
+    assert torch.equal(a, b)
+    assert rel_err(a, ref) < 1e-5
+    acc = torch.randn(rows, H, device=dev)
+    acc0 = acc.clone()
+    native().embedding_bwd(dy, idx, rows, acc, True, 0.125)
+    assert rel_err(acc - acc0, 0.125 * ref) < 1e-4

@@ -5,7 +5,12 @@ Products (in-tree, so they travel to the GPU box with the repo snapshot):
   mipipe/_runtime<EXT_SUFFIX> native runtime (csrc/runtime/*.cpp): process supervisor,
                               DAG scheduler core (CPython API, no torch)
 
-Incremental: an object is rebuilt when its source or any header under csrc/ is newer.
+Incremental: an object is rebuilt when its source or any header under csrc/ is newer.  On top of
+the mtimes, each linked library records the SHA-256 of the sources it was built from
+(``<lib>.srcsha``, next to it): a library whose sources changed — or that arrived without a
+stamp, e.g. a snapshot with stale mtimes — is rebuilt from scratch, and ``MIPIPE_FORCE_BUILD=1``
+(or ``--force``) always rebuilds everything.  Every build appends one line to
+``build/provenance.jsonl`` (library, digest, objects compiled / reused, forced or not).
 Usage: python tools/build_ext.py [-j N] [--force] [--only C|runtime]
 """
 from __future__ import annotations
@@ -13,6 +18,8 @@ from __future__ import annotations
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -31,6 +38,43 @@ def _newest_header() -> float:
     hs = glob.glob(os.path.join(CSRC, "**", "*.hpp"), recursive=True) + \
         glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
     return max([os.path.getmtime(h) for h in hs] or [0.0])
+
+
+def sources_digest(kind: str) -> str:
+    """SHA-256 over the sources (paths + bytes) a library is built from."""
+    if kind == "C":
+        pats = ["kernels/*.hip", "kernels/*.hpp", "bindings.cpp", "comm/*.cpp", "comm/*.h*"]
+    else:
+        pats = ["runtime/*.cpp", "runtime/*.h*"]
+    files = sorted({f for p in pats for f in glob.glob(os.path.join(CSRC, p))})
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.relpath(f, CSRC).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(ARCH.encode())
+    return h.hexdigest()
+
+
+def _stamp_ok(lib: str, digest: str) -> bool:
+    try:
+        with open(lib + ".srcsha") as f:
+            return os.path.exists(lib) and f.read().strip() == digest
+    except OSError:
+        return False
+
+
+def _record(lib: str, digest: str, msgs, forced: bool) -> None:
+    with open(lib + ".srcsha", "w") as f:
+        f.write(digest + "\n")
+    os.makedirs(os.path.dirname(BUILD), exist_ok=True)
+    import time
+    rec = {"time": time.strftime("%Y-%m-%dT%H:%M:%S"), "lib": os.path.relpath(lib, REPO),
+           "sha256": digest, "arch": ARCH, "forced": forced,
+           "compiled": sum(m.startswith("compiled") for m in msgs),
+           "up_to_date": sum(m.startswith("up-to-date") for m in msgs)}
+    with open(os.path.join(os.path.dirname(BUILD), "provenance.jsonl"), "a") as f:
+        f.write(json.dumps(rec) + "\n")
 
 
 def _torch_flags():
@@ -66,6 +110,9 @@ def _compile(src: str, obj: str, flags, force: bool, hdr_time: float) -> str:
 
 
 def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
+    out = os.path.join(PKG, "_C" + EXT)
+    digest = sources_digest("C")
+    force = force or os.environ.get("MIPIPE_FORCE_BUILD") == "1" or not _stamp_ok(out, digest)
     tflags, ldflags = _torch_flags()
     common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC}", "-DNDEBUG", "-Wno-unused-result"]
     hip_flags = common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + tflags
@@ -78,18 +125,20 @@ def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True) -> s
         jobs_list.append((s, os.path.join(BUILD, "C", os.path.basename(s) + ".o"), hip_flags))
     for s in cpps:
         jobs_list.append((s, os.path.join(BUILD, "C", os.path.basename(s) + ".o"), cpp_flags))
+    msgs = []
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_compile, s, o, f, force, hdr) for (s, o, f) in jobs_list]
         for fu in futs:
             msg = fu.result()
+            msgs.append(msg)
             if verbose:
                 print(msg, flush=True)
-    out = os.path.join(PKG, "_C" + EXT)
     objs = [o for (_, o, _) in jobs_list]
     if force or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + ldflags + ["-o", out])
         if verbose:
             print(f"linked {os.path.relpath(out, REPO)}", flush=True)
+    _record(out, digest, msgs, force)
     return out
 
 
@@ -102,7 +151,10 @@ def build_runtime(jobs: int = 8, force: bool = False, verbose: bool = True) -> s
     flags = ["-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"-I{py_inc}",
              f"-I{pybind11.get_include()}", f"-I{CSRC}", "-Wall", "-Wno-unused-result"]
     hdr = _newest_header()
-    objs = []
+    out = os.path.join(PKG, "_runtime" + EXT)
+    digest = sources_digest("runtime")
+    force = force or os.environ.get("MIPIPE_FORCE_BUILD") == "1" or not _stamp_ok(out, digest)
+    objs, msgs = [], []
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = []
         for s in srcs:
@@ -111,13 +163,14 @@ def build_runtime(jobs: int = 8, force: bool = False, verbose: bool = True) -> s
             futs.append(ex.submit(_compile_cxx, s, o, flags, force, hdr))
         for fu in futs:
             msg = fu.result()
+            msgs.append(msg)
             if verbose:
                 print(msg, flush=True)
-    out = os.path.join(PKG, "_runtime" + EXT)
     if force or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
         _run(["g++", "-shared", "-fPIC"] + objs + ["-o", out, "-lpthread"])
         if verbose:
             print(f"linked {os.path.relpath(out, REPO)}", flush=True)
+    _record(out, digest, msgs, force)
     return out
 
 

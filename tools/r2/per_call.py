@@ -31,9 +31,15 @@ def main() -> int:
     a = ap.parse_args()
     rows = []
     for r in csv.DictReader(open(a.trace)):
+        def dim(prefix):  # total over x, y, z (split-K weight-grads launch (tiles, splits, 1))
+            if prefix + "_X" in r:
+                v = 1
+                for ax in "XYZ":
+                    v *= max(1, int(r.get(f"{prefix}_{ax}", 1) or 1))
+                return v
+            return int(r.get(prefix, 0) or 0)
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
-                     int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0),
-                     int(r.get("Workgroup_Size_X", r.get("Workgroup_Size", 0)) or 0),
+                     dim("Grid_Size"), dim("Workgroup_Size"),
                      r.get("VGPR_Count", r.get("Arch_VGPR_Count", "")),
                      r.get("LDS_Block_Size", r.get("LDS_Size", ""))))
     rows.sort()
@@ -53,7 +59,7 @@ def main() -> int:
         prev_end = e
         if us < a.min_us:
             continue
-        wgs = grid // wg if wg else grid
+        wgs = grid // wg if wg else grid  # workgroups of the whole grid (x*y*z)
         print(f"{i:4d} {us:8.1f} {gap:6.1f} {wgs:7d} {wg:4d} {vg:>5} {lds:>6}  {short(n)}")
     return 0
 
