@@ -80,6 +80,8 @@ def parse():
                          "analogue; in deterministic mode only a loaded / shipped table is used); "
                          "0: heuristic tile choice; 2: time candidates even in deterministic mode "
                          "(to build a shipped table with --save-tune)")
+    ap.add_argument("--bert-dropout", type=float, default=None,
+                    help="BERT hidden / attention dropout (default: the model's 0.1)")
     ap.add_argument("--emulate-ranks", type=int, default=1,
                     help="world-1 reference for DDP equivalence tests: every step runs the R "
                          "per-rank batches one after another (each BN sees its own chunk, rank 0's "
@@ -260,20 +262,37 @@ def build_bert(a, world, local, dev, rank):
     V = 30522
     S = a.seq
     P = max(1, round(0.15 * S)) if S != 128 else 20
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    batches = []
-    for _ in range(2):
-        ids = torch.randint(0, V, (a.batch, S), device=dev, generator=g)
-        am = torch.ones(a.batch, S, device=dev, dtype=torch.int64)
-        pos = torch.stack([torch.randperm(S, device=dev, generator=g)[:P] for _ in range(a.batch)])
-        labels = torch.randint(0, V, (a.batch, P), device=dev, generator=g)
-        batches.append((ids, am, pos, labels))
+    R = a.emulate_ranks
+    if R > 1 and (world != 1 or a.impl != "mipipe"):
+        raise SystemExit("--emulate-ranks is a world-1 mipipe reference run")
+
+    def rank_batches(r):
+        g = torch.Generator(device=dev)
+        g.manual_seed(1234 + r)
+        out = []
+        for _ in range(2):
+            ids = torch.randint(0, V, (a.batch, S), device=dev, generator=g)
+            am = torch.ones(a.batch, S, device=dev, dtype=torch.int64)
+            pos = torch.stack([torch.randperm(S, device=dev, generator=g)[:P]
+                               for _ in range(a.batch)])
+            labels = torch.randint(0, V, (a.batch, P), device=dev, generator=g)
+            out.append((ids, am, pos, labels))
+        return out
+
+    if R > 1:
+        # step batch i = the R per-rank batches ranks 0..R-1 would each draw for their step i
+        per = [rank_batches(r) for r in range(R)]
+        batches = [tuple(torch.cat([per[r][i][k] for r in range(R)]) for k in range(4))
+                   for i in range(2)]
+    else:
+        batches = rank_batches(rank)
     if a.impl == "mipipe":
         from mipipe.models import create_model
         from mipipe.optim import AdamW
         from mipipe.parallel import DistributedDataParallel
-        model = create_model(a.model).to(dev)
+        drop = {} if a.bert_dropout is None else {
+            "hidden_dropout_prob": a.bert_dropout, "attention_probs_dropout_prob": a.bert_dropout}
+        model = create_model(a.model, **drop).to(dev)
         model.compute_dtype = _compute_dtype(a)
         if a.distributed:
             model = DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=a.bucket_cap_mb,
@@ -288,12 +307,37 @@ def build_bert(a, world, local, dev, rank):
             opt.step()
             return loss
 
+        if R > 1:
+            def step(ids, am, pos, labels):  # noqa: F811
+                # one forward / backward per emulated rank (its own dropout seeds: the rank's
+                # seed offset at the step counter every rank would be at), loss / R each: the
+                # mean of per-rank gradients that DDP's averaged all-reduce produces
+                opt.zero_grad()
+                s0 = model._step
+                sd0 = model._step_dev.clone() if model._step_dev is not None else None
+                total = 0.0
+                chunks = [t.chunk(R) for t in (ids, am, pos, labels)]
+                for r in range(R):
+                    model.rank_override = r
+                    model._step = s0
+                    if sd0 is not None:
+                        model._step_dev.copy_(sd0)
+                    loss = model(chunks[0][r], chunks[1][r], masked_positions=chunks[2][r],
+                                 labels=chunks[3][r]) / R
+                    loss.backward()
+                    total = total + loss.detach()
+                model.rank_override = None
+                opt.step()
+                return total
+
         # AdamW's step count and the dropout seeds' per-step part live on the device, so the
         # whole step (dropout included) replays from one captured hipGraph
         from mipipe.train.graph import GraphedStep, graph_safe
         ok, why = graph_safe(model, opt)
         if dev.type == "cpu":
             ok, why = False, "no hipGraph on the CPU"
+        if R > 1:
+            ok, why = False, "--emulate-ranks runs eagerly"
         if a.graph == "on" or (a.graph == "auto" and ok):
             if not ok:
                 raise SystemExit(f"--graph on is not possible here: {why}")

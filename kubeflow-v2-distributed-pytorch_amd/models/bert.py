@@ -167,12 +167,16 @@ class BertForMaskedLM(tnn.Module):
         self.bert = _BertModel(c)
         self.cls = _Cls(c)
         self.seed = seed
+        self.rank_override: Optional[int] = None  # dropout-seed rank (bench --emulate-ranks)
         self._step = 0
         self._step_dev: Optional[torch.Tensor] = None  # device step counter (dropout seeds)
         self._vpad = (-c.vocab_size) % 64  # decoder N padded to the GEMM's 64-wide tiles
         self._init_weights()
         # the tied decoder's weight-gradient GEMM runs before the embedding lookup's scatter in
         # the backward: only the latter may report the shared gradient complete (DDP buckets)
+        # — unless DDP exchanges the lookup part sparsely (parallel/ddp.py, a sink on the
+        # weight): then the decoder's dense part is complete at the START of the backward and
+        # DDP puts the weight's flat slot first, into the first gradient bucket
         self.bert.embeddings.word_embeddings.weight._mipipe_tied_later = True
         if self._vpad:
             # the flat parameter space (mipipe.optim) reserves zero rows behind the tied
@@ -215,6 +219,8 @@ class BertForMaskedLM(tnn.Module):
         if self.training:
             self._step += 1
         rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+        if self.rank_override is not None:
+            rank = self.rank_override
         base = (self.seed + 7919 * rank) & 0xFFFFFFFF
         # On the GPU the per-step part of every dropout seed is a device counter advanced here by
         # a device op, so a hipGraph-captured step draws fresh masks on every replay (the host

@@ -898,19 +898,30 @@ class _LinearFn(Function):
             # w_c may carry more rows than the parameter (vocabulary padded to the tile width):
             # then the target is the flat space's padded gradient view
             tgt = _direct_grad_target(ctx.weight, w_c.shape[0]) if K.use_native(dy2) else None
+            # a tied weight (``_mipipe_tied_later``: an MLM decoder sharing the input embedding)
+            # gets another contribution later in the backward — that writer reports it ready,
+            # else DDP would all-reduce a partial gradient.  Unless DDP takes the lookup part as
+            # sparse rows (``_mipipe_sparse_sink``): then this dense part is the whole local
+            # gradient of the weight and it is ready now (its bucket overlaps the encoder's
+            # backward instead of being all-reduced after the last kernel).
+            sink = getattr(ctx.weight, "_mipipe_sparse_sink", None)
+            ready_now = sink is not None or not getattr(ctx.weight, "_mipipe_tied_later", False)
             if tgt is not None:
                 fs, g = tgt
                 K.gemm(dy2, x2, True, False, None, "none", torch.float32,
                        g.reshape(w_c.shape[0], -1), 1.0)
-                # a tied weight (``_mipipe_tied_later``: an MLM decoder sharing the input
-                # embedding) gets another contribution later in the backward — that writer
-                # reports it ready, else DDP would all-reduce a partial gradient
-                if not getattr(ctx.weight, "_mipipe_tied_later", False):
+                if ready_now:
                     fs.grad_ready(ctx.weight)
             else:
                 dw = K.gemm(dy2, x2, True, False, None, "none", gdt)
                 if w_c.shape[0] != ctx.weight.shape[0]:
                     dw = dw[: ctx.weight.shape[0]]
+                if sink is not None:  # write it into the flat gradient now, report it ready
+                    from mipipe.optim.flat import flat_space_for
+                    fs = flat_space_for(ctx.weight)
+                    fs.grad_view(ctx.weight).add_(dw.to(torch.float32))
+                    fs.grad_ready(ctx.weight)
+                    dw = None
         if ctx.has_bias and ctx.needs_input_grad[3]:
             tb = _direct_grad_target(ctx.bias, dy2.shape[1]) if K.use_native(dy2) else None
             if tb is not None:
@@ -1094,6 +1105,12 @@ class _EmbeddingFn(Function):
     @staticmethod
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
+        sink = getattr(ctx.weight, "_mipipe_sparse_sink", None)
+        if ctx.needs_input_grad[1] and sink is not None:
+            # DDP exchanges the lookup gradient as (token id, row) pairs and scatters every
+            # rank's rows after the dense part's all-reduce (parallel/ddp.py)
+            sink(idx, dy)
+            return None, None, None
         if ctx.needs_input_grad[1] and K.use_native(dy):
             tgt = _direct_grad_target(ctx.weight)
             if tgt is not None:  # scatter straight into the flat gradient buffer

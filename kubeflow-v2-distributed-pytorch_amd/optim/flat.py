@@ -8,7 +8,8 @@ offset in all three.  Consequences on MI355X:
   p, g, m; writes p, m and the bf16 shadow) instead of ~160 per-tensor launches;
 * gradient buckets for the all-reduce are contiguous slices of the gradient buffer, so RCCL
   reduces them in place (no pack/unpack copies) — buffers are laid out in *reverse*
-  registration order, the order autograd produces gradients;
+  registration order, the order autograd produces gradients (parameters tagged
+  ``_mipipe_flat_first`` first: ready at the start of the backward);
 * ``zero_grad`` is one memset; the bf16 shadow the kernels read is refreshed by the optimizer
   kernel itself, so no per-layer weight cast runs in the forward.
 
@@ -69,6 +70,12 @@ class FlatParamSpace:
             if not _dense_strides_ok(p):
                 p.data = p.data.contiguous()
         order = list(reversed(self.params))  # gradient-ready order
+        # a parameter tagged ``_mipipe_flat_first`` becomes ready at the START of the backward
+        # although it was registered first (BERT's tied word embedding: its dense gradient is
+        # complete once the MLM decoder's weight-grad ran): it goes to the front
+        first = [p for p in order if getattr(p, "_mipipe_flat_first", False)]
+        if first:
+            order = first + [p for p in order if not getattr(p, "_mipipe_flat_first", False)]
         self.offsets: Dict[int, int] = {}
         off = 0
         for p in order:

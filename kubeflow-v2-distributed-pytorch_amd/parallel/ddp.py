@@ -30,6 +30,18 @@ wire buffer pre-scaled by 1/world and one pass widens the reduced bucket back.  
 reducer below is the fallback when ``_C`` is not built (``MIPIPE_NATIVE_REDUCER=0`` forces it);
 both issue the identical collective sequence.
 
+Tied embeddings (BERT's MLM decoder shares the word-embedding weight, SURVEY §2.6 C5''): the
+weight's gradient has a dense part (the decoder's weight-grad, done at the START of the backward)
+and a sparse part (the lookup's scatter of one row per token, the LAST backward op).  A plain
+bucketed all-reduce of the 94 MB weight could only start after the scatter — fully exposed.
+Here (``sparse_embedding=True``, the default; ``MIPIPE_SPARSE_EMBEDDING=0`` turns it off) the
+weight's flat slot goes first, the dense part is all-reduced in the first bucket while the
+encoder's backward runs, and the lookup part travels as (token id, row) pairs: one
+``all_gather`` of the ids and one of the rows (bf16 on the GPU: 6.3 MB per rank at 32 x 128),
+issued after the last bucket, then every rank scatters every rank's rows, times 1/world, in rank
+order through the ordered embedding backward (one writer per table row, stable id order) — the
+same sum on every rank, bit for bit.
+
 Debug aid (SURVEY §5.2 hazard): ``check_collectives=True`` (or ``MIPIPE_CHECK_COLLECTIVES=1``)
 hashes every collective this wrapper issues and compares the digests across ranks every
 ``check_every`` steps, turning a mismatched collective sequence into an immediate error.
@@ -88,6 +100,63 @@ class _CollectiveLog:
         return self.h.digest()
 
 
+class _SparseRowExchange:
+    """The lookup part of a tied embedding weight's gradient, exchanged as (id, row) pairs.
+
+    Installed as ``param._mipipe_sparse_sink``: the embedding Function's backward hands it the
+    token ids and the per-token gradient rows instead of scattering them (ops/functional.py)."""
+
+    def __init__(self, ddp: "DistributedDataParallel", param: tnn.Parameter):
+        self.ddp = ddp
+        self.param = param
+        self.pending = None
+        self.checked = False
+        self.sent_bytes = 0  # per rank, last exchange (ids + rows)
+
+    def __call__(self, idx: torch.Tensor, dy: torch.Tensor) -> None:
+        idx = idx.reshape(-1)
+        dy = dy.reshape(-1, dy.shape[-1])
+        ddp = self.ddp
+        if not (ddp._comm and ddp._sync_enabled):  # no_sync(): a local scatter, like no DDP
+            self._scatter(dy, idx, 1.0)
+            return
+        self.pending = (idx, dy)
+        # after the reducer's end-of-backward callback (queued at the first ready gradient):
+        # every bucket, the dense part of this weight included, is reduced by then
+        torch.autograd.Variable._execution_engine.queue_callback(self._exchange)
+
+    def _scatter(self, rows, ids, scale):
+        from mipipe.ops import kernels as K
+        from mipipe.optim.flat import flat_space_for
+        fs = flat_space_for(self.param)
+        K.embedding_bwd(rows.contiguous(), ids.contiguous(), self.param.shape[0],
+                        fs.grad_view(self.param), ordered=True, scale=scale)
+
+    def _exchange(self) -> None:
+        idx, dy = self.pending
+        self.pending = None
+        ddp = self.ddp
+        world, pg = ddp.world, ddp.process_group
+        if not self.checked:  # equal token counts on every rank (all_gather_into_tensor needs it)
+            ns: List[Optional[int]] = [None] * world
+            dist.all_gather_object(ns, int(idx.numel()), group=pg)
+            if any(n != ns[0] for n in ns):
+                raise RuntimeError(f"DDP sparse embedding exchange: token counts differ {ns}")
+            self.checked = True
+        n, H = dy.shape
+        ids_all = idx.new_empty(world * n)
+        rows_all = dy.new_empty(world * n, H)
+        ddp._clog.record("all_gather", idx)
+        ddp._clog.record("all_gather", dy)
+        w1 = dist.all_gather_into_tensor(ids_all, idx.contiguous(), group=pg, async_op=True)
+        w2 = dist.all_gather_into_tensor(rows_all, dy.contiguous(), group=pg, async_op=True)
+        w1.wait()  # stream semantics on RCCL: the compute stream waits, the host does not
+        w2.wait()
+        self.sent_bytes = idx.numel() * idx.element_size() + dy.numel() * dy.element_size()
+        # rank order is the all_gather order; the ordered scatter sums equal ids in that order
+        self._scatter(rows_all, ids_all, 1.0 / world)
+
+
 class DistributedDataParallel(tnn.Module):
     def __init__(self, module: tnn.Module, device_ids: Optional[List[int]] = None,
                  output_device=None, broadcast_buffers: bool = True,
@@ -96,7 +165,7 @@ class DistributedDataParallel(tnn.Module):
                  comm_dtype: Optional[torch.dtype] = None, find_unused_parameters: bool = False,
                  check_collectives: Optional[bool] = None, check_every: int = 50,
                  gradient_as_bucket_view: bool = True, static_graph: bool = False,
-                 force_reduce: Optional[bool] = None):
+                 force_reduce: Optional[bool] = None, sparse_embedding: Optional[bool] = None):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -125,7 +194,24 @@ class DistributedDataParallel(tnn.Module):
         # reference's precision), whose kernels read the fp32 master weights directly
         cdt = getattr(module, "compute_dtype", None)
         shadow = torch.bfloat16 if dev.type == "cuda" and cdt != torch.float32 else None
+        if sparse_embedding is None:
+            sparse_embedding = os.environ.get("MIPIPE_SPARSE_EMBEDDING", "1") == "1"
+        tied = [p for p in params if getattr(p, "_mipipe_tied_later", False)]
+        want_sparse = bool(sparse_embedding) and self._comm and bool(tied)
+        if want_sparse:
+            from mipipe.optim.flat import flat_space_for
+            if any(flat_space_for(p) is not None for p in params):
+                want_sparse = False  # the flat order is fixed already (optimizer built first)
+            else:
+                for p in tied:
+                    p._mipipe_flat_first = True  # ready at the start of the backward
         self.space: FlatParamSpace = get_flat_space(params, shadow, module)
+        self._sparse: List[_SparseRowExchange] = []
+        if want_sparse:
+            for p in tied:
+                ex = _SparseRowExchange(self, p)
+                p._mipipe_sparse_sink = ex
+                self._sparse.append(ex)
         backend = dist.get_backend(process_group) if dist.is_initialized() else "none"
         self._avg_supported = backend == "nccl"
         # latency path for the per-forward buffer broadcast (C4): one-shot over IPC peer
@@ -280,11 +366,12 @@ class DistributedDataParallel(tnn.Module):
         cuts.append(i)
         j, acc = n, 0
         if last_bytes > 0:
-            while j > i:  # last bucket, from the end
-                acc += (ranges[j - 1][1] - ranges[j - 1][0]) * 4
-                j -= 1
-                if acc >= last_bytes:
+            while j > i:  # last bucket, from the end: at most last_bytes (at least one param)
+                nb = (ranges[j - 1][1] - ranges[j - 1][0]) * 4
+                if acc > 0 and acc + nb > last_bytes:
                     break
+                acc += nb
+                j -= 1
         if j > i:  # middle: equal buckets of <= cap_bytes
             mid = sum((ranges[k][1] - ranges[k][0]) * 4 for k in range(i, j))
             nb = max(1, int(-(-mid // max(cap_bytes, 1.0))))

@@ -141,3 +141,28 @@ def test_rccl_profiles_env():
         configure_rccl_env({}, profile="fastest")
     rep = rccl_settings({"NCCL_MIN_NCHANNELS": "32", "PATH": "/bin", "TORCH_NCCL_HIGH_PRIORITY": "1"})
     assert rep == {"NCCL_MIN_NCHANNELS": "32", "TORCH_NCCL_HIGH_PRIORITY": "1"}
+
+
+def test_bench_world4_gloo_bert_matches_emulated_ranks(tmp_path):
+    """`bench.py --gpus 4 --model bert_tiny` (4 gloo ranks, mipipe DDP with the tied word
+    embedding's lookup gradient exchanged as sparse (id, row) pairs) ends with bit-identical
+    parameters on every rank, equal to one process that runs the four per-rank batches and
+    averages their gradients (--emulate-ranks 4)."""
+    import torch
+    args = ["--device", "cpu", "--model", "bert_tiny", "--batch", "2", "--seq", "32",
+            "--steps", "2", "--warmup", "1", "--bert-dropout", "0"]
+    d4, d1 = tmp_path / "w4", tmp_path / "w1"
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "4", "--dump-params", str(d4)] + args,
+                       env=_env(), capture_output=True, text=True, timeout=900, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--emulate-ranks", "4",
+                        "--dump-params", str(d1)] + args,
+                       env=_env(), capture_output=True, text=True, timeout=900, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    ranks = [torch.load(d4 / f"rank{i}.pt", weights_only=True) for i in range(4)]
+    ref = torch.load(d1 / "rank0.pt", weights_only=True)
+    for rk in ranks[1:]:
+        for a, b in zip(ranks[0]["params"], rk["params"]):
+            assert torch.equal(a, b)
+    for a, b in zip(ranks[0]["params"], ref["params"]):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a - b).abs().max()

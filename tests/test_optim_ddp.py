@@ -195,3 +195,59 @@ def test_ddp_bucket_layout_small_tail():
     assert mb[-1] <= 4.0 and mb[0] <= 10.0, mb
     assert all(m <= 32.0 for m in mb[1:-1]), mb
     assert len(b) >= 4
+
+
+def _bert_bucket_worker(rank, world, port, out):
+    import copy
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mipipe.models import create_model
+    from mipipe.parallel import DistributedDataParallel
+    torch.manual_seed(0)
+    m = create_model("bert_base", hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    ref = copy.deepcopy(m)
+    d = DistributedDataParallel(m, force_reduce=True)
+    wte = m.bert.embeddings.word_embeddings.weight
+    res = {"buckets": [(b.start, b.end, len(b.params)) for b in d.buckets],
+           "first_is_wte": d.buckets[0].params[0] is wte and len(d.buckets[0].params) == 1,
+           "sparse": len(d._sparse)}
+    # one step: the DDP gradient (dense part all-reduced in bucket 0, lookup rows all-gathered
+    # and scattered in order) equals the plain model's
+    B, S, P = 2, 16, 3
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, 30522, (B, S), generator=g)
+    ids[:, :4] = 7  # repeated tokens
+    am = torch.ones(B, S, dtype=torch.int64)
+    pos = torch.stack([torch.randperm(S, generator=g)[:P] for _ in range(B)])
+    lab = torch.randint(0, 30522, (B, P), generator=g)
+    d(ids, am, masked_positions=pos, labels=lab).backward()
+    ref(ids, am, masked_positions=pos, labels=lab).backward()
+    res["sent_bytes"] = d._sparse[0].sent_bytes
+    errs = []
+    for (n, p), q in zip(m.named_parameters(), ref.parameters()):
+        if not torch.allclose(p.grad, q.grad, rtol=1e-4, atol=1e-6):
+            errs.append((n, float((p.grad - q.grad).abs().max())))
+    res["grad_errs"] = errs
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_ddp_bert_tied_embedding_not_exposed():
+    """BERT-base: the tied word embedding's 94 MB gradient no longer sits in the last bucket.
+    Its dense (decoder) part is reduced in bucket 0 — ready at the start of the backward — and
+    its lookup part is exchanged as (id, row) pairs.  What is left after the last backward kernel
+    is the last bucket + those pairs: <= 8 MB per rank at 32 x 128 tokens (bf16 rows on the GPU).
+    The DDP gradient equals the plain model's (world 1, gloo)."""
+    out = mp.Manager().dict()
+    mp.spawn(_bert_bucket_worker, args=(1, 29350 + os.getpid() % 400, out), nprocs=1)
+    r = out[0]
+    assert r["first_is_wte"] and r["sparse"] == 1
+    b = r["buckets"]
+    assert b[0][0] == 0 and all(b[k][1] == b[k + 1][0] for k in range(len(b) - 1))
+    last_mb = (b[-1][1] - b[-1][0]) * 4 / 2 ** 20
+    tokens, H = 32 * 128, 768
+    pairs_mb = (tokens * H * 2 + tokens * 8) / 2 ** 20  # bf16 rows + int64 ids
+    assert last_mb + pairs_mb <= 8.0, (last_mb, pairs_mb)
+    assert r["sent_bytes"] == 2 * 16 * (768 * 4 + 8)  # this CPU step: fp32 rows + ids
+    assert not r["grad_errs"], r["grad_errs"]
