@@ -172,7 +172,6 @@ int select(const std::string& k, bool f32, bool wgrad, F&& run) {
 // GEMM plans: tile id + 16 * split-K count (0 = heuristic split; accumulating GEMMs only)
 constexpr int kPlanSplit = 16;
 constexpr int kPlanWs = 1024;  // gemm plans: split-K through per-split workspace slices
-constexpr int kPlanLib = 4096;  // gemm plans: the library GEMM (hipBLASLt via at::mm / at::addmm)
 std::vector<int> gemm_candidates(bool f32, bool accumulate) {
   std::vector<int> c;
   for (int t : candidates(f32, accumulate)) {
@@ -945,65 +944,33 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
                 addend->is_contiguous(), "addend must be a contiguous [M, N] tensor");
     add_p = addend->data_ptr();
   }
-  // Split-K for activation-dtype outputs without an epilogue (e.g. the MLM decoder's data-grad:
-  // K = 30528, only 192 output tiles of 128 x 128 for 256 CUs): the splits accumulate into a
-  // zeroed fp32 workspace, one pass rounds it into the bf16 output.  Not in deterministic mode
-  // (float atomics); the tuner times these plans against the unsplit ones.
-  static const bool splitk_on = [] {
-    const char* v = getenv("MIPIPE_GEMM_SPLITK");
-    return v == nullptr || atoi(v) != 0;
-  }();
-  const bool splittable = splitk_on && mode == 0 && bias_p == nullptr && act_i == 0 &&
-                          add_p == nullptr && !f32 && mipipe::g_deterministic == 0;
-  // Workspace split-K for accumulating GEMMs (weight-grads into the flat fp32 gradient): each
-  // split stores its partial tile into its own slice, splitk_sum adds the slices in order.
-  // Plans with kPlanWs set; chosen by the tuner where the output is small against the CU count
-  // (BERT's 768 x 768 / 768 x 3072 weight-grads: 36-144 tiles) and atomics would cost more.
-  // Library plan (kPlanLib): the same product through hipBLASLt (at::mm / at::addmm) for GEMMs
-  // without a ReLU epilogue, where the library's kernels time faster (BERT's weight-grads with
-  // K = 4096 tokens, the MLM decoder: profiles/r3_gemm_vs_blaslt_graph.txt).  The tuner times it
-  // against the MFMA plans; a bias is rounded to the operand dtype first (the library's bias
-  // epilogue).  Never in deterministic mode: the library's algorithm choice is not ours to pin.
-  static const bool lib_on = [] {
-    const char* v = getenv("MIPIPE_GEMM_LIB");
-    return v == nullptr || atoi(v) != 0;
-  }();
-  const bool lib_ok = lib_on && !f32 && act_i == 0 && mipipe::g_deterministic == 0 &&
-                      (bias_p == nullptr || mode == 0);
+  // Workspace split-K: each split stores its partial tile into its own fp32 slice with plain
+  // stores (no atomics: deterministic), then one pass sums the slices in order —
+  //  * accumulating GEMMs (weight-grads into the flat fp32 gradient, mode 2): splitk_sum adds
+  //    them to C.  Chosen by the tuner where the output is small against the CU count (BERT's
+  //    768 x 768 / 768 x 3072 weight-grads: 36-144 tiles) and atomics would cost more;
+  //  * activation-dtype outputs with at most a bias (mode 0: the MLM decoder's data-grad with
+  //    K = 30528 — 30 output tiles for 256 CUs — or BERT's FFN-out projection, K = 3072):
+  //    splitk_sum_bf16 adds the slices and the bias and rounds once to bf16.
+  // Plans with kPlanWs set.  (Round 3 also timed a hipBLASLt "library plan" here; it is gone:
+  // every GEMM of the training step runs on the MFMA kernels, tools/gemm_plans.py.)
+  const bool ws_out0 = mode == 0 && act_i == 0 && add_p == nullptr && !f32 && N % 8 == 0;
   auto launch = [&](void* C, int p) {
-    if (p >= 0 && (p & tune::kPlanLib) != 0) {
-      if (lib_ok) {
-        const Tensor A = trans_a ? a.t() : a;
-        const Tensor B = trans_b ? b.t() : b;
-        Tensor Ct = torch::from_blob(C, {M, N}, out.options());
-        if (mode == 2) at::addmm_out(Ct, Ct, A, B, at::kFloat, 1, 1);
-        else if (mode == 1) at::mm_out(Ct, A, B, at::kFloat);
-        else if (add_p != nullptr) at::addmm_out(Ct, *addend, A, B);
-        else if (bias_p != nullptr) at::addmm_out(Ct, bias->to(a.scalar_type()), A, B);
-        else at::mm_out(Ct, A, B);
-        return;
-      }
-      p = -1;  // a table entry from a non-deterministic run: the heuristic MFMA plan
-    }
+    if (p >= 4096) p = -1;  // a round-3 table's library plan: the heuristic MFMA plan
     const bool ws_plan = p >= 0 && (p & tune::kPlanWs) != 0;
     if (ws_plan) p &= ~tune::kPlanWs;
     const int cfg = p < 0 ? -1 : p % tune::kPlanSplit;
     const int sp = p < 0 ? -1 : (p / tune::kPlanSplit > 0 ? p / tune::kPlanSplit : -1);
-    if (ws_plan && mode == 2 && sp > 1) {
+    if (ws_plan && (mode == 2 || ws_out0) && sp > 1) {
       const int ns = mipipe::gemm_ws_splits((int)K, sp);
       Tensor ws = torch::empty({(int64_t)ns, M, N}, a.options().dtype(at::kFloat));
       mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b,
                    ws.data_ptr(), N, (int)M, (int)N, (int)K, nullptr, 0, 2, stream(), f32, cfg,
                    sp, nullptr, true);
-      mipipe::splitk_sum(ws.data_ptr<float>(), ns, M * N, static_cast<float*>(C), stream());
-      return;
-    }
-    if (splittable && sp > 1) {
-      Tensor ws = torch::zeros({M, N}, a.options().dtype(at::kFloat));
-      mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b,
-                   ws.data_ptr(), N, (int)M, (int)N, (int)K, nullptr, 0, 2, stream(), f32, cfg,
-                   sp, nullptr);
-      torch::from_blob(C, {M, N}, a.options()).copy_(ws);
+      if (mode == 2)
+        mipipe::splitk_sum(ws.data_ptr<float>(), ns, M * N, static_cast<float*>(C), stream());
+      else
+        mipipe::splitk_sum_bf16(ws.data_ptr<float>(), ns, M, (int)N, bias_p, C, N, stream());
       return;
     }
     mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b, C, N,
@@ -1011,15 +978,10 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
   };
   if (plan < 0) {
     std::vector<int> cands = tune::gemm_candidates(f32, mode == 2);
-    if (mode == 2 && K >= 1024) {
-      for (int t : tune::candidates(f32, true))
+    if ((mode == 2 && K >= 1024) || (ws_out0 && K >= 2048)) {
+      for (int t : tune::candidates(f32, mode == 2))
         for (int sp : {2, 4, 8}) cands.push_back((t + tune::kPlanSplit * sp) | tune::kPlanWs);
     }
-    if (splittable && K >= 4096) {
-      for (int t : tune::candidates(f32, false))
-        for (int sp : {2, 4, 8}) cands.push_back(t + tune::kPlanSplit * sp);
-    }
-    if (lib_ok) cands.push_back(tune::kPlanLib);
     plan = tune::select_from(tune::gemm_key(M, N, K, !trans_a, trans_b, add_p != nullptr ? 3 : mode, f32),
                              cands, [&](int p) {
                                auto scratch = mode == 2 ? torch::zeros_like(out)

@@ -153,6 +153,41 @@ __global__ __launch_bounds__(256) void splitk_sum_wide_kernel(const float* __res
   }
 }
 
+// out[m][n] = bf16(sum_s ws[s][m][n] + bias[n]), s in order: the finishing pass of a split-K GEMM
+// with an activation-dtype output (M x N, N % 8 == 0; ws slices are [M][N] contiguous).
+__global__ __launch_bounds__(256) void splitk_sum_bf16_kernel(const float* __restrict__ ws,
+                                                              int splits, long M, int N,
+                                                              const float* __restrict__ bias,
+                                                              __bf16* __restrict__ out, long ldc) {
+  const long n8 = (long)N / 8;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-column chunk
+  if (i >= M * n8) return;
+  const long m = i / n8, c = (i % n8) * 8;
+  const float* src = ws + m * N + c;
+  float f[8];
+  ld_f32x8(src, f);
+  for (int s = 1; s < splits; ++s) {
+    float g[8];
+    ld_f32x8(src + (long)s * M * N, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] += g[e];
+  }
+  if (bias != nullptr) {
+    float b[8];
+    ld_f32x8(bias + c, b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] += b[e];
+  }
+  *reinterpret_cast<uint4*>(out + m * ldc + c) = pack8(f);
+}
+
+void splitk_sum_bf16(const float* ws, int splits, long M, int N, const float* bias, void* out,
+                     long ldc, hipStream_t st) {
+  const long chunks = M * (N / 8);
+  hipLaunchKernelGGL(splitk_sum_bf16_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
+                     st, ws, splits, M, N, bias, (__bf16*)out, ldc);
+}
+
 void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st) {
   // the vector path needs n % 4 == 0 and 16-B aligned rows of ws / out
   const bool vec = (n % 4) == 0 && (reinterpret_cast<uintptr_t>(out) % 16) == 0;

@@ -42,6 +42,9 @@ void det_sum_rows(float* in0, float* in1, int P, int C, float* out0, float* out1
                   bool accumulate, hipStream_t st);
 // out[i] += sum_s ws[s][i] over splits in order.
 void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st);
+// out[m][n] (bf16, row pitch ldc) = sum_s ws[s][m][n] + bias[n] (bias may be null); N % 8 == 0
+void splitk_sum_bf16(const float* ws, int splits, long M, int N, const float* bias, void* out,
+                     long ldc, hipStream_t st);
 int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 // bias / relu: optional per-channel bias and ReLU in the epilogue (convs without BN: VGG, AlexNet)

@@ -158,20 +158,27 @@ def test_gemm_every_plan(M, N, K, ta, tb):
             assert torch.equal(acc, acc2), (cfg, sp, "ws split-K must be deterministic")
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 768, 8192), (200, 136, 4104)])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 8192), (200, 136, 4104), (640, 768, 30528)])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False)])
 def test_gemm_splitk_bf16_output(M, N, K, ta, tb):
-    """Split-K plans of a plain bf16-output GEMM (no epilogue; e.g. the MLM decoder data-grad,
-    K = 30528): the splits accumulate into an fp32 workspace and one pass rounds it to bf16 —
-    every tile config at 2/4/8 splits against the fp32 product."""
+    """Workspace split-K plans (flag 1024) of a bf16-output GEMM (e.g. the MLM decoder data-grad,
+    K = 30528): every split stores its own fp32 slice, one pass adds the slices (and the bias) in
+    order and rounds to bf16 — every tile config at 2/4/8 splits against the fp32 product, with
+    and without a bias; deterministic (bit-identical reruns)."""
     a = bf(M, K)
     b = bf(N, K) if tb else bf(K, N)
+    bias = torch.randn(N, device=dev)
     ref = _ref.gemm(a.float(), b.float(), ta, tb, None, "none", torch.float32)
     for cfg in range(native().CONV_TILE_CONFIGS):
         for sp in (2, 4, 8):
-            out = native().gemm(a, b, ta, tb, None, "none", torch.bfloat16, None, 0.0, cfg + 16 * sp)
+            plan = (cfg + 16 * sp) | 1024
+            out = native().gemm(a, b, ta, tb, None, "none", torch.bfloat16, None, 0.0, plan)
             assert out.dtype == torch.bfloat16 and out.shape == (M, N)
             assert rel_err(out, ref) < 1e-2, (cfg, sp)
+            ob = native().gemm(a, b, ta, tb, bias, "none", torch.bfloat16, None, 0.0, plan)
+            assert rel_err(ob, ref + bias) < 1e-2, (cfg, sp, "bias")
+            assert torch.equal(ob, native().gemm(a, b, ta, tb, bias, "none", torch.bfloat16,
+                                                 None, 0.0, plan)), (cfg, sp, "deterministic")
 
 
 @pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (4096, 768, 3072), (200, 64, 136)])
@@ -185,43 +192,12 @@ def test_gemm_addend_epilogue(M, N, K):
         assert rel_err(out, ref) < 1e-2, cfg
 
 
-@pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (768, 3072, 4096), (200, 136, 72)])
-@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
-def test_gemm_library_plan(M, N, K, ta, tb):
-    """The library plan (hipBLASLt through at::mm / at::addmm, plan flag 4096) computes the same
-    products as the MFMA plans: bf16 output (plain, with a bias, with an addend), fp32 output and
-    fp32 accumulation into C (beta = 1, the weight-grad contract)."""
-    LIB = 4096
-    a = bf(K, M) if ta else bf(M, K)
-    b = bf(N, K) if tb else bf(K, N)
-    ref32 = _ref.gemm(a.float(), b.float(), ta, tb, None, "none", torch.float32)
-    out = native().gemm(a, b, ta, tb, None, "none", torch.bfloat16, None, 0.0, LIB)
-    assert out.dtype == torch.bfloat16 and rel_err(out, ref32) < 1e-2
-    bias = torch.randn(N, device=dev)
-    out = native().gemm(a, b, ta, tb, bias, "none", torch.bfloat16, None, 0.0, LIB)
-    assert rel_err(out, ref32 + bias) < 1e-2
-    out32 = native().gemm(a, b, ta, tb, None, "none", torch.float32, None, 0.0, LIB)
-    assert out32.dtype == torch.float32 and rel_err(out32, ref32) < 2e-3
-    acc = torch.randn(M, N, device=dev)
-    acc0 = acc.clone()
-    native().gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0, LIB)
-    assert rel_err(acc - acc0, ref32) < 2e-3
-    if not ta and not tb:
-        add = bf(M, N)
-        out = native().gemm(a, b, False, False, None, "none", torch.bfloat16, None, 0.0, LIB, add)
-        assert rel_err(out, ref32 + add.float()) < 1e-2
-
-
-def test_gemm_library_plan_not_in_deterministic_mode():
-    """A library plan from a table built without determinism falls back to the MFMA heuristic
-    plan in deterministic mode: the result is bit-identical to the default plan's."""
+def test_gemm_round3_library_plan_entry_falls_back():
+    """A round-3 tuning table may still hold library plans (flag 4096); the library plan is gone,
+    such an entry runs the heuristic MFMA plan: the result is bit-identical to plan -1's."""
     a, b = bf(512, 768), bf(1024, 768)
-    native().set_deterministic(True)
-    try:
-        ref = native().gemm(a, b, False, True, None, "none", torch.float32, None, 0.0, -1)
-        out = native().gemm(a, b, False, True, None, "none", torch.float32, None, 0.0, 4096)
-    finally:
-        native().set_deterministic(False)
+    ref = native().gemm(a, b, False, True, None, "none", torch.float32, None, 0.0, -1)
+    out = native().gemm(a, b, False, True, None, "none", torch.float32, None, 0.0, 4096)
     assert torch.equal(out, ref)
 
 

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""Every GEMM plan (MFMA tile x split-K x workspace split, and the library plan) on the GEMM
-shapes of one BERT-base 32x128 step, timed by hipGraph replay (launch cost excluded, as in the
-graphed training step).  Prints one JSON line per shape: the best MFMA plan, the library plan,
-their ratio, and the five fastest plans — the evidence for (or against) keeping a library plan.
+"""Every GEMM plan (MFMA tile x split-K x workspace split) on the GEMM shapes of one BERT-base
+32x128 step, timed by hipGraph replay (launch cost excluded, as in the graphed training step),
+against the same product through hipBLASLt (torch.mm / addmm — a comparator only: no library
+GEMM runs in the training step).  Prints one JSON line per shape: the best MFMA plan, the
+library time, their ratio, and the five fastest plans.
 
 python tools/gemm_plans.py [--reps 20] [--shapes KEY ...]
-KEY = "M,N,K,a_kc,b_kc,mode" as in the tuning table (mode 0 bf16 out, 2 fp32 accumulate,
-3 bf16 out + addend).
+KEY = "M,N,K,a_kc,b_kc,mode[,bias]" as in the tuning table (mode 0 bf16 out, 2 fp32 accumulate,
+3 bf16 out + addend; bias 1: the call carries a bias, as BERT's forward projections do).
 """
 from __future__ import annotations
 
@@ -22,14 +23,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mipipe.ops._native import native  # noqa: E402
 
 BERT_32x128 = [
-    "4096,2304,768,1,1,0", "4096,768,768,1,1,0", "4096,3072,768,1,1,0", "4096,768,3072,1,1,0",
-    "640,768,768,1,1,0", "640,30528,768,1,1,0",
+    "4096,2304,768,1,1,0,1", "4096,768,768,1,1,0,1", "4096,3072,768,1,1,0,1",
+    "4096,768,3072,1,1,0,1", "640,768,768,1,1,0,1", "640,30528,768,1,1,0,1",
     "4096,768,2304,1,0,3", "4096,768,768,1,0,0", "4096,3072,768,1,0,0", "4096,768,3072,1,0,3",
     "640,768,30528,1,0,0", "640,768,768,1,0,0",
     "2304,768,4096,0,0,2", "768,768,4096,0,0,2", "3072,768,4096,0,0,2", "768,3072,4096,0,0,2",
     "30528,768,640,0,0,2", "768,768,640,0,0,2",
 ]
-LIB, SPLIT, WS = 4096, 16, 1024
+SPLIT, WS = 16, 1024
 
 
 def t_graph(fn, reps):
@@ -69,10 +70,10 @@ def plans(C, mode, K):
                     out.append((t + SPLIT * sp) | WS)
     else:
         out += tiles
-        if mode == 0 and K >= 4096:
+        if mode == 0 and K >= 2048:
             for t in tiles:
                 for sp in (2, 4, 8):
-                    out.append(t + SPLIT * sp)
+                    out.append((t + SPLIT * sp) | WS)
     return out
 
 
@@ -85,32 +86,43 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     for key in a.shapes:
-        M, N, K, akc, bkc, mode = (int(v) for v in key.split(","))
+        f = [int(v) for v in key.split(",")]
+        M, N, K, akc, bkc, mode = f[:6]
+        has_bias = len(f) > 6 and f[6] == 1
         A = (torch.randn(M, K, device=dev) if akc else torch.randn(K, M, device=dev)).bfloat16()
         B = (torch.randn(N, K, device=dev) if bkc else torch.randn(K, N, device=dev)).bfloat16() * 0.05
         add = torch.randn(M, N, device=dev).bfloat16() if mode == 3 else None
         acc = torch.zeros(M, N, device=dev) if mode == 2 else None
+        bias = torch.randn(N, device=dev) if has_bias else None
 
         def run(p):
             if mode == 2:
                 return C.gemm(A, B, not akc, bool(bkc), None, "none", torch.float32, acc, 1.0, p)
-            return C.gemm(A, B, not akc, bool(bkc), None, "none", torch.bfloat16, None, 0.0, p,
+            return C.gemm(A, B, not akc, bool(bkc), bias, "none", torch.bfloat16, None, 0.0, p,
                           add)
 
+        At = A if akc else A.t()
+        Bt = B.t() if bkc else B
+
+        def lib():
+            if mode == 2:
+                return torch.addmm(acc, At, Bt, out_dtype=torch.float32, out=acc)
+            if mode == 3:
+                return torch.addmm(add, At, Bt)
+            if bias is not None:
+                return torch.addmm(bias.bfloat16(), At, Bt)
+            return torch.mm(At, Bt)
+
         res = {}
-        for p in plans(C, mode, K) + [LIB]:
-            try:
-                res[p] = t_graph(lambda: run(p), a.reps)
-            except RuntimeError as e:  # a plan a shape cannot take
-                res[p] = float("inf")
-                print(f"# {key} plan {p}: {str(e)[:80]}", file=sys.stderr)
-        mf = {p: v for p, v in res.items() if p != LIB}
-        best = min(mf, key=mf.get)
+        for p in plans(C, mode, K):
+            res[p] = t_graph(lambda: run(p), a.reps)
+        t_lib = t_graph(lib, a.reps)
+        best = min(res, key=res.get)
         fl = 2.0 * M * N * K
-        print(json.dumps({"shape": key, "best_mfma_plan": best, "best_mfma_us": round(mf[best], 2),
-                          "lib_us": round(res[LIB], 2), "mfma_over_lib": round(mf[best] / res[LIB], 3),
-                          "best_tflops": round(fl / mf[best] / 1e6, 1),
-                          "top5": {str(p): round(v, 2) for p, v in sorted(mf.items(), key=lambda x: x[1])[:5]}}),
+        print(json.dumps({"shape": key, "best_mfma_plan": best, "best_mfma_us": round(res[best], 2),
+                          "lib_us": round(t_lib, 2), "mfma_over_lib": round(res[best] / t_lib, 3),
+                          "best_tflops": round(fl / res[best] / 1e6, 1),
+                          "top5": {str(p): round(v, 2) for p, v in sorted(res.items(), key=lambda x: x[1])[:5]}}),
               flush=True)
 
 
