@@ -1138,6 +1138,28 @@ Tensor gelu_bwd(Tensor dy, Tensor x) {
   return dx;
 }
 
+// dx = gelu_bwd(dy, x) and bias += Σ_rows dx (fp32 [cols], e.g. the flat-gradient view) in one
+// kernel; bias sums the bf16-rounded dx exactly as colsum(dx, bias) would.
+Tensor gelu_bwd_colsum(Tensor dy, Tensor x, Tensor bias) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.sizes() == dy.sizes() && x.is_contiguous() && dy.is_contiguous(),
+              "gelu_bwd_colsum shape mismatch");
+  int64_t cols = x.size(-1), rows = x.numel() / cols;
+  TORCH_CHECK(cols % 8 == 0, "gelu_bwd_colsum needs cols % 8 == 0");
+  check_vec(bias, cols, "bias");
+  auto dx = torch::empty_like(x);
+  optional<Tensor> work;
+  if (mipipe::g_deterministic)
+    work = torch::empty({(int64_t)mipipe::colsum_blocks(rows, (int)cols), cols},
+                        x.options().dtype(at::kFloat));
+  mipipe::gelu_bwd_colsum(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), bias.data_ptr<float>(), rows,
+                          (int)cols, work.has_value() ? work->data_ptr<float>() : nullptr,
+                          stream());
+  return dx;
+}
+
 std::tuple<Tensor, Tensor, Tensor, optional<Tensor>> layernorm_fwd(Tensor x, Tensor gamma,
                                                                    Tensor beta, double eps,
                                                                    optional<Tensor> res,
@@ -1174,7 +1196,7 @@ std::tuple<Tensor, Tensor, Tensor, optional<Tensor>> layernorm_fwd(Tensor x, Ten
 std::tuple<Tensor, optional<Tensor>, optional<Tensor>, optional<Tensor>> layernorm_bwd(
     Tensor dy, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, optional<Tensor> dgamma_acc,
     optional<Tensor> dbeta_acc, double drop_p, int64_t drop_seed,
-    optional<Tensor> drop_seed_dev) {
+    optional<Tensor> drop_seed_dev, optional<Tensor> dbias_acc) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   c10::DeviceGuard g(x.device());
@@ -1196,7 +1218,10 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>, optional<Tensor>> layerno
     pg = dg->data_ptr<float>();
     pb = db->data_ptr<float>();
   }
-  auto work = torch::empty({2 * (int64_t)mipipe::layernorm_bwd_blocks(rows), H}, o);
+  // dbias_acc: also += Σ_rows of the branch gradient (dxd, else dx) — the bias gradient of the
+  // Linear that produced x (fp32 [H], e.g. its flat-gradient view)
+  float* pd = dbias_acc.has_value() ? fptr(dbias_acc, H) : nullptr;
+  auto work = torch::empty({(pd ? 3 : 2) * (int64_t)mipipe::layernorm_bwd_blocks(rows), H}, o);
   TORCH_CHECK(drop_p >= 0.0 && drop_p < 1.0, "dropout p must be in [0, 1)");
   optional<Tensor> dxd;
   const mipipe::DropSpec ds{(float)drop_p, (uint32_t)drop_seed,
@@ -1205,7 +1230,7 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>, optional<Tensor>> layerno
   mipipe::layernorm_bwd(dy.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                         gamma.data_ptr<float>(), dx.data_ptr(), pg, pb, work.data_ptr<float>(),
                         rows, (int)H, stream(), dxd.has_value() ? dxd->data_ptr() : nullptr,
-                        drop_p > 0.0 ? &ds : nullptr);
+                        drop_p > 0.0 ? &ds : nullptr, pd);
   return {dx, dg, db, dxd};
 }
 
@@ -1699,13 +1724,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("synthetic_batch", &synthetic_batch);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
+  m.def("gelu_bwd_colsum", &gelu_bwd_colsum, py::arg("dy"), py::arg("x"), py::arg("bias"));
   m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("res") = py::none(), py::arg("drop_p") = 0.0,
         py::arg("drop_seed") = 0, py::arg("drop_seed_dev") = py::none());
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("mean"),
         py::arg("rstd"), py::arg("gamma"), py::arg("dgamma") = py::none(),
         py::arg("dbeta") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,
-        py::arg("drop_seed_dev") = py::none());
+        py::arg("drop_seed_dev") = py::none(), py::arg("dbias") = py::none());
   m.def("embedding_bwd", &embedding_bwd, py::arg("dy"), py::arg("idx"), py::arg("num_rows"),
         py::arg("out") = py::none(), py::arg("ordered") = false, py::arg("scale") = 1.0);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(),

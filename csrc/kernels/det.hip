@@ -10,18 +10,20 @@ namespace mipipe {
 
 int g_deterministic = 0;
 
-// out[c] (+)= sum_p in[p * stride][c] for up to two row arrays.  Block: 64 channels x 16 row
+// out[c] (+)= sum_p in[p * stride][c] for up to three row arrays (blockIdx.y).  Block: 64 channels x 16 row
 // groups; group g sums rows g, g+16, ... in order, then the 16 group sums are added in index order.
 __global__ __launch_bounds__(1024) void det_sum_rows_kernel(const float* __restrict__ in0,
-                                                            const float* __restrict__ in1, int P,
+                                                            const float* __restrict__ in1,
+                                                            const float* __restrict__ in2, int P,
                                                             int C, float* __restrict__ out0,
                                                             float* __restrict__ out1,
+                                                            float* __restrict__ out2,
                                                             bool accumulate, int stride) {
   __shared__ float part[16][65];
   const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lc;
-  const float* in = blockIdx.y == 0 ? in0 : in1;
-  float* out = blockIdx.y == 0 ? out0 : out1;
+  const float* in = blockIdx.y == 0 ? in0 : blockIdx.y == 1 ? in1 : in2;
+  float* out = blockIdx.y == 0 ? out0 : blockIdx.y == 1 ? out1 : out2;
   const long rs = (long)stride * C;
   float a = 0.f;
   if (c < C) {
@@ -54,12 +56,13 @@ __global__ __launch_bounds__(1024) void det_sum_rows_kernel(const float* __restr
 // CUs for C = 64 — and cost ~11 us per call, 1.2 ms per deterministic ResNet-50 step.
 constexpr int kDetChunkRows = 64;
 __global__ __launch_bounds__(256) void det_chunk_sum_kernel(float* __restrict__ in0,
-                                                            float* __restrict__ in1, int P,
+                                                            float* __restrict__ in1,
+                                                            float* __restrict__ in2, int P,
                                                             int C) {
   __shared__ float part[4][65];
   const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lc;
-  float* in = blockIdx.z == 0 ? in0 : in1;
+  float* in = blockIdx.z == 0 ? in0 : blockIdx.z == 1 ? in1 : in2;
   const int r0 = blockIdx.y * kDetChunkRows;
   const int r1 = min(P, r0 + kDetChunkRows);
   float a = 0.f;
@@ -79,19 +82,20 @@ __global__ __launch_bounds__(256) void det_chunk_sum_kernel(float* __restrict__ 
 }
 
 void det_sum_rows(float* in0, float* in1, int P, int C, float* out0, float* out1,
-                  bool accumulate, hipStream_t st) {
-  const int arrays = in1 != nullptr ? 2 : 1;
+                  bool accumulate, hipStream_t st, float* in2, float* out2) {
+  // arrays are taken in order: in2 only together with in1
+  const int arrays = in1 == nullptr ? 1 : in2 == nullptr ? 2 : 3;
   int stride = 1;
   if (P > 4 * kDetChunkRows) {  // two levels: chunk sums in place, then the chunk sums
     const int nch = (P + kDetChunkRows - 1) / kDetChunkRows;
     hipLaunchKernelGGL(det_chunk_sum_kernel, dim3((C + 63) / 64, nch, arrays), dim3(256), 0, st,
-                       in0, in1, P, C);
+                       in0, in1, in2, P, C);
     P = nch;
     stride = kDetChunkRows;
   }
   dim3 grid((C + 63) / 64, arrays);
-  hipLaunchKernelGGL(det_sum_rows_kernel, grid, dim3(1024), 0, st, in0, in1, P, C, out0, out1,
-                     accumulate, stride);
+  hipLaunchKernelGGL(det_sum_rows_kernel, grid, dim3(1024), 0, st, in0, in1, in2, P, C, out0,
+                     out1, out2, accumulate, stride);
 }
 
 // out[i] += sum_s ws[s][i], s in order (split-K partial tiles of a weight gradient).

@@ -39,7 +39,7 @@ extern int g_deterministic;
 // out[c] (+)= sum over P rows of in[p][c] (and in1 -> out1), fixed order.  The partial rows are
 // SCRATCH: long sums (P > 256) are done in two levels, the first writing chunk sums in place.
 void det_sum_rows(float* in0, float* in1, int P, int C, float* out0, float* out1,
-                  bool accumulate, hipStream_t st);
+                  bool accumulate, hipStream_t st, float* in2 = nullptr, float* out2 = nullptr);
 // out[i] += sum_s ws[s][i] over splits in order.
 void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st);
 // out[m][n] (bf16, row pitch ldc) = sum_s ws[s][m][n] + bias[n] (bias may be null); N % 8 == 0
@@ -303,10 +303,14 @@ void layernorm_fwd(const void* x, const void* res, const float* gamma, const flo
 void layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd,
                    const float* gamma, void* dx, float* dgamma, float* dbeta, float* work,
                    long rows, int H, hipStream_t st, void* dxd = nullptr,
-                   const DropSpec* drop = nullptr);
+                   const DropSpec* drop = nullptr, float* dbias = nullptr);
 int layernorm_bwd_blocks(long rows);  // partial rows of layernorm_bwd's work
 void gelu_fwd(const void* x, void* y, long n, hipStream_t st);
 void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st);
+// gelu_bwd of a [rows, cols] tensor that also accumulates out[c] += Σ_rows dx[:, c] (the GELU
+// Linear's bias gradient); work (deterministic mode): [colsum_blocks(rows, cols)][cols] scratch
+void gelu_bwd_colsum(const void* dy, const void* x, void* dx, float* out, long rows, int cols,
+                     float* work, hipStream_t st);
 // Fused self-attention, head_dim 64, on the packed projection layout (attention.hip):
 //   qkv [B*S][3*H*64] bf16, o [B*S][H*64] bf16, lse [B][H][S] fp32, mask [B][S] additive or null.
 // p_drop > 0 applies attention-probability dropout keyed by (seed, b, h, q, k).

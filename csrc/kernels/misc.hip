@@ -515,6 +515,77 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x,
   }
 }
 
+// dx = gelu'(x) * dy AND Σ_rows dx (the bias gradient of the GELU Linear, computed from the
+// stored bf16 dx as a separate colsum would) in one pass over the [rows, cols] tensors: the
+// colsum kernel's (column chunk, row block) grid, with the GELU backward on the load.
+__global__ __launch_bounds__(256) void gelu_bwd_colsum_kernel(const __bf16* __restrict__ dy,
+                                                              const __bf16* __restrict__ x,
+                                                              __bf16* __restrict__ dx,
+                                                              float* __restrict__ out, long rows,
+                                                              int cols, long rows_per_block,
+                                                              float* __restrict__ part) {
+  __shared__ float red[4][kColsumChunk + 4];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int c0 = blockIdx.x * kColsumChunk + l * 8;
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min(rows, r0 + rows_per_block);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < cols) {
+    long r = r0 + w;
+    for (; r + 4 < r1; r += 8) {  // two rows in flight per wave
+      uint4 gv[2], xv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        gv[u] = *reinterpret_cast<const uint4*>(dy + (r + 4 * u) * cols + c0);
+        xv[u] = *reinterpret_cast<const uint4*>(x + (r + 4 * u) * cols + c0);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float g[8], v[8];
+        unpack8(gv[u], g);
+        unpack8(xv[u], v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float cdf = 0.5f * (1.f + erff(v[q] * 0.70710678118654752f));
+          const float pdf = 0.3989422804014327f * __expf(-0.5f * v[q] * v[q]);
+          g[q] *= cdf + v[q] * pdf;
+        }
+        const uint4 ob = pack8(g);
+        *reinterpret_cast<uint4*>(dx + (r + 4 * u) * cols + c0) = ob;
+        unpack8(ob, g);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += g[q];
+      }
+    }
+    for (; r < r1; r += 4) {
+      float g[8], v[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + r * cols + c0), g);
+      unpack8(*reinterpret_cast<const uint4*>(x + r * cols + c0), v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float cdf = 0.5f * (1.f + erff(v[q] * 0.70710678118654752f));
+        const float pdf = 0.3989422804014327f * __expf(-0.5f * v[q] * v[q]);
+        g[q] *= cdf + v[q] * pdf;
+      }
+      const uint4 ob = pack8(g);
+      *reinterpret_cast<uint4*>(dx + r * cols + c0) = ob;
+      unpack8(ob, g);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += g[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[w][l * 8 + q] = acc[q];
+  __syncthreads();
+  for (int c = threadIdx.x; c < kColsumChunk; c += 256) {
+    const int col = blockIdx.x * kColsumChunk + c;
+    if (col >= cols) break;
+    const float sm = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    if (part != nullptr) part[(long)blockIdx.y * cols + col] = sm;
+    else atomicAdd(out + col, sm);
+  }
+}
+
 int g_colsum_row_blocks = 0;  // > 0: fixed row-block count (tuning experiments)
 
 static void colsum_grid(long rows, int cols, long& G, long& rpb) {
@@ -531,6 +602,16 @@ int colsum_blocks(long rows, int cols) {
   long G, rpb;
   colsum_grid(rows, cols, G, rpb);
   return (int)G;
+}
+
+void gelu_bwd_colsum(const void* dy, const void* x, void* dx, float* out, long rows, int cols,
+                     float* work, hipStream_t st) {
+  long G, rpb;
+  colsum_grid(rows, cols, G, rpb);
+  dim3 grid((cols + kColsumChunk - 1) / kColsumChunk, (unsigned)G);
+  hipLaunchKernelGGL(gelu_bwd_colsum_kernel, grid, dim3(256), 0, st, (const __bf16*)dy,
+                     (const __bf16*)x, (__bf16*)dx, out, rows, cols, rpb, work);
+  if (work != nullptr) det_sum_rows(work, nullptr, (int)G, cols, out, nullptr, true, st);
 }
 
 void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
@@ -831,7 +912,9 @@ void layernorm_fwd(const void* x, const void* res, const float* gamma, const flo
 // it reduces the current one (the kernel is latency-bound otherwise: two dependent wave sums
 // per row); γ is held in registers for the whole block.
 // DROP: also dxd = dropout'(dx) — the gradient of the dropped branch (the residual keeps dx).
-template <int NCH, bool DROP>
+// BSUM: also per-block partials of Σ_rows of the branch gradient (dxd, else dx; bf16-rounded as
+// stored) — the bias gradient of the Linear that produced the LayerNorm's input.
+template <int NCH, bool DROP, bool BSUM>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __restrict__ dy,
                                                             const __bf16* __restrict__ x,
                                                             const float* __restrict__ mean,
@@ -841,17 +924,18 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
                                                             float* __restrict__ pg,
                                                             float* __restrict__ pb, long rows,
                                                             int H, int rows_per_block,
-                                                            __bf16* __restrict__ dxd, DropArgs dr) {
+                                                            __bf16* __restrict__ dxd, DropArgs dr,
+                                                            float* __restrict__ pd) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t dbase = DROP ? drop_base(dr.seed, dr.seed_dev) : 0u;
   const int nc = H / 8;
-  float accg[NCH][8], accb[NCH][8], gam[NCH][8];
+  float accg[NCH][8], accb[NCH][8], accd[NCH][8], gam[NCH][8];
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int c = lane + k * 64;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      accg[k][q] = accb[k][q] = 0.f;
+      accg[k][q] = accb[k][q] = accd[k][q] = 0.f;
       gam[k][q] = c < nc ? gamma[c * 8 + q] : 0.f;
     }
   }
@@ -915,7 +999,17 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
 #pragma unroll
           for (int q = 0; q < 8; ++q)
             od[q] = drop_keep(dbase, row * H + c * 8 + q, dr.thr) ? od[q] * dr.scale : 0.f;
-          *reinterpret_cast<uint4*>(dxd + row * H + c * 8) = pack8(od);
+          const uint4 odb = pack8(od);
+          *reinterpret_cast<uint4*>(dxd + row * H + c * 8) = odb;
+          if constexpr (BSUM) {
+            unpack8(odb, od);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) accd[k][q] += od[q];
+          }
+        } else if constexpr (BSUM) {
+          unpack8(ob, o);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) accd[k][q] += o[q];
         }
       }
     }
@@ -924,17 +1018,18 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
   // (pg / pb: [gridDim.x][H]); summed in a fixed order by det_sum_rows (no atomics: every
   // block would otherwise contend on the same 2H addresses)
   __shared__ float red[4][NCH * 64 * 8];
-  for (int arr = 0; arr < 2; ++arr) {
+  for (int arr = 0; arr < (BSUM ? 3 : 2); ++arr) {
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       int c = lane + k * 64;
       if (c < nc)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) red[w][c * 8 + q] = arr == 0 ? accg[k][q] : accb[k][q];
+        for (int q = 0; q < 8; ++q)
+          red[w][c * 8 + q] = arr == 0 ? accg[k][q] : arr == 1 ? accb[k][q] : accd[k][q];
     }
     __syncthreads();
-    float* dst = (arr == 0 ? pg : pb) + (long)blockIdx.x * H;
+    float* dst = (arr == 0 ? pg : arr == 1 ? pb : pd) + (long)blockIdx.x * H;
     for (int c = threadIdx.x; c < H; c += 256)
       dst[c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
   }
@@ -955,31 +1050,37 @@ int layernorm_bwd_blocks(long rows) {
 
 void layernorm_bwd(const void* dy, const void* x, const float* mean, const float* rstd,
                    const float* gamma, void* dx, float* dgamma, float* dbeta, float* work,
-                   long rows, int H, hipStream_t st, void* dxd, const DropSpec* drop) {
-  // dgamma / dbeta are ACCUMULATED into (zeroed buffers or the flat gradient views) from the
-  // per-block partial rows in work ([2][layernorm_bwd_blocks(rows)][H])
+                   long rows, int H, hipStream_t st, void* dxd, const DropSpec* drop,
+                   float* dbias) {
+  // dgamma / dbeta (and dbias) are ACCUMULATED into (zeroed buffers or the flat gradient views)
+  // from the per-block partial rows in work ([2 or 3][layernorm_bwd_blocks(rows)][H])
   int G, rpb;
   layernorm_bwd_grid(rows, G, rpb);
   float* wg = work;
   float* wb = work + (long)G * H;
+  float* wd = dbias != nullptr ? work + 2l * G * H : nullptr;
   // register arrays sized for H: 2 chunks of 8 per lane up to H = 1024 (BERT-base), else 4
   const DropArgs dr = drop_args(drop);
   const bool dp = dr.thr != 0u && dxd != nullptr;
-  auto go = [&](auto nch, auto drop_c) {
+  auto go = [&](auto nch, auto drop_c, auto bsum_c) {
     constexpr int NCH = decltype(nch)::value;
-    constexpr bool DROP = decltype(drop_c)::value;
-    hipLaunchKernelGGL((layernorm_bwd_kernel<NCH, DROP>), dim3(G), dim3(256), 0, st,
+    constexpr bool DROP = decltype(drop_c)::value, BSUM = decltype(bsum_c)::value;
+    hipLaunchKernelGGL((layernorm_bwd_kernel<NCH, DROP, BSUM>), dim3(G), dim3(256), 0, st,
                        (const __bf16*)dy, (const __bf16*)x, mean, rstd, gamma, (__bf16*)dx, wg,
-                       wb, rows, H, rpb, (__bf16*)dxd, dr);
+                       wb, rows, H, rpb, (__bf16*)dxd, dr, wd);
+  };
+  auto go_b = [&](auto nch, auto drop_c) {
+    if (wd != nullptr) go(nch, drop_c, std::true_type());
+    else go(nch, drop_c, std::false_type());
   };
   if (H <= 1024) {
-    if (dp) go(std::integral_constant<int, 2>(), std::true_type());
-    else go(std::integral_constant<int, 2>(), std::false_type());
+    if (dp) go_b(std::integral_constant<int, 2>(), std::true_type());
+    else go_b(std::integral_constant<int, 2>(), std::false_type());
   } else {
-    if (dp) go(std::integral_constant<int, LN_MAXC>(), std::true_type());
-    else go(std::integral_constant<int, LN_MAXC>(), std::false_type());
+    if (dp) go_b(std::integral_constant<int, LN_MAXC>(), std::true_type());
+    else go_b(std::integral_constant<int, LN_MAXC>(), std::false_type());
   }
-  det_sum_rows(wg, wb, G, H, dgamma, dbeta, true, st);
+  det_sum_rows(wg, wb, G, H, dgamma, dbeta, true, st, wd, dbias);
 }
 
 // ------------------------------------------------------------------------------ dropout

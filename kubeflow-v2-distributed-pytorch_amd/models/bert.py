@@ -103,18 +103,20 @@ class BertLayer(tnn.Module):
         # h and h1 each feed a projection AND a post-LN residual: the LayerNorm backward hands
         # the residual gradient to the projection, whose data-grad GEMM adds it (no extra add)
         s_h, s_h1 = MF.ResidualSlot(), MF.ResidualSlot()
+        # and each post-LN kernel's backward sums its branch's bias gradient (no colsum pass)
+        s_b1, s_b2 = MF.BiasGradSlot(), MF.BiasGradSlot()
         qkv = self.attention.self.qkv(h, res_take=s_h)
         ctx = MF.attention(qkv, B, S, self.heads, mask, p_drop=self.p_attn if train else 0.0,
                            seed=seeds[0])
-        a = self.attention.output.dense(ctx)
+        a = self.attention.output.dense(ctx, bias_slot=s_b1)
         # hidden dropout fused into the post-LN residual kernels (same mask as MF.dropout)
         p = self.p_hidden if train else 0.0
         h1 = self.attention.output.LayerNorm(a, residual=h, res_give=s_h, dropout_p=p,
-                                             dropout_seed=seeds[1])
+                                             dropout_seed=seeds[1], bias_slot=s_b1)
         f = self.intermediate.dense(h1, act="gelu", res_take=s_h1)
-        f2 = self.output.dense(f)
+        f2 = self.output.dense(f, bias_slot=s_b2)
         return self.output.LayerNorm(f2, residual=h1, res_give=s_h1, dropout_p=p,
-                                     dropout_seed=seeds[2])
+                                     dropout_seed=seeds[2], bias_slot=s_b2)
 
 
 class _Encoder(tnn.Module):

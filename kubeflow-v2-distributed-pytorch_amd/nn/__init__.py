@@ -284,10 +284,11 @@ class AdaptiveAvgPool2d(tnn.AdaptiveAvgPool2d):
 class Linear(ShadowMixin, tnn.Linear):
     """``torch.nn.Linear`` state; GEMM on the MFMA kernel with the bias in the epilogue."""
 
-    def forward(self, x: torch.Tensor, act: str = "none", res_take=None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, act: str = "none", res_take=None,
+                bias_slot=None) -> torch.Tensor:
         w_c = self.compute_weight(x.dtype)
         b = None if self.bias is None else self.bias
-        return MF.linear(x, self.weight, w_c, b, act, res_take=res_take)
+        return MF.linear(x, self.weight, w_c, b, act, res_take=res_take, bias_slot=bias_slot)
 
 
 class Embedding(ShadowMixin, tnn.Embedding):
@@ -297,10 +298,12 @@ class Embedding(ShadowMixin, tnn.Embedding):
 
 class LayerNorm(tnn.LayerNorm):
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                res_give=None, dropout_p: float = 0.0, dropout_seed=None) -> torch.Tensor:
-        """LN(dropout(x) [+ residual]); the dropout is fused into the LayerNorm kernels."""
+                res_give=None, dropout_p: float = 0.0, dropout_seed=None,
+                bias_slot=None) -> torch.Tensor:
+        """LN(dropout(x) [+ residual]); the dropout is fused into the LayerNorm kernels
+        (``bias_slot``: see :func:`mipipe.ops.functional.layer_norm`)."""
         return MF.layer_norm(x, self.weight, self.bias, self.eps, residual, res_give,
-                             dropout_p, dropout_seed)
+                             dropout_p, dropout_seed, bias_slot)
 
 
 class Dropout(tnn.Dropout):

@@ -110,6 +110,18 @@ class ResidualSlot:
         return p
 
 
+class BiasGradSlot:
+    """Links a Linear to the LayerNorm that consumes its output (BERT's post-LN branches): the
+    LayerNorm backward, which writes the branch gradient anyway, also sums it over rows into the
+    Linear bias's flat-gradient view, and the Linear's backward skips its column-sum pass."""
+
+    __slots__ = ("bias", "done")
+
+    def __init__(self):
+        self.bias = None
+        self.done = False
+
+
 class BNActToken:
     """Links a BN(+ReLU) output to its single consuming conv: the conv's backward computes the
     BN-backward reductions in its dgrad epilogue and flags the BN's backward to skip them."""
@@ -860,7 +872,7 @@ def global_avg_pool(x: Tensor) -> Tensor:
 # ----------------------------------------------------------------------------- linear
 class _LinearFn(Function):
     @staticmethod
-    def forward(ctx, x, weight, w_c, bias, act, bias_c, res_take):
+    def forward(ctx, x, weight, w_c, bias, act, bias_c, res_take, bias_slot):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         bk = bias if bias_c is None else bias_c  # bias_c: the kernel's (padded) bias vector
@@ -874,14 +886,28 @@ class _LinearFn(Function):
         ctx.act, ctx.shp, ctx.has_bias = act, shp, bias is not None
         ctx.weight, ctx.bias = weight, bias
         ctx.res_take = res_take
+        ctx.bias_slot = bias_slot
+        if bias_slot is not None:  # the consuming LayerNorm may sum this bias's gradient
+            bias_slot.bias = bias if bias_c is None and act == "none" else None
+            bias_slot.done = False
         return y.reshape(*shp[:-1], y.shape[-1])
 
     @staticmethod
     def backward(ctx, dy):
         x2, w_c, aux = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        # the bias gradient's flat-space target (native path): a GELU layer sums it in the GELU
+        # backward's own pass over dy instead of a separate colsum over the result
+        tb = None
+        if ctx.has_bias and ctx.needs_input_grad[3] and K.use_native(dy2):
+            tb = _direct_grad_target(ctx.bias, dy2.shape[1])
+        bias_done = ctx.bias_slot is not None and ctx.bias_slot.done
         if ctx.act == "gelu":
-            dy2 = K.gelu_bwd(dy2, aux)
+            if tb is not None and K.gelu_bwd_colsum_ok(dy2):
+                dy2 = K.gelu_bwd_colsum(dy2, aux, tb[1])
+                bias_done = True
+            else:
+                dy2 = K.gelu_bwd(dy2, aux)
         elif ctx.act == "relu":
             dy2 = (dy2.float() * (aux > 0)).to(dy2.dtype)
         dx = dw = db = None
@@ -923,26 +949,29 @@ class _LinearFn(Function):
                     fs.grad_ready(ctx.weight)
                     dw = None
         if ctx.has_bias and ctx.needs_input_grad[3]:
-            tb = _direct_grad_target(ctx.bias, dy2.shape[1]) if K.use_native(dy2) else None
             if tb is not None:
-                K.colsum(dy2, tb[1])
+                if not bias_done:
+                    K.colsum(dy2, tb[1])
                 tb[0].grad_ready(ctx.bias)
             else:
                 db = K.colsum(dy2)
                 if ctx.bias.shape[0] != db.shape[0]:
                     db = db[: ctx.bias.shape[0]]
                 db = db.to(gdt)
-        return dx, dw, None, db, None, None, None
+        return dx, dw, None, db, None, None, None, None
 
 
 def linear(x: Tensor, weight: Tensor, w_c: Tensor, bias: Optional[Tensor], act: str = "none",
-           bias_c: Optional[Tensor] = None, res_take: Optional["ResidualSlot"] = None):
+           bias_c: Optional[Tensor] = None, res_take: Optional["ResidualSlot"] = None,
+           bias_slot: Optional[BiasGradSlot] = None):
     """y = act(x @ w_c^T + bias).  ``weight`` / ``bias``: the parameters (gradient targets);
     ``w_c``: the compute-dtype operand, ``bias_c``: the bias vector the kernel reads (both may
     be padded along the output dimension — a vocabulary rounded up to the tile width).
     ``res_take``: x is also consumed elsewhere (a residual stream); that consumer's gradient
-    wrt x, handed over through the slot, is added in this layer's data-grad GEMM."""
-    return _LinearFn.apply(x, weight, w_c, bias, act, bias_c, res_take)
+    wrt x, handed over through the slot, is added in this layer's data-grad GEMM.
+    ``bias_slot``: the output feeds :func:`layer_norm` with the same slot, whose backward
+    computes this layer's bias gradient."""
+    return _LinearFn.apply(x, weight, w_c, bias, act, bias_c, res_take, bias_slot)
 
 
 # ----------------------------------------------------------------------------- loss
@@ -970,13 +999,14 @@ def cross_entropy(logits: Tensor, labels: Tensor, label_smoothing: float = 0.0,
 # ----------------------------------------------------------------------------- transformer ops
 class _LayerNormFn(Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps, residual, res_give, drop):
+    def forward(ctx, x, gamma, beta, eps, residual, res_give, drop, bias_slot):
         y, mean, rstd, xs = K.layernorm_fwd(x, gamma, beta, eps, residual, drop)
         ctx.save_for_backward(x if xs is None else xs, mean, rstd, gamma)
         ctx.beta = beta
         ctx.has_res = residual is not None
         ctx.res_give = res_give
         ctx.drop = drop
+        ctx.bias_slot = bias_slot
         return y
 
     @staticmethod
@@ -987,8 +1017,14 @@ class _LayerNormFn(Function):
             tg, tb = _direct_grad_target(gamma), _direct_grad_target(ctx.beta)
             if tg is not None and tb is not None:
                 acc = (tg[1], tb[1])
+        # the producing Linear's bias gradient, summed in this kernel (native, flat space only)
+        slot, tbias = ctx.bias_slot, None
+        if acc is not None and slot is not None and slot.bias is not None:
+            tbias = _direct_grad_target(slot.bias, x.shape[-1])
         dx, dgamma, dbeta, dxd = K.layernorm_bwd(dy.contiguous(), x, mean, rstd, gamma, acc,
-                                                 ctx.drop)
+                                                 ctx.drop, None if tbias is None else tbias[1])
+        if tbias is not None:
+            slot.done = True
         dres = None
         if ctx.has_res:
             # d/d residual = d/dx; handed to the residual's other consumer when it fuses the add
@@ -998,28 +1034,30 @@ class _LayerNormFn(Function):
             fs = _direct_grad_target(gamma)[0]
             fs.grad_ready(gamma)
             fs.grad_ready(ctx.beta)
-            return dxin, None, None, None, dres, None, None
-        return dxin, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), None, dres, None, None
+            return dxin, None, None, None, dres, None, None, None
+        return dxin, dgamma.to(gamma.dtype), dbeta.to(gamma.dtype), None, dres, None, None, None
 
 
 def layer_norm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float = 1e-12,
                residual: Optional[Tensor] = None,
                res_give: Optional["ResidualSlot"] = None, dropout_p: float = 0.0,
-               dropout_seed=None) -> Tensor:
+               dropout_seed=None, bias_slot: Optional[BiasGradSlot] = None) -> Tensor:
     """LN(dropout(x) [+ residual]) — BERT's post-LN residual branch (dropout, add, norm) in one
     kernel each way.  ``res_give``: the residual's gradient goes to the slot (for the residual's
     other consumer to add in its own kernel) instead of through autograd.  ``dropout_p`` > 0
     (with ``residual``): the branch's dropout, mask identical to :func:`dropout` with that
-    seed."""
+    seed.  ``bias_slot``: x is the output of :func:`linear` given the same slot; this backward
+    also computes that layer's bias gradient."""
     drop = None
     if dropout_p > 0.0:
         if residual is None:
             x = dropout(x, dropout_p, dropout_seed)
+            bias_slot = None  # the branch gradient is not this kernel's any more
         else:
             seed = dropout_seed if isinstance(dropout_seed, K.DevSeed) \
                 else int(dropout_seed) & 0xFFFFFFFF
             drop = (float(dropout_p), seed)
-    return _LayerNormFn.apply(x, gamma, beta, eps, residual, res_give, drop)
+    return _LayerNormFn.apply(x, gamma, beta, eps, residual, res_give, drop, bias_slot)
 
 
 class _GeluFn(Function):

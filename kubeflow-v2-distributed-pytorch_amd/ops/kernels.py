@@ -358,18 +358,21 @@ def layernorm_fwd(x, gamma, beta, eps, residual=None, drop=None):
     return _ref.layernorm_fwd(x, gamma, beta, eps, residual)
 
 
-def layernorm_bwd(dy, x, mean, rstd, gamma, acc=None, drop=None):
+def layernorm_bwd(dy, x, mean, rstd, gamma, acc=None, drop=None, dbias=None):
     """-> (dx, dgamma, dbeta, dxd); with ``acc=(dgamma_buf, dbeta_buf)`` the parameter grads are
     accumulated into those buffers and returned as None.  ``drop=(p, seed)``: dxd = dropout'(dx),
-    the gradient of the dropped branch (else None)."""
+    the gradient of the dropped branch (else None).  ``dbias`` (fp32 [H]): also += Σ_rows of the
+    branch gradient (dxd, else dx) — the bias gradient of the Linear that produced x."""
     if use_native(dy):
         a = acc if acc is not None else (None, None)
         if drop is not None and drop[0] > 0.0:
             sd, dev = _split_seed(drop[1])
-            return native().layernorm_bwd(dy, x, mean, rstd, gamma, *a, drop[0], sd, dev)
-        return native().layernorm_bwd(dy, x, mean, rstd, gamma, *a)
+            return native().layernorm_bwd(dy, x, mean, rstd, gamma, *a, drop[0], sd, dev, dbias)
+        return native().layernorm_bwd(dy, x, mean, rstd, gamma, *a, dbias=dbias)
     dx, dg, db = _ref.layernorm_bwd(dy, x, mean, rstd, gamma)
     dxd = dropout_fwd(dx, drop[0], drop[1]) if drop is not None and drop[0] > 0.0 else None
+    if dbias is not None:
+        colsum((dxd if dxd is not None else dx).reshape(-1, dx.shape[-1]), dbias)
     if acc is not None:
         acc[0].add_(dg.to(acc[0].dtype))
         acc[1].add_(db.to(acc[1].dtype))
@@ -460,6 +463,21 @@ def gelu_bwd(dy, x):
     if use_native(dy):
         return native().gelu_bwd(dy, x)
     return _ref.gelu_bwd(dy, x)
+
+
+def gelu_bwd_colsum_ok(dy) -> bool:
+    """gelu_bwd_colsum runs as one native kernel for this [rows, cols] bf16 gradient."""
+    return use_native(dy) and dy.dtype == torch.bfloat16 and dy.shape[-1] % 8 == 0
+
+
+def gelu_bwd_colsum(dy, x, bias):
+    """dx = gelu_bwd(dy, x), and bias (fp32 [cols]) += Σ_rows dx — the bf16-rounded dx, so the
+    result equals colsum(gelu_bwd(dy, x), bias) bit for bit (same per-column summation order)."""
+    if gelu_bwd_colsum_ok(dy):
+        return native().gelu_bwd_colsum(dy.contiguous(), x.contiguous(), bias)
+    dx = gelu_bwd(dy, x)
+    colsum(dx.reshape(-1, dx.shape[-1]), bias)
+    return dx
 
 
 def stem_pack(x, dtype, pad: int, Hp: int, Wsp: int):

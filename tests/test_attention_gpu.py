@@ -364,3 +364,64 @@ def test_layernorm_fused_dropout_matches_unfused(dev_seed):
         assert torch.equal(a, b)
     keep = (dxd1 != 0).float().mean().item()
     assert 0.88 < keep < 0.92
+
+
+@pytest.mark.parametrize("drop", [False, True])
+def test_layernorm_bwd_bias_sum(drop):
+    """The LayerNorm backward's fused branch-gradient sum (the producing Linear's bias
+    gradient) == colsum of the branch gradient it returns (dxd with dropout, else dx); every
+    other output unchanged by it."""
+    from mipipe.ops import kernels as K
+    torch.manual_seed(5)
+    rows, H = 1000, 768
+    x = torch.randn(rows, H, device="cuda").to(torch.bfloat16)
+    gamma = torch.rand(H, device="cuda") + 0.5
+    beta = torch.randn(H, device="cuda")
+    dr = (0.1, 123) if drop else None
+    y, m, r, s = K.layernorm_fwd(x, gamma, beta, 1e-12, x, dr)
+    dy = torch.randn(rows, H, device="cuda").to(torch.bfloat16)
+    dx0, g0, b0, dxd0 = K.layernorm_bwd(dy, s, m, r, gamma, None, dr)
+    bias0 = torch.randn(H, device="cuda")
+    want = bias0.clone()
+    K.colsum(dxd0 if drop else dx0, want)
+    bias = bias0.clone()
+    dx1, g1, b1, dxd1 = K.layernorm_bwd(dy, s, m, r, gamma, None, dr, bias)
+    for a, b in ((dx0, dx1), (g0, g1), (b0, b1)):
+        assert torch.equal(a, b)
+    if drop:
+        assert torch.equal(dxd0, dxd1)
+    torch.testing.assert_close(bias, want, rtol=1e-5, atol=1e-3)
+    # against a float64 sum of the returned branch gradient
+    br = (dxd1 if drop else dx1).double().sum(0)
+    torch.testing.assert_close(bias.double() - bias0.double(), br, rtol=1e-4, atol=1e-2)
+
+
+def test_gelu_bwd_colsum_matches_separate():
+    """gelu_bwd_colsum == gelu_bwd then colsum: dx bit-identical, and the bias sum bit-identical
+    in deterministic mode (same per-column order; atomic mode: same up to fp32 rounding)."""
+    from mipipe.ops import kernels as K
+    from mipipe.ops._native import native
+    torch.manual_seed(6)
+    rows, cols = 4096, 3072
+    x = torch.randn(rows, cols, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(rows, cols, device="cuda").to(torch.bfloat16)
+    b0 = torch.randn(cols, device="cuda")
+    ref_dx = (dy.float() * torch.ops.aten.gelu_backward(torch.ones_like(x.float()), x.float())).bfloat16()
+    C = native()
+    for det in (1, 0):
+        C.set_deterministic(det)
+        try:
+            dx0 = K.gelu_bwd(dy, x)
+            s0 = b0.clone()
+            K.colsum(dx0, s0)
+            s1 = b0.clone()
+            dx1 = K.gelu_bwd_colsum(dy, x, s1)
+        finally:
+            C.set_deterministic(0)
+        assert torch.equal(dx0, dx1)
+        if det:
+            assert torch.equal(s0, s1)
+        else:
+            torch.testing.assert_close(s0, s1, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(dx1.float(), ref_dx.float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(s1.double() - b0.double(), dx1.double().sum(0), rtol=1e-4, atol=1e-2)

@@ -13,6 +13,7 @@
 #   bench NAME ARGS...     bench.py ARGS -> gpurun_out/bench_NAME.jsonl (appends)
 #   prof NAME ARGS...      rocprofv3 --kernel-trace --stats of bench.py ARGS -> gpurun_out/prof_NAME/
 #                          + tools/kernel_stats.py summary gpurun_out/prof_NAME/summary.txt
+#                          (PROF_MARKER=<kernel ending a step> PROF_LAST=N: the last N steps only)
 #   lab [SHAPE] [ROUNDS]   tools/gemm_lab/pp_lab (built on the CPU host beforehand)
 # Every GPU step runs under its own timeout; the first failing step ends the script.
 set -o pipefail
@@ -60,9 +61,10 @@ for r in "${PARTS[@]}"; do
       rc=$?
       if [ $rc -ne 0 ]; then tail -20 "$P/bench.txt"; exit $rc; fi
       csv=$(find "$P" -name '*kernel_trace.csv' | head -1)
-      python3 tools/kernel_stats.py "$csv" --top 40 > "$P/summary.txt" 2>&1
+      python3 tools/kernel_stats.py "$csv" --top 40 ${PROF_MARKER:+--step-marker $PROF_MARKER} \
+        ${PROF_LAST:+--last $PROF_LAST} > "$P/summary.txt" 2>&1
       head -30 "$P/summary.txt"
-      exit 0 ;;
+      continue ;;
     lab)
       step 600 "$O/pp_lab.jsonl" tools/gemm_lab/pp_lab "${1:--1}" "${2:-5}"
       cat "$O/pp_lab.jsonl"
