@@ -949,12 +949,15 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
   //  * accumulating GEMMs (weight-grads into the flat fp32 gradient, mode 2): splitk_sum adds
   //    them to C.  Chosen by the tuner where the output is small against the CU count (BERT's
   //    768 x 768 / 768 x 3072 weight-grads: 36-144 tiles) and atomics would cost more;
-  //  * activation-dtype outputs with at most a bias (mode 0: the MLM decoder's data-grad with
-  //    K = 30528 — 30 output tiles for 256 CUs — or BERT's FFN-out projection, K = 3072):
-  //    splitk_sum_bf16 adds the slices and the bias and rounds once to bf16.
+  //  * activation-dtype outputs with at most a bias or an addend (mode 0: the MLM decoder's
+  //    data-grad with K = 30528 — 30 output tiles for 256 CUs — or BERT's FFN-out projection,
+  //    K = 3072; mode 3: the FFN-in / QKV data-grads with the residual gradient added):
+  //    splitk_sum_bf16 adds the slices, the bias / addend and rounds once to bf16.
+  // Split counts 2..8 (not only powers of two): tiles x splits can then land near a whole
+  // number of waves over the 256 CUs.
   // Plans with kPlanWs set.  (Round 3 also timed a hipBLASLt "library plan" here; it is gone:
   // every GEMM of the training step runs on the MFMA kernels, tools/gemm_plans.py.)
-  const bool ws_out0 = mode == 0 && act_i == 0 && add_p == nullptr && !f32 && N % 8 == 0;
+  const bool ws_out0 = mode == 0 && act_i == 0 && !f32 && N % 8 == 0;
   auto launch = [&](void* C, int p) {
     if (p >= 4096) p = -1;  // a round-3 table's library plan: the heuristic MFMA plan
     const bool ws_plan = p >= 0 && (p & tune::kPlanWs) != 0;
@@ -970,7 +973,8 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
       if (mode == 2)
         mipipe::splitk_sum(ws.data_ptr<float>(), ns, M * N, static_cast<float*>(C), stream());
       else
-        mipipe::splitk_sum_bf16(ws.data_ptr<float>(), ns, M, (int)N, bias_p, C, N, stream());
+        mipipe::splitk_sum_bf16(ws.data_ptr<float>(), ns, M, (int)N, bias_p, C, N, stream(),
+                                add_p);
       return;
     }
     mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b, C, N,
@@ -980,7 +984,7 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
     std::vector<int> cands = tune::gemm_candidates(f32, mode == 2);
     if ((mode == 2 && K >= 1024) || (ws_out0 && K >= 2048)) {
       for (int t : tune::candidates(f32, mode == 2))
-        for (int sp : {2, 4, 8}) cands.push_back((t + tune::kPlanSplit * sp) | tune::kPlanWs);
+        for (int sp : {2, 3, 4, 6, 8}) cands.push_back((t + tune::kPlanSplit * sp) | tune::kPlanWs);
     }
     plan = tune::select_from(tune::gemm_key(M, N, K, !trans_a, trans_b, add_p != nullptr ? 3 : mode, f32),
                              cands, [&](int p) {
@@ -1139,7 +1143,7 @@ Tensor gelu_bwd(Tensor dy, Tensor x) {
 }
 
 // dx = gelu_bwd(dy, x) and bias += Σ_rows dx (fp32 [cols], e.g. the flat-gradient view) in one
-// kernel; bias sums the bf16-rounded dx exactly as colsum(dx, bias) would.
+// kernel; bias sums the bf16-rounded dx (fixed order in deterministic mode).
 Tensor gelu_bwd_colsum(Tensor dy, Tensor x, Tensor bias) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
@@ -1152,7 +1156,7 @@ Tensor gelu_bwd_colsum(Tensor dy, Tensor x, Tensor bias) {
   auto dx = torch::empty_like(x);
   optional<Tensor> work;
   if (mipipe::g_deterministic)
-    work = torch::empty({(int64_t)mipipe::colsum_blocks(rows, (int)cols), cols},
+    work = torch::empty({(int64_t)mipipe::gelu_bwd_colsum_blocks(rows, (int)cols), cols},
                         x.options().dtype(at::kFloat));
   mipipe::gelu_bwd_colsum(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), bias.data_ptr<float>(), rows,
                           (int)cols, work.has_value() ? work->data_ptr<float>() : nullptr,

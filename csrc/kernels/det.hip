@@ -114,6 +114,27 @@ __global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict
   }
 }
 
+// Same sum with the split count a template constant: every slice load of an element is issued
+// before the first add (one memory latency per element instead of `splits` dependent ones).
+template <int S>
+__global__ __launch_bounds__(256) void splitk_sum_fixed_kernel(const float* __restrict__ ws, long n4,
+                                                               float* __restrict__ out) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (long)gridDim.x * blockDim.x) {
+    float4 v[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) v[s] = reinterpret_cast<const float4*>(ws + (long)s * n4 * 4)[i];
+    float4 o = reinterpret_cast<float4*>(out)[i];
+    float4 a = v[0];
+#pragma unroll
+    for (int s = 1; s < S; ++s) {
+      a.x += v[s].x; a.y += v[s].y; a.z += v[s].z; a.w += v[s].w;
+    }
+    o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+    reinterpret_cast<float4*>(out)[i] = o;
+  }
+}
+
 __global__ void splitk_sum_tail_kernel(const float* __restrict__ ws, int splits, long n0, long n,
                                        float* __restrict__ out) {
   const long i = n0 + (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -157,11 +178,13 @@ __global__ __launch_bounds__(256) void splitk_sum_wide_kernel(const float* __res
   }
 }
 
-// out[m][n] = bf16(sum_s ws[s][m][n] + bias[n]), s in order: the finishing pass of a split-K GEMM
-// with an activation-dtype output (M x N, N % 8 == 0; ws slices are [M][N] contiguous).
+// out[m][n] = bf16(sum_s ws[s][m][n] + bias[n] + addend[m][n]), s in order: the finishing pass of
+// a split-K GEMM with an activation-dtype output (M x N, N % 8 == 0; ws slices are [M][N]
+// contiguous; addend: the data-grad's second gradient, [M][N] bf16, as the GEMM epilogue adds it).
 __global__ __launch_bounds__(256) void splitk_sum_bf16_kernel(const float* __restrict__ ws,
                                                               int splits, long M, int N,
                                                               const float* __restrict__ bias,
+                                                              const __bf16* __restrict__ addend,
                                                               __bf16* __restrict__ out, long ldc) {
   const long n8 = (long)N / 8;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-column chunk
@@ -182,14 +205,20 @@ __global__ __launch_bounds__(256) void splitk_sum_bf16_kernel(const float* __res
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] += b[e];
   }
+  if (addend != nullptr) {  // the GEMM epilogue's order: bf16(acc + float(addend))
+    float a[8];
+    unpack8(*reinterpret_cast<const uint4*>(addend + m * (long)N + c), a);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] += a[e];
+  }
   *reinterpret_cast<uint4*>(out + m * ldc + c) = pack8(f);
 }
 
 void splitk_sum_bf16(const float* ws, int splits, long M, int N, const float* bias, void* out,
-                     long ldc, hipStream_t st) {
+                     long ldc, hipStream_t st, const void* addend) {
   const long chunks = M * (N / 8);
   hipLaunchKernelGGL(splitk_sum_bf16_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
-                     st, ws, splits, M, N, bias, (__bf16*)out, ldc);
+                     st, ws, splits, M, N, bias, (const __bf16*)addend, (__bf16*)out, ldc);
 }
 
 void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st) {
@@ -203,6 +232,17 @@ void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st)
     const long n4 = n / 4;
     hipLaunchKernelGGL(splitk_sum_wide_kernel<4>, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0,
                        st, ws, splits, n4, out);
+  } else if (vec && splits >= 2 && splits <= 7) {
+    const long n4 = n / 4;
+    const dim3 grid((unsigned)std::max<long>(1, std::min<long>(4096, (n4 + 255) / 256)));
+    switch (splits) {
+      case 2: hipLaunchKernelGGL(splitk_sum_fixed_kernel<2>, grid, dim3(256), 0, st, ws, n4, out); break;
+      case 3: hipLaunchKernelGGL(splitk_sum_fixed_kernel<3>, grid, dim3(256), 0, st, ws, n4, out); break;
+      case 4: hipLaunchKernelGGL(splitk_sum_fixed_kernel<4>, grid, dim3(256), 0, st, ws, n4, out); break;
+      case 5: hipLaunchKernelGGL(splitk_sum_fixed_kernel<5>, grid, dim3(256), 0, st, ws, n4, out); break;
+      case 6: hipLaunchKernelGGL(splitk_sum_fixed_kernel<6>, grid, dim3(256), 0, st, ws, n4, out); break;
+      default: hipLaunchKernelGGL(splitk_sum_fixed_kernel<7>, grid, dim3(256), 0, st, ws, n4, out); break;
+    }
   } else if (vec) {
     const long n4 = n / 4;
     const long g = std::min<long>(4096, (n4 + 255) / 256);

@@ -44,7 +44,7 @@ void det_sum_rows(float* in0, float* in1, int P, int C, float* out0, float* out1
 void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st);
 // out[m][n] (bf16, row pitch ldc) = sum_s ws[s][m][n] + bias[n] (bias may be null); N % 8 == 0
 void splitk_sum_bf16(const float* ws, int splits, long M, int N, const float* bias, void* out,
-                     long ldc, hipStream_t st);
+                     long ldc, hipStream_t st, const void* addend = nullptr);
 int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 // bias / relu: optional per-channel bias and ReLU in the epilogue (convs without BN: VGG, AlexNet)
@@ -308,9 +308,10 @@ int layernorm_bwd_blocks(long rows);  // partial rows of layernorm_bwd's work
 void gelu_fwd(const void* x, void* y, long n, hipStream_t st);
 void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st);
 // gelu_bwd of a [rows, cols] tensor that also accumulates out[c] += Σ_rows dx[:, c] (the GELU
-// Linear's bias gradient); work (deterministic mode): [colsum_blocks(rows, cols)][cols] scratch
+// Linear's bias gradient); work (deterministic mode): [gelu_bwd_colsum_blocks(rows, cols)][cols]
 void gelu_bwd_colsum(const void* dy, const void* x, void* dx, float* out, long rows, int cols,
                      float* work, hipStream_t st);
+int gelu_bwd_colsum_blocks(long rows, int cols);
 // Fused self-attention, head_dim 64, on the packed projection layout (attention.hip):
 //   qkv [B*S][3*H*64] bf16, o [B*S][H*64] bf16, lse [B][H][S] fp32, mask [B][S] additive or null.
 // p_drop > 0 applies attention-probability dropout keyed by (seed, b, h, q, k).

@@ -435,6 +435,20 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const __bf16* __restrict_
   }
 }
 
+// gelu'(v) = Φ(v) + v·φ(v).  Φ through erfc(|v|/√2) = poly(t)·exp(-v²/2), t = 1/(1 + p|v|/√2)
+// (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7) sharing φ's exponential: one exp and one
+// reciprocal per element instead of libm's erff, so the backward pass stays HBM-bound.
+__device__ __forceinline__ float gelu_grad(float v) {
+  const float e = __expf(-0.5f * v * v);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, fabsf(v), 1.f));
+  const float poly =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f),
+                       -0.284496736f), 0.254829592f);
+  const float half_erfc = 0.5f * poly * e;  // Φ(-|v|)
+  const float cdf = v >= 0.f ? 1.f - half_erfc : half_erfc;
+  return cdf + v * (0.3989422804014327f * e);
+}
+
 __global__ __launch_bounds__(256) void gelu_bwd_kernel(const __bf16* __restrict__ dy,
                                                        const __bf16* __restrict__ x,
                                                        __bf16* __restrict__ dx, long n8) {
@@ -444,11 +458,7 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const __bf16* __restrict_
     unpack8(reinterpret_cast<const uint4*>(dy)[i], g);
     unpack8(reinterpret_cast<const uint4*>(x)[i], v);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      float cdf = 0.5f * (1.f + erff(v[q] * 0.70710678118654752f));
-      float pdf = 0.3989422804014327f * __expf(-0.5f * v[q] * v[q]);
-      g[q] *= cdf + v[q] * pdf;
-    }
+    for (int q = 0; q < 8; ++q) g[q] *= gelu_grad(v[q]);
     reinterpret_cast<uint4*>(dx)[i] = pack8(g);
   }
 }
@@ -515,9 +525,13 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x,
   }
 }
 
-// dx = gelu'(x) * dy AND Σ_rows dx (the bias gradient of the GELU Linear, computed from the
-// stored bf16 dx as a separate colsum would) in one pass over the [rows, cols] tensors: the
-// colsum kernel's (column chunk, row block) grid, with the GELU backward on the load.
+// dx = gelu'(x) * dy AND Σ_rows dx (the bias gradient of the GELU Linear, summed from the
+// stored bf16 dx) in one pass over the [rows, cols] tensors.  Grid (column chunk, row block):
+// each wave loads 4 rows of dy and x (8 16-B loads per lane in flight) before the math —
+// the pass is HBM-bound only with ~1.5k blocks resident (the colsum grid, sized for a pure read
+// pass, left it latency-bound at half the bandwidth).
+constexpr int kGeluColsumRowsPerBlock = 16;
+
 __global__ __launch_bounds__(256) void gelu_bwd_colsum_kernel(const __bf16* __restrict__ dy,
                                                               const __bf16* __restrict__ x,
                                                               __bf16* __restrict__ dx,
@@ -530,49 +544,33 @@ __global__ __launch_bounds__(256) void gelu_bwd_colsum_kernel(const __bf16* __re
   const long r0 = (long)blockIdx.y * rows_per_block;
   const long r1 = min(rows, r0 + rows_per_block);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto row_op = [&](uint4 gv, uint4 xv, long r) {
+    float g[8], v[8];
+    unpack8(gv, g);
+    unpack8(xv, v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) g[q] *= gelu_grad(v[q]);
+    const uint4 ob = pack8(g);
+    *reinterpret_cast<uint4*>(dx + r * cols + c0) = ob;
+    unpack8(ob, g);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += g[q];
+  };
   if (c0 < cols) {
     long r = r0 + w;
-    for (; r + 4 < r1; r += 8) {  // two rows in flight per wave
-      uint4 gv[2], xv[2];
+    for (; r + 12 < r1; r += 16) {
+      uint4 gv[4], xv[4];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < 4; ++u) {
         gv[u] = *reinterpret_cast<const uint4*>(dy + (r + 4 * u) * cols + c0);
         xv[u] = *reinterpret_cast<const uint4*>(x + (r + 4 * u) * cols + c0);
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        float g[8], v[8];
-        unpack8(gv[u], g);
-        unpack8(xv[u], v);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float cdf = 0.5f * (1.f + erff(v[q] * 0.70710678118654752f));
-          const float pdf = 0.3989422804014327f * __expf(-0.5f * v[q] * v[q]);
-          g[q] *= cdf + v[q] * pdf;
-        }
-        const uint4 ob = pack8(g);
-        *reinterpret_cast<uint4*>(dx + (r + 4 * u) * cols + c0) = ob;
-        unpack8(ob, g);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc[q] += g[q];
-      }
+      for (int u = 0; u < 4; ++u) row_op(gv[u], xv[u], r + 4 * u);
     }
-    for (; r < r1; r += 4) {
-      float g[8], v[8];
-      unpack8(*reinterpret_cast<const uint4*>(dy + r * cols + c0), g);
-      unpack8(*reinterpret_cast<const uint4*>(x + r * cols + c0), v);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float cdf = 0.5f * (1.f + erff(v[q] * 0.70710678118654752f));
-        const float pdf = 0.3989422804014327f * __expf(-0.5f * v[q] * v[q]);
-        g[q] *= cdf + v[q] * pdf;
-      }
-      const uint4 ob = pack8(g);
-      *reinterpret_cast<uint4*>(dx + r * cols + c0) = ob;
-      unpack8(ob, g);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] += g[q];
-    }
+    for (; r < r1; r += 4)
+      row_op(*reinterpret_cast<const uint4*>(dy + r * cols + c0),
+             *reinterpret_cast<const uint4*>(x + r * cols + c0), r);
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) red[w][l * 8 + q] = acc[q];
@@ -584,6 +582,20 @@ __global__ __launch_bounds__(256) void gelu_bwd_colsum_kernel(const __bf16* __re
     if (part != nullptr) part[(long)blockIdx.y * cols + col] = sm;
     else atomicAdd(out + col, sm);
   }
+}
+
+static void gelu_colsum_grid(long rows, int cols, long& G, long& rpb) {
+  const long chunks = (cols + kColsumChunk - 1) / kColsumChunk;
+  G = std::max<long>(1, std::min<long>((rows + kGeluColsumRowsPerBlock - 1) / kGeluColsumRowsPerBlock,
+                                       std::max<long>(1, 1536 / chunks)));
+  rpb = (rows + G - 1) / G;
+  G = (rows + rpb - 1) / rpb;
+}
+
+int gelu_bwd_colsum_blocks(long rows, int cols) {
+  long G, rpb;
+  gelu_colsum_grid(rows, cols, G, rpb);
+  return (int)G;
 }
 
 int g_colsum_row_blocks = 0;  // > 0: fixed row-block count (tuning experiments)
@@ -607,7 +619,7 @@ int colsum_blocks(long rows, int cols) {
 void gelu_bwd_colsum(const void* dy, const void* x, void* dx, float* out, long rows, int cols,
                      float* work, hipStream_t st) {
   long G, rpb;
-  colsum_grid(rows, cols, G, rpb);
+  gelu_colsum_grid(rows, cols, G, rpb);
   dim3 grid((cols + kColsumChunk - 1) / kColsumChunk, (unsigned)G);
   hipLaunchKernelGGL(gelu_bwd_colsum_kernel, grid, dim3(256), 0, st, (const __bf16*)dy,
                      (const __bf16*)x, (__bf16*)dx, out, rows, cols, rpb, work);
@@ -1036,8 +1048,10 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
 }
 
 static void layernorm_bwd_grid(long rows, int& G, int& rpb) {
-  // >= 8 rows (2 per wave, the second prefetched) per block; <= 4 blocks per CU
-  G = (int)std::max<long>(1, std::min<long>(1024, (rows + 7) / 8));
+  // >= 16 rows (4 per wave, each next one prefetched) per block and <= 256 blocks: the partial
+  // rows then take ONE fixed-order summing pass (det_sum_rows goes two-level above 256 rows;
+  // BERT 32x128: 512 blocks of 8 rows cost a second launch per call)
+  G = (int)std::max<long>(1, std::min<long>(256, (rows + 15) / 16));
   rpb = (int)((rows + G - 1) / G);
   G = (int)((rows + rpb - 1) / rpb);
 }

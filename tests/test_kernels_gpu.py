@@ -146,7 +146,7 @@ def test_gemm_every_plan(M, N, K, ta, tb):
             acc0 = acc.clone()
             native().gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0, cfg + 16 * sp)
             assert rel_err(acc - acc0, ref32) < 2e-3, (cfg, sp)
-        for sp in (2, 4, 8):  # workspace split-K (kPlanWs): per-split slices + ordered sum
+        for sp in (2, 3, 4, 6, 8):  # workspace split-K (kPlanWs): slices + ordered sum
             acc = torch.randn(M, N, device=dev)
             acc0 = acc.clone()
             native().gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0,
@@ -190,6 +190,14 @@ def test_gemm_addend_epilogue(M, N, K):
     for cfg in range(native().CONV_TILE_CONFIGS):
         out = native().gemm(a, b, False, False, None, "none", torch.bfloat16, None, 0.0, cfg, add)
         assert rel_err(out, ref) < 1e-2, cfg
+        if K >= 1024:  # workspace split-K: the ordered slice sum adds the addend
+            for sp in (3, 6):
+                plan = (cfg + 16 * sp) | 1024
+                ow = native().gemm(a, b, False, False, None, "none", torch.bfloat16, None, 0.0,
+                                   plan, add)
+                assert rel_err(ow, ref) < 1e-2, (cfg, sp, "ws")
+                assert torch.equal(ow, native().gemm(a, b, False, False, None, "none",
+                                                     torch.bfloat16, None, 0.0, plan, add))
 
 
 def test_gemm_round3_library_plan_entry_falls_back():

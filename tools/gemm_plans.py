@@ -66,13 +66,13 @@ def plans(C, mode, K):
             for sp in (1, 2, 4):
                 out.append(t + SPLIT * sp)
             if K >= 1024:
-                for sp in (2, 4, 8):
+                for sp in (2, 3, 4, 6, 8):
                     out.append((t + SPLIT * sp) | WS)
     else:
         out += tiles
-        if mode == 0 and K >= 2048:
+        if K >= 2048:  # bf16 output with a bias (mode 0) or an addend (mode 3)
             for t in tiles:
-                for sp in (2, 4, 8):
+                for sp in (2, 3, 4, 6, 8):
                     out.append((t + SPLIT * sp) | WS)
     return out
 
