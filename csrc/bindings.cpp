@@ -892,6 +892,44 @@ Tensor avgpool_bwd(Tensor dy, std::vector<int64_t> xs) {
 }
 
 // ------------------------------------------------------------------------------- GEMM
+// WsFinish tickets (launchers.hpp): one zeroed int array per device, handed out as a ring of
+// per-call slices.  Every launch leaves its slice zeroed again (the last split of a tile resets
+// its ticket), so a slice is reusable as soon as its kernel completed; a graph replays the
+// slices it captured.  Created eagerly (never inside a stream capture: the zero-fill would be
+// captured and the buffer would live in the graph's pool) — before that, plans fall back to the
+// separate slice sum.
+namespace {
+struct TicketRing {
+  Tensor buf;
+  long next = 0;
+};
+std::unordered_map<int, TicketRing> g_ticket_rings;
+constexpr long kTicketCap = 1 << 20;
+
+// Opt-in (MIPIPE_WS_FINISH=1): measured SLOWER on BERT-base — 4,125 vs 4,384 seq/s, GEMM time
+// 5.27 vs 4.74 ms/step with the sum kernels (profiles/r4_ws_finish_experiment.txt).  The
+// agent-scope release / acquire fences around the ticket are an L2 write-back and an L2
+// INVALIDATE of the whole XCD (buffer_wbl2 / buffer_inv sc1): every block that finishes a split
+// throws away the operand tiles its neighbours on that XCD were reusing.
+bool g_ws_finish = [] {
+  const char* v = getenv("MIPIPE_WS_FINISH");
+  return v != nullptr && atoi(v) != 0;
+}();
+
+int* ws_tickets(const Tensor& like, long n) {
+  if (!g_ws_finish || n <= 0 || n > kTicketCap) return nullptr;
+  TicketRing& r = g_ticket_rings[like.get_device()];
+  if (!r.buf.defined()) {
+    if (tune::capturing()) return nullptr;
+    r.buf = torch::zeros({kTicketCap}, like.options().dtype(at::kInt));
+  }
+  if (r.next + n > kTicketCap) r.next = 0;
+  int* p = r.buf.data_ptr<int>() + r.next;
+  r.next = (r.next + n + 63) & ~63l;
+  return p;
+}
+}  // namespace
+
 Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bias,
             std::string act, at::ScalarType out_dtype, optional<Tensor> c, double beta,
             int64_t plan, optional<Tensor> addend) {
@@ -967,9 +1005,17 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
     if (ws_plan && (mode == 2 || ws_out0) && sp > 1) {
       const int ns = mipipe::gemm_ws_splits((int)K, sp);
       Tensor ws = torch::empty({(int64_t)ns, M, N}, a.options().dtype(at::kFloat));
+      mipipe::WsFinish fin;
+      fin.ticket = ns > 1 && N % 4 == 0 ? ws_tickets(a, mipipe::gemm_max_tiles(M, N)) : nullptr;
+      fin.out = C;
+      fin.ldo = N;
+      fin.bias = bias_p;
+      fin.addend = add_p;
+      fin.bf16 = mode == 2 ? 0 : 1;
       mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b,
                    ws.data_ptr(), N, (int)M, (int)N, (int)K, nullptr, 0, 2, stream(), f32, cfg,
-                   sp, nullptr, true);
+                   sp, nullptr, true, fin.ticket != nullptr ? &fin : nullptr);
+      if (fin.ticket != nullptr) return;  // the GEMM's last split per tile summed the slices
       if (mode == 2)
         mipipe::splitk_sum(ws.data_ptr<float>(), ns, M * N, static_cast<float*>(C), stream());
       else
@@ -1658,6 +1704,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_force_tune", [](bool on) { tune::g_force_tune = on; });
   m.def("set_wgrad3x3", [](bool on) { mipipe::g_wgrad3x3 = on; });
   m.def("get_wgrad3x3", []() { return mipipe::g_wgrad3x3; });
+  m.def("set_ws_finish", [](bool on) { g_ws_finish = on; });
+  m.def("get_ws_finish", []() { return g_ws_finish; });
   m.def("set_deterministic", [](bool on) { mipipe::g_deterministic = on ? 1 : 0; });
   m.def("get_deterministic", []() { return mipipe::g_deterministic != 0; });
   m.def("tune_table", []() { return tune::g_table; });

@@ -256,31 +256,36 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(FwdArgs a) {
 
 // δ[b,h,q] = Σ_d dO·O  (one thread per (token, head)); also zeroes that (token, head)'s 64
 // fp32 dQ accumulators (the backward kernel adds into them) — no separate memset
+// δ[b][h][q] = Σ_d dO·O over the head's 64 values, and the fp32 dQ accumulator zeroed.  Eight
+// lanes per (token, head) — one 16-byte chunk each, summed across the 8 lanes with xor shuffles
+// (fixed order) — so loads and stores are contiguous across a wave and the grid has 8x the
+// blocks of a thread-per-row mapping (192 blocks at BERT-base 32x128: under one per CU).
 __global__ __launch_bounds__(256) void attn_delta_kernel(const __bf16* __restrict__ dout,
                                                          const __bf16* __restrict__ o,
                                                          float* __restrict__ delta,
                                                          float* __restrict__ dq_acc, int B, int S,
                                                          int H) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)B * S * H) return;
-  const int h = i % H;
-  const long tok = i / H;
-  const int b = tok / S, q = tok % S;
-  const uint4* dp = reinterpret_cast<const uint4*>(dout + tok * H * D + h * D);
-  const uint4* op = reinterpret_cast<const uint4*>(o + tok * H * D + h * D);
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long row = gid >> 3;  // (token, head); rows * 8 is a multiple of 8: groups stay whole
+  const int c = (int)(gid & 7);
+  if (row >= (long)B * S * H) return;
+  const int h = (int)(row % H);
+  const long tok = row / H;
+  const int b = (int)(tok / S), q = (int)(tok % S);
+  const long off = tok * H * D + h * D + c * 8;
+  float x[8], y[8];
+  unpack8(*reinterpret_cast<const uint4*>(dout + off), x);
+  unpack8(*reinterpret_cast<const uint4*>(o + off), y);
   float acc = 0.f;
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    float x[8], y[8];
-    unpack8(dp[c], x);
-    unpack8(op[c], y);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc += x[e] * y[e];
-  }
-  delta[((long)b * H + h) * S + q] = acc;
-  float4* dq = reinterpret_cast<float4*>(dq_acc + tok * H * D + h * D);
-#pragma unroll
-  for (int c = 0; c < D / 4; ++c) dq[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int e = 0; e < 8; ++e) acc += x[e] * y[e];
+  acc += __shfl_xor(acc, 1);
+  acc += __shfl_xor(acc, 2);
+  acc += __shfl_xor(acc, 4);
+  if (c == 0) delta[((long)b * H + h) * S + q] = acc;
+  float4* dq = reinterpret_cast<float4*>(dq_acc + off);
+  dq[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+  dq[1] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 struct BwdArgs {
@@ -542,7 +547,7 @@ void attention_bwd(const void* dout, const void* qkv, const void* o, const float
   // fixed order instead of fp32 atomics (one key block: its single add is already exact)
   const int slabs = attention_dq_slabs(S);
   const int det = slabs > 1 ? 1 : 0;
-  hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
+  hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, st,
                      (const __bf16*)dout, (const __bf16*)o, delta, dq_acc, B, S, H);
   attn::BwdArgs a{(const __bf16*)qkv, (const __bf16*)dout, lse, delta, mask, dq_acc,
                   (__bf16*)dqkv, det, B, S, H, scale, scale * attn::kLog2e, p_drop,

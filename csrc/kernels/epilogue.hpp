@@ -50,7 +50,61 @@ struct EpiParams {
   int rmw;
   // optional BN-backward collect done by block (0,0) of this launch (launchers.hpp BnCollect)
   BnCollect col;
+  // workspace split-K finished by the last-arriving split (det_rows path; launchers.hpp)
+  WsFinish fin;
 };
+
+// The last split of a workspace split-K tile sums the tile's slices (slice order) into the final
+// output.  Release: each split fences its slice stores (agent scope) before taking its ticket;
+// acquire: the last one fences again before reading the other splits' slices.
+template <int BM, int BN, int kThreads>
+__device__ void ws_finish(char* smem, const EpiParams& e, uint32_t m0, uint32_t n0) {
+  __threadfence();
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);
+  if (threadIdx.x == 0) {
+    const int old = atomicAdd(e.fin.ticket + blockIdx.x, 1);
+    *flag = old == (int)gridDim.y - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  if (*flag == 0) return;
+  __threadfence();
+  const int S = (int)gridDim.y;
+  const float* ws = reinterpret_cast<const float*>(e.C);
+  const long slice = (long)e.M * e.ldc;
+  constexpr int CPR = BN / 4;  // float4 chunks per tile row
+  for (int c = threadIdx.x; c < BM * CPR; c += kThreads) {
+    const uint32_t m = m0 + c / CPR, n = n0 + (c % CPR) * 4;
+    if (m >= e.M || n >= e.N) continue;
+    const float* p = ws + (long)m * e.ldc + n;
+    float4 a = *reinterpret_cast<const float4*>(p);
+    for (int s = 1; s < S; ++s) {
+      const float4 b = *reinterpret_cast<const float4*>(p + s * slice);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    if (e.fin.bf16 == 0) {
+      float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(e.fin.out) + (long)m * e.fin.ldo + n);
+      float4 v = *o;
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      *o = v;
+    } else {
+      float f[4] = {a.x, a.y, a.z, a.w};
+      if (e.fin.bias != nullptr) {
+        const float4 b = *reinterpret_cast<const float4*>(e.fin.bias + n);
+        f[0] += b.x; f[1] += b.y; f[2] += b.z; f[3] += b.w;
+      }
+      if (e.fin.addend != nullptr) {
+        const uint2 ad = *reinterpret_cast<const uint2*>(
+            reinterpret_cast<const __bf16*>(e.fin.addend) + (long)m * e.N + n);
+        f[0] += __uint_as_float(ad.x << 16); f[1] += __uint_as_float(ad.x & 0xffff0000u);
+        f[2] += __uint_as_float(ad.y << 16); f[3] += __uint_as_float(ad.y & 0xffff0000u);
+      }
+      *reinterpret_cast<uint2*>(reinterpret_cast<__bf16*>(e.fin.out) + (long)m * e.fin.ldo + n) =
+          make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3]));
+    }
+  }
+  if (threadIdx.x == 0) atomicExch(e.fin.ticket + blockIdx.x, 0);  // ready for the next launch
+}
 
 // BnCollect riding in a kernel: the block sums the replica rows of a bwd slab that the previous
 // kernel filled, re-zeroes them and writes Σg / Σg·x̂ (+ dβ, dγ).  Each thread issues all of a
@@ -589,6 +643,12 @@ __device__ void epilogue_f32(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
           }
         }
       }
+    }
+  }
+  if constexpr (ATOMIC) {
+    if (e.det_rows > 0 && e.fin.ticket != nullptr) {
+      __syncthreads();  // the staging reads of the last pass are done (ws_finish reuses smem)
+      ws_finish<BM, BN, kThreads>(smem, e, m0, n0);
     }
   }
 }

@@ -103,7 +103,7 @@ int gemm_ws_splits(int K, int splits) {
 template <class C, class T>
 static void launch_tile(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc,
                         int M, int N, int K, int out, EpiParams e, int splits_req,
-                        hipStream_t st, bool ws_split) {
+                        hipStream_t st, bool ws_split, const WsFinish* fin) {
   uint32_t tN = cdiv_u(N, C::BN), tiles = cdiv_u(M, C::BM) * tN;
   int nk = (int)cdiv_u(K, 64);
   int splits = 1, per = nk;
@@ -111,6 +111,7 @@ static void launch_tile(const void* A, long lda, bool a_kc, const void* B, long 
     splits = gemm_ws_splits(K, splits_req);
     per = (int)cdiv_u(nk, splits);
     e.det_rows = 1;
+    if (fin != nullptr) e.fin = *fin;  // the last split of each tile finishes the sum
   } else if (out == 2) {
     splits = plan_splits(tiles, nk, splits_req);
     per = (int)cdiv_u(nk, splits);
@@ -137,11 +138,11 @@ int default_gemm_cfg(int M, int N, bool f32) {
 template <class T>
 static void gemm_t(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, int M,
                    int N, int K, int out, const EpiParams& e, int cfg, int splits,
-                   hipStream_t st, bool ws_split) {
+                   hipStream_t st, bool ws_split, const WsFinish* fin) {
   if (cfg < 0 || !tile_ok_for<T>(cfg)) cfg = default_gemm_cfg(M, N, std::is_same<T, float>::value);
   auto go = [&](auto tile) {
     typedef decltype(tile) C;
-    launch_tile<C, T>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, splits, st, ws_split);
+    launch_tile<C, T>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, splits, st, ws_split, fin);
   };
   // fp32-output modes stage BM x BN fp32 in LDS: no 256 x 256 tile there
   if (out == 0 || out == 3) with_tile<T, false>(cfg, go);
@@ -150,7 +151,7 @@ static void gemm_t(const void* A, long lda, bool a_kc, const void* B, long ldb, 
 
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
           long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
-          bool f32, int cfg, int splits, const void* addend, bool ws_split) {
+          bool f32, int cfg, int splits, const void* addend, bool ws_split, const WsFinish* fin) {
   EpiParams e{};
   e.C = C; e.ldc = ldc; e.M = (uint32_t)M; e.N = (uint32_t)N; e.bias = bias; e.act = act;
   if (addend != nullptr && out == 0 && a_kc && !b_kc) {
@@ -158,8 +159,9 @@ void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc
     out = 3;
   }
   ws_split = ws_split && out == 2 && splits > 1 && bias == nullptr;
-  if (f32) gemm_t<float>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st, ws_split);
-  else gemm_t<__bf16>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st, ws_split);
+  if (fin != nullptr && (!ws_split || N % 4 != 0 || ldc != N || fin->ticket == nullptr)) fin = nullptr;
+  if (f32) gemm_t<float>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st, ws_split, fin);
+  else gemm_t<__bf16>(A, lda, a_kc, B, ldb, b_kc, M, N, K, out, e, cfg, splits, st, ws_split, fin);
 }
 
 }  // namespace mipipe

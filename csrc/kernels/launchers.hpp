@@ -99,6 +99,19 @@ struct BnCollect {
   bool two = false;
   float *dgamma2 = nullptr, *dbeta2 = nullptr;
 };
+// Finishing a workspace split-K GEMM inside the GEMM: every split stores its partial tile to its
+// workspace slice, then takes a ticket (one int per output tile, a zeroed self-resetting array);
+// the split that arrives last sums the tile's slices in slice order (bit-identical to
+// splitk_sum / splitk_sum_bf16) and writes the result — no second kernel, no second pass over
+// the slices of tiles that finished early.
+struct WsFinish {
+  int* ticket = nullptr;   // [tiles] zeroed ints (re-zeroed by the last split); null: off
+  void* out = nullptr;     // fp32 accumulate target (out += Σ) or bf16 output
+  long ldo = 0;
+  const float* bias = nullptr;   // bf16 output: + bias[n]
+  const void* addend = nullptr;  // bf16 output: + addend[m][n] (bf16, row pitch N)
+  int bf16 = 0;
+};
 // col: optional collect riding in this launch (see BnCollect)
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
                 int cfg = -1, float* ws = nullptr, int splits = -1, const BnCollect* col = nullptr);
@@ -162,10 +175,14 @@ void avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho,
 //  ws_split (out 2, splits > 1): C is a [splits][M][ldc] fp32 WORKSPACE; split s stores its
 //  partial tile into slice s with plain stores (no atomics; the caller sums the slices in order
 //  with splitk_sum) — deterministic, and for small outputs faster than atomics (~1.3 TB/s).
+//  fin (with ws_split, N % 4 == 0): the GEMM finishes the sum itself (WsFinish), the caller
+//  runs no splitk_sum.
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
           long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
           bool f32 = false, int cfg = -1, int splits = -1, const void* addend = nullptr,
-          bool ws_split = false);
+          bool ws_split = false, const WsFinish* fin = nullptr);
+// WsFinish tickets a gemm needs at most: one per output tile of the smallest tile config
+inline long gemm_max_tiles(long M, long N) { return ((M + 63) / 64) * ((N + 63) / 64); }
 // the split count a ws_split gemm of this K actually uses for `splits` requested
 int gemm_ws_splits(int K, int splits);
 int default_gemm_cfg(int M, int N, bool f32);

@@ -200,6 +200,71 @@ def test_gemm_addend_epilogue(M, N, K):
                                                      torch.bfloat16, None, 0.0, plan, add))
 
 
+@pytest.mark.parametrize("M,N,K,ta,tb,mode", [
+    (768, 3072, 4096, True, False, 2), (2304, 768, 4096, True, False, 2),
+    (200, 136, 4104, True, False, 2), (640, 768, 30528, False, True, 0),
+    (4096, 768, 3072, False, False, 3), (1000, 776, 2048, False, True, 0)])
+def test_gemm_ws_finish_in_kernel_matches_slice_sum(M, N, K, ta, tb, mode):
+    """Workspace split-K finished inside the GEMM (the last split of each tile sums the slices,
+    WsFinish) == the separate ordered slice-sum kernel, bit for bit, for every tile config and
+    2..8 splits (the separate fp32 sum of >= 8 slices runs a strided order: there equal to fp32
+    rounding); repeated launches give bit-identical results (the self-resetting tickets), also
+    replayed from a graph."""
+    C = native()
+    a = bf(K, M) if ta else bf(M, K)
+    b = bf(N, K, scale=0.05) if tb else bf(K, N, scale=0.05)
+    bias = torch.randn(N, device=dev) if mode == 0 else None
+    add = bf(M, N) if mode == 3 else None
+    acc0 = torch.randn(M, N, device=dev)
+
+    def run(plan):
+        if mode == 2:
+            acc = acc0.clone()
+            C.gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0, plan)
+            return acc
+        return C.gemm(a, b, ta, tb, bias, "none", torch.bfloat16, None, 0.0, plan, add)
+    run.mode = mode
+
+    C.set_ws_finish(True)  # opt-in path (off by default: slower, see bindings.cpp)
+    try:
+        _ws_finish_cases(C, run)
+    finally:
+        C.set_ws_finish(False)
+
+
+def _ws_finish_cases(C, run):
+    mode = run.mode
+    for cfg in range(C.CONV_TILE_CONFIGS):
+        for sp in (2, 3, 5, 8):
+            plan = (cfg + 16 * sp) | 1024
+            C.set_ws_finish(False)
+            try:
+                want = run(plan)
+            finally:
+                C.set_ws_finish(True)
+            got = run(plan)
+            if mode == 2 and sp >= 8:
+                torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-4)
+            else:
+                assert torch.equal(got, want), (cfg, sp)
+            assert torch.equal(run(plan), got), (cfg, sp, "rerun")
+    # graph replay: the captured launches keep their ticket slices and leave them zeroed
+    plan = (2 + 16 * 3) | 1024
+    want = run(plan)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        run(plan)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = run(plan)
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, want)
+
+
 def test_gemm_round3_library_plan_entry_falls_back():
     """A round-3 tuning table may still hold library plans (flag 4096); the library plan is gone,
     such an entry runs the heuristic MFMA plan: the result is bit-identical to plan -1's."""
