@@ -806,9 +806,13 @@ std::tuple<Tensor, Tensor, optional<Tensor>> stem_fwd_pool(Tensor xp, Tensor w, 
 // Backward of the fused stem: Σg, Σg·x̂ (bwd slab `rep` [3][R][64], re-zeroed; + dγ / dβ
 // accumulators) -> packed dW [64][7][4][8] fp32 with the BN-apply folded into the weight-grad.
 // Returns (dW, Σg, Σg·x̂).
+// The BN-backward statistics come from the POOLED tensors: Σg = Σ_p dp·[z>0] and
+// Σg·x̂ = Σ_p dp·[z>0]·(z-β)/γ, z the stored pooled output (= relu(γ·x̂ + β) at the window's
+// argmax pixel) — a reduce over 2 x 103 MB (bn_act_bwd_reduce with mean = β, invstd = 1, the
+// division by γ in its collect) instead of routing dp to the 411 MB conv output y (143 us).
 std::tuple<Tensor, Tensor, Tensor> stem_bwd(Tensor xp, Tensor y, Tensor dp, Tensor idx, Tensor pout,
-                                            Tensor mean, Tensor invstd, Tensor gamma, Tensor rep,
-                                            int64_t count, optional<Tensor> dgamma,
+                                            Tensor mean, Tensor invstd, Tensor gamma, Tensor beta,
+                                            Tensor rep, int64_t count, optional<Tensor> dgamma,
                                             optional<Tensor> dbeta) {
   check_bf16(xp, "xp");
   c10::DeviceGuard dg(xp.device());
@@ -822,32 +826,26 @@ std::tuple<Tensor, Tensor, Tensor> stem_bwd(Tensor xp, Tensor y, Tensor dp, Tens
   check_cuda(idx, "idx");
   const std::vector<int64_t> ps = {N, Ho / 2, 56, 64}, ys = {N, Ho, 112, 64};
   TORCH_CHECK(dp.sizes() == ps && idx.sizes() == ps && pout.sizes() == ps && y.sizes() == ys &&
-                  idx.scalar_type() == at::kByte, "stem_bwd: shape mismatch");
-  for (const Tensor* t : {&mean, &invstd, &gamma}) check_vec(*t, 64, "BN vector");
+                  idx.scalar_type() == at::kByte && dp.is_contiguous() && pout.is_contiguous(),
+              "stem_bwd: shape mismatch");
+  for (const Tensor* t : {&mean, &invstd, &gamma, &beta}) check_vec(*t, 64, "BN vector");
   check_f32(rep, "rep");
   const int R = mipipe::kStatReplicas;
   TORCH_CHECK(rep.numel() == 3ll * R * 64, "rep must be [3,R,64]");
   TORCH_CHECK(dgamma.has_value() == dbeta.has_value(), "pass both accumulators or none");
   float* r = rep.data_ptr<float>();
-  const long pixels = (long)N * Ho * 112;
-  if (mipipe::g_deterministic) {
-    const int G = mipipe::pool_bn_bwd_reduce_blocks(pixels, 64);
-    auto part = torch::empty({2, G, 64}, dp.options().dtype(at::kFloat));
-    float* p0 = part.data_ptr<float>();
-    // pout = nullptr: the stem's argmax carries the ReLU mask, the pooled output is not read
-    mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), nullptr, y.data_ptr(),
-                               mean.data_ptr<float>(), invstd.data_ptr<float>(), N, Ho, 112, 64,
-                               Ho / 2, 56, 3, 2, 1, p0, G, stream(), false);
-    mipipe::det_sum_rows(p0, p0 + (long)G * 64, G, 64, r, r + (long)R * 64, false, stream());
-  } else {
-    mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), nullptr, y.data_ptr(),
-                               mean.data_ptr<float>(), invstd.data_ptr<float>(), N, Ho, 112, 64,
-                               Ho / 2, 56, 3, 2, 1, r, 0, stream(), false);
-  }
+  const long pooled = (long)N * (Ho / 2) * 56;
   auto o = rep.options();
   auto sg = torch::empty({64}, o), sgx = torch::empty({64}, o);
-  mipipe::bn_bwd_collect(r, 64, sg.data_ptr<float>(), sgx.data_ptr<float>(), fptr(dgamma, 64),
-                         fptr(dbeta, 64), stream());
+  optional<Tensor> det_ws;
+  if (mipipe::g_deterministic)
+    det_ws = torch::empty({3, (int64_t)mipipe::bn_bwd_reduce_blocks(pooled, 64), 64}, o);
+  mipipe::bn_act_bwd_reduce(dp.data_ptr(), pout.data_ptr(), pout.data_ptr(),
+                            beta.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, true,
+                            pooled, 64, sg.data_ptr<float>(), sgx.data_ptr<float>(), nullptr, r,
+                            fptr(dgamma, 64), fptr(dbeta, 64), nullptr, nullptr, stream(), false,
+                            det_ws.has_value() ? det_ws->data_ptr<float>() : nullptr,
+                            gamma.data_ptr<float>());
   const int G2 = mipipe::stem_wgrad_blocks(N, Ho);
   auto ws = torch::empty({(int64_t)G2 * 64 * 224}, o);
   auto dw = torch::zeros({64, 7, 4, 8}, o);
@@ -1759,8 +1757,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("stem_fwd_pool", &stem_fwd_pool, py::arg("xp"), py::arg("w"), py::arg("scale"),
         py::arg("bias"), py::arg("want_y") = true);
   m.def("stem_bwd", &stem_bwd, py::arg("xp"), py::arg("y"), py::arg("dp"), py::arg("idx"),
-        py::arg("pout"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("rep"),
-        py::arg("count"), py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
+        py::arg("pout"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("beta"),
+        py::arg("rep"), py::arg("count"), py::arg("dgamma") = py::none(),
+        py::arg("dbeta") = py::none());
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("trans_a"), py::arg("trans_b"),

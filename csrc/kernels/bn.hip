@@ -247,7 +247,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         mu[q] = mean[c0 + q];
-        is[q] = invstd[c0 + q];
+        is[q] = invstd != nullptr ? invstd[c0 + q] : 1.f;
         if (TWO) {
           mu2[q] = mean2[c0 + q];
           is2[q] = invstd2[c0 + q];
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 // the flat gradient buffer, replacing autograd's AccumulateGrad kernels.
 __global__ void bn_bwd_collect_kernel(float* __restrict__ rep, int C, float* og, float* ogx,
                                       float* ogx2, float* dgamma, float* dbeta, float* dgamma2,
-                                      float* dbeta2) {
+                                      float* dbeta2, const float* gx_div) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const long rs = (long)kStatReplicas * C;
@@ -349,6 +349,10 @@ __global__ void bn_bwd_collect_kernel(float* __restrict__ rep, int C, float* og,
     rep[o] = 0.f;
     rep[rs + o] = 0.f;
     rep[2 * rs + o] = 0.f;
+  }
+  if (gx_div != nullptr) {  // Σg·(z-β) -> Σg·x̂ = Σg·(z-β)/γ (x̂ recovered from the BN output)
+    const float gd = gx_div[c];
+    b = fabsf(gd) > 1e-30f ? b / gd : 0.f;
   }
   og[c] = a;
   ogx[c] = b;
@@ -375,7 +379,8 @@ void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float
                        const float* invstd, const void* y2, const float* mean2,
                        const float* invstd2, bool relu, long M, int C, float* out_g,
                        float* out_gx, float* out_gx2, float* rep, float* dgamma, float* dbeta,
-                       float* dgamma2, float* dbeta2, hipStream_t st, bool f32, float* det_ws) {
+                       float* dgamma2, float* dbeta2, hipStream_t st, bool f32, float* det_ws,
+                       const float* gx_div) {
   const int G = bn_bwd_reduce_blocks(M, C);
   const int det_rows = det_ws != nullptr ? G : 0;
   float* part = det_ws != nullptr ? det_ws : rep;
@@ -398,7 +403,7 @@ void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float
   }
   hipLaunchKernelGGL(bn_bwd_collect_kernel, dim3((C + 255) / 256), dim3(256), 0, st, rep, C, out_g,
                      out_gx, y2 ? out_gx2 : nullptr, dgamma, dbeta, y2 ? dgamma2 : nullptr,
-                     y2 ? dbeta2 : nullptr);
+                     y2 ? dbeta2 : nullptr, gx_div);
 }
 
 template <int MODE, class T>  // MODE 0: dy only, 1: dy + dres (=g), 2: dy + dy2 (second branch)
@@ -502,7 +507,7 @@ void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float*
 void bn_bwd_collect(float* rep, int C, float* out_g, float* out_gx, float* dgamma, float* dbeta,
                     hipStream_t st) {
   hipLaunchKernelGGL(bn_bwd_collect_kernel, dim3((C + 255) / 256), dim3(256), 0, st, rep, C, out_g,
-                     out_gx, nullptr, dgamma, dbeta, nullptr, nullptr);
+                     out_gx, nullptr, dgamma, dbeta, nullptr, nullptr, nullptr);
 }
 
 }  // namespace mipipe

@@ -206,7 +206,9 @@ void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float
                        const float* invstd2, bool relu, long M, int C, float* out_g,
                        float* out_gx, float* out_gx2, float* rep, float* dgamma, float* dbeta,
                        float* dgamma2, float* dbeta2, hipStream_t st, bool f32 = false,
-                       float* det_ws = nullptr);
+                       float* det_ws = nullptr, const float* gx_div = nullptr);
+// (invstd may be null: 1.  gx_div: out_gx /= gx_div[c] before dγ — with y = z = a post-ReLU BN
+// output, mean = β and invstd = null this turns Σg·(z-β) into Σg·x̂, x̂ = (z-β)/γ where z > 0.)
 // grid size of the reduce pass: deterministic mode needs det_ws = [3][blocks][C] floats
 int bn_bwd_reduce_blocks(long M, int C);
 // Sum the replica rows of a bwd slab (filled by a fused dgrad epilogue) into out_g / out_gx,

@@ -783,9 +783,11 @@ class _StemFusedFn(Function):
     """maxpool_3x3/2/1(relu(bn(conv7x7/2(x)))) for the packed stem (stem.hip).  Forward: a
     statistics pass that recomputes the conv instead of storing y, then one pass that computes
     the conv again and writes y, the pooled output and argmax (BN-apply + ReLU + pool in
-    registers / LDS).  Backward: the BN reduction over (y, dp, argmax) (pool.hip), then ONE pass
-    that routes the pooled gradient, forms dy = A·g + B·y + C in LDS and accumulates the weight
-    gradient from it — dy never reaches HBM.  Numerics follow the unfused conv -> pool_bn path."""
+    registers / LDS).  Backward: the BN reduction over the POOLED gradient and output (x̂ of the
+    window's argmax pixel recovered as (z-β)/γ: no pass over the 4x larger conv output), then ONE
+    pass that routes the pooled gradient, forms dy = A·g + B·y + C in LDS and accumulates the
+    weight gradient from it — dy never reaches HBM.  Numerics follow the unfused conv -> pool_bn
+    path to bf16 rounding (x̂ from the stored bf16 z instead of the stored bf16 y)."""
 
     @staticmethod
     def forward(ctx, xp, weight, w_c, gamma, beta, bn):
@@ -809,7 +811,7 @@ class _StemFusedFn(Function):
             if tg is not None and tb is not None:
                 direct = (tg[1], tb[1])
         dwp, sg, sgx = K.stem_bwd(xp, y, dp.contiguous(), idx, out, st.mean, st.invstd,
-                                  gamma.detach(), rep, st.count, acc=direct)
+                                  gamma.detach(), ctx.beta.detach(), rep, st.count, acc=direct)
         _ws_done(bn, "bwd")
         dw = None
         if ctx.needs_input_grad[1]:

@@ -223,13 +223,13 @@ def stem_fwd_pool(xp, w, scale, bias, want_y=True):
     return native().stem_fwd_pool(xp, w, scale.contiguous(), bias.contiguous(), bool(want_y))
 
 
-def stem_bwd(xp, y, dp, idx, pout, mean, invstd, gamma, rep, count, acc=None):
+def stem_bwd(xp, y, dp, idx, pout, mean, invstd, gamma, beta, rep, count, acc=None):
     """Backward of the fused stem: (packed dW [64,7,4,8] fp32, Σg, Σg·x̂) — the BN reduction over
-    (y, dp, argmax), then the BN-apply folded into the weight-grad; ``acc`` = (dγ, dβ)
-    accumulators or None; ``rep``: zeroed bwd replica slab (native)."""
+    the pooled (dp, output) pair (x̂ = (z-β)/γ where z > 0), then the BN-apply folded into the
+    weight-grad; ``acc`` = (dγ, dβ) accumulators or None; ``rep``: zeroed bwd replica slab."""
     a = acc if acc is not None else (None, None)
-    return native().stem_bwd(xp, y, dp, idx, pout, mean, invstd, gamma.float().contiguous(), rep,
-                             int(count), *a)
+    return native().stem_bwd(xp, y, dp, idx, pout, mean, invstd, gamma.float().contiguous(),
+                             beta.float().contiguous(), rep, int(count), *a)
 
 
 def pool_bn_supported(y) -> bool:
