@@ -59,7 +59,9 @@ struct EpiParams {
 // acquire: the last one fences again before reading the other splits' slices.
 template <int BM, int BN, int kThreads>
 __device__ void ws_finish(char* smem, const EpiParams& e, uint32_t m0, uint32_t n0) {
-  __threadfence();
+  // release only (L2 write-back, no invalidate): a full __threadfence() also invalidates the
+  // XCD's L2 in every block
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   int* flag = reinterpret_cast<int*>(smem);
   if (threadIdx.x == 0) {
@@ -68,7 +70,7 @@ __device__ void ws_finish(char* smem, const EpiParams& e, uint32_t m0, uint32_t 
   }
   __syncthreads();
   if (*flag == 0) return;
-  __threadfence();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the last split only
   const int S = (int)gridDim.y;
   const float* ws = reinterpret_cast<const float*>(e.C);
   const long slice = (long)e.M * e.ldc;
