@@ -342,12 +342,12 @@ def build_bert(a, world, local, dev, rank):
             if not ok:
                 raise SystemExit(f"--graph on is not possible here: {why}")
             model.train()
-            gs = GraphedStep(step, batches[0], warmup=max(2, a.warmup), inputs=batches)
-            a.graph_used = True
-            ids_of = {id(b[0]): k for k, b in enumerate(batches)}
+            gs = _capture(GraphedStep, step, batches, a)
+            if gs is not None:
+                ids_of = {id(b[0]): k for k, b in enumerate(batches)}
 
-            def step(ids, am, pos, labels):  # noqa: F811
-                return gs.replay(ids_of[id(ids)])
+                def step(ids, am, pos, labels):  # noqa: F811
+                    return gs.replay(ids_of[id(ids)])
     else:
         from mipipe.models.reference import ref_bert
         model = ref_bert(a.model).to(dev)
@@ -365,6 +365,33 @@ def build_bert(a, world, local, dev, rank):
             opt.step()
             return loss
     return step, model, batches
+
+
+def _capture(GraphedStep, step, batches, a):
+    """Capture the step into hipGraphs; with ``--graph auto`` a capture that fails on ANY rank
+    makes every rank run eagerly (one MIN all-reduce of a success flag after the attempt —
+    captured collectives never execute during capture, so a failed rank cannot leave peers
+    waiting inside one).  ``--graph on`` re-raises."""
+    import torch.distributed as dist
+    gs, err = None, None
+    try:
+        gs = GraphedStep(step, batches[0], warmup=max(2, a.warmup), inputs=batches)
+    except Exception as exc:  # noqa: BLE001 — reported, then handled uniformly across ranks
+        err = exc
+        if a.graph == "on":
+            raise
+    ok = torch.tensor([0 if err is not None else 1], dtype=torch.int32,
+                      device=batches[0][0].device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        torch.cuda.synchronize()
+        print(f"[bench] hipGraph capture failed ({err!r} on this rank or a peer); running the "
+              "step eagerly", file=sys.stderr, flush=True)
+        a.graph_used = False
+        return None
+    a.graph_used = True
+    return gs
 
 
 def _rccl_settings():
@@ -452,12 +479,12 @@ def build_cnn(a, world, local, dev, rank):
             model.train()
             # one captured step per resident synthetic batch: replays issue every kernel of the
             # step (fwd, bwd, SGD) from one launch; no batch copies
-            gs = GraphedStep(step, batches[0], warmup=max(2, a.warmup), inputs=batches)
-            a.graph_used = True
-            ids = {id(b[0]): k for k, b in enumerate(batches)}
+            gs = _capture(GraphedStep, step, batches, a)
+            if gs is not None:
+                ids = {id(b[0]): k for k, b in enumerate(batches)}
 
-            def step(x, y):  # noqa: F811
-                return gs.replay(ids[id(x)])
+                def step(x, y):  # noqa: F811
+                    return gs.replay(ids[id(x)])
     else:
         from mipipe.models.reference import _RESNET_CFG, ref_resnet
         if a.model in _RESNET_CFG:
