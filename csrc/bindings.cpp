@@ -456,21 +456,56 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
                           ws.data_ptr<float>(), S, colp);
     return dw;
   }
-  // plan = tile id + 16 * split count (0: heuristic split)
+  // plan = tile id + 16 * split count (0: heuristic split) [| kPlanWs: the split partial tiles
+  // go to workspace slices summed in order (the deterministic mode's path) instead of fp32
+  // atomics — cheaper where splits x Co x K x 4 B of atomics would run at ~1.3 TB/s]
   int plan = cfg;
+  auto run_ws = [&](float* out, int tile, int sp) {
+    const int splits = mipipe::conv_wgrad_splits(s, tile, sp);
+    if (splits == 1) {  // one writer per element: the plain read-modify-write is deterministic
+      mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), out, s, stream(), tile, nullptr, 1, colp);
+      return;
+    }
+    auto ws = torch::empty({splits, (int64_t)s.Co * kh * kw * s.Ci}, dy.options().dtype(at::kFloat));
+    mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), out, s, stream(), tile, ws.data_ptr<float>(),
+                       sp, colp);
+  };
   if (plan < 0) {
     std::vector<int> cands;
-    for (int t : tune::candidates(s.f32, true))
+    for (int t : tune::candidates(s.f32, true)) {
       for (int sp : {0, 1, 2, 4, 8, 16}) cands.push_back(t + tune::kPlanSplit * sp);
+      static const bool ws_cands = [] {  // MIPIPE_WGRAD_WS=0: atomic split-K only (A/B)
+        const char* v = getenv("MIPIPE_WGRAD_WS");
+        return v == nullptr || atoi(v) != 0;
+      }();
+      if (!mipipe::g_deterministic && ws_cands)
+        for (int sp : {4, 8, 16, 32}) cands.push_back((t + tune::kPlanSplit * sp) | tune::kPlanWs);
+    }
     plan = tune::select_from(tune::key("wgrad", s), cands, [&](int p) {
       auto dws = torch::zeros_like(dw);
+      const bool wsp = (p & tune::kPlanWs) != 0;
+      p &= ~tune::kPlanWs;
       const int sp = p / tune::kPlanSplit;
+      if (wsp) {  // collect off while timing (col rides in the real launch only)
+        const int splits = mipipe::conv_wgrad_splits(s, p % tune::kPlanSplit, sp);
+        auto ws = torch::empty({splits, (int64_t)s.Co * kh * kw * s.Ci},
+                               dy.options().dtype(at::kFloat));
+        mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dws.data_ptr<float>(), s, stream(),
+                           p % tune::kPlanSplit, ws.data_ptr<float>(), sp);
+        return;
+      }
       mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dws.data_ptr<float>(), s, stream(),
                          p % tune::kPlanSplit, nullptr, sp > 0 ? sp : -1);
     });
   }
+  const bool ws_plan = plan >= 0 && (plan & tune::kPlanWs) != 0;
+  if (ws_plan) plan &= ~tune::kPlanWs;
   const int tile = plan < 0 ? -1 : plan % tune::kPlanSplit;
   const int sp = plan < 0 ? -1 : (plan / tune::kPlanSplit > 0 ? plan / tune::kPlanSplit : -1);
+  if (ws_plan && !mipipe::g_deterministic) {
+    run_ws(dw.data_ptr<float>(), tile, sp);
+    return dw;
+  }
   if (mipipe::g_deterministic) {
     const int splits = mipipe::conv_wgrad_splits(s, tile, sp);
     if (splits == 1) {  // one writer per element: the plain read-modify-write is deterministic

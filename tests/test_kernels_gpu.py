@@ -93,6 +93,28 @@ def test_conv_wgrad(case):
     assert rel_err(dw, dwr) < 5e-3
 
 
+@pytest.mark.parametrize("shape", [(32, 14, 14, 256, 1024, 1, 1, 0), (16, 28, 28, 64, 64, 3, 1, 1),
+                                   (16, 56, 56, 64, 128, 3, 2, 1)])
+def test_conv_wgrad_workspace_plans(shape):
+    """Workspace split-K weight-grad plans (flag 1024: per-split slices + ordered sum instead of
+    fp32 atomics) against the fp32 reference, accumulating into an existing gradient, for
+    several tiles and split counts; bit-identical reruns."""
+    N, H, W, Ci, Co, k, s, p = shape
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy, x = bf(N, Ho, Wo, Co), bf(N, H, W, Ci)
+    dwr = _ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)
+    base = torch.randn_like(dwr)
+    for cfg in (0, 2, 9):
+        for sp in (4, 16, 32):
+            plan = (cfg + 16 * sp) | 1024
+            out = base.clone()
+            native().conv_wgrad(dy, x, k, k, s, p, out, cfg=plan)
+            assert rel_err(out - base, dwr) < 5e-3, (cfg, sp)
+            out2 = base.clone()
+            native().conv_wgrad(dy, x, k, k, s, p, out2, cfg=plan)
+            assert torch.equal(out, out2), (cfg, sp)
+
+
 def test_conv_wgrad_large_k_splitk():
     # K = N*Ho*Wo large enough to exercise split-K atomics
     x = bf(16, 28, 28, 64)
