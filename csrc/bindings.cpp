@@ -197,12 +197,20 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
                                                                 optional<Tensor> slab_sum,
                                                                 optional<Tensor> slab_sq,
                                                                 optional<Tensor> bias, bool relu,
-                                                                int stride_w, int pad_w, int cfg) {
+                                                                int stride_w, int pad_w, int cfg,
+                                                                optional<Tensor> wflip) {
   check_act(x, "x");
   check_same(w, x, "w");
   c10::DeviceGuard g(x.device());
   auto s = conv_shape(x, w, stride, pad, stride_w, pad_w);
   s.f32 = is_f32(x);
+  // wflip: the launch also writes the tap-flipped weight of this conv's stride-1 data-grad
+  void* wfp = nullptr;
+  if (wflip.has_value() && mipipe::dgrad_preflip_ok(s)) {
+    check_same(*wflip, w, "wflip");
+    TORCH_CHECK(wflip->numel() == w.numel() && wflip->is_contiguous(), "wflip must match w's size");
+    wfp = wflip->data_ptr();
+  }
   if (bias.has_value()) check_vec(*bias, s.Co, "bias");
   TORCH_CHECK(!(shift.has_value() && (bias.has_value() || relu)),
               "BN-statistics epilogue and bias/ReLU epilogue are exclusive");
@@ -249,12 +257,12 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
     auto part = torch::empty({2, P, s.Co}, x.options().dtype(at::kFloat));
     float* p0 = part.data_ptr<float>();
     mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), p0, p0 + (long)P * s.Co, sh, s,
-                     stream(), bp, relu, cfg, P);
+                     stream(), bp, relu, cfg, P, wfp);
     mipipe::det_sum_rows(p0, p0 + (long)P * s.Co, P, s.Co, psp, pssp, false, stream());
     return {y, ps, pss};
   }
   mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), psp, pssp, sh, s, stream(), bp, relu,
-                   cfg);
+                   cfg, 0, wfp);
   return {y, ps, pss};
 }
 
@@ -263,7 +271,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
                   optional<Tensor> bn_invstd, optional<Tensor> bn_scale, optional<Tensor> bn_bias,
                   optional<Tensor> bn_rep, optional<Tensor> bn_z, int pad_w, int cfg,
                   optional<Tensor> bn_mask, optional<Tensor> bn_y2, optional<Tensor> bn_mean2,
-                  optional<Tensor> bn_invstd2) {
+                  optional<Tensor> bn_invstd2, optional<Tensor> wflip_pre) {
   check_act(dy, "dy");
   check_same(w, dy, "w");
   c10::DeviceGuard g(dy.device());
@@ -285,16 +293,23 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
   auto dx = torch::empty({s.N, s.H, s.W, s.Ci}, dy.options());
   // data-grads run as forward convolutions over tap-flipped (sub-)kernels, per stride-parity
   // class; MIPIPE_DGRAD_FWD=0: the data-grad gather kernels everywhere, =2: also 1x1 stride-1
-  static const int fwd_style_mode = [] {
-    const char* v = getenv("MIPIPE_DGRAD_FWD");
-    return v == nullptr ? 1 : atoi(v);
-  }();
+  const int fwd_style_mode = mipipe::dgrad_fwd_style_mode();
   Tensor wflip;
   void* wfp = nullptr;
+  bool preflipped = false;
   if (fwd_style_mode > 0 && mipipe::conv_dgrad_fwd_style(s, fwd_style_mode >= 2) &&
       !bn_y2.has_value()) {
-    wflip = torch::empty({(int64_t)s.Ci * s.KH * s.KW * s.Co}, w.options());  // w: [Co,KH,KW,Ci]
-    wfp = wflip.data_ptr();
+    if (wflip_pre.has_value() && mipipe::dgrad_preflip_ok(s)) {
+      // written by this conv's forward launch (conv_fwd's wflip): no flip kernel here
+      check_same(*wflip_pre, w, "wflip_pre");
+      TORCH_CHECK(wflip_pre->numel() == w.numel() && wflip_pre->is_contiguous(),
+                  "wflip_pre must match w's size");
+      wfp = wflip_pre->data_ptr();
+      preflipped = true;
+    } else {
+      wflip = torch::empty({(int64_t)s.Ci * s.KH * s.KW * s.Co}, w.options());  // w: [Co,KH,KW,Ci]
+      wfp = wflip.data_ptr();
+    }
   }
   mipipe::DgradFusion fz;
   bool any = false;
@@ -360,7 +375,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
         f2.bn_rep = reps.data_ptr<float>();
       }
       mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dxs.data_ptr(), s, stream(),
-                         any ? &f2 : nullptr, c, wfp);
+                         any ? &f2 : nullptr, c, wfp, preflipped);
     });
   }
   if (mipipe::g_deterministic && fz.bn_rep != nullptr) {
@@ -370,7 +385,8 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     float* rep = fz.bn_rep;
     fz.bn_rep = part.data_ptr<float>();
     fz.det_rows = P;
-    mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), &fz, cfg, wfp);
+    mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), &fz, cfg, wfp,
+                       preflipped);
     const long rs = (long)mipipe::kStatReplicas * s.Ci, ps = (long)P * s.Ci;
     mipipe::det_sum_rows(fz.bn_rep, fz.bn_rep + ps, P, s.Ci, rep, rep + rs, false, stream());
     if (two)
@@ -379,7 +395,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     return dx;
   }
   mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), any ? &fz : nullptr,
-                     cfg, wfp);
+                     cfg, wfp, preflipped);
   return dx;
 }
 
@@ -1709,7 +1725,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("shift") = py::none(), py::arg("slab_sum") = py::none(),
         py::arg("slab_sq") = py::none(), py::arg("bias") = py::none(), py::arg("relu") = false,
-        py::arg("stride_w") = 0, py::arg("pad_w") = -1, py::arg("cfg") = -1);
+        py::arg("stride_w") = 0, py::arg("pad_w") = -1, py::arg("cfg") = -1,
+        py::arg("wflip") = py::none());
   m.attr("STAT_REPLICAS") = mipipe::kStatReplicas;
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("x_shape"),
         py::arg("stride"), py::arg("pad"), py::arg("addend") = py::none(),
@@ -1718,7 +1735,17 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bn_bias") = py::none(), py::arg("bn_rep") = py::none(),
         py::arg("bn_z") = py::none(), py::arg("pad_w") = -1, py::arg("cfg") = -1,
         py::arg("bn_mask") = py::none(), py::arg("bn_y2") = py::none(),
-        py::arg("bn_mean2") = py::none(), py::arg("bn_invstd2") = py::none());
+        py::arg("bn_mean2") = py::none(), py::arg("bn_invstd2") = py::none(),
+        py::arg("wflip_pre") = py::none());
+  m.def("dgrad_preflip_ok", [](std::vector<int64_t> x_shape, std::vector<int64_t> w_shape,
+                               int stride, int pad) {
+    // whether conv_fwd(wflip=...) prepares this conv's data-grad weight (dgrad_preflip_ok)
+    mipipe::ConvShape s;
+    s.N = (int)x_shape[0]; s.H = (int)x_shape[1]; s.W = (int)x_shape[2]; s.Ci = (int)x_shape[3];
+    s.Co = (int)w_shape[0]; s.KH = (int)w_shape[1]; s.KW = (int)w_shape[2];
+    s.stride = stride; s.pad = pad; s.stride_w = 0; s.pad_w = -1;
+    return mipipe::dgrad_preflip_ok(s);
+  });
   m.def("bn_bwd_collect", &bn_bwd_collect, py::arg("rep"), py::arg("C"),
         py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),

@@ -155,7 +155,17 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_fwd_kerne
   __shared__ __attribute__((aligned(16))) char smem[lds_bytes_out<T, C>()];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const uint32_t id = xcd_remap(blockIdx.x, gridDim.x);
+  uint32_t ntile = gridDim.x;
+  if constexpr (!DGRAD_EPI) {
+    if (e.fl_wt != nullptr) {  // trailing blocks: the data-grad's flipped weight
+      if (blockIdx.x >= e.fl_tiles) {
+        flip_block<T, C::THREADS>(e, blockIdx.x - e.fl_tiles, smem);
+        return;
+      }
+      ntile = e.fl_tiles;
+    }
+  }
+  const uint32_t id = xcd_remap(blockIdx.x, ntile);
   const uint32_t tm = id / tilesN, tn = id % tilesN;
   const uint32_t m0 = tm * BM, n0 = tn * BN;
   const uint32_t K = (uint32_t)(g.KH * g.KW * g.C);

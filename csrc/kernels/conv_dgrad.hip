@@ -78,6 +78,36 @@ bool conv_dgrad_fwd_style(const ConvShape& s, bool dense_too) {
   return sq && (dense_too || !is_dense(s));
 }
 
+int dgrad_fwd_style_mode() {
+  static const int mode = [] {
+    const char* v = getenv("MIPIPE_DGRAD_FWD");
+    return v == nullptr ? 1 : atoi(v);
+  }();
+  return mode;
+}
+
+bool dgrad_preflip_ok(const ConvShape& s) {
+  const int mode = dgrad_fwd_style_mode();
+  return mode > 0 && s.stride <= 2 && s.KH * s.KW > 1 && conv_dgrad_fwd_style(s, mode >= 2);
+}
+
+void dgrad_flip_plan(const ConvShape& s, FlipPlan& p) {
+  p = FlipPlan{};
+  p.S = s.stride;
+  long off = 0;
+  const uint32_t tiles = cdiv(s.Ci, 64) * cdiv(s.Co, 64);
+  for_each_class(s, [&](const DgradClass& c, uint32_t) {
+    if (c.ntaps <= 0 || p.ncls >= 4) return;
+    const int nkh = c.kh0 < s.KH ? (s.KH - c.kh0 + c.S - 1) / c.S : 0;
+    FlipClass& f = p.cls[p.ncls++];
+    f.kh0 = c.kh0; f.kw0 = c.kw0; f.nkh = nkh; f.nkw = c.nkw;
+    f.off = off;
+    f.b0 = p.nblk;
+    off += (long)s.Ci * c.ntaps * s.Co;  // conv_dgrad_t's flip_off progression
+    p.nblk += tiles * (uint32_t)(nkh * c.nkw);
+  });
+}
+
 // Tap-flipped sub-kernel as 64x64 LDS-tiled transposes, one per tap: wt[ci][a][b][co] =
 // w[co][kh0 + S(nkh-1-a)][kw0 + S(nkw-1-b)][ci].  Reads run along ci and writes along co (both
 // coalesced; the one-thread-per-element gather it replaces cost ~7 us per call).
@@ -119,7 +149,8 @@ static void weight_flip(const T* w, T* wt, const ConvShape& s, const DgradClass&
 
 template <class T>
 static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShape& s,
-                         hipStream_t st, const DgradFusion* fz, int cfg_in, void* wflip) {
+                         hipStream_t st, const DgradFusion* fz, int cfg_in, void* wflip,
+                         bool preflipped) {
   const bool dense = is_dense(s);
   long flip_off = 0;  // this class's slice of the flipped-weight workspace
   const bool aligned = s.Co % BK == 0;
@@ -155,7 +186,8 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
         // this class as a stride-1 forward convolution of dy (see conv_dgrad_fwd_style)
         T* wt = (T*)wflip + flip_off;
         flip_off += (long)s.Ci * c.ntaps * s.Co;
-        weight_flip<T>(wp, wt, s, c, nkh, st);
+        // preflipped: the forward launch wrote it (conv_fwd's trailing blocks, dgrad_flip_plan)
+        if (!preflipped) weight_flip<T>(wp, wt, s, c, nkh, st);
         ConvShape s2 = s;
         s2.H = s.Ho; s2.W = s.Wo; s2.Ci = s.Co; s2.Co = s.Ci;
         s2.Ho = c.Hc; s2.Wo = c.Wc;
@@ -199,9 +231,10 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
 }
 
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
-                const DgradFusion* fz, int cfg, void* w_flip) {
-  if (s.f32) conv_dgrad_t<float>(dy, w, dx, s, st, fz, cfg, w_flip);
-  else conv_dgrad_t<__bf16>(dy, w, dx, s, st, fz, cfg, w_flip);
+                const DgradFusion* fz, int cfg, void* w_flip, bool preflipped) {
+  preflipped = preflipped && w_flip != nullptr && dgrad_preflip_ok(s);
+  if (s.f32) conv_dgrad_t<float>(dy, w, dx, s, st, fz, cfg, w_flip, preflipped);
+  else conv_dgrad_t<__bf16>(dy, w, dx, s, st, fz, cfg, w_flip, preflipped);
 }
 
 }  // namespace mipipe

@@ -35,13 +35,20 @@ int conv_fwd_tiles_m(const ConvShape& s, int cfg) {
 template <class T>
 static void conv_fwd_t(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
                        const float* st_shift, const ConvShape& s, hipStream_t st,
-                       const float* bias, bool relu, int cfg, int det_rows) {
+                       const float* bias, bool relu, int cfg, int det_rows, void* wflip) {
   ConvGeom g = make_geom(s);
   const uint32_t M = (uint32_t)s.N * s.Ho * s.Wo;
   EpiParams e{};
   e.C = y; e.ldc = s.Co; e.M = M; e.N = s.Co; e.bias = bias; e.act = relu ? 1 : 0;
   e.st_sum = st_sum; e.st_sq = st_sq; e.st_shift = st_shift; e.st_R = g_stat_rows;
   e.det_rows = det_rows;
+  uint32_t nflip = 0;
+  if (wflip != nullptr && dgrad_preflip_ok(s)) {
+    e.fl_w = w; e.fl_wt = wflip;
+    e.fl_Co = s.Co; e.fl_KH = s.KH; e.fl_KW = s.KW; e.fl_Ci = s.Ci;
+    dgrad_flip_plan(s, e.fl);
+    nflip = e.fl.nblk;
+  }
   const bool dense = is_dense(s);
   const bool aligned = s.Ci % BK == 0;
   const T* xp = (const T*)x;
@@ -50,21 +57,23 @@ static void conv_fwd_t(const void* x, const void* w, void* y, float* st_sum, flo
   with_tile<T>(cfg, [&](auto tile) {
     typedef decltype(tile) C;
     const uint32_t tN = cdiv(s.Co, C::BN), tiles = cdiv(M, C::BM) * tN;
-    const dim3 grid(tiles), block(C::THREADS);
+    EpiParams ee = e;
+    ee.fl_tiles = tiles;
+    const dim3 grid(tiles + nflip), block(C::THREADS);
     if (dense)
-      hipLaunchKernelGGL((conv_fwd_kernel<C, true, false, T>), grid, block, 0, st, xp, wp, g, M, tN, e);
+      hipLaunchKernelGGL((conv_fwd_kernel<C, true, false, T>), grid, block, 0, st, xp, wp, g, M, tN, ee);
     else if (aligned)
-      hipLaunchKernelGGL((conv_fwd_kernel<C, false, true, T>), grid, block, 0, st, xp, wp, g, M, tN, e);
+      hipLaunchKernelGGL((conv_fwd_kernel<C, false, true, T>), grid, block, 0, st, xp, wp, g, M, tN, ee);
     else
-      hipLaunchKernelGGL((conv_fwd_kernel<C, false, false, T>), grid, block, 0, st, xp, wp, g, M, tN, e);
+      hipLaunchKernelGGL((conv_fwd_kernel<C, false, false, T>), grid, block, 0, st, xp, wp, g, M, tN, ee);
   });
 }
 
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
               const float* st_shift, const ConvShape& s, hipStream_t st, const float* bias,
-              bool relu, int cfg, int det_rows) {
-  if (s.f32) conv_fwd_t<float>(x, w, y, st_sum, st_sq, st_shift, s, st, bias, relu, cfg, det_rows);
-  else conv_fwd_t<__bf16>(x, w, y, st_sum, st_sq, st_shift, s, st, bias, relu, cfg, det_rows);
+              bool relu, int cfg, int det_rows, void* wflip) {
+  if (s.f32) conv_fwd_t<float>(x, w, y, st_sum, st_sq, st_shift, s, st, bias, relu, cfg, det_rows, wflip);
+  else conv_fwd_t<__bf16>(x, w, y, st_sum, st_sq, st_shift, s, st, bias, relu, cfg, det_rows, wflip);
 }
 
 }  // namespace mipipe

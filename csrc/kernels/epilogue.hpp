@@ -52,7 +52,49 @@ struct EpiParams {
   BnCollect col;
   // workspace split-K finished by the last-arriving split (det_rows path; launchers.hpp)
   WsFinish fin;
+  // conv forward only: blocks >= fl_tiles write the tap-flipped sub-kernels its data-grad will
+  // use (launchers.hpp FlipPlan: conv_dgrad's workspace layout) instead of an output tile
+  const void* fl_w;
+  void* fl_wt;
+  int fl_Co, fl_KH, fl_KW, fl_Ci;
+  uint32_t fl_tiles;
+  FlipPlan fl;
 };
+
+// One 64 x 64 (co x ci) transpose of one tap of one parity class's flipped sub-kernel, riding in
+// a conv forward launch (the work of conv_dgrad.hip's conv_weight_flip_kernel).
+template <class T, int THREADS>
+__device__ void flip_block(const EpiParams& e, uint32_t b, char* smem) {
+  T(*tile)[65] = reinterpret_cast<T(*)[65]>(smem);
+  int c = 0;  // this block's parity class (block-uniform)
+  while (c + 1 < e.fl.ncls && b >= e.fl.cls[c + 1].b0) ++c;
+  const FlipClass& fc = e.fl.cls[c];
+  b -= fc.b0;
+  const int nci = (e.fl_Ci + 63) / 64, nco = (e.fl_Co + 63) / 64;
+  const int bx = (int)(b % (uint32_t)nci), by = (int)((b / (uint32_t)nci) % (uint32_t)nco);
+  const int tap = (int)(b / (uint32_t)(nci * nco));
+  const int a = tap / fc.nkw, bb = tap - a * fc.nkw;
+  const int kh = fc.kh0 + e.fl.S * (fc.nkh - 1 - a), kw = fc.kw0 + e.fl.S * (fc.nkw - 1 - bb);
+  const T* w = reinterpret_cast<const T*>(e.fl_w);
+  T* wt = reinterpret_cast<T*>(e.fl_wt) + fc.off;
+  constexpr int NY = THREADS / 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int ci0 = bx * 64, co0 = by * 64;
+#pragma unroll
+  for (int r = ty; r < 64; r += NY) {
+    const int co = co0 + r, ci = ci0 + tx;
+    tile[r][tx] = (co < e.fl_Co && ci < e.fl_Ci)
+                      ? w[(((long)co * e.fl_KH + kh) * e.fl_KW + kw) * e.fl_Ci + ci]
+                      : T(0.f);
+  }
+  __syncthreads();
+  const long taps = (long)fc.nkh * fc.nkw;
+#pragma unroll
+  for (int r = ty; r < 64; r += NY) {
+    const int ci = ci0 + r, co = co0 + tx;
+    if (co < e.fl_Co && ci < e.fl_Ci) wt[((long)ci * taps + tap) * e.fl_Co + co] = tile[tx][r];
+  }
+}
 
 // The last split of a workspace split-K tile sums the tile's slices (slice order) into the final
 // output.  Release: each split fences its slice stores (agent scope) before taking its ticket;

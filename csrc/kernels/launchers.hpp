@@ -52,9 +52,31 @@ int conv_fwd_stat_rows(const ConvShape& s);
 constexpr int kConvTileConfigs = 14;
 //  det_rows > 0 (deterministic mode): st_sum / st_sq are [det_rows][Co] partial slabs, one row
 //  per M-tile (det_rows = conv_fwd_tiles_m(s, cfg)), written without atomics.
+// wflip (Ci*KH*KW*Co elements, w's dtype): when dgrad_preflip_ok(s), trailing blocks of the
+// launch also write the tap-flipped weight the stride-1 data-grad reads (conv_dgrad's
+// `preflipped`) — no flip kernel in the backward.
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
               const float* st_shift, const ConvShape& s, hipStream_t st,
-              const float* bias = nullptr, bool relu = false, int cfg = -1, int det_rows = 0);
+              const float* bias = nullptr, bool relu = false, int cfg = -1, int det_rows = 0,
+              void* wflip = nullptr);
+// The data-grad of s runs as forward-style parity classes over tap-flipped sub-kernels (see
+// conv_dgrad_fwd_style; stride <= 2), so a forward launch can produce those weights.
+bool dgrad_preflip_ok(const ConvShape& s);
+// The flipped sub-kernels in conv_dgrad's workspace layout: class c holds
+// wt[off + (ci*taps + a*nkw + b)*Co + co] = w[co][kh0 + S(nkh-1-a)][kw0 + S(nkw-1-b)][ci];
+// blocks: one per (64-ci, 64-co, tap), class c's from b0.
+struct FlipClass {
+  int kh0, kw0, nkh, nkw;
+  long off;
+  uint32_t b0;
+};
+struct FlipPlan {
+  FlipClass cls[4];
+  int ncls = 0, S = 1;
+  uint32_t nblk = 0;
+};
+void dgrad_flip_plan(const ConvShape& s, FlipPlan& p);
+int dgrad_fwd_style_mode();  // MIPIPE_DGRAD_FWD (0 off, 1 non-dense, 2 also dense 1x1)
 int conv_fwd_tiles_m(const ConvShape& s, int cfg);
 // Optional dgrad epilogue fusions:
 //  addend: [N*H*W][Ci] (activation dtype) added to dx (the block input's other gradient, e.g. the residual);
@@ -75,8 +97,10 @@ struct DgradFusion {
 // w_flip: a workspace of Co*KH*KW*Ci elements — when given, every stride-parity class with taps
 // runs as a stride-1 FORWARD im2col convolution of dy over its tap-flipped sub-kernel (written
 // into the workspace by this call); allocate it only when conv_dgrad_fwd_style(s, ...) holds
+// preflipped: w_flip already holds the flipped weight (conv_fwd's wflip, dgrad_preflip_ok(s))
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
-                const DgradFusion* fz = nullptr, int cfg = -1, void* w_flip = nullptr);
+                const DgradFusion* fz = nullptr, int cfg = -1, void* w_flip = nullptr,
+                bool preflipped = false);
 bool conv_dgrad_fwd_style(const ConvShape& s, bool dense_too);
 int conv_dgrad_tiles_m(const ConvShape& s, int cfg);  // M-tiles over all stride classes
 // dw is ACCUMULATED into (split-K fp32 atomics, or a plain read-modify-write when unsplit): pass

@@ -159,7 +159,18 @@ class _ConvFn(Function):
     @staticmethod
     def forward(ctx, x, weight, w_c, stride, pad, shift, slabs=None, prev=None, res_take=None,
                 res_give=None):
-        y, psum, psumsq = K.conv_fwd(x, w_c, stride, pad, shift, slabs)
+        # stride-1 k x k convs: the forward launch also writes the tap-flipped weight the
+        # data-grad reads (a persistent buffer per weight; no flip kernel in the backward)
+        wflip = None
+        if (x.requires_grad and K.use_native(x) and isinstance(stride, int)
+                and isinstance(pad, int) and K.dgrad_preflip_ok(x.shape, w_c.shape, stride, pad)):
+            wflip = weight.__dict__.get("_mipipe_wflip")
+            if (wflip is None or wflip.numel() != w_c.numel() or wflip.dtype != w_c.dtype
+                    or wflip.device != w_c.device):
+                wflip = torch.empty(w_c.numel(), dtype=w_c.dtype, device=w_c.device)
+                weight.__dict__["_mipipe_wflip"] = wflip
+        y, psum, psumsq = K.conv_fwd(x, w_c, stride, pad, shift, slabs, wflip=wflip)
+        ctx.wflip = wflip
         ctx.set_materialize_grads(False)  # stats outputs never get gradients: no zero fills
         ctx.save_for_backward(x, w_c)
         ctx.weight = weight
@@ -202,7 +213,8 @@ class _ConvFn(Function):
                     if tok.z is not None:
                         bnr = bnr + (tok.mask if tok.mask is not None else tok.z,)
             bnr2 = (tok.y2, tok.st2.mean, tok.st2.invstd) if bnr is not None and two else None
-            dx = K.conv_dgrad(dy, w_c, x.shape, stride, pad, addend=addend, bnr=bnr, bnr2=bnr2)
+            dx = K.conv_dgrad(dy, w_c, x.shape, stride, pad, addend=addend, bnr=bnr, bnr2=bnr2,
+                              wflip=ctx.wflip)
             if bnr is not None:
                 tok.pre_reduced = True
             if ctx.res_give is not None:

@@ -45,15 +45,19 @@ def _pads(pad):
     return (pad, -1) if isinstance(pad, int) else (int(pad[0]), int(pad[1]))
 
 
-def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None, bias=None, relu=False):
+def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None, bias=None, relu=False,
+             wflip=None):
     """``slabs``: persistent zeroed (sum, sumsq) replica slabs the GPU epilogue accumulates BN
     statistics into (re-zeroed by :func:`bn_finalize`).  ``bias`` / ``relu``: epilogue bias and
-    ReLU for convolutions without BatchNorm (exclusive with the statistics epilogue)."""
+    ReLU for convolutions without BatchNorm (exclusive with the statistics epilogue).
+    ``wflip`` (native, :func:`dgrad_preflip_ok` shapes): extra blocks of the same launch write
+    the tap-flipped weight the data-grad reads — pass it to :func:`conv_dgrad` as ``wflip``."""
     sh, sw = (stride, 0) if isinstance(stride, int) else (stride[0], stride[1])
     ph, pw = _pads(pad)
     if use_native(x):
         s1, s2 = slabs if slabs is not None else (None, None)
-        return native().conv_fwd(x, w, sh, ph, stats_shift, s1, s2, bias, relu, sw, pw)
+        return native().conv_fwd(x, w, sh, ph, stats_shift, s1, s2, bias, relu, sw, pw,
+                                 wflip=wflip)
     y, a, b = _ref.conv_fwd(x, w, stride if isinstance(stride, int) else tuple(stride),
                             pad if isinstance(pad, int) else tuple(pad), stats_shift)
     if bias is not None or relu:
@@ -62,7 +66,14 @@ def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None, bias=None, relu=Fa
     return y, a, b
 
 
-def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None, bnr2=None):
+def dgrad_preflip_ok(x_shape, w_shape, stride, pad) -> bool:
+    """The conv forward can write this conv's flipped data-grad weight (stride 1, k > 1)."""
+    if not (isinstance(stride, int) and isinstance(pad, int)) or not native_available():
+        return False
+    return bool(native().dgrad_preflip_ok(list(x_shape), list(w_shape), stride, pad))
+
+
+def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None, bnr2=None, wflip=None):
     """dx of an NHWC conv.  ``addend``: tensor added to dx in the epilogue (residual gradient).
     ``bnr = (y, mean, invstd, scale, bias, rep[, z])``: the conv input was relu(bn(y)[+res]);
     dx becomes g = dx·[z > 0] (z recomputed from y unless given — as the stored tensor, or as
@@ -72,7 +83,8 @@ def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None, bnr2=None):
     if use_native(dy):
         ph, pw = _pads(pad)
         if bnr is None:
-            return native().conv_dgrad(dy, w, list(x_shape), stride, ph, addend, pad_w=pw)
+            return native().conv_dgrad(dy, w, list(x_shape), stride, ph, addend, pad_w=pw,
+                                       wflip_pre=wflip)
         y, mean, invstd, scale, bias, rep = bnr[:6]
         z = bnr[6] if len(bnr) > 6 else None
         mask = None
@@ -81,7 +93,7 @@ def conv_dgrad(dy, w, x_shape, stride, pad, addend=None, bnr=None, bnr2=None):
         y2, mean2, invstd2 = bnr2 if bnr2 is not None else (None, None, None)
         return native().conv_dgrad(dy, w, list(x_shape), stride, ph, addend, y, mean, invstd,
                                    scale, bias, rep, z, pw, bn_mask=mask, bn_y2=y2,
-                                   bn_mean2=mean2, bn_invstd2=invstd2)
+                                   bn_mean2=mean2, bn_invstd2=invstd2, wflip_pre=wflip)
     if bnr is not None:
         raise RuntimeError("BN-reduce dgrad fusion is a native-kernel path")
     dx = _ref.conv_dgrad(dy, w, x_shape, stride, pad if isinstance(pad, int) else tuple(pad))

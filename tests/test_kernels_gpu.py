@@ -93,6 +93,36 @@ def test_conv_wgrad(case):
     assert rel_err(dw, dwr) < 5e-3
 
 
+@pytest.mark.parametrize("shape", [(8, 28, 28, 64, 64, 3, 1, 1), (4, 14, 14, 256, 512, 3, 1, 1),
+                                   (4, 17, 17, 96, 40, 3, 1, 1), (2, 12, 12, 64, 64, 5, 1, 2),
+                                   (8, 56, 56, 128, 128, 3, 2, 1), (4, 15, 15, 64, 96, 3, 2, 1),
+                                   (2, 20, 20, 64, 64, 5, 2, 2)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_conv_fwd_writes_dgrad_flipped_weight(shape, dt):
+    """conv_fwd(wflip=buf) writes the tap-flipped (per stride-parity class) sub-kernels in extra
+    blocks of the same launch; conv_dgrad(wflip_pre=buf) then skips its flip kernels: y
+    unchanged, dx bit-identical to the self-flipping data-grad, and both against the fp32
+    reference (stride 1 and 2)."""
+    N, H, W, Ci, Co, k, s, p = shape
+    C = native()
+    if not C.dgrad_preflip_ok([N, H, W, Ci], [Co, k, k, Ci], s, p):
+        pytest.skip("not a forward-style stride-1 data-grad shape")
+    x = torch.randn(N, H, W, Ci, device=dev).to(dt)
+    w = (torch.randn(Co, k, k, Ci, device=dev) * 0.05).to(dt)
+    buf = torch.full((w.numel(),), float("nan"), device=dev).to(dt)
+    y0 = C.conv_fwd(x, w, s, p)[0]
+    y1 = C.conv_fwd(x, w, s, p, wflip=buf)[0]
+    assert torch.equal(y0, y1)
+    assert not torch.isnan(buf.float()).any()
+    Ho = (H + 2 * p - k) // s + 1
+    dy = torch.randn(N, Ho, Ho, Co, device=dev).to(dt)
+    dx0 = C.conv_dgrad(dy, w, [N, H, W, Ci], s, p)
+    dx1 = C.conv_dgrad(dy, w, [N, H, W, Ci], s, p, wflip_pre=buf)
+    assert torch.equal(dx0, dx1)
+    dxr = _ref.conv_dgrad(dy.float(), w.float(), (N, H, W, Ci), s, p)
+    assert rel_err(dx1, dxr) < (1e-2 if dt == torch.bfloat16 else 1e-4)
+
+
 @pytest.mark.parametrize("shape", [(32, 14, 14, 256, 1024, 1, 1, 0), (16, 28, 28, 64, 64, 3, 1, 1),
                                    (16, 56, 56, 64, 128, 3, 2, 1)])
 def test_conv_wgrad_workspace_plans(shape):
