@@ -238,6 +238,14 @@ __device__ __forceinline__ uint32_t ld32(uint32_t a) {
   asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(a) : "memory");
   return v;
 }
+__device__ __forceinline__ uint32_t ld16(uint32_t a) {
+  uint32_t v;
+  asm volatile("ds_read_u16 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ void st16(uint32_t a, uint32_t x) {
+  asm volatile("ds_write_b16 %0, %1" ::"v"(a), "v"(x) : "memory");
+}
 __device__ __forceinline__ u32x2 ld64(uint32_t a) {
   u32x2 v;
   asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a) : "memory");
@@ -537,6 +545,57 @@ __device__ __forceinline__ uint32_t img_off(uint32_t k, int j, int grp) {
   return mc_off<64>(k, (uint32_t)(2 * j + (grp >> 1))) + 8 * (grp & 1);
 }
 
+// g of band bb (conv rows 4bb..4bb+3) by SCATTER: every pooled (row, col, channel) of the three
+// staged pooled rows adds its gradient to its argmax pixel, if that pixel is in the band, in the
+// bf16 g image (zeroed before).  Windows of pooled rows / columns of equal parity are disjoint,
+// so four parity phases (barrier between) need no atomics and sum each pixel in a fixed order.
+// ~1/4 of the gather's VALU: one visit per pooled element instead of up to four window tests
+// per conv pixel and channel (but not faster end to end: see stem_bwd_wgrad).
+__device__ __forceinline__ void scatter_band(uint32_t pst, uint32_t img, int bb, int tid) {
+  const int hb = 4 * bb;
+#pragma unroll 1
+  for (int phase = 0; phase < 4; ++phase) {
+    const int pr = phase >> 1, pc = phase & 1;
+    const int count = (pr == 0 ? 2 : 1) * 28 * 16;  // (staged rows) x (cols of parity pc) x quads
+#pragma unroll 1
+    for (int t = tid; t < count; t += 256) {
+      const int ri = t / (28 * 16), rem = t - ri * (28 * 16);
+      const int wo = 2 * (rem >> 4) + pc, cq = rem & 15;
+      const int r3 = pr == 0 ? 2 * ri : 1;  // staged pooled row (pooled row 2bb + r3)
+      const int po = 2 * bb + r3;
+      const uint32_t adp = pst + (uint32_t)(r3 * kDpRow + wo * 128) +
+                           ((uint32_t)((cq >> 1) ^ (((wo >> 1) & 3) << 1)) << 4) + (cq & 1) * 8;
+      const uint32_t aix = pst + (uint32_t)(3 * kDpRow + r3 * kIxRow + wo * 64) +
+                           ((uint32_t)((cq >> 2) ^ ((wo >> 2) & 1)) << 4) + (cq & 3) * 4;
+      const u32x2 d = ld64(adp);
+      const uint32_t x = ld32(aix);
+      wait_lgkm<0>();
+      uint32_t addr[4], old[4];
+      bool ok[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int tap = (int)((x >> (8 * q)) & 0xffu);
+        const int th = (tap * 11) >> 5;  // tap / 3 for tap < 9
+        const int h = 2 * po - 1 + th, w = 2 * wo - 1 + (tap - 3 * th);
+        ok[q] = tap < 9 && h >= hb && h < hb + 4 && w >= 0 && w < kWo;
+        const int ch = 4 * cq + q;
+        const uint32_t k = (uint32_t)((h - hb) * kWo + w);
+        addr[q] = img + img_off(ok[q] ? k : 0u, ch >> 4, (ch >> 2) & 3) + 2 * (ch & 3);
+        old[q] = 0u;
+        if (ok[q]) old[q] = ld16(addr[q]);
+      }
+      wait_lgkm<0>();
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float dv = __uint_as_float((q & 1) ? (d[q >> 1] & 0xffff0000u) : (d[q >> 1] << 16));
+        const float v = __uint_as_float(old[q] << 16) + dv;
+        if (ok[q]) st16(addr[q], (uint32_t)__builtin_bit_cast(unsigned short, f2bf(v)));
+      }
+    }
+    lds_barrier_raw();
+  }
+}
+
 // Per band (4 conv rows of one image, one per wave): y of the wave's row arrives in registers
 // (loaded one band ahead), g is routed from the staged pooled rows, dy = bf16(A·g + B·y + C) goes
 // into an MC image [448 band pixels][64 co]; then dW[co][k] += Σ_px dy[px][co] · X[px][k] over the
@@ -545,6 +604,7 @@ __device__ __forceinline__ uint32_t img_off(uint32_t k, int j, int grp) {
 // tap's pixel address).  Wave w owns k-column blocks w, w+4, w+8, w+12 (< 14) for all 64
 // channels.  Partial dW per block -> workspace slice blockIdx.x (fixed-order sum afterwards).
 constexpr int kImg = 4 * kWo * 128;  // band image: 448 px x 64 co bf16 (57,344 B)
+template <bool SCATTER>  // g by scatter_band (opt-in) or by the per-pixel gather route_row
 __global__ __launch_bounds__(256, 1) void stem_bwd_wgrad_kernel(
     Geo g, PoolGrad pg, const __bf16* __restrict__ y, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma,
@@ -621,8 +681,6 @@ __global__ __launch_bounds__(256, 1) void stem_bwd_wgrad_kernel(
       }
       wait_lgkm<0>();
       const uint32_t k0 = (uint32_t)(wave * kWo + (ln & 15));
-      RouteOffs ro;
-      ro.init(ln);
       auto mkdy = [&](int i, int j, const float (&gq)[4]) {
         const float a4[4] = {__uint_as_float(A[j][0]), __uint_as_float(A[j][1]),
                              __uint_as_float(A[j][2]), __uint_as_float(A[j][3])};
@@ -637,8 +695,33 @@ __global__ __launch_bounds__(256, 1) void stem_bwd_wgrad_kernel(
         for (int q = 0; q < 4; ++q) d[q] = a4[q] * bfr(gq[q]) + b4[q] * yq[q] + c4[q];
         st64(img + img_off(k0 + 16 * i, j, grp), pack2(d[0], d[1]), pack2(d[2], d[3]));
       };
-      if (wave & 1) route_row<true>(lds_u32(pst), ro, wave, ln, mkdy);
-      else route_row<false>(lds_u32(pst), ro, wave, ln, mkdy);
+      if constexpr (SCATTER) {
+#pragma unroll 1
+        for (int c = tid; c < kImg / 16; c += 256) st128(img + 16 * c, u32x4{0u, 0u, 0u, 0u});
+        lds_barrier_raw();
+        scatter_band(lds_u32(pst), img, b % bands_per_img, tid);
+        // dy = A·g + B·y + C in place: each lane rewrites exactly the 8 bytes it reads
+#pragma unroll
+        for (int i = 0; i < kPB; ++i) {
+          u32x2 gv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) gv[j] = ld64(img + img_off(k0 + 16 * i, j, grp));
+          wait_lgkm<0>();
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float gq[4] = {__uint_as_float(gv[j][0] << 16),
+                                 __uint_as_float(gv[j][0] & 0xffff0000u),
+                                 __uint_as_float(gv[j][1] << 16),
+                                 __uint_as_float(gv[j][1] & 0xffff0000u)};
+            mkdy(i, j, gq);
+          }
+        }
+      } else {
+        RouteOffs ro;
+        ro.init(ln);
+        if (wave & 1) route_row<true>(lds_u32(pst), ro, wave, ln, mkdy);
+        else route_row<false>(lds_u32(pst), ro, wave, ln, mkdy);
+      }
     }
     lds_barrier_raw();  // the band's dy image is complete; every wave is done with the pooled rows
     if (nxt < nb) stage_pooled(pst, pg, nxt / bands_per_img, nxt % bands_per_img, wave, ln);
@@ -757,9 +840,22 @@ void stem_bwd_wgrad(const void* xp, const void* y, int N, int Ho, int Hp, const 
                     hipStream_t st) {
   stem::PoolGrad pg{(const __bf16*)dp, idx, Ho / 2};
   const int G = stem_wgrad_blocks(N, Ho);
-  hipLaunchKernelGGL(stem::stem_bwd_wgrad_kernel, dim3(G), dim3(256), 0, st,
-                     stem_geo(xp, nullptr, N, Ho, Hp), pg, (const __bf16*)y, mean, invstd, gamma,
-                     sum_g, sum_gx, 1.f / (float)count, ws);
+  // MIPIPE_STEM_SCATTER=1: g by scatter_band.  Measured equal to the gather (ResNet-50 step
+  // 20.949 vs 20.942 ms, same box, alternating; profiles/r4_stem_scatter_ab.txt): a quarter of
+  // the routing VALU, but five more barriers and dependent LDS round trips per band at one wave
+  // per SIMD.  Off by default.
+  static const bool scatter = [] {
+    const char* v = getenv("MIPIPE_STEM_SCATTER");
+    return v != nullptr && atoi(v) != 0;
+  }();
+  if (scatter)
+    hipLaunchKernelGGL(stem::stem_bwd_wgrad_kernel<true>, dim3(G), dim3(256), 0, st,
+                       stem_geo(xp, nullptr, N, Ho, Hp), pg, (const __bf16*)y, mean, invstd, gamma,
+                       sum_g, sum_gx, 1.f / (float)count, ws);
+  else
+    hipLaunchKernelGGL(stem::stem_bwd_wgrad_kernel<false>, dim3(G), dim3(256), 0, st,
+                       stem_geo(xp, nullptr, N, Ho, Hp), pg, (const __bf16*)y, mean, invstd, gamma,
+                       sum_g, sum_gx, 1.f / (float)count, ws);
   splitk_sum(ws, G, (long)stem::kCo * 224, dw, st);
 }
 
