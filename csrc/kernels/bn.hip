@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y
                                                          const float* __restrict__ rbias,
                                                          T* __restrict__ z, long M, int C,
                                                          bool relu,
-                                                         uint8_t* __restrict__ mask) {
+                                                         uint8_t* __restrict__ mask, bool nt) {
   const RowMap mp = row_map(C);
   const int t = threadIdx.x;
   const int rg = t / mp.tpr;
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y
         for (int q = 0; q < 8; ++q) bits |= (as_stored<T>(v[q]) > 0.f ? 1u : 0u) << q;
         mask[row * (C / 8) + cg] = (uint8_t)bits;
       }
-      store8(z + off, v);
+      store8(z + off, v, nt);
     }
   }
 }
@@ -201,15 +201,16 @@ static void bn_act_fwd_t(const void* y, const float* scale, const float* bias, c
                          bool relu, hipStream_t st, uint8_t* mask) {
   RowMap mp = row_map(C);
   int grid = grid_for_tiles(M, mp.rpb);
+  const bool nt = (g_nt_store & 4) != 0;
   const T* yp = (const T*)y;
   const T* rp = (const T*)r;
   T* zp = (T*)z;
   if (r == nullptr)
-    hipLaunchKernelGGL((bn_act_fwd_kernel<0, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<0, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt);
   else if (rscale == nullptr)
-    hipLaunchKernelGGL((bn_act_fwd_kernel<1, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<1, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt);
   else
-    hipLaunchKernelGGL((bn_act_fwd_kernel<2, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<2, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt);
 }
 
 void bn_act_fwd(const void* y, const float* scale, const float* bias, const void* r,
@@ -414,7 +415,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ sum_gx, const T* __restrict__ y2,
     const float* __restrict__ mean2, const float* __restrict__ invstd2,
     const float* __restrict__ gamma2, const float* __restrict__ sum_gx2, float inv_n, bool relu,
-    T* __restrict__ dy, T* __restrict__ dother, long M, int C) {
+    T* __restrict__ dy, T* __restrict__ dother, long M, int C, bool nt) {
   const RowMap mp = row_map(C);
   const int t = threadIdx.x;
   const int rg = t / mp.tpr;
@@ -466,15 +467,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       unpack_raw(ry[u], yv);
 #pragma unroll
       for (int q = 0; q < 8; ++q) o[q] = A[q] * g[q] + Bc[q] * yv[q] + Cc[q];
-      store8(dy + off, o);
+      store8(dy + off, o, nt);
       if (MODE == 1) {
-        store8(dother + off, g);
+        store8(dother + off, g, nt);
       } else if (MODE == 2) {
         float y2v[8];
         unpack_raw(ry2[u], y2v);
 #pragma unroll
         for (int q = 0; q < 8; ++q) o[q] = A2[q] * g[q] + B2[q] * y2v[q] + C2[q];
-        store8(dother + off, o);
+        store8(dother + off, o, nt);
       }
     }
   }
@@ -487,6 +488,7 @@ void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float*
                       bool relu, bool want_dres, void* dy, void* dother, long M, int C,
                       hipStream_t st, bool f32) {
   RowMap mp = row_map(C);
+  const bool nt = (g_nt_store & 4) != 0;
   int grid = grid_for_tiles(M, mp.rpb);
   float inv_n = 1.f / (float)count;
   auto launch = [&](auto tag) {
@@ -494,11 +496,11 @@ void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float*
       const T *dzp = (const T*)dz, *zp = (const T*)z, *yp = (const T*)y, *y2p = (const T*)y2;
     T *dyp = (T*)dy, *dop = (T*)dother;
     if (y2 != nullptr)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<2, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<2, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt);
     else if (want_dres)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt);
     else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<0, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<0, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt);
   };
   if (f32) launch(float{});
   else launch(__bf16{});

@@ -73,6 +73,15 @@ __device__ __forceinline__ void store8(float* p, const float* f) {
   reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
   reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
 }
+// store8 with an optional non-temporal (streaming) hint: activations written once and read by a
+// later kernel, larger than the caches (g_nt_store)
+typedef __attribute__((ext_vector_type(4))) unsigned int u32v4;
+__device__ __forceinline__ void store8(__bf16* p, const float* f, bool nt) {
+  const uint4 v = pack8(f);
+  if (nt) __builtin_nontemporal_store(u32v4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32v4*>(p));
+  else *reinterpret_cast<uint4*>(p) = v;
+}
+__device__ __forceinline__ void store8(float* p, const float* f, bool) { store8(p, f); }
 // 8 raw elements of T held in registers (prefetched before they are needed).
 template <class T>
 struct Raw8 {

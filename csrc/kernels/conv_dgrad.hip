@@ -162,6 +162,7 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
   for_each_class(s, [&](const DgradClass& c, uint32_t M) {
       EpiParams e{};
       e.C = dx; e.ldc = s.Ci; e.M = M; e.N = s.Ci;
+      e.nt = (g_nt_store >> 1) & 1;
       if (fz != nullptr) {
         e.addend = fz->addend;
         e.bnr_y = fz->bn_y;

@@ -52,6 +52,8 @@ struct EpiParams {
   BnCollect col;
   // workspace split-K finished by the last-arriving split (det_rows path; launchers.hpp)
   WsFinish fin;
+  // non-temporal (streaming) stores of the output tile (plain epilogue store loop only)
+  int nt;
   // conv forward only: blocks >= fl_tiles write the tap-flipped sub-kernels its data-grad will
   // use (launchers.hpp FlipPlan: conv_dgrad's workspace layout) instead of an output tile
   const void* fl_w;
@@ -529,7 +531,7 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
           for (int q = 0; q < 8; ++q) sgx2[q] += w * f[q] * (y2v[q] - b_mu2[q]) * b_is2[q];
         }
       }
-      if (ok) store8(C + out_row(e, m) * e.ldc + n, f);
+      if (ok) store8(C + out_row(e, m) * e.ldc + n, f, e.nt != 0);
       if (it + PF < ITER) ops.issue(e, m0, n0, it + PF, it % PF);
     }
   } else {
@@ -541,9 +543,15 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
       if (m < e.M && n < e.N) {
         const long orow = out_row(e, m);
 #pragma unroll
-        for (int h = 0; h < (int)(sizeof(T) / 2); ++h)
-          reinterpret_cast<uint4*>(C + orow * e.ldc + n)[h] =
-              *reinterpret_cast<const uint4*>(smem + r * P + cc * 8 * sizeof(T) + 16 * h);
+        for (int h = 0; h < (int)(sizeof(T) / 2); ++h) {
+          const uint4 v = *reinterpret_cast<const uint4*>(smem + r * P + cc * 8 * sizeof(T) + 16 * h);
+          uint4* dst = reinterpret_cast<uint4*>(C + orow * e.ldc + n) + h;
+          if (e.nt) {  // streaming output (g_nt_store)
+            __builtin_nontemporal_store(u32v4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32v4*>(dst));
+          } else {
+            *dst = v;
+          }
+        }
       }
     }
   }

@@ -390,5 +390,6 @@ void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float
                 hipStream_t st);
 int colsum_blocks(long rows, int cols);
 extern int g_colsum_row_blocks;
+extern int g_nt_store;  // non-temporal activation stores: 1 conv fwd, 2 dgrad, 4 BN passes
 
 }  // namespace mipipe
