@@ -201,7 +201,7 @@ static void bn_act_fwd_t(const void* y, const float* scale, const float* bias, c
                          bool relu, hipStream_t st, uint8_t* mask) {
   RowMap mp = row_map(C);
   int grid = grid_for_tiles(M, mp.rpb);
-  const bool nt = (g_nt_store & 4) != 0;
+  const bool nt = (g_nt_store & 4) != 0;  // BN forward apply
   const T* yp = (const T*)y;
   const T* rp = (const T*)r;
   T* zp = (T*)z;
@@ -488,7 +488,7 @@ void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float*
                       bool relu, bool want_dres, void* dy, void* dother, long M, int C,
                       hipStream_t st, bool f32) {
   RowMap mp = row_map(C);
-  const bool nt = (g_nt_store & 4) != 0;
+  const bool nt = (g_nt_store & 8) != 0;  // BN backward apply
   int grid = grid_for_tiles(M, mp.rpb);
   float inv_n = 1.f / (float)count;
   auto launch = [&](auto tag) {

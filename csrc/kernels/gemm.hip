@@ -16,7 +16,8 @@ int g_splitk_target = 512;
 int g_ns1_max_k_gather = 1152;  // measured: tools/sweep_ns1_gather.py (profiles/r1_ns1_gather_sweep.jsonl)
 int g_stat_rows = kStatReplicas;
 // Non-temporal (streaming) stores of large activation outputs, a bit mask: 1 conv forward,
-// 2 conv data-grad, 4 BN apply passes (MIPIPE_NT_STORE overrides; A/B in profiles/r4_nt_store_ab.txt)
+// 2 conv data-grad, 4 BN forward apply, 8 BN backward apply, 16 the stem's stored conv output
+// (MIPIPE_NT_STORE overrides; A/B in profiles/r4_nt_store_ab.txt)
 int g_nt_store = [] {
   const char* v = getenv("MIPIPE_NT_STORE");
   return v != nullptr ? atoi(v) : 3;  // conv forward + data-grad (measured)

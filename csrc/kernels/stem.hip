@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256, 1) void stem_pool_kernel(Geo g, const float* _
                                                             const float* __restrict__ bias,
                                                             __bf16* __restrict__ out,
                                                             uint8_t* __restrict__ idx,
-                                                            __bf16* __restrict__ yout) {
+                                                            __bf16* __restrict__ yout, bool nt) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kPatchB + kWB + 5 * kKeyRow];
   char* wl = smem + 2 * kPatchB;
   char* ring = wl + kWB;
@@ -339,8 +339,13 @@ __global__ __launch_bounds__(256, 1) void stem_pool_kernel(Geo g, const float* _
       for (int i = 0; i < kPB; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          *reinterpret_cast<uint2*>(yr + 16 * i * kCo + 16 * j) =
-              make_uint2(pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3]));
+        {
+          typedef __attribute__((ext_vector_type(2))) unsigned int u32v2;
+          const u32v2 v = {pack2(acc[i][j][0], acc[i][j][1]), pack2(acc[i][j][2], acc[i][j][3])};
+          // y is read only by the backward: streaming stores when g_nt_store & 16
+          if (nt) __builtin_nontemporal_store(v, reinterpret_cast<u32v2*>(yr + 16 * i * kCo + 16 * j));
+          else *reinterpret_cast<u32v2*>(yr + 16 * i * kCo + 16 * j) = v;
+        }
     }
     // even lanes m hold output column wo = 8i + m/2 after the horizontal max
     const uint32_t kb = lds_u32(ring + (row % 5) * kKeyRow) + (m >> 1) * kKeyPix + 16 * grp;
@@ -829,7 +834,7 @@ void stem_fwd_stats(const void* xp, const void* w, int N, int Ho, int Hp, const 
 void stem_fwd_pool(const void* xp, const void* w, int N, int Ho, int Hp, const float* scale,
                    const float* bias, void* out, uint8_t* idx, void* y, hipStream_t st) {
   hipLaunchKernelGGL(stem::stem_pool_kernel, dim3(N), dim3(256), 0, st, stem_geo(xp, w, N, Ho, Hp),
-                     scale, bias, (__bf16*)out, idx, (__bf16*)y);
+                     scale, bias, (__bf16*)out, idx, (__bf16*)y, (g_nt_store & 16) != 0);
 }
 
 int stem_wgrad_blocks(int N, int Ho) { return std::min(N * (Ho / stem::kRB), 256); }
