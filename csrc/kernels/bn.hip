@@ -134,7 +134,8 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y
                                                          const float* __restrict__ rbias,
                                                          T* __restrict__ z, long M, int C,
                                                          bool relu,
-                                                         uint8_t* __restrict__ mask, bool nt) {
+                                                         uint8_t* __restrict__ mask, bool nt,
+                                                         bool ntl) {
   const RowMap mp = row_map(C);
   const int t = threadIdx.x;
   const int rg = t / mp.tpr;
@@ -148,8 +149,8 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y
 #pragma unroll
     for (int u = 0; u < kApplyU; ++u) {
       const long off = min(row0 + (long)u * mp.rpb, M - 1) * C + c0;
-      ry[u] = ld_raw8(y + off);
-      if (RES != 0) rr[u] = ld_raw8(r + off);
+      ry[u] = ld_raw8(y + off, ntl);
+      if (RES != 0) rr[u] = ld_raw8(r + off, ntl);
     }
     float sc[8], bi[8], rs[8], rb[8];
 #pragma unroll
@@ -202,15 +203,16 @@ static void bn_act_fwd_t(const void* y, const float* scale, const float* bias, c
   RowMap mp = row_map(C);
   int grid = grid_for_tiles(M, mp.rpb);
   const bool nt = (g_nt_store & 4) != 0;  // BN forward apply
+  const bool ntl = (g_nt_store & 32) != 0;  // its loads streaming
   const T* yp = (const T*)y;
   const T* rp = (const T*)r;
   T* zp = (T*)z;
   if (r == nullptr)
-    hipLaunchKernelGGL((bn_act_fwd_kernel<0, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<0, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
   else if (rscale == nullptr)
-    hipLaunchKernelGGL((bn_act_fwd_kernel<1, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<1, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
   else
-    hipLaunchKernelGGL((bn_act_fwd_kernel<2, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<2, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
 }
 
 void bn_act_fwd(const void* y, const float* scale, const float* bias, const void* r,
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ sum_gx, const T* __restrict__ y2,
     const float* __restrict__ mean2, const float* __restrict__ invstd2,
     const float* __restrict__ gamma2, const float* __restrict__ sum_gx2, float inv_n, bool relu,
-    T* __restrict__ dy, T* __restrict__ dother, long M, int C, bool nt) {
+    T* __restrict__ dy, T* __restrict__ dother, long M, int C, bool nt, bool ntl) {
   const RowMap mp = row_map(C);
   const int t = threadIdx.x;
   const int rg = t / mp.tpr;
@@ -429,10 +431,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 #pragma unroll
     for (int u = 0; u < kApplyU; ++u) {
       const long off = min(row0 + (long)u * mp.rpb, M - 1) * C + c0;
-      rgv[u] = ld_raw8(dz + off);
-      if (relu) rz[u] = ld_raw8(z + off);
-      ry[u] = ld_raw8(y + off);
-      if (MODE == 2) ry2[u] = ld_raw8(y2 + off);
+      rgv[u] = ld_raw8(dz + off, ntl);
+      if (relu) rz[u] = ld_raw8(z + off, ntl);
+      ry[u] = ld_raw8(y + off, ntl);
+      if (MODE == 2) ry2[u] = ld_raw8(y2 + off, ntl);
     }
     // dy = A*g + B*y + Cc   with A = γ·is, B = -A·is·k2, Cc = -A·k1 + A·is·k2·μ
     float A[8], Bc[8], Cc[8], A2[8], B2[8], C2[8];
@@ -489,6 +491,7 @@ void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float*
                       hipStream_t st, bool f32) {
   RowMap mp = row_map(C);
   const bool nt = (g_nt_store & 8) != 0;  // BN backward apply
+  const bool ntl = (g_nt_store & 64) != 0;  // its loads streaming
   int grid = grid_for_tiles(M, mp.rpb);
   float inv_n = 1.f / (float)count;
   auto launch = [&](auto tag) {
@@ -496,11 +499,11 @@ void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float*
       const T *dzp = (const T*)dz, *zp = (const T*)z, *yp = (const T*)y, *y2p = (const T*)y2;
     T *dyp = (T*)dy, *dop = (T*)dother;
     if (y2 != nullptr)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<2, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<2, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
     else if (want_dres)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
     else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<0, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<0, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
   };
   if (f32) launch(float{});
   else launch(__bf16{});

@@ -94,6 +94,19 @@ __device__ __forceinline__ Raw8<T> ld_raw8(const T* p) {
   for (int i = 0; i < (int)(sizeof(T) / 2); ++i) r.v[i] = reinterpret_cast<const uint4*>(p)[i];
   return r;
 }
+// ld_raw8 with an optional non-temporal (streaming) hint
+template <class T>
+__device__ __forceinline__ Raw8<T> ld_raw8(const T* p, bool nt) {
+  if (!nt) return ld_raw8(p);
+  typedef __attribute__((ext_vector_type(4))) unsigned int u4;
+  Raw8<T> r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 2); ++i) {
+    const u4 v = __builtin_nontemporal_load(reinterpret_cast<const u4*>(p) + i);
+    r.v[i] = make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return r;
+}
 __device__ __forceinline__ void unpack_raw(const Raw8<__bf16>& r, float* f) { unpack8(r.v[0], f); }
 __device__ __forceinline__ void unpack_raw(const Raw8<float>& r, float* f) {
 #pragma unroll

@@ -16,11 +16,12 @@ int g_splitk_target = 512;
 int g_ns1_max_k_gather = 1152;  // measured: tools/sweep_ns1_gather.py (profiles/r1_ns1_gather_sweep.jsonl)
 int g_stat_rows = kStatReplicas;
 // Non-temporal (streaming) stores of large activation outputs, a bit mask: 1 conv forward,
-// 2 conv data-grad, 4 BN forward apply, 8 BN backward apply, 16 the stem's stored conv output
+// 2 conv data-grad, 4 BN forward apply, 8 BN backward apply, 16 the stem's stored conv output,
+// 32 / 64 streaming LOADS in the BN forward / backward apply, 128 Linear (GEMM) outputs
 // (MIPIPE_NT_STORE overrides; A/B in profiles/r4_nt_store_ab.txt)
 int g_nt_store = [] {
   const char* v = getenv("MIPIPE_NT_STORE");
-  return v != nullptr ? atoi(v) : 3;  // conv forward + data-grad (measured)
+  return v != nullptr ? atoi(v) : 99;  // conv fwd + dgrad stores, BN-pass loads (measured)
 }();
 int g_ns1_max_k = 512;  // measured: tools/sweep_ns1.py (profiles/r1_ns1_sweep.jsonl)
 namespace gk {
@@ -161,6 +162,7 @@ void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc
           bool f32, int cfg, int splits, const void* addend, bool ws_split, const WsFinish* fin) {
   EpiParams e{};
   e.C = C; e.ldc = ldc; e.M = (uint32_t)M; e.N = (uint32_t)N; e.bias = bias; e.act = act;
+  e.nt = (g_nt_store >> 7) & 1;
   if (addend != nullptr && out == 0 && a_kc && !b_kc) {
     e.addend = addend;
     out = 3;
