@@ -163,6 +163,7 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
       EpiParams e{};
       e.C = dx; e.ldc = s.Ci; e.M = M; e.N = s.Ci;
       e.nt = (g_nt_store >> 1) & 1;
+      e.ntl = (g_nt_store >> 8) & 1;
       if (fz != nullptr) {
         e.addend = fz->addend;
         e.bnr_y = fz->bn_y;

@@ -52,8 +52,9 @@ struct EpiParams {
   BnCollect col;
   // workspace split-K finished by the last-arriving split (det_rows path; launchers.hpp)
   WsFinish fin;
-  // non-temporal (streaming) stores of the output tile (plain epilogue store loop only)
-  int nt;
+  // non-temporal (streaming) stores of the output tile; streaming loads of the fused
+  // data-grad epilogue's operand ring (addend / y / z)
+  int nt, ntl;
   // conv forward only: blocks >= fl_tiles write the tap-flipped sub-kernels its data-grad will
   // use (launchers.hpp FlipPlan: conv_dgrad's workspace layout) instead of an output tile
   const void* fl_w;
@@ -293,10 +294,11 @@ struct EpiOps {
     const uint32_t m = min(m0 + r, e.M - 1);
     const long orow = out_row(e, m);
     const long off = orow * e.ldc + ld_n;  // one element offset shared by every present stream
-    ad[slot] = ld_raw8(p_ad + (h_ad ? off : 0));
-    y[slot] = ld_raw8(p_y + (h_y ? off : 0));
-    z[slot] = ld_raw8(p_z + (h_z ? off : 0));
-    if constexpr (TWO) y2[slot] = ld_raw8(p_y2 + (h_y2 ? off : 0));
+    const bool ntl = e.ntl != 0;  // streaming operand loads (g_nt_store & 256)
+    ad[slot] = ld_raw8(p_ad + (h_ad ? off : 0), ntl);
+    y[slot] = ld_raw8(p_y + (h_y ? off : 0), ntl);
+    z[slot] = ld_raw8(p_z + (h_z ? off : 0), ntl);
+    if constexpr (TWO) y2[slot] = ld_raw8(p_y2 + (h_y2 ? off : 0), ntl);
     mk[slot] = p_mk[h_mk ? off / 8 : 0];  // ldc % 8 == 0: the mask byte of columns ld_n..+7
   }
   __device__ __forceinline__ void prime(const EpiParams& e, uint32_t m0, uint32_t n0) {

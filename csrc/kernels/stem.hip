@@ -614,7 +614,7 @@ __global__ __launch_bounds__(256, 1) void stem_bwd_wgrad_kernel(
     Geo g, PoolGrad pg, const __bf16* __restrict__ y, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma,
     const float* __restrict__ sum_g, const float* __restrict__ sum_gx, float inv_n,
-    float* __restrict__ ws) {
+    float* __restrict__ ws, bool nty) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kPatchB + kPoolStage + kImg + 3 * kCo * 4];
   char* pst = smem + 2 * kPatchB;
   char* gim = pst + kPoolStage;
@@ -644,7 +644,8 @@ __global__ __launch_bounds__(256, 1) void stem_bwd_wgrad_kernel(
     for (int i = 0; i < kPB; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        yv[i][j] = *reinterpret_cast<const u32x2*>(yr + 16 * i * kCo + 16 * j);
+        yv[i][j] = nty ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(yr + 16 * i * kCo + 16 * j))
+                       : *reinterpret_cast<const u32x2*>(yr + 16 * i * kCo + 16 * j);
   };
   __syncthreads();
   int b = blockIdx.x;
@@ -856,11 +857,11 @@ void stem_bwd_wgrad(const void* xp, const void* y, int N, int Ho, int Hp, const 
   if (scatter)
     hipLaunchKernelGGL(stem::stem_bwd_wgrad_kernel<true>, dim3(G), dim3(256), 0, st,
                        stem_geo(xp, nullptr, N, Ho, Hp), pg, (const __bf16*)y, mean, invstd, gamma,
-                       sum_g, sum_gx, 1.f / (float)count, ws);
+                       sum_g, sum_gx, 1.f / (float)count, ws, (g_nt_store & 512) != 0);
   else
     hipLaunchKernelGGL(stem::stem_bwd_wgrad_kernel<false>, dim3(G), dim3(256), 0, st,
                        stem_geo(xp, nullptr, N, Ho, Hp), pg, (const __bf16*)y, mean, invstd, gamma,
-                       sum_g, sum_gx, 1.f / (float)count, ws);
+                       sum_g, sum_gx, 1.f / (float)count, ws, (g_nt_store & 512) != 0);
   splitk_sum(ws, G, (long)stem::kCo * 224, dw, st);
 }
 
