@@ -18,11 +18,12 @@ int g_stat_rows = kStatReplicas;
 // Non-temporal (streaming) stores of large activation outputs, a bit mask: 1 conv forward,
 // 2 conv data-grad, 4 BN forward apply, 8 BN backward apply, 16 the stem's stored conv output,
 // 32 / 64 streaming LOADS in the BN forward / backward apply, 128 Linear (GEMM) outputs,
-// 256 streaming loads of the fused data-grad epilogue operands, 512 the stem backward's y
+// 256 streaming loads of the fused data-grad epilogue operands, 512 the stem backward's y,
+// 1024 streaming fp32 state in AdamW
 // (MIPIPE_NT_STORE overrides; A/B in profiles/r4_nt_store_ab.txt)
 int g_nt_store = [] {
   const char* v = getenv("MIPIPE_NT_STORE");
-  return v != nullptr ? atoi(v) : 355;  // conv fwd/dgrad stores, BN-pass + dgrad-epi loads
+  return v != nullptr ? atoi(v) : 1379;  // conv stores, BN-pass + dgrad-epi loads, AdamW state
 }();
 int g_ns1_max_k = 512;  // measured: tools/sweep_ns1.py (profiles/r1_ns1_sweep.jsonl)
 namespace gk {

@@ -290,6 +290,29 @@ void grad_unpack_bf16(const void* wire, float* g, long n, hipStream_t st) {
                      (const uint4*)wire, g, n8);
 }
 
+// NT: streaming (non-temporal) loads / stores of the fp32 state (p, g, m, v: 16 B per parameter
+// each, touched once per step); the bf16 shadow the next forward reads stays cached
+template <bool NT>
+__device__ __forceinline__ float4 ldf4(const float* p, long i) {
+  if constexpr (NT) {
+    typedef __attribute__((ext_vector_type(4))) float f4;
+    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p) + i);
+    return make_float4(v.x, v.y, v.z, v.w);
+  } else {
+    return reinterpret_cast<const float4*>(p)[i];
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void stf4(float* p, long i, float a, float b, float c, float d) {
+  if constexpr (NT) {
+    typedef __attribute__((ext_vector_type(4))) float f4;
+    __builtin_nontemporal_store(f4{a, b, c, d}, reinterpret_cast<f4*>(p) + i);
+  } else {
+    reinterpret_cast<float4*>(p)[i] = make_float4(a, b, c, d);
+  }
+}
+
+template <bool NT>
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     __bf16* __restrict__ sh, long n4, float lr,
@@ -304,10 +327,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   const float rbc2 = rsqrtf(bc2);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long)gridDim.x * blockDim.x) {
-    float4 pv = reinterpret_cast<float4*>(p)[i];
-    float4 gv = reinterpret_cast<const float4*>(g)[i];
-    float4 mv = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float4 pv = ldf4<NT>(p, i);
+    float4 gv = ldf4<NT>(g, i);
+    float4 mv = ldf4<NT>(m, i);
+    float4 vv = ldf4<NT>(v, i);
     float pa[4] = {pv.x, pv.y, pv.z, pv.w}, ga[4] = {gv.x, gv.y, gv.z, gv.w};
     float ma[4] = {mv.x, mv.y, mv.z, mv.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
@@ -319,9 +342,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
       float denom = sqrtf(va[q]) * rbc2 + eps;
       pa[q] -= (lr / bc1) * ma[q] / denom;
     }
-    reinterpret_cast<float4*>(p)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
-    reinterpret_cast<float4*>(m)[i] = make_float4(ma[0], ma[1], ma[2], ma[3]);
-    reinterpret_cast<float4*>(v)[i] = make_float4(va[0], va[1], va[2], va[3]);
+    stf4<NT>(p, i, pa[0], pa[1], pa[2], pa[3]);
+    stf4<NT>(m, i, ma[0], ma[1], ma[2], ma[3]);
+    stf4<NT>(v, i, va[0], va[1], va[2], va[3]);
     if (sh != nullptr)
       reinterpret_cast<uint2*>(sh)[i] = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));
   }
@@ -337,8 +360,12 @@ void adamw_step(float* p, const float* g, float* m, float* v, void* shadow, long
     const char* e = getenv("MIPIPE_ADAMW_BLOCKS");
     return e == nullptr ? 32768 : atoi(e);
   }();
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid1d(n4, 1, cap)), dim3(256), 0, st, p, g, m, v,
-                     (__bf16*)shadow, n4, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, t_dev);
+  if (g_nt_store & 1024)
+    hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid1d(n4, 1, cap)), dim3(256), 0, st, p, g, m, v,
+                       (__bf16*)shadow, n4, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, t_dev);
+  else
+    hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid1d(n4, 1, cap)), dim3(256), 0, st, p, g, m, v,
+                       (__bf16*)shadow, n4, lr, b1, b2, eps, wd, bc1, bc2, grad_scale, t_dev);
 }
 
 // ------------------------------------------------------------------------------ layout / data
