@@ -1092,6 +1092,41 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
   return out;
 }
 
+// GELU Linear forward in one GEMM: (y = gelu(A B^T + bias), h = A B^T + bias), bf16, A [M][K],
+// B [N][K] (the nn.Linear layout).  The plan comes from the plain bf16 GEMM's table entry of the
+// same shape (same main loop), timed with the GELU epilogue when missing.
+std::tuple<Tensor, Tensor> gemm_gelu(Tensor a, Tensor b, optional<Tensor> bias, int64_t plan) {
+  check_bf16(a, "A");
+  check_same(b, a, "B");
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_gelu shapes");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous(), "gemm_gelu operands must be contiguous");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(N % 8 == 0 && K % 8 == 0 && M < (1ll << 31), "gemm_gelu needs N, K % 8 == 0");
+  const float* bias_p = nullptr;
+  if (bias.has_value()) {
+    check_vec(*bias, N, "bias");
+    bias_p = bias->data_ptr<float>();
+  }
+  auto y = torch::empty({M, N}, a.options()), h = torch::empty({M, N}, a.options());
+  auto launch = [&](void* yo, void* ho, int p) {
+    if (p >= 0) p &= ~tune::kPlanWs;  // a workspace plan of the plain GEMM: its tile
+    if (p >= 4096) p = -1;
+    const int cfg = p < 0 ? -1 : p % tune::kPlanSplit;
+    mipipe::gemm(a.data_ptr(), K, true, b.data_ptr(), K, true, yo, N, (int)M, (int)N, (int)K,
+                 bias_p, 2, 0, stream(), false, cfg, -1, nullptr, false, nullptr, ho);
+  };
+  if (plan < 0) {
+    plan = tune::select_from(tune::gemm_key(M, N, K, true, true, 0, false),
+                             tune::gemm_candidates(false, false), [&](int p) {
+                               auto ys = torch::empty_like(y), hs = torch::empty_like(h);
+                               launch(ys.data_ptr(), hs.data_ptr(), p);
+                             });
+  }
+  launch(y.data_ptr(), h.data_ptr(), (int)plan);
+  return {y, h};
+}
+
 // ------------------------------------------------------------------------------- loss / optim
 std::tuple<Tensor, Tensor> cross_entropy_fwd_bwd(Tensor logits, Tensor labels, double smoothing,
                                                  int64_t ignore_index, int64_t valid_cols) {
@@ -1764,6 +1799,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_force_tune", [](bool on) { tune::g_force_tune = on; });
   m.def("set_wgrad3x3", [](bool on) { mipipe::g_wgrad3x3 = on; });
   m.def("get_wgrad3x3", []() { return mipipe::g_wgrad3x3; });
+  m.def("set_nt_store", [](int mask) { mipipe::g_nt_store = mask; });
+  m.def("get_nt_store", []() { return mipipe::g_nt_store; });
   m.def("set_ws_finish", [](bool on) { g_ws_finish = on; });
   m.def("get_ws_finish", []() { return g_ws_finish; });
   m.def("set_deterministic", [](bool on) { mipipe::g_deterministic = on ? 1 : 0; });
@@ -1837,6 +1874,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("synthetic_batch", &synthetic_batch);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
+  m.def("gemm_gelu", &gemm_gelu, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(),
+        py::arg("plan") = -1);
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum, py::arg("dy"), py::arg("x"), py::arg("bias"));
   m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("res") = py::none(), py::arg("drop_p") = 0.0,

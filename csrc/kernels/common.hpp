@@ -73,6 +73,10 @@ __device__ __forceinline__ void store8(float* p, const float* f) {
   reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
   reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
 }
+// GELU (erf form, BERT's) of one value: the gelu_fwd kernel's and the GEMM epilogue's formula
+__device__ __forceinline__ float gelu_erf(float v) {
+  return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+}
 // store8 with an optional non-temporal (streaming) hint: activations written once and read by a
 // later kernel, larger than the caches (g_nt_store)
 typedef __attribute__((ext_vector_type(4))) unsigned int u32v4;

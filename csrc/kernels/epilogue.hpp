@@ -55,6 +55,8 @@ struct EpiParams {
   // non-temporal (streaming) stores of the output tile; streaming loads of the fused
   // data-grad epilogue's operand ring (addend / y / z)
   int nt, ntl;
+  // act == 2 (GELU, plain bf16 store loop): the pre-activation goes to aux, GELU of it to C
+  void* aux;
   // conv forward only: blocks >= fl_tiles write the tap-flipped sub-kernels its data-grad will
   // use (launchers.hpp FlipPlan: conv_dgrad's workspace layout) instead of an output tile
   const void* fl_w;
@@ -546,8 +548,19 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
         const long orow = out_row(e, m);
 #pragma unroll
         for (int h = 0; h < (int)(sizeof(T) / 2); ++h) {
-          const uint4 v = *reinterpret_cast<const uint4*>(smem + r * P + cc * 8 * sizeof(T) + 16 * h);
+          uint4 v = *reinterpret_cast<const uint4*>(smem + r * P + cc * 8 * sizeof(T) + 16 * h);
           uint4* dst = reinterpret_cast<uint4*>(C + orow * e.ldc + n) + h;
+          if constexpr (!std::is_same<T, float>::value) {
+            if (e.aux != nullptr) {  // GELU Linear: h to aux, gelu(h) (bf16-rounded h, as the
+              // gelu_fwd kernel computes it) to C
+              reinterpret_cast<uint4*>(reinterpret_cast<T*>(e.aux) + orow * e.ldc + n)[h] = v;
+              float f[8];
+              unpack8(v, f);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) f[q] = gelu_erf(f[q]);
+              v = pack8(f);
+            }
+          }
           if (e.nt) {  // streaming output (g_nt_store)
             __builtin_nontemporal_store(u32v4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32v4*>(dst));
           } else {

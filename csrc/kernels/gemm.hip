@@ -161,9 +161,14 @@ static void gemm_t(const void* A, long lda, bool a_kc, const void* B, long ldb, 
 
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
           long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
-          bool f32, int cfg, int splits, const void* addend, bool ws_split, const WsFinish* fin) {
+          bool f32, int cfg, int splits, const void* addend, bool ws_split, const WsFinish* fin,
+          void* aux) {
   EpiParams e{};
   e.C = C; e.ldc = ldc; e.M = (uint32_t)M; e.N = (uint32_t)N; e.bias = bias; e.act = act;
+  if (act == 2) {  // GELU: bf16 activation output with the pre-activation in aux
+    e.act = 0;
+    e.aux = aux;
+  }
   e.nt = (g_nt_store >> 7) & 1;
   if (addend != nullptr && out == 0 && a_kc && !b_kc) {
     e.addend = addend;

@@ -204,7 +204,9 @@ void avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho,
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
           long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
           bool f32 = false, int cfg = -1, int splits = -1, const void* addend = nullptr,
-          bool ws_split = false, const WsFinish* fin = nullptr);
+          bool ws_split = false, const WsFinish* fin = nullptr, void* aux = nullptr);
+//  act 2 (GELU, bf16 output mode 0): C = gelu(A B + bias) and aux = A B + bias (the
+//  pre-activation the backward needs), both [M][ldc]
 // WsFinish tickets a gemm needs at most: one per output tile of the smallest tile config
 inline long gemm_max_tiles(long M, long N) { return ((M + 63) / 64) * ((N + 63) / 64); }
 // the split count a ws_split gemm of this K actually uses for `splits` requested

@@ -457,7 +457,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const __bf16* __restrict_
     float v[8];
     unpack8(reinterpret_cast<const uint4*>(x)[i], v);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = 0.5f * v[q] * (1.f + erff(v[q] * 0.70710678118654752f));
+    for (int q = 0; q < 8; ++q) v[q] = gelu_erf(v[q]);
     reinterpret_cast<uint4*>(y)[i] = pack8(v);
   }
 }

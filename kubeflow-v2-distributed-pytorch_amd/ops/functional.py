@@ -890,9 +890,8 @@ class _LinearFn(Function):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         bk = bias if bias_c is None else bias_c  # bias_c: the kernel's (padded) bias vector
-        if act == "gelu":
-            h = K.gemm(x2, w_c, False, True, bk, "none", x.dtype)
-            y = K.gelu_fwd(h)
+        if act == "gelu":  # GELU in the GEMM epilogue (h, the pre-activation, saved)
+            y, h = K.gemm_gelu(x2.contiguous(), w_c, bk)
             ctx.save_for_backward(x2, w_c, h)
         else:
             y = K.gemm(x2, w_c, False, True, bk, act, x.dtype)

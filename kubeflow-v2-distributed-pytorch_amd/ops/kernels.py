@@ -270,6 +270,26 @@ def _pad2(t, r, c):
     return out
 
 
+_GEMM_GELU = os.environ.get("MIPIPE_GEMM_GELU", "1") != "0"  # 0: GEMM then gelu_fwd (A/B)
+
+
+def gemm_gelu_ok(x, w) -> bool:
+    """gemm_gelu runs as one native GEMM for x [M, K] @ w [N, K]^T (bf16, multiples of 8)."""
+    return (_GEMM_GELU and use_native(x) and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16
+            and x.dim() == 2 and w.dim() == 2 and x.shape[1] % 8 == 0 and w.shape[0] % 8 == 0
+            and x.is_contiguous() and w.is_contiguous())
+
+
+def gemm_gelu(x, w, bias=None):
+    """(gelu(x @ w^T + bias), x @ w^T + bias): the GELU Linear forward with the activation in
+    the GEMM epilogue (the pre-activation is the backward's saved tensor)."""
+    if gemm_gelu_ok(x, w):
+        return native().gemm_gelu(x, w, bias)
+    h = gemm(x, w, False, True, bias, "none", x.dtype)
+    return gelu_fwd(h), h
+
+
 def gemm(a, b, trans_a=False, trans_b=False, bias=None, act="none", out_dtype=None, c=None,
          beta=0.0, addend=None):
     """act(op(a) @ op(b) + bias) [+ beta * c] [+ addend]; ``addend`` (same shape / dtype as the

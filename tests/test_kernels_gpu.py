@@ -838,3 +838,21 @@ def test_embedding_bwd_ordered(rows, H, n):
     acc0 = acc.clone()
     native().embedding_bwd(dy, idx, rows, acc, True, 0.125)
     assert rel_err(acc - acc0, 0.125 * ref) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (640, 768, 768), (200, 136, 72)])
+def test_gemm_gelu_epilogue_matches_gemm_then_gelu(M, N, K):
+    """The GELU Linear forward in one GEMM (pre-activation to aux, GELU to the output) ==
+    the plain bias GEMM followed by the gelu_fwd kernel, bit for bit, for every tile config."""
+    from mipipe.ops import kernels as Kk
+    C = native()
+    x, w = bf(M, K), bf(N, K, scale=0.05)
+    bias = torch.randn(N, device=dev)
+    for cfg in range(C.CONV_TILE_CONFIGS):
+        h0 = C.gemm(x, w, False, True, bias, "none", torch.bfloat16, None, 0.0, cfg)
+        y0 = Kk.gelu_fwd(h0)
+        y1, h1 = C.gemm_gelu(x, w, bias, cfg)
+        assert torch.equal(h0, h1), cfg
+        assert torch.equal(y0, y1), cfg
+    ref = torch.nn.functional.gelu(x.float() @ w.float().t() + bias)
+    assert rel_err(y1, ref) < 1e-2

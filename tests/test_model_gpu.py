@@ -274,3 +274,41 @@ def test_task_hip_graph_matches_eager(tmp_path, monkeypatch):
     b = torch.cat([v.float().flatten() for k, v in sds[1].items() if v.is_floating_point()])
     cos = float(torch.nn.functional.cosine_similarity(a, b, dim=0))
     assert cos > 0.9999, cos
+
+
+def test_cache_policy_hints_do_not_change_results():
+    """The non-temporal / streaming cache hints (g_nt_store bit mask) change only where data is
+    cached: ResNet-50 training steps (conv fwd / dgrad stores, BN-pass and fused-epilogue
+    loads, the stem) and an AdamW step give bit-identical results with every hint off and on."""
+    import copy
+    from mipipe.ops._native import native
+    from mipipe.ops import functional as MF
+    from mipipe.optim import AdamW
+    C = native()
+    saved = C.get_nt_store()
+    torch.manual_seed(0)
+    base = create_model("resnet50", num_classes=10).cuda()
+    x = torch.randn(4, 3, 224, 224, device="cuda")
+    y = torch.randint(0, 10, (4,), device="cuda")
+    outs = []
+    try:
+        for mask in (0, 0xFFFF):
+            C.set_nt_store(mask)
+            m = copy.deepcopy(base)
+            opt = SGD(m.parameters(), lr=0.1, momentum=0.9)
+            for _ in range(2):
+                opt.zero_grad()
+                loss = MF.cross_entropy(m(x), y)
+                loss.backward()
+                opt.step()
+            p = torch.nn.Parameter(torch.randn(4096, device="cuda"))
+            p.grad = torch.randn(4096, device="cuda")
+            a = AdamW([p], lr=1e-3)
+            a.step()
+            outs.append(([q.detach().clone() for q in m.parameters()], loss.detach(), p.detach().clone()))
+    finally:
+        C.set_nt_store(saved)
+    for u, v in zip(outs[0][0], outs[1][0]):
+        assert torch.equal(u, v)
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][2], outs[1][2])
