@@ -270,7 +270,10 @@ def _pad2(t, r, c):
     return out
 
 
-_GEMM_GELU = os.environ.get("MIPIPE_GEMM_GELU", "1") != "0"  # 0: GEMM then gelu_fwd (A/B)
+# MIPIPE_GEMM_GELU=1: the GELU in the GEMM epilogue.  Measured neutral on BERT-base (7.296 vs
+# 7.277 ms/step, same box, alternating: profiles/r4_gemm_gelu_ab.txt) — the epilogue's erf
+# VALU costs what the separate HBM-bound pass did — so off by default.
+_GEMM_GELU = os.environ.get("MIPIPE_GEMM_GELU", "0") == "1"
 
 
 def gemm_gelu_ok(x, w) -> bool:

@@ -279,17 +279,21 @@ def test_task_hip_graph_matches_eager(tmp_path, monkeypatch):
 def test_cache_policy_hints_do_not_change_results():
     """The non-temporal / streaming cache hints (g_nt_store bit mask) change only where data is
     cached: ResNet-50 training steps (conv fwd / dgrad stores, BN-pass and fused-epilogue
-    loads, the stem) and an AdamW step give bit-identical results with every hint off and on."""
+    loads, the stem) and an AdamW step give bit-identical results with every hint off and on
+    (deterministic mode: no atomics, so two runs are comparable bit for bit)."""
     import copy
     from mipipe.ops._native import native
     from mipipe.ops import functional as MF
     from mipipe.optim import AdamW
     C = native()
     saved = C.get_nt_store()
+    from mipipe.ops import determinism
+    determinism.set_deterministic(True)  # atomics would make even two identical runs differ
     torch.manual_seed(0)
     base = create_model("resnet50", num_classes=10).cuda()
     x = torch.randn(4, 3, 224, 224, device="cuda")
     y = torch.randint(0, 10, (4,), device="cuda")
+    p0, g0 = torch.randn(4096, device="cuda"), torch.randn(4096, device="cuda")
     outs = []
     try:
         for mask in (0, 0xFFFF):
@@ -301,13 +305,14 @@ def test_cache_policy_hints_do_not_change_results():
                 loss = MF.cross_entropy(m(x), y)
                 loss.backward()
                 opt.step()
-            p = torch.nn.Parameter(torch.randn(4096, device="cuda"))
-            p.grad = torch.randn(4096, device="cuda")
+            p = torch.nn.Parameter(p0.clone())
+            p.grad = g0.clone()
             a = AdamW([p], lr=1e-3)
             a.step()
             outs.append(([q.detach().clone() for q in m.parameters()], loss.detach(), p.detach().clone()))
     finally:
         C.set_nt_store(saved)
+        determinism.set_deterministic(False)
     for u, v in zip(outs[0][0], outs[1][0]):
         assert torch.equal(u, v)
     assert torch.equal(outs[0][1], outs[1][1])
