@@ -125,7 +125,7 @@ void bn_finalize(float* psum, float* psq, int P, int C, long count, const float*
 // one row in flight (4-8 rows per thread measured no better, grid-strided rows worse).
 constexpr int kApplyU = 2;
 
-template <int RES, class T>  // RES: 0 none, 1 raw residual, 2 BN'd residual
+template <int RES, class T, int U = kApplyU>  // RES: 0 none, 1 raw residual, 2 BN'd residual
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ bias,
@@ -140,14 +140,14 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y
   const int t = threadIdx.x;
   const int rg = t / mp.tpr;
   if (rg >= mp.rpb) return;
-  const long row0 = (long)blockIdx.x * mp.rpb * kApplyU + rg;
+  const long row0 = (long)blockIdx.x * mp.rpb * U + rg;
   for (int pass = 0; pass < mp.passes; ++pass) {
     const int cg = pass * mp.tpr + (t % mp.tpr);
     if (cg * 8 >= C) continue;
     const int c0 = cg * 8;
-    Raw8<T> ry[kApplyU], rr[kApplyU];
+    Raw8<T> ry[U], rr[U];
 #pragma unroll
-    for (int u = 0; u < kApplyU; ++u) {
+    for (int u = 0; u < U; ++u) {
       const long off = min(row0 + (long)u * mp.rpb, M - 1) * C + c0;
       ry[u] = ld_raw8(y + off, ntl);
       if (RES != 0) rr[u] = ld_raw8(r + off, ntl);
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y
       }
     }
 #pragma unroll
-    for (int u = 0; u < kApplyU; ++u) {
+    for (int u = 0; u < U; ++u) {
       const long row = row0 + (long)u * mp.rpb;
       if (row >= M) break;
       const long off = row * C + c0;
@@ -192,8 +192,16 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const T* __restrict__ y
   }
 }
 
-inline int grid_for_tiles(long M, int rpb) {
-  return (int)std::max<long>(1, (M + (long)rpb * kApplyU - 1) / ((long)rpb * kApplyU));
+inline int grid_for_tiles(long M, int rpb, int u = kApplyU) {
+  return (int)std::max<long>(1, (M + (long)rpb * u - 1) / ((long)rpb * u));
+}
+// rows in flight per thread of the BN apply passes (MIPIPE_BN_U = 2 or 4; A/B knob)
+static int bn_u() {
+  static const int u = [] {
+    const char* v = getenv("MIPIPE_BN_U");
+    return v != nullptr && atoi(v) == 4 ? 4 : 2;
+  }();
+  return u;
 }
 
 template <class T>
@@ -201,18 +209,28 @@ static void bn_act_fwd_t(const void* y, const float* scale, const float* bias, c
                          const float* rscale, const float* rbias, void* z, long M, int C,
                          bool relu, hipStream_t st, uint8_t* mask) {
   RowMap mp = row_map(C);
-  int grid = grid_for_tiles(M, mp.rpb);
+  const int u = bn_u();
+  int grid = grid_for_tiles(M, mp.rpb, u);
   const bool nt = (g_nt_store & 4) != 0;  // BN forward apply
   const bool ntl = (g_nt_store & 32) != 0;  // its loads streaming
   const T* yp = (const T*)y;
   const T* rp = (const T*)r;
   T* zp = (T*)z;
   if (r == nullptr)
-    hipLaunchKernelGGL((bn_act_fwd_kernel<0, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
+    {
+      if (u == 4) hipLaunchKernelGGL((bn_act_fwd_kernel<0, T, 4>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
+      else hipLaunchKernelGGL((bn_act_fwd_kernel<0, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
+    }
   else if (rscale == nullptr)
-    hipLaunchKernelGGL((bn_act_fwd_kernel<1, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
+    {
+      if (u == 4) hipLaunchKernelGGL((bn_act_fwd_kernel<1, T, 4>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
+      else hipLaunchKernelGGL((bn_act_fwd_kernel<1, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
+    }
   else
-    hipLaunchKernelGGL((bn_act_fwd_kernel<2, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
+    {
+      if (u == 4) hipLaunchKernelGGL((bn_act_fwd_kernel<2, T, 4>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
+      else hipLaunchKernelGGL((bn_act_fwd_kernel<2, T>), dim3(grid), dim3(256), 0, st, yp, scale, bias, rp, rscale, rbias, zp, M, C, relu, mask, nt, ntl);
+    }
 }
 
 void bn_act_fwd(const void* y, const float* scale, const float* bias, const void* r,
@@ -409,7 +427,7 @@ void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float
                      y2 ? dbeta2 : nullptr, gx_div);
 }
 
-template <int MODE, class T>  // MODE 0: dy only, 1: dy + dres (=g), 2: dy + dy2 (second branch)
+template <int MODE, class T, int U = kApplyU>  // MODE 0: dy only, 1: dy + dres (=g), 2: dy + dy2 (second branch)
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const T* __restrict__ dz, const T* __restrict__ z, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -422,14 +440,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const int t = threadIdx.x;
   const int rg = t / mp.tpr;
   if (rg >= mp.rpb) return;
-  const long row0 = (long)blockIdx.x * mp.rpb * kApplyU + rg;
+  const long row0 = (long)blockIdx.x * mp.rpb * U + rg;
   for (int pass = 0; pass < mp.passes; ++pass) {
     const int cg = pass * mp.tpr + (t % mp.tpr);
     const int c0 = cg * 8;
     if (c0 >= C) continue;
-    Raw8<T> rgv[kApplyU], rz[kApplyU], ry[kApplyU], ry2[kApplyU];
+    Raw8<T> rgv[U], rz[U], ry[U], ry2[U];
 #pragma unroll
-    for (int u = 0; u < kApplyU; ++u) {
+    for (int u = 0; u < U; ++u) {
       const long off = min(row0 + (long)u * mp.rpb, M - 1) * C + c0;
       rgv[u] = ld_raw8(dz + off, ntl);
       if (relu) rz[u] = ld_raw8(z + off, ntl);
@@ -454,7 +472,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       }
     }
 #pragma unroll
-    for (int u = 0; u < kApplyU; ++u) {
+    for (int u = 0; u < U; ++u) {
       const long row = row0 + (long)u * mp.rpb;
       if (row >= M) break;
       const long off = row * C + c0;
@@ -492,18 +510,28 @@ void bn_act_bwd_apply(const void* dz, const void* z, const void* y, const float*
   RowMap mp = row_map(C);
   const bool nt = (g_nt_store & 8) != 0;  // BN backward apply
   const bool ntl = (g_nt_store & 64) != 0;  // its loads streaming
-  int grid = grid_for_tiles(M, mp.rpb);
+  const int u = bn_u();
+  int grid = grid_for_tiles(M, mp.rpb, u);
   float inv_n = 1.f / (float)count;
   auto launch = [&](auto tag) {
     typedef decltype(tag) T;
       const T *dzp = (const T*)dz, *zp = (const T*)z, *yp = (const T*)y, *y2p = (const T*)y2;
     T *dyp = (T*)dy, *dop = (T*)dother;
     if (y2 != nullptr)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<2, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
+      {
+        if (u == 4) hipLaunchKernelGGL((bn_bwd_apply_kernel<2, T, 4>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
+        else hipLaunchKernelGGL((bn_bwd_apply_kernel<2, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
+      }
     else if (want_dres)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
+      {
+        if (u == 4) hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T, 4>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
+        else hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
+      }
     else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<0, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
+      {
+        if (u == 4) hipLaunchKernelGGL((bn_bwd_apply_kernel<0, T, 4>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
+        else hipLaunchKernelGGL((bn_bwd_apply_kernel<0, T>), dim3(grid), dim3(256), 0, st, dzp, zp, yp, mean, invstd, gamma, sum_g, sum_gx, y2p, mean2, invstd2, gamma2, sum_gx2, inv_n, relu, dyp, dop, M, C, nt, ntl);
+      }
   };
   if (f32) launch(float{});
   else launch(__bf16{});
