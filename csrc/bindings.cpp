@@ -489,13 +489,21 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
   if (plan < 0) {
     std::vector<int> cands;
     for (int t : tune::candidates(s.f32, true)) {
-      for (int sp : {0, 1, 2, 4, 8, 16}) cands.push_back(t + tune::kPlanSplit * sp);
+      // 3 / 6 / 12 / 24 as well: tiles x splits lands nearer a whole number of waves
+      // (MIPIPE_WGRAD_WIDE_SPLITS=0: powers of two only, A/B)
+      static const bool wide = [] {
+        const char* v = getenv("MIPIPE_WGRAD_WIDE_SPLITS");
+        return v == nullptr || atoi(v) != 0;
+      }();
+      for (int sp : {0, 1, 2, 3, 4, 6, 8, 12, 16})
+        if (wide || (sp & (sp - 1)) == 0) cands.push_back(t + tune::kPlanSplit * sp);
       static const bool ws_cands = [] {  // MIPIPE_WGRAD_WS=0: atomic split-K only (A/B)
         const char* v = getenv("MIPIPE_WGRAD_WS");
         return v == nullptr || atoi(v) != 0;
       }();
       if (!mipipe::g_deterministic && ws_cands)
-        for (int sp : {4, 8, 16, 32}) cands.push_back((t + tune::kPlanSplit * sp) | tune::kPlanWs);
+        for (int sp : {4, 6, 8, 12, 16, 24, 32})
+          if (wide || (sp & (sp - 1)) == 0) cands.push_back((t + tune::kPlanSplit * sp) | tune::kPlanWs);
     }
     plan = tune::select_from(tune::key("wgrad", s), cands, [&](int p) {
       auto dws = torch::zeros_like(dw);
