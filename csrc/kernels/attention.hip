@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const __bf16* __restric
                                                          const __bf16* __restrict__ o,
                                                          float* __restrict__ delta,
                                                          float* __restrict__ dq_acc, int B, int S,
-                                                         int H) {
+                                                         int H, bool zero_dq) {
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long row = gid >> 3;  // (token, head); rows * 8 is a multiple of 8: groups stay whole
   const int c = (int)(gid & 7);
@@ -283,6 +283,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const __bf16* __restric
   acc += __shfl_xor(acc, 2);
   acc += __shfl_xor(acc, 4);
   if (c == 0) delta[((long)b * H + h) * S + q] = acc;
+  if (!zero_dq) return;
   float4* dq = reinterpret_cast<float4*>(dq_acc + off);
   dq[0] = make_float4(0.f, 0.f, 0.f, 0.f);
   dq[1] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -297,6 +298,7 @@ struct BwdArgs {
   float* dq_acc;       // [B*S][H*64] fp32, zeroed; det: [nkb][B*S][H*64] slabs, written
   __bf16* dqkv;
   int det;             // deterministic mode: each key block STORES its dQ part in its own slab
+  int direct;          // one key block per (b, h): its dQ tiles are complete -> bf16 into dqkv
   int B, S, H;
   float scale, scale_log2;
   float p_drop;
@@ -314,7 +316,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(BwdArgs a) {
   constexpr int KB = 32 * NW;  // keys per block
   constexpr int kKT = KB * 128;
   constexpr int kDsOff = kKT + 2 * kQStage;
-  __shared__ __attribute__((aligned(16))) char smem[kDsOff + KB * 64];
+  constexpr int kDqOff = kDsOff + KB * 64;  // direct mode: finished dQ tile [32 q][64 d] bf16
+  __shared__ __attribute__((aligned(16))) char smem[kDqOff + 32 * 128];
   const int S = a.S, H = a.H;
   const long ld = 3l * H * D, ldq = (long)H * D;
   const int nkb = (S + KB - 1) / KB;
@@ -451,7 +454,13 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(BwdArgs a) {
         const int qg = it * 32 + qr0 + 4 * g + i;
         if (qg < S) {
           float* dst = a.dq_acc + ((long)b * S + qg) * ldq + h * D + dc0 + li;
-          if (a.det) {
+          if (a.direct) {
+            // the block holds every key of (b, h): this is the finished dQ value -> LDS tile,
+            // stored to dqkv below as whole 16-byte chunks
+            __bf16* dql = reinterpret_cast<__bf16*>(smem + kDqOff) + (qr0 + 4 * g + i) * D + dc0 + li;
+#pragma unroll
+            for (int dt = 0; dt < DT; ++dt) dql[16 * dt] = f2bf(cacc[dt][i]);
+          } else if (a.det) {
             // deterministic: this key block's slab; every (q, d) of it is written exactly once
             // (one q tile per iteration), and attn_dq_store_kernel sums the slabs in key order
             dst += (long)kbk * a.B * S * ldq;
@@ -462,6 +471,19 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(BwdArgs a) {
             for (int dt = 0; dt < DT; ++dt) atomicAdd(dst + 16 * dt, cacc[dt][i]);
           }
         }
+      }
+    }
+    if (a.direct) {  // 32 x 64 bf16 tile: 256 chunks of 16 B (the next iteration's barrier
+                     // orders these reads before the tile is rewritten)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int c = tid; c < 256; c += 64 * NW) {
+        const int row = c >> 3, qg = it * 32 + row;
+        const uint4 v = *reinterpret_cast<const uint4*>(smem + kDqOff + 16 * c);
+        if (qg < S)
+          *reinterpret_cast<uint4*>(a.dqkv + ((long)b * S + qg) * ld + h * D + 8 * (c & 7)) = v;
       }
     }
   }
@@ -532,7 +554,12 @@ void attention_fwd(const void* qkv, const float* mask, void* o, float* lse, int 
     hipLaunchKernelGGL(attn::attn_fwd_kernel<4>, dim3(B * H * ((S + 127) / 128)), dim3(256), 0, st, a);
 }
 
+// S within one backward key block: every dQ tile is finished inside its block and stored as bf16
+// directly (no fp32 accumulator to zero, no atomics, no dq_store pass)
+bool attention_dq_direct(int S) { return S <= (attn_waves(1, S, 1) == 2 ? 64 : 128); }
+
 int attention_dq_slabs(int S) {
+  if (attention_dq_direct(S)) return 0;
   if (!g_deterministic) return 1;
   const int kb = attn_waves(1, S, 1) == 2 ? 64 : 128;  // keys per backward block
   return (S + kb - 1) / kb;
@@ -545,17 +572,19 @@ void attention_bwd(const void* dout, const void* qkv, const void* o, const float
   const long rows = (long)B * S * H;
   // deterministic mode with several key blocks per (b, h): per-key-block dQ slabs summed in a
   // fixed order instead of fp32 atomics (one key block: its single add is already exact)
+  const bool direct = attention_dq_direct(S);
   const int slabs = attention_dq_slabs(S);
   const int det = slabs > 1 ? 1 : 0;
   hipLaunchKernelGGL(attn::attn_delta_kernel, dim3((rows * 8 + 255) / 256), dim3(256), 0, st,
-                     (const __bf16*)dout, (const __bf16*)o, delta, dq_acc, B, S, H);
+                     (const __bf16*)dout, (const __bf16*)o, delta, dq_acc, B, S, H, !direct);
   attn::BwdArgs a{(const __bf16*)qkv, (const __bf16*)dout, lse, delta, mask, dq_acc,
-                  (__bf16*)dqkv, det, B, S, H, scale, scale * attn::kLog2e, p_drop,
-                  drop_threshold(p_drop), seed, seed_dev};
+                  (__bf16*)dqkv, det, direct ? 1 : 0, B, S, H, scale, scale * attn::kLog2e,
+                  p_drop, drop_threshold(p_drop), seed, seed_dev};
   if (attn_waves(B, S, H) == 2)
     hipLaunchKernelGGL(attn::attn_bwd_kernel<2>, dim3(B * H * ((S + 63) / 64)), dim3(128), 0, st, a);
   else
     hipLaunchKernelGGL(attn::attn_bwd_kernel<4>, dim3(B * H * ((S + 127) / 128)), dim3(256), 0, st, a);
+  if (direct) return;
   const long chunks = (long)B * S * H * attn::D / 8;
   hipLaunchKernelGGL(attn::attn_dq_store_kernel, dim3((chunks + 255) / 256), dim3(256), 0, st,
                      dq_acc, (__bf16*)dqkv, (long)B * S, H * attn::D, det ? slabs : 1);

@@ -365,8 +365,10 @@ void attention_fwd(const void* qkv, const float* mask, void* o, float* lse, int 
                    float scale, float p_drop, uint32_t seed, hipStream_t st,
                    const uint32_t* seed_dev = nullptr);
 // dqkv [B*S][3*H*64]; delta [B][H][S] and dq_acc [attention_dq_slabs(S)][B*S][H*64] fp32 are
-// scratch (deterministic mode: one dQ slab per key block, summed in order; else 1 slab + atomics).
+// scratch (deterministic mode: one dQ slab per key block, summed in order; else 1 slab + atomics;
+// 0 slabs when S fits one key block: dQ is then stored as bf16 by the backward kernel itself).
 int attention_dq_slabs(int S);
+bool attention_dq_direct(int S);
 void attention_bwd(const void* dout, const void* qkv, const void* o, const float* lse,
                    const float* mask, void* dqkv, float* delta, float* dq_acc, int B, int S,
                    int H, float scale, float p_drop, uint32_t seed, hipStream_t st,
