@@ -368,11 +368,25 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(BwdArgs a) {
   f32x16 dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
   const float inv_keep = a.p_drop > 0.f ? 1.f / (1.f - a.p_drop) : 1.f;
   char* dsT = smem + kDsOff;
+  // direct mode: the finished 32 x 64 bf16 dQ tile of q tile t, 256 chunks of 16 B, from LDS to
+  // dqkv.  Tile t is written to LDS in iteration t and stored after the next barrier (the top of
+  // iteration t + 1, or after the loop); every wave reads it before the mid-iteration barrier
+  // that precedes the next rewrite.
+  auto store_dq = [&](int t) {
+#pragma unroll
+    for (int c = tid; c < 256; c += 64 * NW) {
+      const int row = c >> 3, qg = t * 32 + row;
+      const uint4 v = *reinterpret_cast<const uint4*>(smem + kDqOff + 16 * c);
+      if (qg < S)
+        *reinterpret_cast<uint4*>(a.dqkv + ((long)b * S + qg) * ld + h * D + 8 * (c & 7)) = v;
+    }
+  };
   for (int it = 0; it < nqt; ++it) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const char* cur = smem + kKT + (it & 1) * kQStage;
     if (it + 1 < nqt) stage(smem + kKT + ((it + 1) & 1) * kQStage, (it + 1) * 32);
+    if (a.direct && it > 0) store_dq(it - 1);
     const float* lsel = reinterpret_cast<const float*>(cur + 8192);
     const float* dell = lsel + 32;
     // X = S[q][key] (rows q, lane = key) and dP = dO·Vᵀ in the same layout
@@ -473,19 +487,12 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(BwdArgs a) {
         }
       }
     }
-    if (a.direct) {  // 32 x 64 bf16 tile: 256 chunks of 16 B (the next iteration's barrier
-                     // orders these reads before the tile is rewritten)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int c = tid; c < 256; c += 64 * NW) {
-        const int row = c >> 3, qg = it * 32 + row;
-        const uint4 v = *reinterpret_cast<const uint4*>(smem + kDqOff + 16 * c);
-        if (qg < S)
-          *reinterpret_cast<uint4*>(a.dqkv + ((long)b * S + qg) * ld + h * D + 8 * (c & 7)) = v;
-      }
-    }
+  }
+  if (a.direct) {  // the last q tile's dQ
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    store_dq(nqt - 1);
   }
   // dKᵀ / dVᵀ: lane = key column, regs = d rows -> 8-byte stores into dqkv's k / v columns
   if (key < S) {
