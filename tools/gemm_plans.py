@@ -58,7 +58,11 @@ def t_graph(fn, reps):
     return best
 
 
-def plans(C, mode, K):
+def plans(C, mode, K, all_ws=False):
+    """``all_ws``: workspace split-K plans at every K (the training-step tuner offers them from
+    K >= 1024 / 2048 only)."""
+    if all_ws:
+        K = 1 << 30
     tiles = list(range(C.CONV_TILE_CONFIGS))
     out = []
     if mode == 2:
@@ -81,6 +85,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--shapes", nargs="*", default=BERT_32x128)
+    ap.add_argument("--all-ws", action="store_true", help="workspace split plans at every K")
     a = ap.parse_args()
     C = native()
     dev = torch.device("cuda", 0)
@@ -114,7 +119,7 @@ def main():
             return torch.mm(At, Bt)
 
         res = {}
-        for p in plans(C, mode, K):
+        for p in plans(C, mode, K, a.all_ws):
             res[p] = t_graph(lambda: run(p), a.reps)
         t_lib = t_graph(lib, a.reps)
         best = min(res, key=res.get)
