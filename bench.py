@@ -38,12 +38,12 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 METRIC = "samples/sec (whole node) task.py DDP at 1/2/4/8 MI355X; scaling efficiency"
-# Measured comparator: stock PyTorch-ROCm 2.10 (MIOpen + hipBLASLt, channels_last,
+# Measured comparators: stock PyTorch-ROCm 2.10 (MIOpen + hipBLASLt, channels_last,
 # bf16 autocast, torch SGD) on ONE MI355X, ResNet-50 b256 224x224: 6580.1 samples/s.
 # vs_baseline = value / (comparator_per_gpu * n_gpus)  (ideal linear scaling of the comparator).
 # BERT-base MLM (B=32 x S=128 / B=8 x S=512 per GPU, AdamW fused, SDPA, bf16 autocast): stock
 # torch measured on the same MI355X with tools/gpu_bert.sh / gpu_prof_bert.sh.
-STOCK_1GPU = {"resnet50": 6580.1, "resnet18_32": 76880.3, "resnet18_32_fp32": 75965.3,
+STOCK_1GPU = {"resnet50": 6580.1, "resnet18_32": 76880.3, "resnet18_32_fp32": 76305.2,
               "bert_base_128": 2184.8, "bert_base_512": 540.8}
 
 
@@ -91,6 +91,13 @@ def parse():
                     help="directory: each rank saves its final parameters and buffers there")
     ap.add_argument("--save-tune", default=None,
                     help="write the tuning table after the warm-up steps (JSON)")
+    ap.add_argument("--reference-config", default="auto", choices=["auto", "on", "off"],
+                    help="also time the reference's config of record in the same process "
+                         "(ResNet-18 32x32, 1000 classes, fp32, deterministic, --ref-batch per "
+                         "GPU) and report it as 'reference_config' in the JSON line; auto = with "
+                         "the default mipipe ResNet-50 headline on the GPU")
+    ap.add_argument("--ref-batch", type=int, default=1024,
+                    help="per-process batch of the reference config (task.py:58,153: 1024)")
     return ap.parse_args()
 
 
@@ -162,6 +169,87 @@ def main() -> int:
                   f"expected {a.gpus}", file=sys.stderr)
             return 3
     a.distributed = distributed
+    if rank == 0:
+        _heartbeat()
+    r = _run(a, world, rank, local, dev, distributed, cpu)
+    ref = None
+    if _want_reference_config(a, cpu):
+        # the reference's own config of record in the same process, same timing discipline:
+        # ResNet-18 on 32x32 (CIFAR shape), 1000-class head (task.py:171), 1024 images per
+        # process (task.py:153), fp32 (task.py:303-312: no autocast), deterministic kernels
+        # (task.py:25: cudnn.deterministic = True)
+        import copy
+        b = copy.copy(a)
+        b.model, b.res, b.classes, b.dtype, b.deterministic = "resnet18", 32, 1000, "fp32", 1
+        b.batch = a.ref_batch
+        b.emulate_ranks, b.dump_params, b.save_tune = 1, None, None
+        del r["model"]
+        if not cpu:
+            torch.cuda.empty_cache()
+        rr = _run(b, world, rank, local, dev, distributed, cpu)
+        ref = {"model": "resnet18", "image_size": 32, "classes": 1000,
+               "batch_per_gpu": b.batch, "global_batch": b.batch * world,
+               "dtype": "fp32", "deterministic": True, "steps": b.steps, "warmup": b.warmup,
+               "value": round(rr["value"], 2), "unit": "samples/s",
+               "ms_per_step": round(rr["dt"] / b.steps * 1e3, 3),
+               "vs_stock_fp32": (round(rr["value"] / (STOCK_1GPU["resnet18_32_fp32"] * world), 4)
+                                 if not cpu else None),
+               "hip_graph": bool(getattr(b, "graph_used", False)),
+               "final_loss": rr["loss"], "gpu_clocks": rr["clocks"],
+               "source": "task.py:25,153,171,212-214,303-312"}
+    value, dt = r["value"], r["dt"]
+    is_bert = a.model.startswith("bert")
+    if is_bert:
+        key = f"{a.model}_{a.seq}"
+        opt_s = "AdamW(lr=1e-4,wd=0.01)"
+    else:
+        key = a.model if a.res == 224 else f"{a.model}_{a.res}"
+        if a.dtype == "fp32":
+            key += "_fp32"
+        opt_s = "SGD(lr=0.1,momentum=0.9,wd=1e-4)"
+    base = STOCK_1GPU.get(key)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / (base * world), 4) if base else None,
+            "dtype": "fp32" if (cpu or a.dtype == "fp32") else "bf16",
+            "data": "synthetic (on-device, random-init weights)",
+            "config": {"model": a.model, "global_batch": a.batch * world,
+                       "seq_len": a.seq if is_bert else None,
+                       "image_size": None if is_bert else a.res, "batch_per_gpu": a.batch,
+                       "parallelism": f"dp{world}", "impl": a.impl, "optimizer": opt_s,
+                       "hip_graph": bool(getattr(a, "graph_used", False)),
+                       "deterministic": bool(a.deterministic),
+                       "force_reduce": bool(a.force_reduce),
+                       "comm_dtype": a.comm_dtype,
+                       "native_reducer": bool(r.get("native_reducer", False)),
+                       "rccl": _rccl_settings() if distributed else None,
+                       "rccl_transports": _transports(rccl_log)},
+            "final_loss": r["loss"], "gpu_clocks": r["clocks"]}
+        if ref is not None:
+            line["reference_config"] = ref
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def _want_reference_config(a, cpu: bool) -> bool:
+    if a.reference_config == "off":
+        return False
+    if a.reference_config == "on":
+        return True
+    # auto: alongside the default headline (mipipe ResNet-50) on the GPU
+    return (not cpu and a.impl == "mipipe" and a.model == "resnet50" and a.emulate_ranks == 1
+            and not a.dump_params)
+
+
+def _run(a, world, rank, local, dev, distributed, cpu):
+    """Build one config, W untimed warm-up steps, then exactly K timed steps bracketed by a
+    barrier + device sync on both sides; the time is the MAX over ranks."""
     torch.manual_seed(0)
     if not cpu and a.impl == "mipipe":
         # per-shape conv tile autotuning during the (untimed, eager) warm-up steps — the
@@ -171,8 +259,6 @@ def main() -> int:
         tuning.set_benchmark(a.tune > 0, verbose=False, force=a.tune == 2)
         from mipipe.ops import determinism
         determinism.set_deterministic(bool(a.deterministic))
-    if rank == 0:
-        _heartbeat()
 
     is_bert = a.model.startswith("bert")
     if a.batch is None:
@@ -186,7 +272,7 @@ def main() -> int:
     for i in range(a.warmup):
         loss = step(*batches[i % 2])
         if rank == 0:  # progress for long first steps (kernel autotuning, graph capture)
-            print(f"warmup step {i + 1}/{a.warmup}", file=sys.stderr, flush=True)
+            print(f"warmup step {i + 1}/{a.warmup} ({a.model})", file=sys.stderr, flush=True)
     _sync(dev)
     if a.save_tune and rank == 0:
         from mipipe.ops import tuning
@@ -219,41 +305,9 @@ def main() -> int:
         torch.save({"params": [p.detach().cpu() for p in inner.parameters()],
                     "buffers": [b.detach().cpu() for b in inner.buffers()]},
                    os.path.join(a.dump_params, f"rank{rank}.pt"))
-    value = a.batch * world * a.steps / dt
-    if is_bert:
-        key = f"{a.model}_{a.seq}"
-        opt_s = "AdamW(lr=1e-4,wd=0.01)"
-    else:
-        key = a.model if a.res == 224 else f"{a.model}_{a.res}"
-        if a.dtype == "fp32":
-            key += "_fp32"
-        opt_s = "SGD(lr=0.1,momentum=0.9,wd=1e-4)"
-    base = STOCK_1GPU.get(key)
-    loss_v = float(loss.detach().float().item())
-    if rank == 0:
-        print(json.dumps({
-            "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": round(value / (base * world), 4) if base else None,
-            "dtype": "fp32" if (cpu or a.dtype == "fp32") else "bf16",
-            "data": "synthetic (on-device, random-init weights)",
-            "config": {"model": a.model, "global_batch": a.batch * world,
-                       "seq_len": a.seq if is_bert else None,
-                       "image_size": None if is_bert else a.res, "batch_per_gpu": a.batch,
-                       "parallelism": f"dp{world}", "impl": a.impl, "optimizer": opt_s,
-                       "hip_graph": bool(getattr(a, "graph_used", False)),
-                       "deterministic": bool(a.deterministic),
-                       "force_reduce": bool(a.force_reduce),
-                       "comm_dtype": a.comm_dtype,
-                       "native_reducer": bool(getattr(model, "native_reducer", False)),
-                       "rccl": _rccl_settings() if distributed else None,
-                       "rccl_transports": _transports(rccl_log)},
-            "final_loss": loss_v, "gpu_clocks": sampler.summary()}), flush=True)
-    if distributed:
-        dist.barrier()
-        dist.destroy_process_group()
-    return 0
+    return {"value": a.batch * world * a.steps / dt, "dt": dt,
+            "loss": float(loss.detach().float().item()), "clocks": sampler.summary(),
+            "native_reducer": bool(getattr(model, "native_reducer", False)), "model": model}
 
 
 def build_bert(a, world, local, dev, rank):

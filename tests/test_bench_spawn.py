@@ -166,3 +166,22 @@ def test_bench_world4_gloo_bert_matches_emulated_ranks(tmp_path):
             assert torch.equal(a, b)
     for a, b in zip(ranks[0]["params"], ref["params"]):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a - b).abs().max()
+
+
+def test_bench_reference_config_block_gloo():
+    """`--reference-config on` times the reference's config of record (ResNet-18 32x32, 1000
+    classes, fp32, deterministic) after the headline in the same process (and, here, under a
+    2-rank gloo DDP), and reports it inside the ONE JSON line."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--reference-config", "on",
+                        "--ref-batch", "4"] + CPU_ARGS, env=_env(),
+                       capture_output=True, text=True, timeout=600, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    j = lines[0]
+    assert j["config"]["model"] == "mnist_cnn" and j["n_gpus"] == 2
+    ref = j["reference_config"]
+    assert ref["model"] == "resnet18" and ref["classes"] == 1000 and ref["image_size"] == 32
+    assert ref["dtype"] == "fp32" and ref["deterministic"] is True
+    assert ref["batch_per_gpu"] == 4 and ref["global_batch"] == 8
+    assert ref["value"] > 0 and ref["ms_per_step"] > 0 and ref["steps"] == 2

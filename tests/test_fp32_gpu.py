@@ -215,35 +215,50 @@ def test_layout_kernels_fp32():
     assert p.dtype == torch.float32 and rel_err(p, pb.float()) < 1e-2
 
 
-def test_resnet18_cifar_fp32_step_matches_float64():
-    """One ResNet-18 (32x32, 10 classes, batch 64) fwd + bwd in fp32 on the HIP kernels vs the
-    same module tree evaluated in float64 by plain torch ops on the CPU.  Gradients are compared
-    by relative L2 error per tensor: a ReLU whose pre-activation lies within fp32 rounding of 0
-    may legitimately decide differently from float64 and move one tensor's max-abs error."""
+@pytest.mark.parametrize("det", [False, True], ids=["default", "deterministic"])
+def test_resnet18_cifar_fp32_step_matches_float64(det):
+    """One ResNet-18 (32x32, 10 classes, batch 64) fwd + bwd in fp32 on the HIP kernels vs a
+    float64 evaluation of the same weights and inputs that takes every ReLU / max-pool DECISION
+    from the GPU run (tests/pinned_ref.py).  Round 4's driver box saw one tensor at 1.16e-2
+    relative L2 against an unpinned float64 reference: a ReLU pre-activation within fp32
+    rounding of 0 (atomics order in the BN statistics moves which ones) decides differently and
+    moves a small layer-4 BatchNorm gradient by ~1/64.  With decisions pinned, what is left is
+    arithmetic, and every tensor must be within 1e-4 in both modes (default = fp32 atomics in the
+    BN statistics / split-K; deterministic = fixed-order sums, task.py:25)."""
     from mipipe.models import create_model
+    from mipipe.ops.determinism import deterministic
     from mipipe.train.task import CrossEntropyLoss
+    from pinned_ref import flipped_decisions, pinned_grads, record_gpu_decisions
     torch.manual_seed(0)
     m = create_model("resnet18", num_classes=10)
-    ref = create_model("resnet18", num_classes=10, compute_dtype=torch.float64).double()
-    ref.load_state_dict(m.state_dict())
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+    names = [n for n, _ in m.named_parameters()]
     m = m.to(dev)
     m.compute_dtype = torch.float32
     x = torch.randn(64, 3, 32, 32)
     yl = torch.randint(0, 10, (64,))
-    out = m(x.to(dev))
-    loss = CrossEntropyLoss()(out, yl.to(dev))
-    loss.backward()
-    out_r = ref(x.double())
-    loss_r = torch.nn.functional.cross_entropy(out_r, yl)
-    loss_r.backward()
+    with deterministic(det), record_gpu_decisions() as tape:
+        out = m(x.to(dev))
+        loss = CrossEntropyLoss()(out, yl.to(dev))
+        loss.backward()
+    torch.cuda.synchronize()
+    assert len(tape.relu_masks) == 16 and tape.pool is not None, tape.summary()
+    out_r, loss_r, g_pin, _ = pinned_grads(state, names, x, yl, tape)
+    _, _, g_own, pin_own = pinned_grads(state, names, x, yl, None)
+    flips = flipped_decisions(tape, pin_own.own)
     assert out.dtype == torch.float32
     assert rel_err(out, out_r) < 1e-4
     assert abs(loss.item() - loss_r.item()) < 1e-5 * max(1.0, abs(loss_r.item()))
-    pr = dict(ref.named_parameters())
-    e2 = sorted(((p.grad.double().cpu() - pr[n].grad).norm() / pr[n].grad.norm()).item()
-                for n, p in m.named_parameters())
-    assert e2[len(e2) // 2] < 1e-4, e2
-    assert e2[-1] < 5e-3, e2
+    grads = dict(m.named_parameters())
+
+    def rl2(a, b):
+        return ((a.double().cpu() - b).norm() / b.norm()).item()
+    pinned = sorted(((rl2(grads[n].grad, g_pin[n]), n) for n in names), reverse=True)
+    unpinned = sorted(((rl2(grads[n].grad, g_own[n]), n) for n in names), reverse=True)
+    report = (f"decisions flipped vs float64: {flips or 'none'}; worst pinned: {pinned[:4]}; "
+              f"worst unpinned: {unpinned[:4]}")
+    print(report)
+    assert all(e < 1e-4 for e, _ in pinned), report
 
 
 # vision.hip kernels (grouped / depthwise / non-square direct conv, any-C BatchNorm, k x k avg

@@ -31,13 +31,32 @@ def _gpu():
 
 
 def rel_err(a, b):
-    a = a.float()
-    b = b.float()
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
     return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
 
 
 def bf(*shape, scale=1.0):
     return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+def rnd(dt, *shape, scale=1.0):
+    """Random operand in the kernel dtype (bf16 inputs are quantised before the reference)."""
+    return (torch.randn(*shape, device=dev) * scale).to(dt)
+
+
+# tolerances per operand dtype: bf16 outputs / fp32 accumulation of bf16 products / fp32 (the
+# reference's precision: split-bf16x3 main loop, ~1e-6 measured)
+TOL_OUT = {torch.bfloat16: 1e-2, torch.float32: 1e-4}
+TOL_ACC = {torch.bfloat16: 2e-3, torch.float32: 1e-4}
+TOL_WGRAD = {torch.bfloat16: 5e-3, torch.float32: 1e-4}
+DTYPES = pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32], ids=["bf16", "fp32"])
+
+
+def hi_ref(t):
+    """Reference operand: float64 on the CPU for fp32 kernels (MIOpen has no float64 conv),
+    fp32 on the GPU for bf16 kernels."""
+    return t.detach().double().cpu() if t.dtype in (torch.float32, torch.float64) else t.float()
 
 
 CONV_CASES = [
@@ -125,21 +144,25 @@ def test_conv_fwd_writes_dgrad_flipped_weight(shape, dt):
 
 @pytest.mark.parametrize("shape", [(32, 14, 14, 256, 1024, 1, 1, 0), (16, 28, 28, 64, 64, 3, 1, 1),
                                    (16, 56, 56, 64, 128, 3, 2, 1)])
-def test_conv_wgrad_workspace_plans(shape):
+@DTYPES
+def test_conv_wgrad_workspace_plans(shape, dt):
     """Workspace split-K weight-grad plans (flag 1024: per-split slices + ordered sum instead of
     fp32 atomics) against the fp32 reference, accumulating into an existing gradient, for
-    several tiles and split counts; bit-identical reruns."""
+    every tile and the split counts the tuner tries (incl. 3 / 6 / 12 / 24); bit-identical
+    reruns.  fp32 operands run the split-bf16x3 main loop (tiles 0 / 2 / 8; others resolve to
+    the default) and must stay within fp32-class error."""
     N, H, W, Ci, Co, k, s, p = shape
     Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    dy, x = bf(N, Ho, Wo, Co), bf(N, H, W, Ci)
-    dwr = _ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)
-    base = torch.randn_like(dwr)
-    for cfg in (0, 2, 9):
-        for sp in (4, 16, 32):
+    dy, x = rnd(dt, N, Ho, Wo, Co), rnd(dt, N, H, W, Ci)
+    dwr = _ref.conv_wgrad(hi_ref(dy), hi_ref(x), k, k, s, p)
+    base = torch.randn(dwr.shape, device=dev)
+    cfgs = (0, 2, 8) if dt == torch.float32 else (0, 2, 9)
+    for cfg in cfgs:
+        for sp in (3, 4, 6, 12, 16, 24, 32):
             plan = (cfg + 16 * sp) | 1024
             out = base.clone()
             native().conv_wgrad(dy, x, k, k, s, p, out, cfg=plan)
-            assert rel_err(out - base, dwr) < 5e-3, (cfg, sp)
+            assert rel_err(hi_ref(out) - hi_ref(base), dwr) < TOL_WGRAD[dt], (cfg, sp)
             out2 = base.clone()
             native().conv_wgrad(dy, x, k, k, s, p, out2, cfg=plan)
             assert torch.equal(out, out2), (cfg, sp)
@@ -179,31 +202,33 @@ def test_gemm(M, N, K, ta, tb):
 
 @pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (300, 72, 200), (768, 256, 4096)])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
-def test_gemm_every_plan(M, N, K, ta, tb):
-    """Every (tile config x split-K) plan of the GEMM gives the same product: bf16 output with the
-    bias / ReLU epilogue, and fp32 accumulation into C (split-K atomics or the non-atomic
-    read-modify-write of splits == 1)."""
+@DTYPES
+def test_gemm_every_plan(M, N, K, ta, tb, dt):
+    """Every (tile config x split-K) plan of the GEMM gives the same product: activation-dtype
+    output with the bias / ReLU epilogue, and fp32 accumulation into C (split-K atomics, the
+    non-atomic read-modify-write of splits == 1, and workspace split-K: slices + ordered sum).
+    fp32 operands (split-bf16x3) against a float64 reference at 1e-4."""
     if (ta and M % 8) or (not ta and K % 8) or N % 8:
         pytest.skip("layout constraint")
-    a = bf(K, M) if ta else bf(M, K)
-    b = bf(N, K) if tb else bf(K, N)
+    a = rnd(dt, K, M) if ta else rnd(dt, M, K)
+    b = rnd(dt, N, K) if tb else rnd(dt, K, N)
     bias = torch.randn(N, device=dev)
-    ref = _ref.gemm(a.float(), b.float(), ta, tb, bias, "relu", torch.float32)
-    ref32 = _ref.gemm(a.float(), b.float(), ta, tb, None, "none", torch.float32)
+    ref = _ref.gemm(a.double(), b.double(), ta, tb, bias.double(), "relu", torch.float64)
+    ref32 = _ref.gemm(a.double(), b.double(), ta, tb, None, "none", torch.float64)
     for cfg in range(native().CONV_TILE_CONFIGS):
-        out = native().gemm(a, b, ta, tb, bias, "relu", torch.bfloat16, None, 0.0, cfg)
-        assert rel_err(out, ref) < 1e-2, cfg
-        for sp in (1, 2, 4):
+        out = native().gemm(a, b, ta, tb, bias, "relu", dt, None, 0.0, cfg)
+        assert out.dtype == dt and rel_err(out, ref) < TOL_OUT[dt], cfg
+        for sp in (1, 2, 3, 4):
             acc = torch.randn(M, N, device=dev)
             acc0 = acc.clone()
             native().gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0, cfg + 16 * sp)
-            assert rel_err(acc - acc0, ref32) < 2e-3, (cfg, sp)
-        for sp in (2, 3, 4, 6, 8):  # workspace split-K (kPlanWs): slices + ordered sum
+            assert rel_err(acc.double() - acc0.double(), ref32) < TOL_ACC[dt], (cfg, sp)
+        for sp in (2, 3, 4, 6, 8, 12, 24):  # workspace split-K (kPlanWs): slices + ordered sum
             acc = torch.randn(M, N, device=dev)
             acc0 = acc.clone()
             native().gemm(a, b, ta, tb, None, "none", torch.float32, acc, 1.0,
                           (cfg + 16 * sp) | 1024)
-            assert rel_err(acc - acc0, ref32) < 2e-3, (cfg, sp, "ws")
+            assert rel_err(acc.double() - acc0.double(), ref32) < TOL_ACC[dt], (cfg, sp, "ws")
             acc2 = acc0.clone()
             native().gemm(a, b, ta, tb, None, "none", torch.float32, acc2, 1.0,
                           (cfg + 16 * sp) | 1024)
@@ -638,28 +663,34 @@ TILE_CASES = [
 
 @pytest.mark.parametrize("cfg", list(range(14)))
 @pytest.mark.parametrize("case", TILE_CASES)
-def test_conv_every_tile_config(cfg, case):
+@DTYPES
+def test_conv_every_tile_config(cfg, case, dt):
     """Every tile config of the tuning table (block tile / LDS stages / 4- or 8-wave grid) gives
-    the same convolution: fwd (+BN statistics), dgrad (+fused BN-backward epilogue), wgrad."""
+    the same convolution: fwd (+BN statistics), dgrad (+fused BN-backward epilogue), wgrad
+    (heuristic / unsplit / 3-way / 6-way / 12-way split-K).  fp32 (the reference's precision)
+    runs tiles 0 / 2 / 8 on the split-bf16x3 loop (other ids resolve to the default tile) and
+    is compared with a float64 reference at 1e-4."""
     N, H, W, Ci, Co, k, s, p = case
+    f32 = dt == torch.float32
+    R = (lambda t: t.detach().double().cpu()) if f32 else (lambda t: t.float())
     Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    x = bf(N, H, W, Ci)
-    w = bf(Co, k, k, Ci, scale=1.0 / math.sqrt(Ci * k * k))
+    x = rnd(dt, N, H, W, Ci)
+    w = rnd(dt, Co, k, k, Ci, scale=1.0 / math.sqrt(Ci * k * k))
     shift = torch.randn(Co, device=dev) * 0.1
     y, ps, pss = native().conv_fwd(x, w, s, p, shift, cfg=cfg)
-    yr, psr, pssr = _ref.conv_fwd(x.float(), w.float(), s, p, shift)
-    assert rel_err(y, yr) < 1e-2
-    assert rel_err(ps.sum(0), psr[0]) < 2e-3 and rel_err(pss.sum(0), pssr[0]) < 2e-3
+    yr, psr, pssr = _ref.conv_fwd(R(x), R(w), s, p, R(shift))
+    assert y.dtype == dt and rel_err(y, yr) < TOL_OUT[dt]
+    assert rel_err(ps.sum(0), psr[0]) < TOL_ACC[dt] and rel_err(pss.sum(0), pssr[0]) < TOL_ACC[dt]
     bias = torch.randn(Co, device=dev) * 0.1
     yb = native().conv_fwd(x, w, s, p, None, bias=bias, relu=True, cfg=cfg)[0]
-    assert rel_err(yb, torch.relu(yr + bias)) < 1e-2
-    dy = bf(N, Ho, Wo, Co)
+    assert rel_err(yb, torch.relu(yr + R(bias))) < TOL_OUT[dt]
+    dy = rnd(dt, N, Ho, Wo, Co)
     dx = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, cfg=cfg)
-    dxr = _ref.conv_dgrad(dy.float(), w.float(), (N, H, W, Ci), s, p)
-    assert rel_err(dx, dxr) < 1e-2
+    dxr = _ref.conv_dgrad(R(dy), R(w), (N, H, W, Ci), s, p)
+    assert dx.dtype == dt and rel_err(dx, dxr) < TOL_OUT[dt]
     # fused epilogue: dx of relu(bn(yin)) with residual addend, BN-backward sums
-    yin = bf(N, H, W, Ci)
-    add = bf(N, H, W, Ci)
+    yin = rnd(dt, N, H, W, Ci)
+    add = rnd(dt, N, H, W, Ci)
     mean = torch.randn(Ci, device=dev) * 0.1
     invstd = torch.rand(Ci, device=dev) + 0.5
     scale = torch.rand(Ci, device=dev) + 0.5
@@ -668,21 +699,23 @@ def test_conv_every_tile_config(cfg, case):
     g = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, add, yin, mean, invstd, scale, bias, rep,
                             cfg=cfg)
     sg, sgx = native().bn_bwd_collect(rep, Ci)
-    gr = (dxr + add.float()) * ((yin.float() * scale + bias) > 0)
-    assert rel_err(g, gr) < 1e-2
-    grb = gr.to(torch.bfloat16).float()
-    # sums of the stored bf16 g: the kernel's g and the reference's differ by bf16 rounding of
-    # slightly different dx, so the bound is the bf16 sum noise, not fp32's
-    assert rel_err(sg, grb.reshape(-1, Ci).sum(0)) < 8e-3
-    xhat = (yin.float() - mean) * invstd
-    assert rel_err(sgx, (grb * xhat).reshape(-1, Ci).sum(0)) < 8e-3
-    dwr = _ref.conv_wgrad(dy.float(), x.float(), k, k, s, p)
-    for sp in (0, 1, 3):  # weight-grad plans: heuristic split, unsplit (read-modify-write), 3-way
+    gr = (dxr + R(add)) * ((R(yin) * R(scale) + R(bias)) > 0)
+    assert rel_err(g, gr) < TOL_OUT[dt]
+    # sums of the stored g: in bf16 the kernel's g and the reference's differ by bf16 rounding
+    # of slightly different dx, so the bound is the bf16 sum noise, not fp32's
+    grb = gr if f32 else gr.to(torch.bfloat16).float()
+    xhat = (R(yin) - R(mean)) * R(invstd)
+    tol_sum = 1e-4 if f32 else 8e-3
+    assert rel_err(sg, grb.reshape(-1, Ci).sum(0)) < tol_sum
+    assert rel_err(sgx, (grb * xhat).reshape(-1, Ci).sum(0)) < tol_sum
+    dwr = _ref.conv_wgrad(R(dy), R(x), k, k, s, p)
+    # weight-grad plans: heuristic split, unsplit (read-modify-write), 3 / 6 / 12-way split
+    for sp in (0, 1, 3, 6, 12):
         dw = native().conv_wgrad(dy, x, k, k, s, p, cfg=cfg + 16 * sp)
-        assert rel_err(dw, dwr) < 5e-3, sp
+        assert rel_err(dw, dwr) < TOL_WGRAD[dt], sp
         acc = torch.ones_like(dw)
         native().conv_wgrad(dy, x, k, k, s, p, acc, cfg=cfg + 16 * sp)
-        assert rel_err(acc - 1, dwr) < 5e-3, sp
+        assert rel_err(R(acc) - 1, dwr) < TOL_WGRAD[dt], sp
 
 
 def test_tile_benchmark_mode_picks_and_caches():
