@@ -129,7 +129,11 @@ class CustomTrainingJob:
             base_output_dir: Optional[str] = None, model_display_name: Optional[str] = None,
             environment_variables: Optional[Dict[str, str]] = None, sync: bool = True,
             timeout: Optional[float] = None, nproc_per_node: Optional[int] = None,
-            **_: Any) -> Optional[Model]:
+            gpu_visibility: str = "auto", **_: Any) -> Optional[Model]:
+        """``gpu_visibility`` (mipipe extension, launch/env.py): "slice" = each replica sees
+        only its ``accelerator_count`` GPUs (a Vertex VM; default when replicas share the
+        node), "all" = every GPU visible, slice named by MIPIPE_DEVICE_OFFSET (xGMI P2P across
+        replicas; for mipipe-aware scripts)."""
         if replica_count < 1:
             raise ValueError("replica_count must be >= 1")
         base = (base_output_dir or f"{self.staging_bucket.rstrip('/')}/"
@@ -152,7 +156,7 @@ class CustomTrainingJob:
                           checkpoint_dir=f"{base}/checkpoints/",
                           tensorboard_dir=f"{base}/logs/",
                           log_dir=uri_to_local_path(f"{base}/logs"), timeout=timeout,
-                          cwd=os.path.dirname(script))
+                          cwd=os.path.dirname(script), gpu_visibility=gpu_visibility)
         self.last_launch = spec
         record = {"displayName": self.display_name, "containerUri": self.container_uri,
                   "machineType": machine_type, "acceleratorType": accel,

@@ -8,11 +8,14 @@ every replica with the rendezvous env contract task.py consumes — ``WORLD_SIZE
 (``RANK``/``LOCAL_RANK``/``WORLD_SIZE``/``LOCAL_WORLD_SIZE`` per GPU rank).
 
 MI355X specifics: each replica OWNS a disjoint slice of the node's GPUs (one process per GPU is
-the RCCL/xGMI sweet spot) but every process still SEES all of them: RCCL's xGMI P2P/IPC
-transport needs the peers visible.  The slice is passed as ``MIPIPE_DEVICE_OFFSET`` /
-``MIPIPE_LOCAL_GPUS`` and the rank picks ``cuda:(offset + local index)`` — the one policy of
-:mod:`mipipe.launch.env`, shared with ``bench.py``'s launcher.  ``HSA_ENABLE_IPC_MODE_LEGACY=0``
-is forced so RCCL's dmabuf IPC works.
+the RCCL/xGMI sweet spot).  ``gpu_visibility`` picks how the slice is presented
+(:mod:`mipipe.launch.env`): ``"slice"`` narrows ``HIP_VISIBLE_DEVICES`` to the replica's GPUs
+(what a Vertex VM looks like: the unmodified reference task.py, which counts
+``torch.cuda.device_count()`` GPUs (task.py:102), stays on its slice); ``"all"`` keeps every GPU
+visible and names the slice by ``MIPIPE_DEVICE_OFFSET`` / ``MIPIPE_LOCAL_GPUS`` (RCCL's xGMI
+P2P/IPC transport needs the peers visible — opt-in for mipipe-aware programs).  ``"auto"``
+(default) is "slice" unless one replica owns every GPU, or ``MIPIPE_GPU_VISIBILITY`` says
+otherwise.  ``HSA_ENABLE_IPC_MODE_LEGACY=0`` is forced so RCCL's dmabuf IPC works.
 
 Failure semantics: fail-fast — the first replica that exits non-zero causes
 every other replica's process group to get SIGTERM, then SIGKILL after a grace period; the
@@ -87,6 +90,7 @@ class LaunchSpec:
     timeout: Optional[float] = None
     grace_period: float = 10.0
     cwd: Optional[str] = None
+    gpu_visibility: str = "auto"            # "auto" | "slice" | "all" (see module docstring)
 
 
 @dataclass
@@ -127,6 +131,13 @@ def build_envs(spec: LaunchSpec) -> List[Dict[str, str]]:
     if per_replica and total_needed > len(gpus):
         raise RuntimeError(f"job needs {spec.replica_count}x{per_replica}={total_needed} GPUs, "
                            f"node exposes {len(gpus)} ({gpus})")
+    mode = spec.gpu_visibility
+    if mode == "auto":
+        mode = os.environ.get("MIPIPE_GPU_VISIBILITY", "auto")
+    if mode == "auto":
+        mode = "all" if (not per_replica or total_needed == len(gpus)) else "slice"
+    if mode not in ("slice", "all"):
+        raise ValueError(f"gpu_visibility must be auto, slice or all, not {mode!r}")
     port = spec.master_port or free_port()
     envs = []
     procs_per_replica = nproc or 1
@@ -140,8 +151,10 @@ def build_envs(spec: LaunchSpec) -> List[Dict[str, str]]:
                            local_world=procs_per_replica, group_rank=r)
             else:  # one process per replica that spawns its GPU workers (task.py:117-124)
                 ids = dict(world=spec.replica_count, rank=r)
+            own = gpus[r * per_replica:(r + 1) * per_replica]
             e = rank_env(os.environ, master_addr=spec.master_addr, master_port=port,
                          gpu_offset=r * per_replica, replica_gpus=per_replica, extra=spec.env,
+                         visible=",".join(own) if (mode == "slice" and per_replica) else None,
                          **ids)
             if spec.model_dir:
                 e["AIP_MODEL_DIR"] = spec.model_dir

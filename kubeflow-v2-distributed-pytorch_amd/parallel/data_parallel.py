@@ -189,7 +189,13 @@ class DataParallel(tnn.Module):
         self.module = module
         self.dim = dim
         if device_ids is None:
-            device_ids = list(range(torch.cuda.device_count())) if torch.cuda.is_available() else []
+            # the replica's own GPUs when a launcher named a slice (launch/env.py), else every
+            # visible device (torch.nn.DataParallel's default, task.py:204)
+            from mipipe.launch.env import local_device_ids
+            device_ids = local_device_ids()
+            if device_ids is None:
+                device_ids = (list(range(torch.cuda.device_count())) if torch.cuda.is_available()
+                              else [])
         self.device_ids = list(device_ids)
         self.devices: List[torch.device] = [_as_device(d) for d in self.device_ids]
         self.output_device = (_as_device(output_device) if output_device is not None

@@ -217,8 +217,8 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def _ngpus() -> int:
-    """GPUs of this node (replica): the launcher's MIPIPE_LOCAL_GPUS when it set one (every GPU
-    of the node stays visible, launch/env.py), else every visible device."""
+    """GPUs of this node (replica): the launcher's MIPIPE_LOCAL_GPUS when it set one
+    (launch/env.py), else every visible device."""
     if os.environ.get("MIPIPE_FORCE_CPU") == "1":
         return 0
     n = local_gpus()
@@ -333,8 +333,8 @@ def main_worker(gpu, ngpus_per_node, args) -> dict:
         model = DistributedDataParallel(model, device_ids=[device.index] if use_gpu else None,
                                         bucket_cap_mb=args.bucket_cap_mb,
                                         broadcast_buffers=not args.no_broadcast_buffers)
-    elif use_gpu and args.gpu is None and torch.cuda.device_count() > 1:
-        model = DataParallel(model)  # task.py:201-208 path (d)
+    elif use_gpu and args.gpu is None and _ngpus() > 1:
+        model = DataParallel(model)  # task.py:201-208 path (d), on this replica's GPUs
     criterion = CrossEntropyLoss().to(device)
     optimizer = SGD(model.parameters(), args.learning_rate, momentum=args.momentum,
                     weight_decay=args.weight_decay,

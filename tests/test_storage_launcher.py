@@ -37,25 +37,71 @@ def test_google_alias():
 
 def test_env_contract(monkeypatch):
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    monkeypatch.delenv("MIPIPE_GPU_VISIBILITY", raising=False)
     envs = build_envs(LaunchSpec(command=["x"], replica_count=3, accelerator_count=2,
                                  model_dir="gs://b/m/"))
     assert [e["RANK"] for e in envs] == ["0", "1", "2"]
     assert all(e["WORLD_SIZE"] == "3" for e in envs)
-    # every replica sees the whole node (RCCL xGMI P2P) and owns a slice of it
-    assert all(e["HIP_VISIBLE_DEVICES"] == "0,1,2,3,4,5,6,7" for e in envs)
+    # default (replicas share the node): each replica SEES only its own slice, like a Vertex VM
+    assert [e["HIP_VISIBLE_DEVICES"] for e in envs] == ["0,1", "2,3", "4,5"]
     assert [(e["MIPIPE_DEVICE_OFFSET"], e["MIPIPE_LOCAL_GPUS"]) for e in envs] == \
-        [("0", "2"), ("2", "2"), ("4", "2")]
+        [("0", "2"), ("0", "2"), ("0", "2")]
     assert all(e["AIP_MODEL_DIR"] == "gs://b/m/" for e in envs)
     assert all(e["MASTER_ADDR"] == "127.0.0.1" for e in envs)
     assert len({e["MASTER_PORT"] for e in envs}) == 1
+    # opt-in "all": every replica sees the whole node (RCCL xGMI P2P) and owns a slice of it
+    envs = build_envs(LaunchSpec(command=["x"], replica_count=3, accelerator_count=2,
+                                 gpu_visibility="all"))
+    assert all(e["HIP_VISIBLE_DEVICES"] == "0,1,2,3,4,5,6,7" for e in envs)
+    assert [(e["MIPIPE_DEVICE_OFFSET"], e["MIPIPE_LOCAL_GPUS"]) for e in envs] == \
+        [("0", "2"), ("2", "2"), ("4", "2")]
+    monkeypatch.setenv("MIPIPE_GPU_VISIBILITY", "all")
+    assert build_envs(LaunchSpec(command=["x"], replica_count=3, accelerator_count=2))[1][
+        "MIPIPE_DEVICE_OFFSET"] == "2"
+    monkeypatch.delenv("MIPIPE_GPU_VISIBILITY")
     envs = build_envs(LaunchSpec(command=["x"], replica_count=2, accelerator_count=4,
                                  nproc_per_node=4))
     assert [e["RANK"] for e in envs] == [str(i) for i in range(8)]
     assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"] * 2
+    # two replicas x 4 GPUs own the whole node: nothing to hide, xGMI P2P between all ranks
     assert envs[5]["HIP_VISIBLE_DEVICES"] == "0,1,2,3,4,5,6,7"
     assert envs[5]["MIPIPE_DEVICE_OFFSET"] == "4" and envs[5]["LOCAL_RANK"] == "1"  # -> cuda:5
+    envs = build_envs(LaunchSpec(command=["x"], replica_count=1, accelerator_count=2,
+                                 nproc_per_node=2))
+    assert [e["HIP_VISIBLE_DEVICES"] for e in envs] == ["0,1", "0,1"]
     cpu = build_envs(LaunchSpec(command=["x"], replica_count=2, accelerator_count=0))
     assert all(e["MIPIPE_FORCE_CPU"] == "1" and e["HIP_VISIBLE_DEVICES"] == "" for e in cpu)
+    with pytest.raises(ValueError):
+        build_envs(LaunchSpec(command=["x"], replica_count=1, accelerator_count=2,
+                              gpu_visibility="some"))
+
+
+def test_device_count_worker_stays_on_its_slice(tmp_path, monkeypatch):
+    """The unmodified reference task.py sizes its mp.spawn by torch.cuda.device_count()
+    (task.py:102); under the default visibility every replica of the 3 x 2 topology must count
+    exactly its 2 GPUs and no two replicas may share one.  (No GPU here: the worker counts the
+    devices HIP would enumerate from its HIP_VISIBLE_DEVICES.)  mipipe's own consumers name the
+    same slice through local_device_ids()."""
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    monkeypatch.delenv("MIPIPE_GPU_VISIBILITY", raising=False)
+    out = tmp_path / "out"
+    out.mkdir()
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import os, sys\n"
+        "vis = [v for v in os.environ['HIP_VISIBLE_DEVICES'].split(',') if v]\n"
+        "ngpus_per_node = len(vis)  # what torch.cuda.device_count() returns under it\n"
+        "from mipipe.launch.env import local_device_ids\n"
+        "own = [vis[i] for i in local_device_ids()]\n"
+        f"open(os.path.join({str(out)!r}, os.environ['RANK']), 'w').write("
+        "f'{ngpus_per_node} ' + ','.join(own))\n")
+    rc = launch(LaunchSpec(command=[sys.executable, str(script)], replica_count=3,
+                           accelerator_count=2, echo=False,
+                           env={"PYTHONPATH": os.path.dirname(os.path.dirname(__file__))}))
+    assert rc == 0
+    got = [(out / str(r)).read_text().split() for r in range(3)]
+    assert [int(g[0]) for g in got] == [2, 2, 2]
+    assert [g[1] for g in got] == ["0,1", "2,3", "4,5"]
 
 
 def test_launchers_share_one_env_builder(monkeypatch):
