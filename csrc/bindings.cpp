@@ -1379,14 +1379,17 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>, optional<Tensor>> layerno
 // ordered (or deterministic mode): no float atomics — large tables through a stable sort of the
 // ids and one writer per row (embedding_bwd_sorted), small tables through per-block partial
 // tables summed in block order.  scale multiplies the scattered rows (ordered path only).
+// sorted_ids / perm: a stable sort of idx computed ahead (DDP sorts the world's ids during the
+// forward); ids may then be negative (padding rows: skipped).
 Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows, optional<Tensor> out, bool ordered,
-                     double scale) {
+                     double scale, optional<Tensor> sorted_ids, optional<Tensor> perm) {
   check_bf16(dy, "dy");
   check_cuda(idx, "idx");
   c10::DeviceGuard g(dy.device());
   int64_t H = dy.size(-1), n = dy.numel() / H;
   TORCH_CHECK(idx.numel() == n && idx.scalar_type() == at::kLong, "embedding_bwd idx mismatch");
   TORCH_CHECK(H % 8 == 0 && H <= 2048, "embedding_bwd needs H % 8 == 0, H <= 2048");
+  TORCH_CHECK(sorted_ids.has_value() == perm.has_value(), "embedding_bwd: sorted_ids with perm");
   Tensor o;
   if (out.has_value()) {  // accumulate into (e.g. the flat-gradient view of the table)
     check_f32(*out, "out");
@@ -1395,22 +1398,34 @@ Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows, optional<Tensor> o
   } else {
     o = torch::zeros({num_rows, H}, dy.options().dtype(at::kFloat));
   }
-  const bool det = ordered || mipipe::g_deterministic;
+  const bool pre = sorted_ids.has_value();
+  const bool det = ordered || mipipe::g_deterministic || pre;
   TORCH_CHECK(scale == 1.0 || det, "embedding_bwd: scale needs the ordered path");
   if (det && n > 0) {
     auto dyc = dy.contiguous();
-    if (num_rows <= 8) {
+    if (num_rows <= 8 && !pre) {
       auto part = torch::empty({mipipe::embedding_bwd_small_blocks(n), num_rows * H},
                                dy.options().dtype(at::kFloat));
       if (scale != 1.0) dyc = (dyc.to(at::kFloat) * scale).to(at::kBFloat16);
       mipipe::embedding_bwd(dyc.data_ptr(), idx.data_ptr<int64_t>(), o.data_ptr<float>(), n,
                             (int)H, (int)num_rows, stream(), part.data_ptr<float>());
     } else {
-      auto srt = at::sort(idx.reshape({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
-      auto sid = std::get<0>(srt).contiguous();
-      auto perm = std::get<1>(srt).contiguous();
-      mipipe::embedding_bwd_sorted(dyc.data_ptr(), sid.data_ptr<int64_t>(),
-                                   perm.data_ptr<int64_t>(), o.data_ptr<float>(), n, (int)H,
+      Tensor sid, pm;
+      if (pre) {
+        sid = sorted_ids->contiguous();
+        pm = perm->contiguous();
+        TORCH_CHECK(sid.numel() == n && pm.numel() == n && sid.scalar_type() == at::kLong &&
+                        pm.scalar_type() == at::kLong && sid.is_cuda() && pm.is_cuda(),
+                    "embedding_bwd: sorted_ids / perm must be int64 [n] on the GPU");
+      } else {
+        auto srt = at::sort(idx.reshape({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
+        sid = std::get<0>(srt).contiguous();
+        pm = std::get<1>(srt).contiguous();
+      }
+      auto ws = torch::empty({mipipe::embedding_bwd_sorted_ws_floats(n, (int)H)},
+                             dy.options().dtype(at::kFloat));
+      mipipe::embedding_bwd_sorted(dyc.data_ptr(), sid.data_ptr<int64_t>(), pm.data_ptr<int64_t>(),
+                                   o.data_ptr<float>(), ws.data_ptr<float>(), n, (int)H,
                                    (float)scale, stream());
     }
     return o;
@@ -1893,7 +1908,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dbeta") = py::none(), py::arg("drop_p") = 0.0, py::arg("drop_seed") = 0,
         py::arg("drop_seed_dev") = py::none(), py::arg("dbias") = py::none());
   m.def("embedding_bwd", &embedding_bwd, py::arg("dy"), py::arg("idx"), py::arg("num_rows"),
-        py::arg("out") = py::none(), py::arg("ordered") = false, py::arg("scale") = 1.0);
+        py::arg("out") = py::none(), py::arg("ordered") = false, py::arg("scale") = 1.0,
+        py::arg("sorted_ids") = py::none(), py::arg("perm") = py::none());
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(),
         py::arg("two_pass") = false);
   m.def("set_colsum_row_blocks", [](int v) { mipipe::g_colsum_row_blocks = v; });

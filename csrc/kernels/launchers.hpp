@@ -385,10 +385,13 @@ void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H
                    hipStream_t st, float* partial = nullptr);
 int embedding_bwd_small_blocks(long n);
 // Deterministic scatter-add: out[sorted_ids[i]] += scale * dy[perm[i]], tokens stably sorted by
-// id (perm: their positions); one writer per output row, rows summed in position order.
+// id (perm: their positions); one writer per output row, rows summed in position order in
+// fixed 64-entry chunks (long runs in parallel, then the chunk partials in order).  ws:
+// embedding_bwd_sorted_ws_floats(n, H) floats of scratch.  Negative ids are skipped.
 // H % 8 == 0, H <= 2048.
+long embedding_bwd_sorted_ws_floats(long n, int H);
 void embedding_bwd_sorted(const void* dy, const int64_t* sorted_ids, const int64_t* perm,
-                          float* out, long n, int H, float scale, hipStream_t st);
+                          float* out, float* ws, long n, int H, float scale, hipStream_t st);
 // work (deterministic mode, else null): [colsum_blocks(rows, cols)][cols] floats of partials
 void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float* work,
                 hipStream_t st);

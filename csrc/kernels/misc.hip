@@ -712,71 +712,150 @@ __global__ __launch_bounds__(256) void embedding_bwd_small_kernel(
 }
 
 // Deterministic scatter-add over tokens SORTED by row id (stable sort: position order inside a
-// run of equal ids).  One wave per sorted index; the wave that starts a run sums the run's dy
-// rows in that order (8 bf16 columns per 16-B chunk, NC chunks per lane, four rows of loads in
-// flight) and adds scale * sum to its output row — exactly one writer per row, no atomics, so
-// the result is bit-identical run to run and on every rank that scatters the same tokens.
+// run of equal ids), in fixed-size CHUNKS of kEmbChunk sorted entries — one wave per chunk — so
+// a long run of one id (the [PAD] token of a padded batch: thousands of rows) is summed by many
+// waves in parallel instead of serially by one:
+//   pass 1: each wave sums the runs of its chunk in position order (8 bf16 columns per 16-B
+//           chunk, NC chunks per lane, four rows of loads in flight).  A run that lies wholly
+//           inside the chunk is added (x scale) to its output row — its only writer.  A run
+//           that enters from the previous chunk leaves its partial in ws[chunk][0] (head), one
+//           that continues into the next chunk in ws[chunk][1] (tail); a chunk covered by one
+//           run that does both uses the head slot.
+//   pass 2: the wave of the chunk where a crossing run STARTS adds its tail partial and the
+//           head partials of the following chunks, in chunk order, and writes the row.
+// Every output row has exactly one writer and a fixed summation order: bit-identical run to run
+// and on every rank that scatters the same tokens.  Negative ids (padding of a fixed-capacity
+// exchange, parallel/ddp.py) sort first and are skipped.
+constexpr int kEmbChunk = 64;
+
+template <int NC>
+__device__ __forceinline__ void emb_add_row(float* __restrict__ o, const float (&acc)[NC][8],
+                                            int lane, int nch, float scale) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      float* q = o + ch * 8;
+      const float4 a = reinterpret_cast<float4*>(q)[0], b = reinterpret_cast<float4*>(q)[1];
+      reinterpret_cast<float4*>(q)[0] = make_float4(a.x + scale * acc[c][0], a.y + scale * acc[c][1],
+                                                    a.z + scale * acc[c][2], a.w + scale * acc[c][3]);
+      reinterpret_cast<float4*>(q)[1] = make_float4(b.x + scale * acc[c][4], b.y + scale * acc[c][5],
+                                                    b.z + scale * acc[c][6], b.w + scale * acc[c][7]);
+    }
+  }
+}
+
+template <int NC>
+__device__ __forceinline__ void emb_store_row(float* __restrict__ o, const float (&acc)[NC][8],
+                                              int lane, int nch) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      reinterpret_cast<float4*>(o + ch * 8)[0] =
+          make_float4(acc[c][0], acc[c][1], acc[c][2], acc[c][3]);
+      reinterpret_cast<float4*>(o + ch * 8)[1] =
+          make_float4(acc[c][4], acc[c][5], acc[c][6], acc[c][7]);
+    }
+  }
+}
+
 template <int NC>
 __global__ __launch_bounds__(256) void embedding_bwd_sorted_kernel(
     const __bf16* __restrict__ dy, const int64_t* __restrict__ sid,
-    const int64_t* __restrict__ perm, float* __restrict__ out, long n, int H, float scale) {
-  const long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t* __restrict__ perm, float* __restrict__ out, float* __restrict__ ws, long n,
+    int H, float scale) {
+  const long chunk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (i >= n) return;
-  const int64_t id = sid[i];
-  if (i > 0 && sid[i - 1] == id) return;  // not the start of a run
+  const long c0 = chunk * kEmbChunk;
+  if (c0 >= n) return;
+  const long c1 = min(n, c0 + kEmbChunk);
+  const int nch = H / 8;
+  long i = c0;
+  while (i < c1) {
+    const int64_t id = sid[i];
+    long e = i + 1;
+    while (e < c1 && sid[e] == id) ++e;
+    if (id >= 0) {
+      float acc[NC][8];
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[c][q] = 0.f;
+      for (long j = i; j < e; j += 4) {
+        long p[4];
+        const int cnt = (int)min<long>(4, e - j);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) p[u] = perm[u < cnt ? j + u : j];
+        uint4 v[4][NC];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            const int ch = lane + 64 * c;
+            v[u][c] = ch < nch ? *reinterpret_cast<const uint4*>(dy + p[u] * H + ch * 8)
+                               : make_uint4(0, 0, 0, 0);
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (u < cnt) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+              float f[8];
+              unpack8(v[u][c], f);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) acc[c][q] += f[q];
+            }
+          }
+        }
+      }
+      const bool head = i == c0 && c0 > 0 && sid[c0 - 1] == id;
+      const bool tail = e == c1 && c1 < n && sid[c1] == id;
+      if (!head && !tail) emb_add_row<NC>(out + id * H, acc, lane, nch, scale);
+      else emb_store_row<NC>(ws + (chunk * 2 + (head ? 0 : 1)) * H, acc, lane, nch);
+    }
+    i = e;
+  }
+}
+
+template <int NC>
+__global__ __launch_bounds__(256) void embedding_bwd_sorted_fix_kernel(
+    const int64_t* __restrict__ sid, const float* __restrict__ ws, float* __restrict__ out,
+    long n, int H, float scale) {
+  const long chunk = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const long c0 = chunk * kEmbChunk;
+  if (c0 >= n) return;
+  const long c1 = min(n, c0 + kEmbChunk);
+  if (c1 >= n) return;
+  const int64_t id = sid[c1 - 1];
+  if (id < 0 || sid[c1] != id) return;                   // the chunk's last run ends inside it
+  if (c0 > 0 && sid[c0] == id && sid[c0 - 1] == id) return;  // started before: not its owner
   const int nch = H / 8;
   float acc[NC][8];
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[c][e] = 0.f;
-  long j = i;
-  while (j < n && sid[j] == id) {
-    // up to four rows of this run per iteration, all loads issued before the adds (in order)
-    long p[4];
-    int cnt = 0;
+    for (int q = 0; q < 8; ++q) acc[c][q] = 0.f;
+  auto add = [&](const float* src) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const bool in = j + u < n && sid[j + u] == id;
-      p[u] = in ? perm[j + u] : perm[j];
-      cnt += in ? 1 : 0;
-    }
-    uint4 v[4][NC];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int ch = lane + 64 * c;
-        v[u][c] = ch < nch ? *reinterpret_cast<const uint4*>(dy + p[u] * H + ch * 8)
-                           : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (u < cnt) {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          float f[8];
-          unpack8(v[u][c], f);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) acc[c][e] += f[e];
-        }
+    for (int c = 0; c < NC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        const float4 a = reinterpret_cast<const float4*>(src + ch * 8)[0];
+        const float4 b = reinterpret_cast<const float4*>(src + ch * 8)[1];
+        acc[c][0] += a.x; acc[c][1] += a.y; acc[c][2] += a.z; acc[c][3] += a.w;
+        acc[c][4] += b.x; acc[c][5] += b.y; acc[c][6] += b.z; acc[c][7] += b.w;
       }
     }
-    j += cnt;
+  };
+  add(ws + (chunk * 2 + 1) * H);                          // this chunk's tail partial
+  for (long k = chunk + 1;; ++k) {                         // following chunks' head partials
+    add(ws + (k * 2) * H);
+    const long k1 = min(n, (k + 1) * kEmbChunk);
+    if (k1 >= n || sid[k1] != id) break;                   // the run ends inside chunk k
   }
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int ch = lane + 64 * c;
-    if (ch < nch) {
-      float* o = out + id * H + ch * 8;
-      const float4 a = reinterpret_cast<float4*>(o)[0], b = reinterpret_cast<float4*>(o)[1];
-      reinterpret_cast<float4*>(o)[0] = make_float4(a.x + scale * acc[c][0], a.y + scale * acc[c][1],
-                                                    a.z + scale * acc[c][2], a.w + scale * acc[c][3]);
-      reinterpret_cast<float4*>(o)[1] = make_float4(b.x + scale * acc[c][4], b.y + scale * acc[c][5],
-                                                    b.z + scale * acc[c][6], b.w + scale * acc[c][7]);
-    }
-  }
+  emb_add_row<NC>(out + id * H, acc, lane, nch, scale);
 }
 
 int embedding_bwd_small_blocks(long n) {
@@ -800,19 +879,26 @@ void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H
                      (const __bf16*)dy, idx, out, n, H);
 }
 
+long embedding_bwd_sorted_ws_floats(long n, int H) {
+  return ((n + kEmbChunk - 1) / kEmbChunk) * 2 * (long)H;
+}
+
 void embedding_bwd_sorted(const void* dy, const int64_t* sorted_ids, const int64_t* perm,
-                          float* out, long n, int H, float scale, hipStream_t st) {
-  const unsigned g = (unsigned)((n + 3) / 4);
+                          float* out, float* ws, long n, int H, float scale, hipStream_t st) {
+  const long chunks = (n + kEmbChunk - 1) / kEmbChunk;
+  const unsigned g = (unsigned)((chunks + 3) / 4);
   const int nc = (H / 8 + 63) / 64;
-  if (nc <= 1)
-    hipLaunchKernelGGL(embedding_bwd_sorted_kernel<1>, dim3(g), dim3(256), 0, st,
-                       (const __bf16*)dy, sorted_ids, perm, out, n, H, scale);
-  else if (nc == 2)
-    hipLaunchKernelGGL(embedding_bwd_sorted_kernel<2>, dim3(g), dim3(256), 0, st,
-                       (const __bf16*)dy, sorted_ids, perm, out, n, H, scale);
-  else
-    hipLaunchKernelGGL(embedding_bwd_sorted_kernel<4>, dim3(g), dim3(256), 0, st,
-                       (const __bf16*)dy, sorted_ids, perm, out, n, H, scale);
+  auto go = [&](auto tag) {
+    constexpr int NC = decltype(tag)::value;
+    hipLaunchKernelGGL(embedding_bwd_sorted_kernel<NC>, dim3(g), dim3(256), 0, st,
+                       (const __bf16*)dy, sorted_ids, perm, out, ws, n, H, scale);
+    if (chunks > 1)
+      hipLaunchKernelGGL(embedding_bwd_sorted_fix_kernel<NC>, dim3(g), dim3(256), 0, st,
+                         sorted_ids, (const float*)ws, out, n, H, scale);
+  };
+  if (nc <= 1) go(std::integral_constant<int, 1>());
+  else if (nc == 2) go(std::integral_constant<int, 2>());
+  else go(std::integral_constant<int, 4>());
 }
 
 // ------------------------------------------------------------------------------ dropout hash

@@ -1172,4 +1172,7 @@ class _EmbeddingFn(Function):
 
 
 def embedding(idx: Tensor, weight: Tensor, w_c: Tensor) -> Tensor:
+    sink = getattr(weight, "_mipipe_sparse_sink", None)
+    if sink is not None and weight.requires_grad and torch.is_grad_enabled():
+        sink.on_forward(idx)  # DDP: the ids' all_gather starts with the forward
     return _EmbeddingFn.apply(idx, weight, w_c)

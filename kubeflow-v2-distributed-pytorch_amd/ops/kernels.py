@@ -472,13 +472,22 @@ def dropout_fwd(x, p, seed):
     return _ref.dropout_fwd(x, p, _host_seed(seed))
 
 
-def embedding_bwd(dy, idx, num_rows, out=None, ordered: bool = False, scale: float = 1.0):
+def embedding_bwd(dy, idx, num_rows, out=None, ordered: bool = False, scale: float = 1.0,
+                  presorted=None):
     """Scatter-add of ``scale`` * dy rows into a [num_rows, H] fp32 table gradient (``out``:
     accumulate into it, e.g. the parameter's flat-gradient view; else a fresh zeroed tensor).
     ``ordered`` (implied in deterministic mode): no float atomics — rows are summed per table row
-    in token order (stable sort of the ids), so the result is bit-reproducible."""
+    in token order (stable sort of the ids), so the result is bit-reproducible.  ``presorted``:
+    (sorted ids, positions) of a stable sort of ``idx`` computed ahead (implies ordered); ids may
+    then be negative — padding rows, skipped."""
     if use_native(dy):
-        return native().embedding_bwd(dy, idx, num_rows, out, bool(ordered), float(scale))
+        sid, perm = presorted if presorted is not None else (None, None)
+        return native().embedding_bwd(dy, idx, num_rows, out, bool(ordered), float(scale),
+                                      sid, perm)
+    if presorted is not None or bool((idx < 0).any()):
+        keep = idx.reshape(-1) >= 0
+        dy = dy.reshape(-1, dy.shape[-1])[keep]
+        idx = idx.reshape(-1)[keep]
     g = _ref.embedding_bwd(dy, idx, num_rows)
     if scale != 1.0:
         g = g * scale

@@ -103,58 +103,124 @@ class _CollectiveLog:
 class _SparseRowExchange:
     """The lookup part of a tied embedding weight's gradient, exchanged as (id, row) pairs.
 
-    Installed as ``param._mipipe_sparse_sink``: the embedding Function's backward hands it the
-    token ids and the per-token gradient rows instead of scattering them (ops/functional.py)."""
+    Installed as ``param._mipipe_sparse_sink``.  The ids are known at FORWARD time, so the
+    embedding op hands them over there (:meth:`on_forward`): their ``all_gather`` is issued at
+    once, and the stable sort of the world's ids that the ordered scatter needs runs on a side
+    stream during the forward (:meth:`after_forward`) — after the last backward kernel only the
+    rows' ``all_gather`` and the scatter are left.  The backward hands over the per-token
+    gradient rows instead of scattering them (ops/functional.py ``_EmbeddingFn``).
+
+    Fixed-capacity protocol: ``all_gather_into_tensor`` needs equal sizes on every rank, so the
+    capacity is agreed once (the largest first-step token count, one host exchange) and every
+    later step pads its ids with -1 (skipped by the scatter) and its rows with zeros up to it.
+    A ragged / dynamically padded batch with fewer tokens therefore still matches; a step with
+    MORE tokens than the capacity raises before issuing any collective.  The capacity is part of
+    the collective digest (``check_collectives``)."""
 
     def __init__(self, ddp: "DistributedDataParallel", param: tnn.Parameter):
         self.ddp = ddp
         self.param = param
         self.pending = None
-        self.checked = False
-        self.sent_bytes = 0  # per rank, last exchange (ids + rows)
+        self.cap: Optional[int] = None
+        self.fwd = None          # {n, ids_all, work, sorted, event} of the current step
+        self.sent_bytes = 0      # per rank, last exchange (ids + rows)
+        self.ids_issued_in_forward = 0  # steps whose ids gather was issued by the forward
+
+    def _active(self) -> bool:
+        return self.ddp._comm and self.ddp._sync_enabled
+
+    def _capacity(self, n: int) -> int:
+        if self.cap is None:
+            ns: List[Optional[int]] = [None] * self.ddp.world
+            dist.all_gather_object(ns, int(n), group=self.ddp.process_group)
+            self.cap = max(int(v) for v in ns)
+        if n > self.cap:
+            raise RuntimeError(
+                f"DDP sparse embedding exchange: {n} tokens this step exceed the capacity of "
+                f"{self.cap} agreed at the first step (all ranks' maximum); build the DDP wrapper "
+                "on the largest batch shape or pass sparse_embedding=False")
+        return self.cap
+
+    def on_forward(self, idx: torch.Tensor) -> None:
+        """Grad-enabled forward of the lookup: issue the ids' all_gather now."""
+        if not self._active():
+            self.fwd = None
+            return
+        idx = idx.reshape(-1)
+        n = int(idx.numel())
+        cap = self._capacity(n)
+        ids = idx if n == cap else torch.cat([idx, idx.new_full((cap - n,), -1)])
+        ddp = self.ddp
+        ids_all = ids.new_empty(ddp.world * cap)
+        ddp._clog.record("all_gather", ids)
+        work = dist.all_gather_into_tensor(ids_all, ids.contiguous(), group=ddp.process_group,
+                                           async_op=True)
+        self.fwd = {"n": n, "ids_all": ids_all, "work": work, "sorted": None, "event": None}
+        self.ids_issued_in_forward += 1
+
+    def after_forward(self) -> None:
+        """Stable-sort the gathered ids (rank order, then position: the scatter's summation
+        order) on a side stream that waits for the gather — off the compute stream's path."""
+        f = self.fwd
+        if f is None or f["sorted"] is not None:
+            return
+        ids_all = f["ids_all"]
+        if not ids_all.is_cuda:
+            f["work"].wait()
+            f["sorted"] = torch.sort(ids_all, stable=True)
+            return
+        from mipipe.ops.functional import _side_stream
+        cur = torch.cuda.current_stream(ids_all.device)
+        side = _side_stream(ids_all)
+        side.wait_stream(cur)  # fork from the compute stream (joins a hipGraph capture too)
+        with torch.cuda.stream(side):
+            f["work"].wait()  # stream semantics: the side stream waits for the gather
+            sid, perm = torch.sort(ids_all, stable=True)
+        for t in (sid, perm):
+            t.record_stream(cur)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        f["sorted"], f["event"] = (sid, perm), ev
 
     def __call__(self, idx: torch.Tensor, dy: torch.Tensor) -> None:
         idx = idx.reshape(-1)
         dy = dy.reshape(-1, dy.shape[-1])
-        ddp = self.ddp
-        if not (ddp._comm and ddp._sync_enabled):  # no_sync(): a local scatter, like no DDP
+        if not self._active():  # no_sync(): a local scatter, like no DDP
             self._scatter(dy, idx, 1.0)
             return
-        self.pending = (idx, dy)
+        if self.fwd is None or self.fwd["n"] != idx.numel():
+            self.on_forward(idx)  # forward ran outside this wrapper: gather the ids now
+        self.after_forward()
+        self.pending = dy
         # after the reducer's end-of-backward callback (queued at the first ready gradient):
         # every bucket, the dense part of this weight included, is reduced by then
         torch.autograd.Variable._execution_engine.queue_callback(self._exchange)
 
-    def _scatter(self, rows, ids, scale):
+    def _scatter(self, rows, ids, scale, presorted=None):
         from mipipe.ops import kernels as K
         from mipipe.optim.flat import flat_space_for
         fs = flat_space_for(self.param)
         K.embedding_bwd(rows.contiguous(), ids.contiguous(), self.param.shape[0],
-                        fs.grad_view(self.param), ordered=True, scale=scale)
+                        fs.grad_view(self.param), ordered=True, scale=scale, presorted=presorted)
 
     def _exchange(self) -> None:
-        idx, dy = self.pending
-        self.pending = None
+        dy, f = self.pending, self.fwd
+        self.pending, self.fwd = None, None
         ddp = self.ddp
         world, pg = ddp.world, ddp.process_group
-        if not self.checked:  # equal token counts on every rank (all_gather_into_tensor needs it)
-            ns: List[Optional[int]] = [None] * world
-            dist.all_gather_object(ns, int(idx.numel()), group=pg)
-            if any(n != ns[0] for n in ns):
-                raise RuntimeError(f"DDP sparse embedding exchange: token counts differ {ns}")
-            self.checked = True
         n, H = dy.shape
-        ids_all = idx.new_empty(world * n)
-        rows_all = dy.new_empty(world * n, H)
-        ddp._clog.record("all_gather", idx)
+        cap = self.cap
+        if n < cap:
+            dy = torch.cat([dy, dy.new_zeros(cap - n, H)])
+        rows_all = dy.new_empty(world * cap, H)
         ddp._clog.record("all_gather", dy)
-        w1 = dist.all_gather_into_tensor(ids_all, idx.contiguous(), group=pg, async_op=True)
-        w2 = dist.all_gather_into_tensor(rows_all, dy.contiguous(), group=pg, async_op=True)
-        w1.wait()  # stream semantics on RCCL: the compute stream waits, the host does not
-        w2.wait()
-        self.sent_bytes = idx.numel() * idx.element_size() + dy.numel() * dy.element_size()
+        w = dist.all_gather_into_tensor(rows_all, dy.contiguous(), group=pg, async_op=True)
+        w.wait()  # stream semantics on RCCL: the compute stream waits, the host does not
+        if f["event"] is not None:
+            torch.cuda.current_stream(dy.device).wait_event(f["event"])
+        self.sent_bytes = cap * (8 + H * dy.element_size())
         # rank order is the all_gather order; the ordered scatter sums equal ids in that order
-        self._scatter(rows_all, ids_all, 1.0 / world)
+        self._scatter(rows_all, f["ids_all"], 1.0 / world, presorted=f["sorted"])
 
 
 class DistributedDataParallel(tnn.Module):
@@ -406,7 +472,10 @@ class DistributedDataParallel(tnn.Module):
             self.require_forward_param_sync = True
         else:
             self.require_forward_param_sync = False
-        return self.module(*args, **kwargs)
+        out = self.module(*args, **kwargs)
+        for ex in self._sparse:
+            ex.after_forward()
+        return out
 
     @contextlib.contextmanager
     def no_sync(self):

@@ -873,6 +873,39 @@ def test_embedding_bwd_ordered(rows, H, n):
     assert rel_err(acc - acc0, 0.125 * ref) < 1e-4
 
 
+@pytest.mark.parametrize("n,pad_frac,run_frac", [(32768, 0.0, 0.3), (32768, 0.25, 0.0),
+                                                  (4096, 0.1, 0.9), (130, 0.0, 1.0),
+                                                  (64, 0.5, 0.0), (65, 0.0, 1.0)])
+def test_embedding_bwd_presorted_chunked(n, pad_frac, run_frac):
+    """The DDP exchange's scatter: ids sorted ahead (presorted), padding rows with id -1
+    (skipped), and one id repeated over a long run spanning many 64-entry chunks (a [PAD]
+    token) — summed in parallel per chunk, then the chunk partials in order.  Equals the
+    float64 reference, bit-identical run to run and to the self-sorting ordered path."""
+    rows, H = 30528, 768
+    dy = bf(n, H)
+    idx = torch.randint(0, rows, (n,), device=dev)
+    idx[: int(n * run_frac)] = 3
+    npad = int(n * pad_frac)
+    if npad:
+        idx[-npad:] = -1
+        dy[-npad:] = float("nan")  # must never be read
+    sid, perm = torch.sort(idx, stable=True)
+    keep = idx >= 0
+    ref = torch.zeros(rows, H, dtype=torch.float64, device=dev)
+    ref.index_add_(0, idx[keep], dy[keep].double())
+    a = torch.zeros(rows, H, device=dev)
+    native().embedding_bwd(dy, idx, rows, a, True, 0.5, sid, perm)
+    b = torch.zeros(rows, H, device=dev)
+    native().embedding_bwd(dy, idx, rows, b, True, 0.5, sid, perm)
+    assert torch.equal(a, b)
+    assert not torch.isnan(a).any()
+    assert rel_err(a, 0.5 * ref) < 1e-6
+    if not npad:
+        c = torch.zeros(rows, H, device=dev)
+        native().embedding_bwd(dy, idx, rows, c, True, 0.5)
+        assert torch.equal(a, c)
+
+
 @pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (640, 768, 768), (200, 136, 72)])
 def test_gemm_gelu_epilogue_matches_gemm_then_gelu(M, N, K):
     """The GELU Linear forward in one GEMM (pre-activation to aux, GELU to the output) ==

@@ -251,3 +251,68 @@ def test_ddp_bert_tied_embedding_not_exposed():
     assert last_mb + pairs_mb <= 8.0, (last_mb, pairs_mb)
     assert r["sent_bytes"] == 2 * 16 * (768 * 4 + 8)  # this CPU step: fp32 rows + ids
     assert not r["grad_errs"], r["grad_errs"]
+
+
+def _ids_in_forward_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mipipe.models import create_model
+    from mipipe.parallel import DistributedDataParallel
+    torch.manual_seed(0)
+    m = create_model("bert_tiny", hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    d = DistributedDataParallel(m)
+    ex = d._sparse[0]
+    V = m.bert.embeddings.word_embeddings.weight.shape[0]
+    res = {}
+
+    def batch(B, S, seed):
+        g = torch.Generator().manual_seed(seed)
+        ids = torch.randint(0, V, (B, S), generator=g)
+        ids[:, :S // 2] = 0  # a [PAD]-like run: one id repeated across many chunks
+        am = torch.ones(B, S, dtype=torch.int64)
+        pos = torch.stack([torch.randperm(S, generator=g)[:3] for _ in range(B)])
+        lab = torch.randint(0, V, (B, 3), generator=g)
+        return ids, am, pos, lab
+
+    ids, am, pos, lab = batch(4, 32, 10 + rank)
+    loss = d(ids, am, masked_positions=pos, labels=lab)
+    # the ids' all_gather was issued by the forward and already sorted: before backward()
+    res["issued_before_backward"] = (ex.fwd is not None and ex.fwd["sorted"] is not None
+                                     and ex.ids_issued_in_forward == 1)
+    loss.backward()
+    res["cap"] = ex.cap
+    # ragged step (fewer tokens on rank 1): padded to the agreed capacity, same collectives
+    B = 4 if rank == 0 else 3
+    ids, am, pos, lab = batch(B, 32, 20 + rank)
+    d.zero_grad() if hasattr(d, "zero_grad") else None
+    d(ids, am, masked_positions=pos, labels=lab).backward()
+    res["ragged_ok"] = ex.ids_issued_in_forward == 2
+    wg = m.bert.embeddings.word_embeddings.weight.grad.clone()
+    gathered = [torch.zeros_like(wg) for _ in range(world)]
+    dist.all_gather(gathered, wg)
+    res["same_on_all_ranks"] = all(torch.equal(gathered[0], x) for x in gathered)
+    # more tokens than the capacity: a clear error before any collective
+    try:
+        ids, am, pos, lab = batch(5, 32, 30)
+        d(ids, am, masked_positions=pos, labels=lab)
+        res["grow_raises"] = False
+    except RuntimeError as e:
+        res["grow_raises"] = "capacity" in str(e)
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_ddp_bert_lookup_ids_exchanged_during_forward():
+    """World 4 (gloo): the tied word embedding's lookup ids are all-gathered and stably sorted
+    during the FORWARD (SURVEY §2.6 C5''): after the last backward kernel only the rows' gather
+    and the scatter remain.  A ragged step with fewer tokens on one rank is padded to the
+    capacity agreed at the first step (same collectives on every rank, identical gradients);
+    more tokens than the capacity raises instead of mismatching the collective."""
+    out = mp.Manager().dict()
+    mp.spawn(_ids_in_forward_worker, args=(4, 29400 + os.getpid() % 400, out), nprocs=4)
+    for r in range(4):
+        assert out[r]["issued_before_backward"], out[r]
+        assert out[r]["cap"] == 4 * 32
+        assert out[r]["ragged_ok"] and out[r]["same_on_all_ranks"], out[r]
+        assert out[r]["grow_raises"], out[r]
