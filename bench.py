@@ -422,15 +422,19 @@ def build_bert(a, world, local, dev, rank):
 
 
 def _capture(GraphedStep, step, batches, a):
-    """Capture the step into hipGraphs; with ``--graph auto`` a capture that fails on ANY rank
+    """Capture the step into hipGraphs; with ``--graph auto`` a CAPTURE that fails on any rank
     makes every rank run eagerly (one MIN all-reduce of a success flag after the attempt —
-    captured collectives never execute during capture, so a failed rank cannot leave peers
-    waiting inside one).  ``--graph on`` re-raises."""
+    captured collectives never execute during capture, so a rank whose capture failed cannot
+    leave peers waiting inside one).  A failure in GraphedStep's eager warm-up steps (real DDP
+    collectives) is not caught: that rank exits non-zero and the launcher's fail-fast ends the
+    job, instead of a MIN all-reduce that would pair with its peers' bucket collectives.
+    ``--graph on`` re-raises."""
     import torch.distributed as dist
+    from mipipe.train.graph import CaptureFailed
     gs, err = None, None
     try:
         gs = GraphedStep(step, batches[0], warmup=max(2, a.warmup), inputs=batches)
-    except Exception as exc:  # noqa: BLE001 — reported, then handled uniformly across ranks
+    except CaptureFailed as exc:  # reported, then handled uniformly across ranks
         err = exc
         if a.graph == "on":
             raise

@@ -96,6 +96,14 @@ def step_stream(device: torch.device) -> "torch.cuda.Stream":
     return _STEP_STREAMS[key]
 
 
+class CaptureFailed(RuntimeError):
+    """The hipGraph CAPTURE of a step failed (its eager warm-up steps succeeded).  Captured
+    collectives never execute during capture, so every rank can still agree to run eagerly;
+    an exception from a warm-up step is NOT wrapped: those steps issue real collectives, and a
+    rank that failed there must exit instead of joining a fallback protocol its peers are not
+    in."""
+
+
 class GraphedStep:
     """Capture ``step_fn(*batch) -> loss`` into hipGraph(s) after ``warmup`` eager steps.
 
@@ -123,16 +131,19 @@ class GraphedStep:
         self.graphs: List[torch.cuda.CUDAGraph] = []
         self.losses: List[torch.Tensor] = []
         pool = None
-        for batch in self.static:
-            g = torch.cuda.CUDAGraph()
-            # thread_local: the process group's watchdog thread may still poll its (retired)
-            # work events while this thread captures; global mode would fail those queries
-            with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode="thread_local"):
-                loss = self.fn(*batch).detach()  # drop the autograd graph: no stale grad nodes
-            pool = g.pool()
-            self.graphs.append(g)
-            self.losses.append(loss)
-        torch.cuda.synchronize(dev)
+        try:
+            for batch in self.static:
+                g = torch.cuda.CUDAGraph()
+                # thread_local: the process group's watchdog thread may still poll its
+                # (retired) work events while this thread captures; global mode would fail them
+                with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode="thread_local"):
+                    loss = self.fn(*batch).detach()  # drop the autograd graph: no stale nodes
+                pool = g.pool()
+                self.graphs.append(g)
+                self.losses.append(loss)
+            torch.cuda.synchronize(dev)
+        except Exception as exc:  # noqa: BLE001 — re-raised as the capture-phase failure
+            raise CaptureFailed(f"hipGraph capture failed: {exc!r}") from exc
 
     def replay(self, i: int = 0) -> torch.Tensor:
         """Run one step on resident batch ``i``; returns the (device) loss."""
