@@ -16,5 +16,5 @@ ARGS="$*"
 pass A SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU || exit 1
 pass B SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE || exit 1
 pass C FETCH_SIZE GRBM_COUNT || exit 1
-python3 "$R/tools/r3/pmc_summary.py" gemm_dense "$O/A" "$O/B" "$O/C" > "$O/summary.txt" 2>&1
+python3 "$R/tools/pmc_summary.py" gemm_dense "$O/A" "$O/B" "$O/C" > "$O/summary.txt" 2>&1
 cat "$O/summary.txt"
