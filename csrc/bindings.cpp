@@ -79,6 +79,11 @@ mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int p
   TORCH_CHECK((int64_t)s.N * s.H * s.W * s.Ci < (1ll << 31) &&
                   (int64_t)s.N * s.Ho * s.Wo * s.Co < (1ll << 31),
               "conv tensors beyond 2^31 elements are not supported");
+  // bf16 operands go through buffer descriptors with 32-bit byte offsets (gemm_core.hpp kOOB)
+  const int64_t esz = x.scalar_type() == at::kFloat ? 4 : 2;
+  TORCH_CHECK(esz == 4 || ((int64_t)s.N * s.H * s.W * s.Ci * esz < (1ll << 31) - (1ll << 24) &&
+                           (int64_t)s.N * s.Ho * s.Wo * s.Co * esz < (1ll << 31) - (1ll << 24)),
+              "bf16 conv tensors beyond 2 GiB are not supported");
   return s;
 }
 
@@ -1030,6 +1035,10 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
     TORCH_CHECK(act_i == 0, "fp32 gemm output has no activation epilogue");
   }
   const bool f32 = is_f32(a);
+  // bf16 operands go through buffer descriptors with 32-bit byte offsets (gemm_core.hpp kOOB)
+  TORCH_CHECK(f32 || ((trans_a ? K : M) * a.stride(0) * 2 < (1ll << 31) - (1ll << 24) &&
+                      (trans_b ? N : K) * b.stride(0) * 2 < (1ll << 31) - (1ll << 24)),
+              "bf16 gemm operands beyond 2 GiB are not supported");
   const void* add_p = nullptr;
   if (addend.has_value()) {
     TORCH_CHECK(mode == 0 && !trans_a && !trans_b && bias_p == nullptr && act_i == 0,

@@ -94,15 +94,43 @@ constexpr int lds_bytes_f32out() {
 }
 
 // Operand-policy families: template <int R, int NW> using type = <policy over R rows, NW waves>.
-template <class T> struct PolKCDense { template <int R, int NW> using type = KCDense<R, T, NW>; };
-template <class T> struct PolMCDense { template <int R, int NW> using type = MCDense<R, T, NW>; };
+// bf16 operands take the buffer-descriptor policies (KCDenseBuf / MCDenseBuf / KCIm2colBuf:
+// fixed per-lane voffsets, k-step in soffset); fp32 operands feed the split-bf16x3 loop through
+// registers and keep the pointer policies.  MIPIPE_NO_BUF_OPERANDS (compile-time) restores the
+// pointer policies everywhere (A/B).
+#ifdef MIPIPE_NO_BUF_OPERANDS
+constexpr bool kBufOperands = false;
+#else
+constexpr bool kBufOperands = true;
+#endif
+template <class T>
+constexpr bool use_buf() { return kBufOperands && !std::is_same<T, float>::value; }
+template <class T> struct PolKCDense {
+  template <int R, int NW>
+  using type = typename std::conditional<use_buf<T>(), KCDenseBuf<R, T, NW>, KCDense<R, T, NW>>::type;
+};
+template <class T> struct PolMCDense {
+  template <int R, int NW>
+  using type = typename std::conditional<use_buf<T>(), MCDenseBuf<R, T, NW>, MCDense<R, T, NW>>::type;
+};
+// the buffer im2col needs the ALIGNED tap-uniform k-steps and a <= 32-tap mask; the host sends
+// larger filters (KH*KW > 32) down the unaligned pointer path (conv_fwd.hip)
 template <bool AL, class T> struct PolKCIm2col {
-  template <int R, int NW> using type = KCIm2col<R, AL, T, NW>;
+  template <int R, int NW>
+  using type = typename std::conditional<AL && use_buf<T>(), KCIm2colBuf<R, T, NW>,
+                                         KCIm2col<R, AL, T, NW>>::type;
 };
+// the buffer data-grad operands need Co % 64 == 0 (ALIGNED) and <= 32 class taps
 template <bool AL, class T> struct PolKCDgrad {
-  template <int R, int NW> using type = KCDgrad<R, AL, T, NW>;
+  template <int R, int NW>
+  using type = typename std::conditional<AL && use_buf<T>(), KCDgradBuf<R, T, NW>,
+                                         KCDgrad<R, AL, T, NW>>::type;
 };
-template <class T> struct PolMCDgradW { template <int R, int NW> using type = MCDgradW<R, T, NW>; };
+template <bool AL, class T> struct PolMCDgradW {
+  template <int R, int NW>
+  using type = typename std::conditional<AL && use_buf<T>(), MCDgradWBuf<R, T, NW>,
+                                         MCDgradW<R, T, NW>>::type;
+};
 template <class T> struct PolMCIm2colT {
   template <int R, int NW> using type = MCIm2colT<R, T, NW>;
 };
@@ -188,7 +216,7 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_dgrad_ker
     FastDiv fCo, DgradClass cls, uint32_t M, uint32_t tilesN, EpiParams e) {
   constexpr int BM = C::BM, BN = C::BN;
   typedef typename std::conditional<DENSE, PolKCDense<T>, PolKCDgrad<ALIGNED, T>>::type PA;
-  typedef typename std::conditional<DENSE, PolMCDense<T>, PolMCDgradW<T>>::type PB;
+  typedef typename std::conditional<DENSE, PolMCDense<T>, PolMCDgradW<ALIGNED, T>>::type PB;
   __shared__ __attribute__((aligned(16))) char smem[lds_bytes_out<T, C>()];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;

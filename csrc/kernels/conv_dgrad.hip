@@ -206,7 +206,7 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
           const dim3 grid(tiles), block(C::THREADS);
           if (dense2)
             hipLaunchKernelGGL((conv_fwd_kernel<C, true, false, T, true>), grid, block, 0, st, dyp, wt, g2, M, tN, e);
-          else if (aligned)
+          else if (aligned && (s.f32 || nkh * c.nkw <= 32))  // bf16: buffer im2col tap mask
             hipLaunchKernelGGL((conv_fwd_kernel<C, false, true, T, true>), grid, block, 0, st, dyp, wt, g2, M, tN, e);
           else
             hipLaunchKernelGGL((conv_fwd_kernel<C, false, false, T, true>), grid, block, 0, st, dyp, wt, g2, M, tN, e);
@@ -224,7 +224,7 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
             hipLaunchKernelGGL((conv_dgrad_kernel<C, true, false, T, true>), grid, block, 0, st, dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         } else if (dense)
           hipLaunchKernelGGL((conv_dgrad_kernel<C, true, false, T>), grid, block, 0, st, dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
-        else if (aligned)
+        else if (aligned && (s.f32 || c.ntaps <= 32))  // bf16: buffer operands' tap mask
           hipLaunchKernelGGL((conv_dgrad_kernel<C, false, true, T>), grid, block, 0, st, dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);
         else
           hipLaunchKernelGGL((conv_dgrad_kernel<C, false, false, T>), grid, block, 0, st, dyp, wp, s.Ho, s.Wo, s.Co, taps, fCo, c, M, tN, e);

@@ -51,7 +51,8 @@ static void conv_fwd_t(const void* x, const void* w, void* y, float* st_sum, flo
     nflip = e.fl.nblk;
   }
   const bool dense = is_dense(s);
-  const bool aligned = s.Ci % BK == 0;
+  // bf16 ALIGNED runs the buffer im2col (KCIm2colBuf: <= 32 taps in its bit mask)
+  const bool aligned = s.Ci % BK == 0 && (s.f32 || s.KH * s.KW <= 32);
   const T* xp = (const T*)x;
   const T* wp = (const T*)w;
   cfg = resolve_fwd_cfg(s, cfg);

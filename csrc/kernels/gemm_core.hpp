@@ -51,6 +51,38 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
+// Buffer LDS-DMA (bf16 operand policies with BUF = true): a 128-bit descriptor over the operand
+// (wave-uniform: built from kernel arguments only), a per-lane 32-bit voffset that is FIXED for
+// the whole k-loop, and a wave-uniform soffset (SGPR) that carries the k-step.  A lane that must
+// read zeros (padding tap, row past M / column past N, k past K) gets voffset kOOB, which lies
+// past every descriptor's range (the hardware range check returns zeros): no per-lane 64-bit
+// pointer math and no zero-page selects in the main loop.  Host contract: descriptor bytes
+// < 2^31 (bindings.cpp checks bf16 operand sizes).
+constexpr uint32_t kOOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gk_rsrc(const void* base, uint64_t bytes) {
+  const uint32_t b = bytes < (uint64_t)kOOB ? (uint32_t)bytes : kOOB - 16u;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)b, 0x00020000);
+}
+
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base,
+                                       uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_wave_base, 16, voff, soff, 0, 0);
+}
+
+template <class Op, class = void>
+struct IsBufOp : std::false_type {};
+template <class Op>
+struct IsBufOp<Op, std::void_t<decltype(Op::BUF)>> : std::integral_constant<bool, Op::BUF> {};
+
+// one 1-KiB LDS-DMA wave-instruction of piece i of operand `op` at k-step kt (prep(kt) done)
+template <class Op>
+__device__ __forceinline__ void dma16(const Op& op, int kt, int i, char* lds_wave_base) {
+  if constexpr (IsBufOp<Op>::value)
+    blds16(op.rsrc, lds_wave_base, op.voff(kt, i), op.soff);
+  else
+    glds16(op.src(kt, i), lds_wave_base);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Operand policies.  Each describes one operand (A: rows = M, or B: rows = N) and exposes
 //   static constexpr bool KC;               // image format
@@ -101,6 +133,72 @@ struct KCDense {
   __device__ const void* src(int kt, int i) const {
     uint32_t k = (uint32_t)kt * BK + kcol;
     return (ptr[i] != nullptr && k < K) ? (const void*)(ptr[i] + (long)kt * BK) : zero;
+  }
+};
+
+// Dense K-contiguous rows through a buffer descriptor (bf16): element (r, k) at base[r*ld + k].
+// voffset = the lane's row start + its 16-B chunk (fixed), soffset = k-step * 128 B.  Only the
+// last k-step of a K that is not a multiple of 64 tests k < K.
+template <int R, class T = __bf16, int NW = 4>
+struct KCDenseBuf {
+  static constexpr bool KC = true;
+  static constexpr bool BUF = true;
+  static constexpr int NI = R / (8 * NW);
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t vo[NI];
+  uint32_t soff;
+  uint32_t kcol, K;
+  int kt_tail;  // the k-step whose chunks may pass K (-1: K % 64 == 0)
+  __device__ void prep(int kt) { soff = (uint32_t)kt * (BK * sizeof(T)); }
+  __device__ void init(const T* base, long ld, uint32_t rows_total, uint32_t K_,
+                       uint32_t origin, int wave, int lane, const void*) {
+    K = K_;
+    kcol = KCGeom<R, NW>::chunk(lane) * 8;
+    kt_tail = (K % BK) ? (int)(K / BK) : -1;
+    rsrc = gk_rsrc(base, (uint64_t)rows_total * (uint64_t)ld * sizeof(T));
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const uint32_t r = origin + KCGeom<R, NW>::row(wave, i, lane);
+      vo[i] = r < rows_total ? (uint32_t)(((long)r * ld + kcol) * sizeof(T)) : kOOB;
+    }
+  }
+  __device__ uint32_t voff(int kt, int i) const {
+    if (kt == kt_tail) return (uint32_t)kt * BK + kcol < K ? vo[i] : kOOB;  // wave-uniform test
+    return vo[i];
+  }
+};
+
+// Dense MN-contiguous operand through a buffer descriptor (bf16): element (k, col) at
+// base[k*ld + col].  voffset = the lane's (k row within the step, 8-column chunk), soffset =
+// k-step * 64 * ld * 2 B.
+template <int W, class T = __bf16, int NW = 4>
+struct MCDenseBuf {
+  static constexpr bool KC = false;
+  static constexpr bool BUF = true;
+  static constexpr int NI = W / (8 * NW);
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t vo[NI];
+  uint32_t krow[NI];
+  uint32_t soff, K;
+  long ld;
+  int kt_tail;
+  __device__ void prep(int kt) { soff = (uint32_t)((long)kt * BK * ld * (long)sizeof(T)); }
+  __device__ void init(const T* base, long ld_, uint32_t cols_total, uint32_t K_,
+                       uint32_t origin, int wave, int lane, const void*) {
+    ld = ld_;
+    K = K_;
+    kt_tail = (K % BK) ? (int)(K / BK) : -1;
+    rsrc = gk_rsrc(base, (uint64_t)K * (uint64_t)ld * sizeof(T));
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      krow[i] = MCGeom<W, NW>::row(wave, i, lane);
+      const uint32_t col = origin + MCGeom<W, NW>::chunk(wave, i, lane) * 8;
+      vo[i] = col < cols_total ? (uint32_t)(((long)krow[i] * ld + col) * sizeof(T)) : kOOB;
+    }
+  }
+  __device__ uint32_t voff(int kt, int i) const {
+    if (kt == kt_tail) return (uint32_t)kt * BK + krow[i] < K ? vo[i] : kOOB;
+    return vo[i];
   }
 };
 
@@ -187,6 +285,67 @@ struct KCIm2col {
   }
 };
 
+// Conv forward A operand (bf16, C % 64 == 0, KH*KW <= 32) through a buffer descriptor: the
+// descriptor starts SHIFT = (pad*W + pad_w)*C elements before x, so a lane's row offset
+// rowoff + SHIFT is never negative; per k-step the tap (kh, kw) and channel block are
+// wave-uniform (soffset = ((kh*W + kw)*C + ci0) * 2 B), and a per-row bit mask over the taps,
+// built once per tile, decides whether the tap lies inside the image (else kOOB: zeros).
+// Per piece: one bit test + select, instead of 64-bit address math + bounds compares.
+template <int R, class T = __bf16, int NW = 4>
+struct KCIm2colBuf {
+  static constexpr bool KC = true;
+  static constexpr bool BUF = true;
+  static constexpr int NI = R / (8 * NW);
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t vo[NI];
+  uint32_t mask[NI];
+  uint32_t soff, tap;
+  ConvGeom g;
+  __device__ void init(const T* x_, const ConvGeom& g_, uint32_t M, uint32_t origin, int wave,
+                       int lane, const void*) {
+    g = g_;
+    const long shift = ((long)g.pad * g.W + g.pad_w) * g.C;
+    rsrc = gk_rsrc(x_ - shift, ((uint64_t)g.N * g.H * g.W * g.C + shift) * sizeof(T));
+    const uint32_t kcol = KCGeom<R, NW>::chunk(lane) * 8;
+    // tap bit t = kh*KW + kw.  A row's valid taps are a kh range x a kw range: one KW-bit group
+    // pattern P (the kw range) replicated into every group by a carry-free multiply with
+    // REP = sum_kh 2^(kh*KW), then cut to the kh range.
+    uint64_t rep = 0;
+    for (int kh = 0; kh < g.KH; ++kh) rep |= 1ull << (kh * g.KW);  // wave-uniform
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const uint32_t m = origin + KCGeom<R, NW>::row(wave, i, lane);
+      uint32_t mk = 0u, v = kOOB;
+      if (m < M) {
+        const uint32_t img = fdiv(g.fHoWo, m);
+        const uint32_t rem = m - img * (uint32_t)(g.Ho * g.Wo);
+        const uint32_t ho = fdiv(g.fWo, rem);
+        const uint32_t wo = rem - ho * (uint32_t)g.Wo;
+        const int hi0 = (int)ho * g.stride - g.pad, wi0 = (int)wo * g.stride_w - g.pad_w;
+        v = (uint32_t)(((((long)img * g.H + hi0) * g.W + wi0) * g.C + shift + kcol) * sizeof(T));
+        const int kh_lo = max(0, -hi0), kh_hi = min(g.KH, g.H - hi0);
+        const int kw_lo = max(0, -wi0), kw_hi = min(g.KW, g.W - wi0);
+        if (kh_hi > kh_lo && kw_hi > kw_lo) {
+          const uint64_t pat = ((1ull << (kw_hi - kw_lo)) - 1ull) << kw_lo;
+          const uint64_t rng = ((1ull << (kh_hi * g.KW)) - 1ull) & ~((1ull << (kh_lo * g.KW)) - 1ull);
+          mk = (uint32_t)((pat * rep) & rng);
+        }
+      }
+      vo[i] = v;
+      mask[i] = mk;
+    }
+  }
+  __device__ void prep(int kt) {
+    const uint32_t k0 = (uint32_t)kt * BK;
+    const uint32_t t = fdiv(g.fC, k0);
+    const uint32_t kh = fdiv(g.fKW, t);
+    const uint32_t kw = t - kh * (uint32_t)g.KW;
+    tap = t;
+    soff = (uint32_t)((((long)kh * g.W + kw) * g.C + (k0 - t * (uint32_t)g.C)) * sizeof(T));
+  }
+  __device__ uint32_t voff(int, int i) const { return (mask[i] >> tap) & 1u ? vo[i] : kOOB; }
+};
+
 // Conv data-grad, sub-pixel ("parity class") form.  For stride s the dx pixels split into s*s
 // classes (ph, pw); class pixels (h, w) = (ph + s*i, pw + s*j) receive contributions only from the
 // taps with kh = (ph + pad) mod s (and kw likewise), each through dy[i + dh, j + dw] with a fixed
@@ -271,6 +430,106 @@ struct KCDgrad {
     const bool ok = kok & ((unsigned)ho < (unsigned)Ho) & ((unsigned)wo < (unsigned)Wo);
     return ok ? (const void*)(dy + off) : zero;
   }
+};
+
+// Conv data-grad A operand (bf16, Co % 64 == 0: the class tap is wave-uniform per k-step)
+// through a buffer descriptor.  dy element offset = rowoff - (a*Wo + b)*Co + co0 + kcol; the
+// descriptor starts SH = ((nkh-1)*Wo + nkw-1)*Co elements before dy, so soffset =
+// (SH - (a*Wo + b)*Co + co0) * 2 B is never negative.  Valid taps (ho = ib - a in [0, Ho),
+// wo = jb - b in [0, Wo)) are an a range x b range: a per-row bit mask as in KCIm2colBuf.
+template <int R, class T = __bf16, int NW = 4>
+struct KCDgradBuf {
+  static constexpr bool KC = true;
+  static constexpr bool BUF = true;
+  static constexpr int NI = R / (8 * NW);
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t vo[NI];
+  uint32_t mask[NI];
+  uint32_t soff, tap;
+  int Wo, Co, sh;
+  FastDiv fCo, fnkw;
+  __device__ void init(const T* dy_, int Ho_, int Wo_, int Co_, FastDiv fCo_,
+                       const DgradClass& cls, uint32_t M, uint32_t origin, int wave, int lane,
+                       const void*) {
+    Wo = Wo_; Co = Co_; fCo = fCo_; fnkw = cls.fnkw;
+    const int nkw = (int)cls.fnkw.d;
+    const int nkh = nkw > 0 ? cls.ntaps / nkw : 0;
+    sh = ((nkh > 0 ? nkh - 1 : 0) * Wo + (nkw > 0 ? nkw - 1 : 0)) * Co;
+    const int N = (int)(M / (uint32_t)(cls.Hc * cls.Wc));
+    rsrc = gk_rsrc(dy_ - sh, ((uint64_t)(N > 0 ? N : 1) * Ho_ * Wo_ * Co_ + sh) * sizeof(T));
+    const uint32_t kcol = KCGeom<R, NW>::chunk(lane) * 8;
+    uint64_t rep = 0;
+    for (int a = 0; a < nkh; ++a) rep |= 1ull << (a * nkw);  // wave-uniform
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const uint32_t m = origin + KCGeom<R, NW>::row(wave, i, lane);
+      uint32_t mk = 0u, v = kOOB;
+      if (m < M) {
+        const uint32_t img = fdiv(cls.fHcWc, m);
+        const uint32_t rem = m - img * (uint32_t)(cls.Hc * cls.Wc);
+        const uint32_t ii = fdiv(cls.fWc, rem);
+        const int ib = (int)ii + cls.dh0;
+        const int jb = (int)(rem - ii * (uint32_t)cls.Wc) + cls.dw0;
+        v = (uint32_t)(((((long)img * Ho_ + ib) * Wo + jb) * Co + kcol) * sizeof(T));
+        const int a_lo = max(0, ib - Ho_ + 1), a_hi = min(nkh, ib + 1);
+        const int b_lo = max(0, jb - Wo + 1), b_hi = min(nkw, jb + 1);
+        if (a_hi > a_lo && b_hi > b_lo) {
+          const uint64_t pat = ((1ull << (b_hi - b_lo)) - 1ull) << b_lo;
+          const uint64_t rng = ((1ull << (a_hi * nkw)) - 1ull) & ~((1ull << (a_lo * nkw)) - 1ull);
+          mk = (uint32_t)((pat * rep) & rng);
+        }
+      }
+      vo[i] = v;
+      mask[i] = mk;
+    }
+  }
+  __device__ void prep(int kt) {
+    const uint32_t k0 = (uint32_t)kt * BK;
+    const uint32_t t = fdiv(fCo, k0);
+    const uint32_t a = fdiv(fnkw, t);
+    const uint32_t b = t - a * fnkw.d;
+    tap = t;
+    soff = (uint32_t)(((long)sh - ((long)a * Wo + b) * Co + (k0 - t * (uint32_t)Co)) * sizeof(T));
+  }
+  __device__ uint32_t voff(int, int i) const { return (mask[i] >> tap) & 1u ? vo[i] : kOOB; }
+};
+
+// Conv data-grad B operand (bf16, Co % 64 == 0) through a buffer descriptor: B(k = (t, co),
+// n = ci) = W[co][tap(t)][ci]; per k-step t and co0 are wave-uniform, so the lane's part
+// (krow*taps*Ci + col) is fixed and (co0*taps + tap)*Ci goes to soffset.
+template <int W, class T = __bf16, int NW = 4>
+struct MCDgradWBuf {
+  static constexpr bool KC = false;
+  static constexpr bool BUF = true;
+  static constexpr int NI = W / (8 * NW);
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t vo[NI];
+  uint32_t soff;
+  uint32_t Co, taps, Ci;
+  FastDiv fCo, fnkw;
+  int kh0, kw0, S, KW;
+  __device__ void init(const T* w, uint32_t Co_, uint32_t taps_, uint32_t Ci_, FastDiv fCo_,
+                       const DgradClass& cls, uint32_t origin, int wave, int lane, const void*) {
+    Co = Co_; taps = taps_; Ci = Ci_; fCo = fCo_; fnkw = cls.fnkw;
+    kh0 = cls.kh0; kw0 = cls.kw0; S = cls.S; KW = cls.KW;
+    rsrc = gk_rsrc(w, (uint64_t)Co * taps * Ci * sizeof(T));
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const uint32_t krow = MCGeom<W, NW>::row(wave, i, lane);
+      const uint32_t col = origin + MCGeom<W, NW>::chunk(wave, i, lane) * 8;
+      vo[i] = col < Ci ? (uint32_t)(((long)krow * taps * Ci + col) * sizeof(T)) : kOOB;
+    }
+  }
+  __device__ void prep(int kt) {
+    const uint32_t k0 = (uint32_t)kt * BK;
+    const uint32_t t = fdiv(fCo, k0);
+    const uint32_t co0 = k0 - t * Co;
+    const uint32_t a = fdiv(fnkw, t);
+    const uint32_t b = t - a * fnkw.d;
+    const uint32_t tp = (uint32_t)(kh0 + S * (int)a) * (uint32_t)KW + (uint32_t)(kw0 + S * (int)b);
+    soff = (uint32_t)(((long)co0 * taps + tp) * Ci * sizeof(T));
+  }
+  __device__ uint32_t voff(int, int i) const { return vo[i]; }
 };
 
 // Dense MN-contiguous operand: element (k, col) at base[k*ld + col]; W columns per tile.
@@ -467,8 +726,8 @@ struct MainLoop {
 
   // one LDS-DMA instruction (piece p of LOADS) of stage kt
   __device__ static void piece(char* buf, OpA& a, OpB& b, int kt, int wave, int p) {
-    if (p < OpA::NI) glds16(a.src(kt, p), buf + (wave * OpA::NI + p) * 1024);
-    else glds16(b.src(kt, p - OpA::NI), buf + A_BYTES + (wave * OpB::NI + p - OpA::NI) * 1024);
+    if (p < OpA::NI) dma16(a, kt, p, buf + (wave * OpA::NI + p) * 1024);
+    else dma16(b, kt, p - OpA::NI, buf + A_BYTES + (wave * OpB::NI + p - OpA::NI) * 1024);
   }
 
   __device__ static void stage(char* buf, OpA& a, OpB& b, int kt, int wave) {

@@ -94,7 +94,7 @@ struct MainLoopPP {
   __device__ static void half(Op& op, char* dst, int kt, int wave) {
     op.prep(kt);
 #pragma unroll
-    for (int j = 0; j < Op::NI; ++j) glds16(op.src(kt, j), dst + (wave * Op::NI + j) * 1024);
+    for (int j = 0; j < Op::NI; ++j) dma16(op, kt, j, dst + (wave * Op::NI + j) * 1024);
   }
 
   // DMA of global phase x (x >= -6; compile-time phase-in-tile Q = x & 3)
