@@ -389,20 +389,26 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
 #pragma unroll
       for (int q = 0; q < 4; ++q) bv[j][q] = bp[nc + q];
     }
+    // the activation is a wave-uniform branch (not a per-element select of both results)
+    auto add_bias = [&](auto relu_tag) {
+      constexpr bool RELU = decltype(relu_tag)::value;
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      uint32_t n = n0 + Map::col(wc, j) + lc;
-      float b[4];
+      for (int j = 0; j < NT; ++j) {
+        uint32_t n = n0 + Map::col(wc, j) + lc;
+        float b[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) b[q] = n < e.N ? bv[j][q] : 0.f;
+        for (int q = 0; q < 4; ++q) b[q] = n < e.N ? bv[j][q] : 0.f;
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+        for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float v = acc[i][j][q] + b[q];
-          acc[i][j][q] = e.act == 1 ? fmaxf(v, 0.f) : v;
-        }
-    }
+          for (int q = 0; q < 4; ++q) {
+            const float v = acc[i][j][q] + b[q];
+            acc[i][j][q] = RELU ? fmaxf(v, 0.f) : v;
+          }
+      }
+    };
+    if (e.act == 1) add_bias(std::true_type());
+    else add_bias(std::false_type());
   }
   // BatchNorm partial statistics from the fp32 accumulators, reduced over the block's BM rows
   // and added with fp32 atomics into replica slab (blockIdx % st_R) — 256-B-contiguous
@@ -419,22 +425,25 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
 #pragma unroll
       for (int q = 0; q < 4; ++q) shv[j][q] = e.st_shift[nc + q];
     }
+    // column pairs in packed fp32 (v_pk_add_f32 / v_pk_fma_f32: two columns per instruction)
+    typedef float f2 __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const float* sh = shv[j];
-      float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+      const f2 sh01 = {sh[0], sh[1]}, sh23 = {sh[2], sh[3]};
+      f2 s01 = {0.f, 0.f}, s23 = {0.f, 0.f}, ss01 = {0.f, 0.f}, ss23 = {0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         uint32_t m = m0 + Map::row(wr, i) + lr;
-        if (m < e.M) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float d = as_stored<T>(acc[i][j][q]) - sh[q];
-            s[q] += d;
-            ss[q] += d * d;
-          }
-        }
+        const f2 w = m < e.M ? f2{1.f, 1.f} : f2{0.f, 0.f};  // rows past M add nothing
+        const f2 d01 = (f2{as_stored<T>(acc[i][j][0]), as_stored<T>(acc[i][j][1])} - sh01) * w;
+        const f2 d23 = (f2{as_stored<T>(acc[i][j][2]), as_stored<T>(acc[i][j][3])} - sh23) * w;
+        s01 += d01;
+        s23 += d23;
+        ss01 += d01 * d01;
+        ss23 += d23 * d23;
       }
+      float s[4] = {s01.x, s01.y, s23.x, s23.y}, ss[4] = {ss01.x, ss01.y, ss23.x, ss23.y};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {  // over the 16 lanes (rows) of each DPP row: VALU only
         s[q] = row16_sum(s[q]);

@@ -750,6 +750,9 @@ struct MainLoop {
 
   // Fragments + MFMAs of one stage.  With SPREAD, the next stage's LOADS LDS-DMA pieces
   // (nbuf != nullptr) are issued between MFMA groups instead of in one burst before them.
+  // FIRST: the k-step that starts the accumulation — its first MFMA of each tile takes C = 0
+  // (an inline constant) instead of 64 zeroed accumulator registers
+  template <bool FIRST = false>
   __device__ static void compute(const char* cbuf, f32x4 (&acc)[MT][NT], uint32_t arow0,
                                  uint32_t bcol0, int lane, char* nbuf, OpA& a, OpB& b, int nkt,
                                  int wave) {
@@ -780,8 +783,9 @@ struct MainLoop {
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ks][j], af[ks][i], acc[i][j],
-                                                              0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              bfr[ks][j], af[ks][i], (FIRST && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j],
+              0, 0, 0);
           if constexpr (SPREAD) {
             constexpr int STEP = MFMAS / LOADS > 0 ? MFMAS / LOADS : 1;
             const int idx = (ks * MT + i) * NT + j;  // compile-time after unrolling
@@ -794,11 +798,13 @@ struct MainLoop {
 
   __device__ static void run(char* smem, OpA& a, OpB& b, int kt0, int kt1,
                              f32x4 (&acc)[MT][NT], int wave, int lane) {
+    if (kt0 >= kt1) {
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (kt0 >= kt1) return;
+        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      return;
+    }
     const int wr = wave / WN, wc = wave % WN;
     const uint32_t arow0 = wr * (BM / WM), bcol0 = wc * (BN / WN);
     if constexpr (NS == 1) {
@@ -807,7 +813,8 @@ struct MainLoop {
         stage(smem, a, b, kt, wave);
         wait_vmcnt<0>();
         __syncthreads();
-        compute(smem, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave);
+        if (kt == kt0) compute<true>(smem, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave);
+        else compute(smem, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave);
       }
     } else {
 #pragma unroll
@@ -824,13 +831,17 @@ struct MainLoop {
         }
         barrier();
         const bool more = kt + NS - 1 < kt1;
-        if constexpr (SPREAD) {
-          compute(smem + cur * STAGE_BYTES, acc, arow0, bcol0, lane,
-                  more ? smem + nxt * STAGE_BYTES : nullptr, a, b, kt + NS - 1, wave);
-        } else {
-          if (more) stage(smem + nxt * STAGE_BYTES, a, b, kt + NS - 1, wave);
-          compute(smem + cur * STAGE_BYTES, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave);
+        char* nb = more ? smem + nxt * STAGE_BYTES : nullptr;
+        if constexpr (!SPREAD) {
+          if (more) stage(nb, a, b, kt + NS - 1, wave);
+          nb = nullptr;
         }
+        if (kt == kt0)
+          compute<true>(smem + cur * STAGE_BYTES, acc, arow0, bcol0, lane, nb, a, b,
+                        kt + NS - 1, wave);
+        else
+          compute(smem + cur * STAGE_BYTES, acc, arow0, bcol0, lane, nb, a, b, kt + NS - 1,
+                  wave);
         cur = cur + 1 == NS ? 0 : cur + 1;
         nxt = nxt + 1 == NS ? 0 : nxt + 1;
       }
