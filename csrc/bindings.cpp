@@ -1832,6 +1832,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_wgrad3x3", [](bool on) { mipipe::g_wgrad3x3 = on; });
   m.def("get_wgrad3x3", []() { return mipipe::g_wgrad3x3; });
   m.def("set_nt_store", [](int mask) { mipipe::g_nt_store = mask; });
+  m.def("set_nt_min_bytes", [](long b) { mipipe::g_nt_min_bytes = b; });
+  m.def("get_nt_min_bytes", []() { return mipipe::g_nt_min_bytes; });
   m.def("get_nt_store", []() { return mipipe::g_nt_store; });
   m.def("set_ws_finish", [](bool on) { g_ws_finish = on; });
   m.def("get_ws_finish", []() { return g_ws_finish; });

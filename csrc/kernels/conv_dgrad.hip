@@ -162,7 +162,8 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
   for_each_class(s, [&](const DgradClass& c, uint32_t M) {
       EpiParams e{};
       e.C = dx; e.ldc = s.Ci; e.M = M; e.N = s.Ci;
-      e.nt = (g_nt_store >> 1) & 1;
+      e.nt = ((g_nt_store >> 1) & 1) &&
+             (long)s.N * s.H * s.W * s.Ci * (s.f32 ? 4 : 2) > g_nt_min_bytes;
       e.ntl = (g_nt_store >> 8) & 1;
       if (fz != nullptr) {
         e.addend = fz->addend;

@@ -42,7 +42,7 @@ static void conv_fwd_t(const void* x, const void* w, void* y, float* st_sum, flo
   e.C = y; e.ldc = s.Co; e.M = M; e.N = s.Co; e.bias = bias; e.act = relu ? 1 : 0;
   e.st_sum = st_sum; e.st_sq = st_sq; e.st_shift = st_shift; e.st_R = g_stat_rows;
   e.det_rows = det_rows;
-  e.nt = g_nt_store & 1;
+  e.nt = (g_nt_store & 1) && (long)M * s.Co * (s.f32 ? 4 : 2) > g_nt_min_bytes;
   uint32_t nflip = 0;
   if (wflip != nullptr && dgrad_preflip_ok(s)) {
     e.fl_w = w; e.fl_wt = wflip;

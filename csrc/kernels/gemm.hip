@@ -25,6 +25,14 @@ int g_nt_store = [] {
   const char* v = getenv("MIPIPE_NT_STORE");
   return v != nullptr ? atoi(v) : 1379;  // conv stores, BN-pass + dgrad-epi loads, AdamW state
 }();
+// Outputs up to this many bytes keep the default (cached) store policy even when their g_nt_store
+// bit is set: a tensor that fits the 256 MB MALL is re-read from it by the pass right after
+// (the BN apply reading a layer-3/4 conv output); only larger ones stream past it
+// (MIPIPE_NT_MIN_MB overrides; 0 = the bit alone decides)
+long g_nt_min_bytes = [] {
+  const char* v = getenv("MIPIPE_NT_MIN_MB");
+  return (long)(v != nullptr ? atof(v) : 0.0) * (1l << 20);
+}();
 int g_ns1_max_k = 512;  // measured: tools/sweep_ns1.py (profiles/r1_ns1_sweep.jsonl)
 namespace gk {
 

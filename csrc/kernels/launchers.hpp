@@ -398,5 +398,6 @@ void colsum_f32(const void* x, bool bf16, float* out, long rows, int cols, float
 int colsum_blocks(long rows, int cols);
 extern int g_colsum_row_blocks;
 extern int g_nt_store;  // non-temporal activation stores: 1 conv fwd, 2 dgrad, 4 BN passes
+extern long g_nt_min_bytes;  // outputs up to this size keep cached stores (MALL-resident)
 
 }  // namespace mipipe
