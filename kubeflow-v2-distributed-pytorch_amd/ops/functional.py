@@ -155,10 +155,50 @@ class BNActToken:
         self.rep = None  # the bwd slab the consuming dgrad filled (this pass's own slab)
 
 
+_TAP_CROP = os.environ.get("MIPIPE_TAP_CROP", "1") != "0"
+
+
+def tap_crop(x_shape, w_shape, stride, pad):
+    """Filter taps that can never touch the image for this geometry are dropped (the analogue
+    of cuDNN picking an algorithm per shape): a 3x3 / pad-1 conv on a 1x1 feature map (ResNet-18
+    layer 4 at 32x32, the reference's config of record) only ever reads its centre tap — a 1x1
+    GEMM with K = Ci instead of 9 Ci, 8/9 of the MFMA work spent on padding otherwise.
+
+    Returns (kh0, kh1, kw0, kw1, pad') — the kept tap ranges and the padding that maps every
+    output to the same input pixels — or None when every tap is used somewhere, the output size
+    would change, or the cropped padding is not square."""
+    if not (_TAP_CROP and isinstance(stride, int) and isinstance(pad, int)):
+        return None
+    _, H, W, _ = x_shape
+    _, KH, KW, _ = w_shape
+    Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+
+    def span(L, Lo, K):
+        used = [k for k in range(K) if any(0 <= o * stride - pad + k < L for o in range(Lo))]
+        return (used[0], used[-1] + 1) if used else (0, K)
+    (h0, h1), (w0, w1) = span(H, Ho, KH), span(W, Wo, KW)
+    if (h0, h1, w0, w1) == (0, KH, 0, KW) or pad - h0 != pad - w0:
+        return None
+    p2 = pad - h0
+    if ((H + 2 * p2 - (h1 - h0)) // stride + 1 != Ho
+            or (W + 2 * p2 - (w1 - w0)) // stride + 1 != Wo):
+        return None
+    return h0, h1, w0, w1, p2
+
+
 class _ConvFn(Function):
     @staticmethod
     def forward(ctx, x, weight, w_c, stride, pad, shift, slabs=None, prev=None, res_take=None,
                 res_give=None):
+        # taps that never touch the image are cropped away (forward, data-grad and weight-grad
+        # all run the smaller filter; the weight-grad lands in its slice of the full gradient)
+        crop = (tap_crop(tuple(x.shape), tuple(w_c.shape), stride, pad)
+                if getattr(weight, "_mipipe_wgrad_map", None) is None else None)
+        if crop is not None:
+            kh0, kh1, kw0, kw1, pad = crop
+            w_c = w_c[:, kh0:kh1, kw0:kw1, :].contiguous()
+        ctx.crop = crop
+        ctx.full_k = (weight.shape[2], weight.shape[3])
         # stride-1 k x k convs: the forward launch also writes the tap-flipped weight the
         # data-grad reads (a persistent buffer per weight; no flip kernel in the backward)
         wflip = None
@@ -226,7 +266,7 @@ class _ConvFn(Function):
                    if x.shape[-1] == ci and ctx.wmap is None and K.use_native(dy) else None)
             side = None
             if (_SIDE_WGRAD and tgt is not None and dy.is_cuda and not tgt[0]._ready_listeners
-                    and not (bnr is not None and tok.y2 is not None)):
+                    and not (bnr is not None and tok.y2 is not None) and ctx.crop is None):
                 side = _side_stream(dy)
             if bnr is not None and side is None:
                 # the weight-grad launch also collects the slab the fused dgrad just filled
@@ -261,11 +301,21 @@ class _ConvFn(Function):
                 # gradient accumulates straight into the flat DDP bucket: no zero-fill, no
                 # autograd AccumulateGrad add; tell the reducer the gradient is ready.
                 fs, g = tgt
-                K.conv_wgrad(dy, x, kh, kw, stride, pad, out=g.permute(0, 2, 3, 1),
-                             collect=collect)
+                if ctx.crop is not None:  # the kept taps' slice of the full gradient
+                    kh0, kh1, kw0, kw1, _ = ctx.crop
+                    part = K.conv_wgrad(dy, x, kh, kw, stride, pad, collect=collect)
+                    g.permute(0, 2, 3, 1)[:, kh0:kh1, kw0:kw1, :].add_(part)
+                else:
+                    K.conv_wgrad(dy, x, kh, kw, stride, pad, out=g.permute(0, 2, 3, 1),
+                                 collect=collect)
                 fs.grad_ready(weight)
             else:
                 dw = K.conv_wgrad(dy, x, kh, kw, stride, pad, collect=collect)
+                if ctx.crop is not None:
+                    kh0, kh1, kw0, kw1, _ = ctx.crop
+                    full = dw.new_zeros(dw.shape[0], ctx.full_k[0], ctx.full_k[1], dw.shape[3])
+                    full[:, kh0:kh1, kw0:kw1, :] = dw
+                    dw = full
                 if ctx.wmap is not None:  # kernel layout -> parameter layout (packed stem)
                     dw = ctx.wmap(dw)
                 else:

@@ -173,7 +173,7 @@ def test_bench_reference_config_block_gloo():
     classes, fp32, deterministic) after the headline in the same process (and, here, under a
     2-rank gloo DDP), and reports it inside the ONE JSON line."""
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--reference-config", "on",
-                        "--ref-batch", "4"] + CPU_ARGS, env=_env(),
+                        "--time-deterministic", "on", "--ref-batch", "4"] + CPU_ARGS, env=_env(),
                        capture_output=True, text=True, timeout=600, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
@@ -185,3 +185,6 @@ def test_bench_reference_config_block_gloo():
     assert ref["dtype"] == "fp32" and ref["deterministic"] is True
     assert ref["batch_per_gpu"] == 4 and ref["global_batch"] == 8
     assert ref["value"] > 0 and ref["ms_per_step"] > 0 and ref["steps"] == 2
+    det = j["deterministic_variant"]
+    assert det["deterministic"] is True and det["value"] > 0 and det["steps"] == 2
+    assert j["config"]["deterministic"] is False
