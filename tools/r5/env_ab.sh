@@ -9,6 +9,7 @@ while [ "$1" != "--" ]; do sets+=("$1"); shift; done
 shift
 for i in $(seq $rounds); do
   for st in "${sets[@]}"; do
-    (cd $R && env $st timeout -k 10 300 python -u bench.py "$@" 2>/dev/null | sed "s/^/$st /") >> $out || exit 1
+    tag=$(echo "$st" | tr '/ ' '_+')
+    (cd $R && env $st timeout -k 10 300 python -u bench.py "$@" 2>/dev/null | sed "s|^|$tag |") >> $out || exit 1
   done
 done
