@@ -177,6 +177,9 @@ int select(const std::string& k, bool f32, bool wgrad, F&& run) {
 // GEMM plans: tile id + 16 * split-K count (0 = heuristic split; accumulating GEMMs only)
 constexpr int kPlanSplit = 16;
 constexpr int kPlanWs = 1024;  // gemm plans: split-K through per-split workspace slices
+// deterministic conv forward: up to this many per-M-tile statistics rows go straight to
+// bn_finalize (summed there in row order) instead of through det_sum_rows first
+constexpr int kDetDirectRows = 128;
 std::vector<int> gemm_candidates(bool f32, bool accumulate) {
   std::vector<int> c;
   for (int t : candidates(f32, accumulate)) {
@@ -263,6 +266,11 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
     float* p0 = part.data_ptr<float>();
     mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), p0, p0 + (long)P * s.Co, sh, s,
                      stream(), bp, relu, cfg, P, wfp);
+    if (P <= tune::kDetDirectRows) {
+      // few M tiles (the small-spatial layers): hand the partial rows themselves to bn_finalize,
+      // which sums its P input rows in index order — no separate fixed-order sum launch
+      return {y, part[0], part[1]};
+    }
     mipipe::det_sum_rows(p0, p0 + (long)P * s.Co, P, s.Co, psp, pssp, false, stream());
     return {y, ps, pss};
   }
