@@ -156,6 +156,7 @@ class BNActToken:
 
 
 _TAP_CROP = os.environ.get("MIPIPE_TAP_CROP", "1") != "0"
+_CONV_FLATTEN = os.environ.get("MIPIPE_CONV_FLATTEN", "1") != "0"
 
 
 def tap_crop(x_shape, w_shape, stride, pad):
@@ -197,8 +198,25 @@ class _ConvFn(Function):
         if crop is not None:
             kh0, kh1, kw0, kw1, pad = crop
             w_c = w_c[:, kh0:kh1, kw0:kw1, :].contiguous()
-        ctx.crop = crop
         ctx.full_k = (weight.shape[2], weight.shape[3])
+        # a (cropped) filter that covers the whole unpadded input has ONE output pixel: the conv
+        # is a 1x1 conv of the flattened image ([N, 1, 1, H*W*C] x [Co, 1, 1, KH*KW*C], the NHWC
+        # and [Co, KH, KW, Ci] orders agree) — one dense GEMM for the data-grad instead of a launch
+        # per stride-parity class (ResNet-18 layer 4's stride-2 conv on its 2x2 map)
+        ctx.flat = None
+        if (_TAP_CROP and _CONV_FLATTEN and isinstance(stride, int) and isinstance(pad, int)
+                and pad == 0
+                and getattr(weight, "_mipipe_wgrad_map", None) is None
+                and w_c.shape[1] == x.shape[1] and w_c.shape[2] == x.shape[2]
+                and w_c.shape[3] == x.shape[3] and x.shape[1] * x.shape[2] > 1):
+            if crop is None:
+                crop = (0, w_c.shape[1], 0, w_c.shape[2], 0)
+            ctx.flat = tuple(x.shape)
+            n, h, w_, c = x.shape
+            x = x.reshape(n, 1, 1, h * w_ * c)
+            w_c = w_c.reshape(w_c.shape[0], 1, 1, h * w_ * c)
+            stride = 1
+        ctx.crop = crop
         # stride-1 k x k convs: the forward launch also writes the tap-flipped weight the
         # data-grad reads (a persistent buffer per weight; no flip kernel in the backward)
         wflip = None
@@ -236,7 +254,9 @@ class _ConvFn(Function):
                 raise NotImplementedError("dgrad of a non-square-stride conv")
             addend = ctx.res_take.take() if ctx.res_take is not None else None
             bnr = None
-            tok = ctx.prev
+            tok = ctx.prev if ctx.flat is None else None  # flattened: per-channel BN fusion off
+            if ctx.flat is not None and addend is not None:
+                addend = addend.reshape(x.shape)
             two = tok is not None and tok.y2 is not None
             # the two-branch fusion: bf16 1x1 stride-1 data-grads whose weight-grad launch (which
             # collects the third slab array) follows
@@ -257,13 +277,16 @@ class _ConvFn(Function):
                               wflip=ctx.wflip)
             if bnr is not None:
                 tok.pre_reduced = True
+            if ctx.flat is not None:
+                dx = dx.reshape(ctx.flat)
             if ctx.res_give is not None:
                 dx = ctx.res_give.produce(dx)
         if ctx.needs_input_grad[1]:
             weight = ctx.weight
             collect = None
+            cin = x.shape[-1] if ctx.flat is None else ctx.flat[-1]
             tgt = (_direct_grad_target(weight)
-                   if x.shape[-1] == ci and ctx.wmap is None and K.use_native(dy) else None)
+                   if cin == ci and ctx.wmap is None and K.use_native(dy) else None)
             side = None
             if (_SIDE_WGRAD and tgt is not None and dy.is_cuda and not tgt[0]._ready_listeners
                     and not (bnr is not None and tok.y2 is not None) and ctx.crop is None):
@@ -304,7 +327,8 @@ class _ConvFn(Function):
                 if ctx.crop is not None:  # the kept taps' slice of the full gradient
                     kh0, kh1, kw0, kw1, _ = ctx.crop
                     part = K.conv_wgrad(dy, x, kh, kw, stride, pad, collect=collect)
-                    g.permute(0, 2, 3, 1)[:, kh0:kh1, kw0:kw1, :].add_(part)
+                    g.permute(0, 2, 3, 1)[:, kh0:kh1, kw0:kw1, :].add_(
+                        part.reshape(part.shape[0], kh1 - kh0, kw1 - kw0, -1))
                 else:
                     K.conv_wgrad(dy, x, kh, kw, stride, pad, out=g.permute(0, 2, 3, 1),
                                  collect=collect)
@@ -313,6 +337,7 @@ class _ConvFn(Function):
                 dw = K.conv_wgrad(dy, x, kh, kw, stride, pad, collect=collect)
                 if ctx.crop is not None:
                     kh0, kh1, kw0, kw1, _ = ctx.crop
+                    dw = dw.reshape(dw.shape[0], kh1 - kh0, kw1 - kw0, -1)
                     full = dw.new_zeros(dw.shape[0], ctx.full_k[0], ctx.full_k[1], dw.shape[3])
                     full[:, kh0:kh1, kw0:kw1, :] = dw
                     dw = full

@@ -36,18 +36,38 @@ def _run(x, w, stride, pad, crop_on, dev, dtype):
         MF._TAP_CROP = old
 
 
-@pytest.mark.parametrize("H,stride", [(1, 1), (2, 2)])
-def test_cropped_conv_equals_full_filter_cpu(H, stride):
+@pytest.mark.parametrize("H,stride,k,pad", [(1, 1, 3, 1), (2, 2, 3, 1), (3, 1, 3, 0), (2, 2, 2, 0)])
+def test_cropped_conv_equals_full_filter_cpu(H, stride, k, pad):
+    """(1,1,3,1): centre tap only; (2,2,3,1): 2x2 taps, then the flattened single-output
+    form; (3,1,3,0) / (2,2,2,0): whole-image filters, flattened without a crop."""
     torch.manual_seed(0)
     x = torch.randn(4, H, H, 16, dtype=torch.float64)
-    w = torch.randn(24, 16, 3, 3, dtype=torch.float64)
-    full = _run(x, w, stride, 1, False, "cpu", torch.float64)
-    crop = _run(x, w, stride, 1, True, "cpu", torch.float64)
+    w = torch.randn(24, 16, k, k, dtype=torch.float64)
+    full = _run(x, w, stride, pad, False, "cpu", torch.float64)
+    crop = _run(x, w, stride, pad, True, "cpu", torch.float64)
     for a, b in zip(full, crop):
         assert torch.allclose(a, b, rtol=1e-12, atol=1e-12)
     # the cropped-away taps get exactly zero gradient
     if H == 1:
         assert float(crop[2][:, :, [0, 2], :].abs().max()) == 0.0
+
+
+def test_flattened_conv_inside_resnet_block_cpu():
+    """ResNet-18 at 32x32 runs layer 4's first conv flattened (its input is the previous block's
+    fused BN+ReLU output): the module tree still matches the plain float64 reference (the
+    per-channel BN-backward fusion is skipped for the flattened data-grad)."""
+    from pinned_ref import pinned_grads
+    from mipipe.models import create_model
+    torch.manual_seed(0)
+    m = create_model("resnet18", num_classes=10, compute_dtype=torch.float64).double()
+    state = {kk: v.clone() for kk, v in m.state_dict().items()}
+    names = [n for n, _ in m.named_parameters()]
+    x = torch.randn(4, 3, 32, 32, dtype=torch.float64)
+    y = torch.randint(0, 10, (4,))
+    torch.nn.functional.cross_entropy(m(x), y).backward()
+    _, _, g, _ = pinned_grads(state, names, x, y, None)
+    for n, p in m.named_parameters():
+        assert ((p.grad - g[n]).norm() / g[n].norm()).item() < 1e-10, n
 
 
 @pytest.mark.gpu
