@@ -96,6 +96,10 @@ def parse():
                          "(ResNet-18 32x32, 1000 classes, fp32, deterministic, --ref-batch per "
                          "GPU) and report it as 'reference_config' in the JSON line; auto = with "
                          "the default mipipe ResNet-50 headline on the GPU")
+    ap.add_argument("--time-deterministic", default="auto", choices=["auto", "on", "off"],
+                    help="also time the headline in deterministic mode (the reference's "
+                         "cudnn.deterministic=True, task.py:25) and report it as "
+                         "'deterministic_variant'; auto = together with the reference config")
     ap.add_argument("--ref-batch", type=int, default=1024,
                     help="per-process batch of the reference config (task.py:58,153: 1024)")
     return ap.parse_args()
@@ -172,6 +176,23 @@ def main() -> int:
     if rank == 0:
         _heartbeat()
     r = _run(a, world, rank, local, dev, distributed, cpu)
+    det = None
+    if _want_det_variant(a, cpu):
+        # the headline again in the reference's own mode (task.py:25 cudnn.deterministic=True:
+        # no float atomics, fixed-order reductions, shipped plan tables), same discipline
+        import copy
+        b = copy.copy(a)
+        b.deterministic, b.dump_params, b.save_tune = 1, None, None
+        del r["model"]
+        if not cpu:
+            torch.cuda.empty_cache()
+        rd = _run(b, world, rank, local, dev, distributed, cpu)
+        det = {"value": round(rd["value"], 2), "unit": "samples/s",
+               "ms_per_step": round(rd["dt"] / b.steps * 1e3, 3), "steps": b.steps,
+               "warmup": b.warmup, "deterministic": True,
+               "hip_graph": bool(getattr(b, "graph_used", False)), "final_loss": rd["loss"],
+               "cost_vs_default_pct": round(100.0 * (rd["dt"] / r["dt"] - 1.0), 2),
+               "source": "task.py:25"}
     ref = None
     if _want_reference_config(a, cpu):
         # the reference's own config of record in the same process, same timing discipline:
@@ -183,7 +204,7 @@ def main() -> int:
         b.model, b.res, b.classes, b.dtype, b.deterministic = "resnet18", 32, 1000, "fp32", 1
         b.batch = a.ref_batch
         b.emulate_ranks, b.dump_params, b.save_tune = 1, None, None
-        del r["model"]
+        r.pop("model", None)
         if not cpu:
             torch.cuda.empty_cache()
         rr = _run(b, world, rank, local, dev, distributed, cpu)
@@ -228,6 +249,8 @@ def main() -> int:
                        "rccl": _rccl_settings() if distributed else None,
                        "rccl_transports": _transports(rccl_log)},
             "final_loss": r["loss"], "gpu_clocks": r["clocks"]}
+        if det is not None:
+            line["deterministic_variant"] = det
         if ref is not None:
             line["reference_config"] = ref
         print(json.dumps(line), flush=True)
@@ -235,6 +258,14 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _want_det_variant(a, cpu: bool) -> bool:
+    if a.time_deterministic == "off" or a.deterministic:
+        return False
+    if a.time_deterministic == "on":
+        return True
+    return _want_reference_config(a, cpu) and a.reference_config != "off"
 
 
 def _want_reference_config(a, cpu: bool) -> bool:
@@ -255,6 +286,10 @@ def _run(a, world, rank, local, dev, distributed, cpu):
         # per-shape conv tile autotuning during the (untimed, eager) warm-up steps — the
         # analogue of the reference's cudnn.benchmark = True (task.py:244)
         from mipipe.ops import tuning
+        if a.deterministic:
+            # a deterministic run takes its plans from the shipped / loaded tables only, never
+            # from an earlier run's timing-based picks (bit-reproducible across processes)
+            tuning.clear()
         tuning.from_env(bool(a.deterministic))
         tuning.set_benchmark(a.tune > 0, verbose=False, force=a.tune == 2)
         from mipipe.ops import determinism
