@@ -159,17 +159,21 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // Fast unsigned division by a runtime constant (Granlund-Montgomery "round-up" variant).
+// sh = max(s - 1, 0) is precomputed: clamped on the device it became a VALU op, which made
+// every quotient of a wave-uniform index a VGPR (and the buffer soffsets built from it waterfall
+// loops, see gk_rsrc).
 struct FastDiv {
-  uint32_t d, m, s;
-  __host__ __device__ FastDiv() : d(1), m(0), s(0) {}
+  uint32_t d, m, s, sh;
+  __host__ __device__ FastDiv() : d(1), m(0), s(0), sh(0) {}
   __host__ __device__ explicit FastDiv(uint32_t div) : d(div) {
     s = 0;
     while ((1ull << s) < div) ++s;
     m = (uint32_t)((((1ull << 32) * ((1ull << s) - div)) / div) + 1);
+    sh = s > 0 ? s - 1 : 0;
   }
   __device__ __forceinline__ uint32_t div(uint32_t n) const {
     uint32_t t = __umulhi(n, m);
-    return (t + ((n - t) >> 1)) >> (s > 0 ? s - 1 : 0);
+    return (t + ((n - t) >> 1)) >> sh;
   }
 };
 

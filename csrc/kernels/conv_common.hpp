@@ -132,7 +132,8 @@ template <bool AL, class T> struct PolMCDgradW {
                                          MCDgradW<R, T, NW>>::type;
 };
 template <class T> struct PolMCIm2colT {
-  template <int R, int NW> using type = MCIm2colT<R, T, NW>;
+  template <int R, int NW>
+  using type = typename std::conditional<use_buf<T>(), MCIm2colTBuf<R, T, NW>, MCIm2colT<R, T, NW>>::type;
 };
 
 // The main loop of tile config C over k-steps [kt0, kt1).  Operand policies come from the
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_wgrad_ker
   auto ia = [&](auto& a, uint32_t origin) { a.init(dy, Co, Co, K, origin, wave, lane, g_conv_zero); };
   auto ib = [&](auto& b, uint32_t origin) {
     if constexpr (DENSE) b.init(x, g.C, g.C, K, origin, wave, lane, g_conv_zero);
-    else b.init(x, g, origin, wave, lane, g_conv_zero);
+    else b.init(x, g, origin, wave, lane, g_conv_zero, kt0);  // (the buffer policy starts at kt0)
   };
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
   run_main_loop<T, C, PolMCDense<T>, PB>(smem, ia, ib, m0, n0, kt0, kt1, acc, wave, lane);

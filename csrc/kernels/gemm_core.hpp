@@ -59,9 +59,16 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
 // pointer math and no zero-page selects in the main loop.  Host contract: descriptor bytes
 // < 2^31 (bindings.cpp checks bf16 operand sizes).
 constexpr uint32_t kOOB = 0x80000000u;
+// The operands are uniform by construction; the readfirstlanes pin them to SGPRs, because a
+// descriptor (or soffset) the backend finds in VGPRs turns every LDS-DMA piece into a waterfall
+// loop (measured in the 256x256 dense data-grad before this).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t gk_rsrc(const void* base, uint64_t bytes) {
   const uint32_t b = bytes < (uint64_t)kOOB ? (uint32_t)bytes : kOOB - 16u;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)b, 0x00020000);
+  const uint64_t p = (uint64_t)(uintptr_t)base;
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(lo | (hi << 32)), 0,
+                                           __builtin_amdgcn_readfirstlane((int)b), 0x00020000);
 }
 
 __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base,
@@ -74,14 +81,34 @@ struct IsBufOp : std::false_type {};
 template <class Op>
 struct IsBufOp<Op, std::void_t<decltype(Op::BUF)>> : std::integral_constant<bool, Op::BUF> {};
 
-// one 1-KiB LDS-DMA wave-instruction of piece i of operand `op` at k-step kt (prep(kt) done)
+// Buffer policies whose voffsets need a k < K test on ONE k-step (kt_tail: the last step of a K
+// that is not a multiple of 64) expose tail(kt); every other step takes the fixed voffsets vo[i].
+template <class Op, class = void>
+struct HasTail : std::false_type {};
 template <class Op>
-__device__ __forceinline__ void dma16(const Op& op, int kt, int i, char* lds_wave_base) {
-  if constexpr (IsBufOp<Op>::value)
-    blds16(op.rsrc, lds_wave_base, op.voff(kt, i), op.soff);
-  else
-    glds16(op.src(kt, i), lds_wave_base);
+struct HasTail<Op, std::void_t<decltype(&Op::tail)>> : std::true_type {};
+template <class Op>
+__device__ __forceinline__ bool is_tail(const Op& op, int kt) {
+  if constexpr (HasTail<Op>::value) return op.tail(kt);
+  else return false;
 }
+
+// one 1-KiB LDS-DMA wave-instruction of piece i of operand `op` at k-step kt (prep(kt) done).
+// CHECK = false: the caller knows kt is not op's tail step (no per-piece compare / select).
+template <bool CHECK = true, class Op>
+__device__ __forceinline__ void dma16(const Op& op, int kt, int i, char* lds_wave_base) {
+  if constexpr (IsBufOp<Op>::value) {
+    if constexpr (CHECK || !HasTail<Op>::value) blds16(op.rsrc, lds_wave_base, op.voff(kt, i), op.soff);
+    else blds16(op.rsrc, lds_wave_base, op.vo[i], op.soff);
+  } else {
+    glds16(op.src(kt, i), lds_wave_base);
+  }
+}
+
+// Marks the end of a tail-step DMA block.  The checked and unchecked blocks otherwise end in the
+// same buffer loads, and the optimizer would sink them into one block with a select per voffset
+// (the per-piece compare + cndmask this split exists to remove).
+__device__ __forceinline__ void tail_block_end() { asm volatile("; k-tail stage" ::: "memory"); }
 
 // ---------------------------------------------------------------------------------------------
 // Operand policies.  Each describes one operand (A: rows = M, or B: rows = N) and exposes
@@ -162,6 +189,7 @@ struct KCDenseBuf {
       vo[i] = r < rows_total ? (uint32_t)(((long)r * ld + kcol) * sizeof(T)) : kOOB;
     }
   }
+  __device__ bool tail(int kt) const { return kt == kt_tail; }
   __device__ uint32_t voff(int kt, int i) const {
     if (kt == kt_tail) return (uint32_t)kt * BK + kcol < K ? vo[i] : kOOB;  // wave-uniform test
     return vo[i];
@@ -196,6 +224,7 @@ struct MCDenseBuf {
       vo[i] = col < cols_total ? (uint32_t)(((long)krow[i] * ld + col) * sizeof(T)) : kOOB;
     }
   }
+  __device__ bool tail(int kt) const { return kt == kt_tail; }
   __device__ uint32_t voff(int kt, int i) const {
     if (kt == kt_tail) return (uint32_t)kt * BK + krow[i] < K ? vo[i] : kOOB;
     return vo[i];
@@ -340,8 +369,12 @@ struct KCIm2colBuf {
     const uint32_t t = fdiv(g.fC, k0);
     const uint32_t kh = fdiv(g.fKW, t);
     const uint32_t kw = t - kh * (uint32_t)g.KW;
-    tap = t;
-    soff = (uint32_t)((((long)kh * g.W + kw) * g.C + (k0 - t * (uint32_t)g.C)) * sizeof(T));
+    // wave-uniform, but computed partly on the VALU (the FastDiv shift clamp): without the
+    // readfirstlane the buffer load's soffset is a VGPR and the backend wraps every LDS-DMA piece
+    // in a waterfall loop (readfirstlane / cmp / saveexec / branch per piece)
+    tap = __builtin_amdgcn_readfirstlane(t);
+    soff = __builtin_amdgcn_readfirstlane(
+        (uint32_t)((((long)kh * g.W + kw) * g.C + (k0 - t * (uint32_t)g.C)) * sizeof(T)));
   }
   __device__ uint32_t voff(int, int i) const { return (mask[i] >> tap) & 1u ? vo[i] : kOOB; }
 };
@@ -488,8 +521,9 @@ struct KCDgradBuf {
     const uint32_t t = fdiv(fCo, k0);
     const uint32_t a = fdiv(fnkw, t);
     const uint32_t b = t - a * fnkw.d;
-    tap = t;
-    soff = (uint32_t)(((long)sh - ((long)a * Wo + b) * Co + (k0 - t * (uint32_t)Co)) * sizeof(T));
+    tap = __builtin_amdgcn_readfirstlane(t);  // uniform: keep soffset an SGPR (KCIm2colBuf)
+    soff = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(((long)sh - ((long)a * Wo + b) * Co + (k0 - t * (uint32_t)Co)) * sizeof(T)));
   }
   __device__ uint32_t voff(int, int i) const { return (mask[i] >> tap) & 1u ? vo[i] : kOOB; }
 };
@@ -527,7 +561,7 @@ struct MCDgradWBuf {
     const uint32_t a = fdiv(fnkw, t);
     const uint32_t b = t - a * fnkw.d;
     const uint32_t tp = (uint32_t)(kh0 + S * (int)a) * (uint32_t)KW + (uint32_t)(kw0 + S * (int)b);
-    soff = (uint32_t)(((long)co0 * taps + tp) * Ci * sizeof(T));
+    soff = __builtin_amdgcn_readfirstlane((uint32_t)(((long)co0 * taps + tp) * Ci * sizeof(T)));
   }
   __device__ uint32_t voff(int, int i) const { return vo[i]; }
 };
@@ -613,7 +647,7 @@ struct MCIm2colT {
   const void* zero;
   __device__ void prep(int) {}
   __device__ void init(const T* x_, const ConvGeom& g_, uint32_t origin, int wave, int lane,
-                       const void* zero_page) {
+                       const void* zero_page, int /*kt0*/ = 0) {
     x = x_;
     g = g_;
     zero = zero_page;
@@ -645,6 +679,86 @@ struct MCIm2colT {
     const int off = (((int)img * g.H + hi) * g.W + wi) * g.C + ci[i];
     return ok ? (const void*)(x + off) : zero;
   }
+};
+
+// Conv weight-grad B operand (bf16) through a buffer descriptor, pixel state carried per lane.
+// The k index (output pixel) of a lane's row advances by 64 each k-step; instead of two fast
+// divisions + address math per piece and step (MCIm2colT), each piece keeps its pixel as scaled
+// coordinates (hs = ho*s, ws = wo*s_w) and its descriptor-relative element offset, and prep()
+// adds the mixed-radix digits of 64 (d_img, d_ho, d_wo) with two carries.  prep(kt) must be
+// called for kt0, kt0+1, ... in order (every main loop does; init takes kt0).  The descriptor
+// starts SHIFT = (pad*W + pad_w)*C elements before x, so offsets are never negative; padding
+// taps, pixels past N*Ho*Wo and columns past KH*KW*C get kOOB (zeros).
+template <int W, class T = __bf16, int NW = 4>
+struct MCIm2colTBuf {
+  static constexpr bool KC = false;
+  static constexpr bool BUF = true;
+  static constexpr int NI = W / (8 * NW);
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t soff;            // always 0: the k-step lives in the per-lane state
+  uint32_t vcur[NI];        // this k-step's voffsets (bytes), set by prep()
+  uint32_t off[NI], kk[NI];
+  int hs[NI], ws[NI], th[NI], tw[NI];
+  bool colok[NI];
+  int H, Wd, Hos, Wos, dhs, dws, s;
+  uint32_t K, doff, cw, ch;
+  __device__ void init(const T* x_, const ConvGeom& g, uint32_t origin, int wave, int lane,
+                       const void*, int kt0) {
+    H = g.H;
+    Wd = g.W;
+    s = g.stride;
+    K = (uint32_t)(g.N * g.Ho * g.Wo);
+    soff = 0;
+    const long shift = ((long)g.pad * g.W + g.pad_w) * g.C;
+    rsrc = gk_rsrc(x_ - shift, ((uint64_t)g.N * g.H * g.W * g.C + shift) * sizeof(T));
+    const uint32_t HoWo = (uint32_t)(g.Ho * g.Wo);
+    const uint32_t d_img = (uint32_t)BK / HoWo, rem = (uint32_t)BK - d_img * HoWo;
+    const uint32_t d_ho = rem / (uint32_t)g.Wo, d_wo = rem - d_ho * (uint32_t)g.Wo;
+    dws = (int)d_wo * g.stride_w;
+    dhs = (int)d_ho * g.stride;
+    Wos = g.Wo * g.stride_w;
+    Hos = g.Ho * g.stride;
+    doff = ((d_img * (uint32_t)g.H + (uint32_t)dhs) * (uint32_t)g.W + (uint32_t)dws) * (uint32_t)g.C;
+    cw = (uint32_t)((g.stride * g.W - Wos) * g.C);         // wo wraps: ws -= Wo*s_w, hs += s
+    ch = (uint32_t)((g.H - Hos) * g.W * g.C);              // ho wraps: hs -= Ho*s, img += 1
+    const uint32_t Ntot = (uint32_t)(g.KH * g.KW * g.C);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const uint32_t krow = MCGeom<W, NW>::row(wave, i, lane);
+      const uint32_t n = origin + MCGeom<W, NW>::chunk(wave, i, lane) * 8;
+      colok[i] = n < Ntot;
+      const uint32_t tap = fdiv(g.fC, n);
+      const uint32_t ci = n - tap * (uint32_t)g.C;
+      const uint32_t kh = fdiv(g.fKW, tap), kw = tap - kh * (uint32_t)g.KW;
+      th[i] = (int)kh - g.pad;
+      tw[i] = (int)kw - g.pad_w;
+      const uint32_t k = (uint32_t)kt0 * BK + krow;
+      kk[i] = k;
+      const uint32_t img = fdiv(g.fHoWo, k), r = k - img * HoWo;
+      const uint32_t ho = fdiv(g.fWo, r), wo = r - ho * (uint32_t)g.Wo;
+      hs[i] = (int)ho * g.stride;
+      ws[i] = (int)wo * g.stride_w;
+      off[i] = ((img * (uint32_t)g.H + (uint32_t)hs[i]) * (uint32_t)g.W + (uint32_t)ws[i]) * (uint32_t)g.C +
+               (kh * (uint32_t)g.W + kw) * (uint32_t)g.C + ci;
+    }
+  }
+  __device__ void prep(int) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const bool ok = colok[i] & (kk[i] < K) & ((unsigned)(hs[i] + th[i]) < (unsigned)H) &
+                      ((unsigned)(ws[i] + tw[i]) < (unsigned)Wd);
+      vcur[i] = ok ? off[i] * (uint32_t)sizeof(T) : kOOB;
+      ws[i] += dws;
+      const bool c1 = ws[i] >= Wos;
+      ws[i] -= c1 ? Wos : 0;
+      hs[i] += dhs + (c1 ? s : 0);
+      const bool c2 = hs[i] >= Hos;
+      hs[i] -= c2 ? Hos : 0;
+      off[i] += doff + (c1 ? cw : 0u) + (c2 ? ch : 0u);
+      kk[i] += BK;
+    }
+  }
+  __device__ uint32_t voff(int, int i) const { return vcur[i]; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -725,16 +839,23 @@ struct MainLoop {
   static_assert(NS >= 1 && NS <= 3, "1..3 LDS stages");
 
   // one LDS-DMA instruction (piece p of LOADS) of stage kt
+  template <bool CHECK = true>
   __device__ static void piece(char* buf, OpA& a, OpB& b, int kt, int wave, int p) {
-    if (p < OpA::NI) dma16(a, kt, p, buf + (wave * OpA::NI + p) * 1024);
-    else dma16(b, kt, p - OpA::NI, buf + A_BYTES + (wave * OpB::NI + p - OpA::NI) * 1024);
+    if (p < OpA::NI) dma16<CHECK>(a, kt, p, buf + (wave * OpA::NI + p) * 1024);
+    else dma16<CHECK>(b, kt, p - OpA::NI, buf + A_BYTES + (wave * OpB::NI + p - OpA::NI) * 1024);
   }
 
   __device__ static void stage(char* buf, OpA& a, OpB& b, int kt, int wave) {
     a.prep(kt);  // per-k-step wave-uniform address state (filter tap ...), computed once
     b.prep(kt);
+    if (is_tail(a, kt) || is_tail(b, kt)) {  // wave-uniform branch: at most one k-step
 #pragma unroll
-    for (int p = 0; p < LOADS; ++p) piece(buf, a, b, kt, wave, p);
+      for (int p = 0; p < LOADS; ++p) piece<true>(buf, a, b, kt, wave, p);
+      tail_block_end();
+    } else {
+#pragma unroll
+      for (int p = 0; p < LOADS; ++p) piece<false>(buf, a, b, kt, wave, p);
+    }
   }
 
   // Block barrier.  RAW: this wave's LDS reads retired + s_barrier, WITHOUT the vmcnt(0) a

@@ -93,8 +93,14 @@ struct MainLoopPP {
   template <class Op>
   __device__ static void half(Op& op, char* dst, int kt, int wave) {
     op.prep(kt);
+    if (is_tail(op, kt)) {  // wave-uniform: the last k-step of a K % 64 != 0 operand only
 #pragma unroll
-    for (int j = 0; j < Op::NI; ++j) dma16(op, kt, j, dst + (wave * Op::NI + j) * 1024);
+      for (int j = 0; j < Op::NI; ++j) dma16<true>(op, kt, j, dst + (wave * Op::NI + j) * 1024);
+      tail_block_end();
+    } else {
+#pragma unroll
+      for (int j = 0; j < Op::NI; ++j) dma16<false>(op, kt, j, dst + (wave * Op::NI + j) * 1024);
+    }
   }
 
   // DMA of global phase x (x >= -6; compile-time phase-in-tile Q = x & 3)
