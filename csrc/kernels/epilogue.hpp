@@ -312,6 +312,74 @@ struct EpiOps {
   }
 };
 
+// BatchNorm partial statistics by MFMA from the STAGED bf16 output tile (the stored values, as
+// the VALU path's as_stored): per 16-column group, Σy = 1ᵀY and Σy² = diag(YᵀY) over the tile's
+// rows (bf16 x bf16 products are exact in the fp32 accumulator), from transposed LDS reads (the MC fragment map of FragLoader<false>); then the shifted
+// moments Σ(y-s) = Σy - n·s and Σ(y-s)² = Σy² - 2s·Σy + n·s² per column, in double (n = rows
+// of the tile inside M; rows past M are masked out of the fragments).  Replaces
+// ~4 VALU per output element plus 16 DPP row sums per lane (the VALU path cost the wide
+// ResNet-50 1x1 forwards up to 50 %: profiles/r5_epilogue_cost.jsonl).
+#ifndef MIPIPE_VALU_STATS
+constexpr bool kMfmaStats = true;
+#else
+constexpr bool kMfmaStats = false;
+#endif
+template <int BM, int BN, int NWV>
+__device__ __forceinline__ void stats_mfma(const char* smem, const EpiParams& e, uint32_t m0,
+                                           uint32_t n0, int wave, int lane) {
+  constexpr int P = kEpiPitch<BN, __bf16>();
+  constexpr int NCG = BN / 16, NKC = BM / 32;
+  static_assert(BN % 16 == 0 && BM % 32 == 0, "MFMA statistics tile");
+  const uint32_t g = (uint32_t)lane >> 4, q4 = ((uint32_t)lane & 15) >> 2, p = (uint32_t)lane & 3;
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (__bf16)1.0f;
+  const uint32_t nv = e.M - m0 < (uint32_t)BM ? e.M - m0 : (uint32_t)BM;
+  for (int cg = wave; cg < NCG; cg += NWV) {  // wave-uniform
+    f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+    const uint32_t ch = (uint32_t)cg * 2 + (p >> 1);  // 8-column chunk of this lane's reads
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) {
+      const char* a0 = smem + (kc * 32 + 8 * g + q4) * P + ch * 16 + 8 * (p & 1);
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0 + 4 * P));
+      typedef __attribute__((ext_vector_type(8))) short s16x8;
+      const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bf16x8 y = __builtin_bit_cast(bf16x8, v);
+      if (nv < (uint32_t)BM) {  // partial tile (wave-uniform): rows past M add nothing, whatever
+        // was staged there (a bias, say); this lane's 8 values are rows kc*32 + 8g + 0..7
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if ((uint32_t)(kc * 32) + 8 * g + (uint32_t)r >= nv) y[r] = (__bf16)0.0f;
+      }
+      s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, y, s1, 0, 0, 0);  // rows: Σ_k Y[k][j]
+      s2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y, y, s2, 0, 0, 0);     // Σ_k Y[k][i] Y[k][j]
+    }
+    // lane holds D[i = 4(lane>>4) + q][j = lane & 15]: column j's diagonal sits at q = j & 3 of
+    // the lane with lane >> 4 == j >> 2 (which also holds its column sum)
+    const uint32_t j = (uint32_t)lane & 15;
+    if (g == (j >> 2)) {
+      const uint32_t n = n0 + (uint32_t)cg * 16 + j;
+      if (n < e.N) {
+        const int q = (int)(j & 3);
+        const double sy = (double)s1[q], syy = (double)s2[q], sh = (double)e.st_shift[n];
+        const double nd = (double)nv;
+        const float a = (float)(sy - nd * sh);
+        const float b = (float)(syy - 2.0 * sh * sy + nd * sh * sh);
+        if (e.det_rows > 0) {
+          const long row = (long)(e.det_row0 + m0 / BM) * e.N + n;
+          e.st_sum[row] = a;
+          e.st_sq[row] = b;
+        } else {
+          const long row = (long)(blockIdx.x % e.st_R) * e.N + n;
+          atomicAdd(e.st_sum + row, a);
+          atomicAdd(e.st_sq + row, b);
+        }
+      }
+    }
+  }
+}
+
 // Output in the activation dtype T (bf16, or fp32 on the reference-precision path).
 // acc layout: lane holds C[m][n..n+3] for tile (i, j).
 // FUSE: compile the dgrad fusions (addend / BN-backward reduction); kernels that never use
@@ -412,8 +480,10 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
   }
   // BatchNorm partial statistics from the fp32 accumulators, reduced over the block's BM rows
   // and added with fp32 atomics into replica slab (blockIdx % st_R) — 256-B-contiguous
-  // wave-instructions, no per-block partial rows to reduce later.
-  if (e.st_sum != nullptr) {
+  // wave-instructions, no per-block partial rows to reduce later.  (bf16 outputs: stats_mfma
+  // after the staging below instead.)
+  constexpr bool MSTATS = kMfmaStats && std::is_same<T, __bf16>::value;
+  if (!MSTATS && e.st_sum != nullptr) {
     float* lst = reinterpret_cast<float*>(smem + kStatsLdsOffset<BM, BN, T>());  // [2][WM][BN]
     // every column's shift requested before any is used (clamped column: unconditional loads),
     // so the block waits one memory latency here, not one per 16-column group
@@ -480,7 +550,9 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
     }
   if (early == nullptr) ops.prime(e, m0, n0);  // accumulators are dead now
   lds_barrier();
-  if (e.st_sum != nullptr) {
+  if (MSTATS && e.st_sum != nullptr) {
+    stats_mfma<BM, BN, kThreads / 64>(smem, e, m0, n0, wave, lane);
+  } else if (e.st_sum != nullptr) {
     // one fp32 atomic per column per block into replica row blockIdx % st_R (fire and forget:
     // no barrier below waits for them)
     const float* lst = reinterpret_cast<const float*>(smem + kStatsLdsOffset<BM, BN, T>());
