@@ -485,13 +485,15 @@ struct RouteOffs {
 // Route the pooled gradient to this wave's conv row (band row wr, parity HODD) and hand each
 // (i, j) fragment's 4 channel sums to f(i, j, gq).  The reads of fragment u+1 are in flight while
 // fragment u is consumed.
-template <bool HODD, class F>
+// NDP: staged dp rows (the idx rows follow them); [I0, I1): this wave's pixel blocks (f gets the
+// block's index relative to I0 first)
+template <bool HODD, int NDP = 3, int I0 = 0, int I1 = kPB, class F>
 __device__ __forceinline__ void route_row(uint32_t pst, const RouteOffs& ro, int wr, int lane,
                                           F&& f) {
   const int m = lane & 15;
   const uint32_t dpr0 = pst + (wr >> 1) * kDpRow, dpr1 = pst + ((wr + 1) >> 1) * kDpRow;
-  const uint32_t ixr0 = pst + 3 * kDpRow + (wr >> 1) * kIxRow;
-  const uint32_t ixr1 = pst + 3 * kDpRow + ((wr + 1) >> 1) * kIxRow;
+  const uint32_t ixr0 = pst + NDP * kDpRow + (wr >> 1) * kIxRow;
+  const uint32_t ixr1 = pst + NDP * kDpRow + ((wr + 1) >> 1) * kIxRow;
   const uint32_t wodd = m & 1;
   const uint32_t t00 = 3 * (HODD ? 2 : 1) + wodd + 1, t01 = 3 * (HODD ? 2 : 1);
   const uint32_t t10 = wodd + 1, t11 = 0;
@@ -521,10 +523,10 @@ __device__ __forceinline__ void route_row(uint32_t pst, const RouteOffs& ro, int
       if (on && ((ix >> (8 * q)) & 0xffu) == tap) gq[q] += dv[q];
   };
   Blk blk[2];
-  load(blk[0], 0);
+  load(blk[0], 4 * I0);
 #pragma unroll
-  for (int u = 0; u < 4 * kPB; ++u) {
-    if (u + 1 < 4 * kPB) {
+  for (int u = 4 * I0; u < 4 * I1; ++u) {
+    if (u + 1 < 4 * I1) {
       load(blk[(u + 1) & 1], u + 1);
       wait_lgkm<2 * NW>();  // fragment u's reads landed, u+1's in flight
     } else {
@@ -541,7 +543,7 @@ __device__ __forceinline__ void route_row(uint32_t pst, const RouteOffs& ro, int
       add(gq, k.d[2], k.x[2], t10, true);
       add(gq, k.d[3], k.x[3], t11, on1);
     }
-    f(i, u & 3, gq);
+    f(i - I0, i, u & 3, gq);
   }
 }
 
@@ -687,7 +689,7 @@ __global__ __launch_bounds__(256, 1) void stem_bwd_wgrad_kernel(
       }
       wait_lgkm<0>();
       const uint32_t k0 = (uint32_t)(wave * kWo + (ln & 15));
-      auto mkdy = [&](int i, int j, const float (&gq)[4]) {
+      auto mkdy = [&](int, int i, int j, const float (&gq)[4]) {
         const float a4[4] = {__uint_as_float(A[j][0]), __uint_as_float(A[j][1]),
                              __uint_as_float(A[j][2]), __uint_as_float(A[j][3])};
         const float b4[4] = {__uint_as_float(Bc[j][0]), __uint_as_float(Bc[j][1]),
@@ -719,7 +721,7 @@ __global__ __launch_bounds__(256, 1) void stem_bwd_wgrad_kernel(
                                  __uint_as_float(gv[j][0] & 0xffff0000u),
                                  __uint_as_float(gv[j][1] << 16),
                                  __uint_as_float(gv[j][1] & 0xffff0000u)};
-            mkdy(i, j, gq);
+            mkdy(i, i, j, gq);
           }
         }
       } else {
@@ -801,6 +803,218 @@ __global__ __launch_bounds__(256, 1) void stem_bwd_wgrad_kernel(
   }
 }
 
+
+// ---- half bands: 2 conv rows per band, TWO blocks per CU -------------------------------------
+// The 4-row kernel above holds 138 KB of LDS and runs one wave per SIMD, so a band's VALU routing
+// and its weight-grad MFMAs never overlap (469 us for ResNet-50 b256).  A half band (conv rows
+// 2t, 2t+1 of one image) needs 9 packed input rows (16.6 KB), 2 pooled rows (21 KB) and a 224-px
+// dy image (28 KB): 73 KB, so two blocks share a CU and one's routing runs beside the other's
+// MFMAs.  Waves: band row wr = wave >> 1, pixel blocks [0, 4) (even waves) or [4, 7) (odd).
+// Single LDS buffers, each refilled right after its last read in the band: pooled rows after
+// the routing, the patch after the MFMAs; y (registers) one band ahead.
+constexpr int kRBh = 2;                    // conv rows per half band
+constexpr int kPatchBH = 20 * 1024;        // 9 x 1840 = 16,560 B of packed rows (5 loads per wave)
+constexpr int kPoolStageH = 24 * 1024;     // 2 dp rows (14 KiB) + 2 idx rows (7 KiB), 6 per wave
+constexpr int kImgH = kRBh * kWo * 128;    // 224 px x 64 co bf16
+
+__device__ __forceinline__ void stage_patch_half(char* pb, const Geo& g, int n, int ho0, int wave,
+                                                 int lane) {
+  const auto r = buf_rsrc(g.xp, g.xp_bytes);
+  const uint32_t v = (uint32_t)((n * g.Hp + 2 * ho0) * kRowB + wave * 5 * 1024 + lane * 16);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) buf_lds16(r, pb + (wave * 5 + i) * 1024, v + i * 1024);
+}
+
+// pooled rows t, t+1 of image n (dp: loads 0..13, idx: 14..20; rows past the image read zeros)
+__device__ __forceinline__ void stage_pooled_half(char* buf, const PoolGrad& pg, int n, int t,
+                                                  int wave, int lane) {
+  const auto rd = buf_rsrc(reinterpret_cast<const char*>(pg.dp) + (long)n * pg.Hpo * kDpRow,
+                           (uint32_t)(pg.Hpo * kDpRow));
+  const auto ri = buf_rsrc(pg.idx + (long)n * pg.Hpo * kIxRow, (uint32_t)(pg.Hpo * kIxRow));
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int u = wave * 6 + k;  // wave-uniform
+    if (u < 14) {
+      const uint32_t p = (uint32_t)(u * 1024 + lane * 16);
+      const uint32_t r2 = p / kDpRow, q = p - r2 * kDpRow;
+      const uint32_t wo = q >> 7, ch = ((q >> 4) & 7) ^ (((wo >> 1) & 3) << 1);
+      buf_lds16(rd, buf + u * 1024, (uint32_t)((t + r2) * kDpRow) + wo * 128 + ch * 16);
+    } else if (u < 21) {
+      const uint32_t p = (uint32_t)((u - 14) * 1024 + lane * 16);
+      const uint32_t r2 = p / kIxRow, q = p - r2 * kIxRow;
+      const uint32_t wo = q >> 6, ch = ((q >> 4) & 3) ^ ((wo >> 2) & 1);
+      buf_lds16(ri, buf + u * 1024, (uint32_t)((t + r2) * kIxRow) + wo * 64 + ch * 16);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void stem_bwd_wgrad_half_kernel(
+    Geo g, PoolGrad pg, const __bf16* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ sum_g, const float* __restrict__ sum_gx, float inv_n,
+    float* __restrict__ ws, bool nty) {
+  __shared__ __attribute__((aligned(16))) char smem[kPatchBH + kPoolStageH + kImgH + 3 * kCo * 4];
+  char* pst = smem + kPatchBH;
+  char* gim = pst + kPoolStageH;
+  float* abc = reinterpret_cast<float*>(gim + kImgH);
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int wr = wave >> 1, hp = wave & 1;  // band row, pixel-block half
+  const int hb_per_img = g.Ho / kRBh, nb = g.N * hb_per_img;
+  if (tid < kCo) {
+    const int c = tid;
+    const float is = invstd[c], a = gamma[c] * is;
+    const float k1 = sum_g[c] * inv_n, k2 = sum_gx[c] * inv_n;
+    abc[c] = a;
+    abc[kCo + c] = -a * is * k2;
+    abc[2 * kCo + c] = -a * k1 + a * is * k2 * mean[c];
+  }
+  constexpr int NKB = 4;
+  f32x4 wacc[4][NKB];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < NKB; ++t) wacc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // y of this wave's half row: 4 pixel blocks (the odd half's 4th re-reads block 6: every wave
+  // issues the same 16 loads)
+  u32x2 yv[4][4];
+  auto load_y = [&](int bnd) {
+    const int n = bnd / hb_per_img, h = (bnd % hb_per_img) * kRBh + wr;
+    const __bf16* yr = y + (((long)n * g.Ho + h) * kWo + (lane & 15)) * kCo + 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ig = min(4 * hp + i, kPB - 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        yv[i][j] = nty ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(yr + 16 * ig * kCo + 16 * j))
+                       : *reinterpret_cast<const u32x2*>(yr + 16 * ig * kCo + 16 * j);
+    }
+  };
+  __syncthreads();
+  int b = blockIdx.x;
+  if (b < nb) {
+    load_y(b);
+    stage_patch_half(smem, g, b / hb_per_img, (b % hb_per_img) * kRBh, wave, lane);
+    stage_pooled_half(pst, pg, b / hb_per_img, b % hb_per_img, wave, lane);
+  }
+  const uint32_t img = lds_u32(gim);
+  for (; b < nb; b += gridDim.x) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int grp = ln >> 4, qq = (ln & 15) >> 2, p = ln & 3;
+    const int nxt = b + (int)gridDim.x;
+    wait_vmcnt<0>();
+    lds_barrier_raw();  // y, patch and pooled rows of band b landed
+    u32x2 yc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) yc[i][j] = yv[i][j];
+    if (nxt < nb) load_y(nxt);
+    const uint32_t patch = lds_u32(smem);
+    {
+      u32x4 A[4], Bc[4], Cc[4];
+      const uint32_t ab = lds_u32(abc) + 16 * grp;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        A[j] = ldk128(ab + 64 * j);
+        Bc[j] = ldk128(ab + 4 * kCo + 64 * j);
+        Cc[j] = ldk128(ab + 8 * kCo + 64 * j);
+      }
+      wait_lgkm<0>();
+      const uint32_t k0 = (uint32_t)(wr * kWo + (ln & 15));
+      auto mkdy = [&](int il, int i, int j, const float (&gq)[4]) {
+        const float a4[4] = {__uint_as_float(A[j][0]), __uint_as_float(A[j][1]),
+                             __uint_as_float(A[j][2]), __uint_as_float(A[j][3])};
+        const float b4[4] = {__uint_as_float(Bc[j][0]), __uint_as_float(Bc[j][1]),
+                             __uint_as_float(Bc[j][2]), __uint_as_float(Bc[j][3])};
+        const float c4[4] = {__uint_as_float(Cc[j][0]), __uint_as_float(Cc[j][1]),
+                             __uint_as_float(Cc[j][2]), __uint_as_float(Cc[j][3])};
+        const float yq[4] = {__uint_as_float(yc[il][j][0] << 16), __uint_as_float(yc[il][j][0] & 0xffff0000u),
+                             __uint_as_float(yc[il][j][1] << 16), __uint_as_float(yc[il][j][1] & 0xffff0000u)};
+        float d[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = a4[q] * bfr(gq[q]) + b4[q] * yq[q] + c4[q];
+        st64(img + img_off(k0 + 16 * i, j, grp), pack2(d[0], d[1]), pack2(d[2], d[3]));
+      };
+      RouteOffs ro;
+      ro.init(ln);
+      if (wr == 0) {
+        if (hp == 0) route_row<false, 2, 0, 4>(lds_u32(pst), ro, 0, ln, mkdy);
+        else route_row<false, 2, 4, kPB>(lds_u32(pst), ro, 0, ln, mkdy);
+      } else {
+        if (hp == 0) route_row<true, 2, 0, 4>(lds_u32(pst), ro, 1, ln, mkdy);
+        else route_row<true, 2, 4, kPB>(lds_u32(pst), ro, 1, ln, mkdy);
+      }
+    }
+    lds_barrier_raw();  // the band's dy image is complete; the pooled rows are consumed
+    if (nxt < nb) stage_pooled_half(pst, pg, nxt / hb_per_img, nxt % hb_per_img, wave, ln);
+    {
+      uint32_t dyr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        dyr[i] = img + mc_off<64>((uint32_t)(8 * grp + qq), (uint32_t)(2 * i + (p >> 1))) + 8 * (p & 1);
+      uint32_t toff[NKB];
+#pragma unroll
+      for (int t = 0; t < NKB; ++t) {
+        const int kb = wave + 4 * t;
+        const int tap = 2 * (kb < 14 ? kb : 0) + (p >> 1);
+        toff[t] = (uint32_t)(((tap >> 2) * kWsp + (tap & 3)) * 16 + 8 * (p & 1));
+      }
+      auto issue_a = [&](bf16x8 (&af)[4], int ks) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i] = join(tr_read(dyr[i] + ks * 32 * 128), tr_read(dyr[i] + ks * 32 * 128 + 4 * 128));
+      };
+      auto issue_b = [&](bf16x8 (&bf)[NKB], int ks) {
+        const int K0 = ks * 32 + 8 * grp + qq, K1 = K0 + 4;
+        const int r0 = K0 / kWo, w0 = K0 - r0 * kWo;
+        const int r1 = K1 / kWo, w1 = K1 - r1 * kWo;
+        const uint32_t pb0 = patch + (uint32_t)(((2 * r0) * kWsp + w0) * 16);
+        const uint32_t pb1 = patch + (uint32_t)(((2 * r1) * kWsp + w1) * 16);
+#pragma unroll
+        for (int t = 0; t < NKB; ++t) bf[t] = join(tr_read(pb0 + toff[t]), tr_read(pb1 + toff[t]));
+      };
+      constexpr int KS = kRBh * kWo / 32;  // 7 k-steps of 32 band pixels
+      bf16x8 af[2][4], bfv[2][NKB];
+      issue_a(af[0], 0);
+      issue_b(bfv[0], 0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int s = ks & 1;
+        if (ks + 1 < KS) {
+          issue_a(af[s ^ 1], ks + 1);
+          wait_lgkm<8>();
+          issue_b(bfv[s ^ 1], ks + 1);
+        } else {
+          wait_lgkm<0>();
+        }
+#pragma unroll
+        for (int t = 0; t < NKB; ++t) {
+          if (wave + 4 * t >= 14) continue;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            wacc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfv[s][t], af[s][i], wacc[i][t], 0, 0, 0);
+        }
+      }
+      wait_lgkm<0>();
+    }
+    lds_barrier_raw();  // every wave is done with the image and the patch
+    if (nxt < nb) stage_patch_half(smem, g, nxt / hb_per_img, (nxt % hb_per_img) * kRBh, wave, ln);
+  }
+  float* o = ws + (long)blockIdx.x * (kCo * 224);
+#pragma unroll
+  for (int t = 0; t < NKB; ++t) {
+    const int kb = wave + 4 * t;
+    if (kb >= 14) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = 16 * i + (lane & 15);
+      *reinterpret_cast<float4*>(o + co * 224 + 16 * kb + 4 * (lane >> 4)) =
+          make_float4(wacc[i][t][0], wacc[i][t][1], wacc[i][t][2], wacc[i][t][3]);
+    }
+  }
+}
+
 }  // namespace stem
 
 // ------------------------------------------------------------------------------------ host
@@ -838,7 +1052,18 @@ void stem_fwd_pool(const void* xp, const void* w, int N, int Ho, int Hp, const f
                      scale, bias, (__bf16*)out, idx, (__bf16*)y, (g_nt_store & 16) != 0);
 }
 
-int stem_wgrad_blocks(int N, int Ho) { return std::min(N * (Ho / stem::kRB), 256); }
+// MIPIPE_STEM_HALF=0: the 4-row-band kernel (one block per CU) instead of the half-band one
+static bool stem_half() {
+  static const bool on = [] {
+    const char* v = getenv("MIPIPE_STEM_HALF");
+    return v == nullptr || atoi(v) != 0;
+  }();
+  return on;
+}
+
+int stem_wgrad_blocks(int N, int Ho) {
+  return stem_half() ? std::min(N * (Ho / stem::kRBh), 512) : std::min(N * (Ho / stem::kRB), 256);
+}
 
 void stem_bwd_wgrad(const void* xp, const void* y, int N, int Ho, int Hp, const void* dp,
                     const uint8_t* idx, const float* mean, const float* invstd, const float* gamma,
@@ -854,7 +1079,11 @@ void stem_bwd_wgrad(const void* xp, const void* y, int N, int Ho, int Hp, const 
     const char* v = getenv("MIPIPE_STEM_SCATTER");
     return v != nullptr && atoi(v) != 0;
   }();
-  if (scatter)
+  if (stem_half())
+    hipLaunchKernelGGL(stem::stem_bwd_wgrad_half_kernel, dim3(G), dim3(256), 0, st,
+                       stem_geo(xp, nullptr, N, Ho, Hp), pg, (const __bf16*)y, mean, invstd, gamma,
+                       sum_g, sum_gx, 1.f / (float)count, ws, (g_nt_store & 512) != 0);
+  else if (scatter)
     hipLaunchKernelGGL(stem::stem_bwd_wgrad_kernel<true>, dim3(G), dim3(256), 0, st,
                        stem_geo(xp, nullptr, N, Ho, Hp), pg, (const __bf16*)y, mean, invstd, gamma,
                        sum_g, sum_gx, 1.f / (float)count, ws, (g_nt_store & 512) != 0);

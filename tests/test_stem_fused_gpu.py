@@ -142,3 +142,40 @@ def test_fused_stem_eval_matches_unfused():
         b = mnn.conv_bn_relu_maxpool(xp, conv, bn, pool)
     assert (a.float() - b.float()).abs().max().item() < 0.05
     assert (a != b).float().mean().item() < 1e-2
+
+
+def test_fused_stem_multi_band_blocks_match_unfused():
+    """Enough images that the weight-grad blocks loop over several bands each (the half-band
+    kernel runs min(N*56, 512) blocks)."""
+    conv, bn, pool = _stem(seed=7)
+    conv2, bn2 = copy.deepcopy(conv), copy.deepcopy(bn)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(8)
+    x = torch.randn(24, 3, 224, 224, device="cuda", generator=g)
+    dp = torch.randn(24, 56, 56, 64, device="cuda", generator=g).to(torch.bfloat16)
+    _run(conv, bn, pool, x, dp, fused=True)
+    _run(conv2, bn2, pool, x, dp, fused=False)
+    assert _rel(conv.weight.grad, conv2.weight.grad) < 1e-2
+    assert _rel(bn.weight.grad, bn2.weight.grad) < 1e-2
+    assert _rel(bn.bias.grad, bn2.bias.grad) < 1e-2
+
+
+def test_fused_stem_small_gamma_large_beta():
+    """The fused backward recovers x̂ = (z-β)/γ from the bf16 pooled output, whose rounding error
+    grows with |β/γ|; the unfused path takes x̂ from y.  Pinned here at |β/γ| up to 20 (init
+    values are γ = 1, β = 0)."""
+    conv, bn, pool = _stem(seed=9)
+    with torch.no_grad():
+        bn.weight.uniform_(0.05, 0.1)
+        bn.bias.uniform_(0.5, 1.0)
+    conv2, bn2 = copy.deepcopy(conv), copy.deepcopy(bn)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(10)
+    x = torch.randn(4, 3, 224, 224, device="cuda", generator=g)
+    dp = torch.randn(4, 56, 56, 64, device="cuda", generator=g).to(torch.bfloat16)
+    _run(conv, bn, pool, x, dp, fused=True)
+    _run(conv2, bn2, pool, x, dp, fused=False)
+    e = [_rel(conv.weight.grad, conv2.weight.grad), _rel(bn.weight.grad, bn2.weight.grad),
+         _rel(bn.bias.grad, bn2.bias.grad)]
+    print("small-gamma stem: rel err dW, dgamma, dbeta vs unfused:", e)
+    assert max(e) < 2e-2, e
