@@ -169,8 +169,8 @@ def test_rccl_collective_overlaps_compute():
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
-    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "r3", "overlap_probe.py"),
-                        "--mb", "256", "--gemms", "40", "--compute", "conv", "--n", "1024"],
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "overlap_probe.py"),
+                        "--mb", "1024", "--gemms", "40", "--compute", "conv", "--n", "1024"],
                        env=env, capture_output=True, text=True, timeout=240, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     res = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{"overlap_probe"')][0]

@@ -10,7 +10,7 @@ matmuls on the current stream.  For each mode we time
 and report overlap = (A + B - AB) / min(A, B)  (1.0 = fully hidden, 0.0 = serialised).
 Also a control with no RCCL: a side-stream copy kernel vs the same matmuls.
 
-usage: python tools/r3/overlap_probe.py [--mb 512] [--gemms 12]
+usage: python tools/overlap_probe.py [--mb 512] [--gemms 12]
 """
 from __future__ import annotations
 
@@ -23,10 +23,10 @@ import time
 import torch
 import torch.distributed as dist
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def timeit(fn, reps=5):
+def timeit(fn, reps=9):
     torch.cuda.synchronize()
     ts = []
     for _ in range(reps):
