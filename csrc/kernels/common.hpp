@@ -158,30 +158,26 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Fast unsigned division by a runtime constant (Granlund-Montgomery "round-up" variant).
-// sh = max(s - 1, 0) is precomputed: clamped on the device it became a VALU op, which made
-// every quotient of a wave-uniform index a VGPR (and the buffer soffsets built from it waterfall
-// loops, see gk_rsrc).
+// Fast unsigned division by a runtime constant (Granlund-Montgomery): with l = ceil(log2 d) and
+// m = floor(2^32 (2^l - d) / d) + 1, n / d = (umulhi(n, m) + n) >> l, the sum taken in 64 bits.
+// Exact for every 32-bit n and every d >= 1 (d = 1: l = 0, m = 1 -> n), so no d == 1 branch:
+// the per-k-step operand preps run it on wave-uniform (SGPR) indices, and a branch or a VALU
+// clamp there cost SALU issue slots in every conv main loop.
 struct FastDiv {
-  uint32_t d, m, s, sh;
-  __host__ __device__ FastDiv() : d(1), m(0), s(0), sh(0) {}
+  uint32_t d, m, s;
+  __host__ __device__ FastDiv() : d(1), m(1), s(0) {}
   __host__ __device__ explicit FastDiv(uint32_t div) : d(div) {
     s = 0;
     while ((1ull << s) < div) ++s;
     m = (uint32_t)((((1ull << 32) * ((1ull << s) - div)) / div) + 1);
-    sh = s > 0 ? s - 1 : 0;
   }
   __device__ __forceinline__ uint32_t div(uint32_t n) const {
-    uint32_t t = __umulhi(n, m);
-    return (t + ((n - t) >> 1)) >> sh;
+    const uint32_t t = __umulhi(n, m);
+    return (uint32_t)(((uint64_t)t + n) >> s);
   }
 };
 
-// s == 0 (div by 1) special case handled by callers passing d >= 1: for d == 1, s = 0, m = 1
-// gives t = n>>32=0... guard explicitly.
-__device__ __forceinline__ uint32_t fdiv(const FastDiv& f, uint32_t n) {
-  return f.d == 1 ? n : f.div(n);
-}
+__device__ __forceinline__ uint32_t fdiv(const FastDiv& f, uint32_t n) { return f.div(n); }
 
 // XCD-aware bijective remap of a linear workgroup id (guide §5 "XCD swizzle must be
 // bijective"): consecutive logical tiles land on the same XCD (shared L2).

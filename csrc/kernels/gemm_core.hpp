@@ -181,7 +181,7 @@ struct KCDenseBuf {
                        uint32_t origin, int wave, int lane, const void*) {
     K = K_;
     kcol = KCGeom<R, NW>::chunk(lane) * 8;
-    kt_tail = (K % BK) ? (int)(K / BK) : -1;
+    kt_tail = __builtin_amdgcn_readfirstlane((K % BK) ? (int)(K / BK) : -1);  // SGPR: a scalar branch
     rsrc = gk_rsrc(base, (uint64_t)rows_total * (uint64_t)ld * sizeof(T));
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -215,7 +215,7 @@ struct MCDenseBuf {
                        uint32_t origin, int wave, int lane, const void*) {
     ld = ld_;
     K = K_;
-    kt_tail = (K % BK) ? (int)(K / BK) : -1;
+    kt_tail = __builtin_amdgcn_readfirstlane((K % BK) ? (int)(K / BK) : -1);  // SGPR: a scalar branch
     rsrc = gk_rsrc(base, (uint64_t)K * (uint64_t)ld * sizeof(T));
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -369,9 +369,8 @@ struct KCIm2colBuf {
     const uint32_t t = fdiv(g.fC, k0);
     const uint32_t kh = fdiv(g.fKW, t);
     const uint32_t kw = t - kh * (uint32_t)g.KW;
-    // wave-uniform, but computed partly on the VALU (the FastDiv shift clamp): without the
-    // readfirstlane the buffer load's soffset is a VGPR and the backend wraps every LDS-DMA piece
-    // in a waterfall loop (readfirstlane / cmp / saveexec / branch per piece)
+    // wave-uniform; the readfirstlane keeps it provably so: a soffset the backend finds in a VGPR
+    // turns every LDS-DMA piece into a waterfall loop (readfirstlane / cmp / saveexec / branch)
     tap = __builtin_amdgcn_readfirstlane(t);
     soff = __builtin_amdgcn_readfirstlane(
         (uint32_t)((((long)kh * g.W + kw) * g.C + (k0 - t * (uint32_t)g.C)) * sizeof(T)));

@@ -891,10 +891,13 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_wgrad_half_kernel(
   };
   __syncthreads();
   int b = blockIdx.x;
+  // issue order per band, kept by the loop: y (16 loads), pooled rows (<= 6), patch (5) — so
+  // the routing waits for y and the pooled rows only (vmcnt 5: the patch may still fly) and the
+  // MFMAs for the patch (vmcnt 16: only the next band's y, issued after it, may still fly)
   if (b < nb) {
     load_y(b);
-    stage_patch_half(smem, g, b / hb_per_img, (b % hb_per_img) * kRBh, wave, lane);
     stage_pooled_half(pst, pg, b / hb_per_img, b % hb_per_img, wave, lane);
+    stage_patch_half(smem, g, b / hb_per_img, (b % hb_per_img) * kRBh, wave, lane);
   }
   const uint32_t img = lds_u32(gim);
   for (; b < nb; b += gridDim.x) {
@@ -902,8 +905,8 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_wgrad_half_kernel(
     asm volatile("" : "+v"(ln));
     const int grp = ln >> 4, qq = (ln & 15) >> 2, p = ln & 3;
     const int nxt = b + (int)gridDim.x;
-    wait_vmcnt<0>();
-    lds_barrier_raw();  // y, patch and pooled rows of band b landed
+    wait_vmcnt<5>();
+    lds_barrier_raw();  // y and pooled rows of band b landed (every wave's)
     u32x2 yc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -946,7 +949,9 @@ __global__ __launch_bounds__(256, 2) void stem_bwd_wgrad_half_kernel(
         else route_row<true, 2, 4, kPB>(lds_u32(pst), ro, 1, ln, mkdy);
       }
     }
-    lds_barrier_raw();  // the band's dy image is complete; the pooled rows are consumed
+    if (nxt < nb) wait_vmcnt<16>();
+    else wait_vmcnt<0>();
+    lds_barrier_raw();  // dy image complete, pooled rows consumed, band b's patch landed
     if (nxt < nb) stage_pooled_half(pst, pg, nxt / hb_per_img, nxt % hb_per_img, wave, ln);
     {
       uint32_t dyr[4];
