@@ -51,6 +51,9 @@ struct Tile {
 //     (tools/gemm_lab/pp_lab.hip, profiles/r4_pp_lab_v1.jsonl)
 // 12: 256x128, ping-pong 2x4 waves    — large M, medium N
 // 13: 128x256, ping-pong 2x4 waves    — medium M, large N
+// 14: 128x128, ping-pong 2x4 waves    — the 8-wave schedule for mid-size convs whose 256-wide
+//     tiles leave CUs idle (e.g. 14x14x256 3x3: 196 tiles of 256x256 for 256 CUs); 64 KB of LDS,
+//     two blocks per CU
 typedef Tile<128, 128, 2, 2, 2> T0;
 typedef Tile<128, 128, 1, 2, 2> T1;
 typedef Tile<128, 64, 2, 2, 2> T2;
@@ -65,7 +68,8 @@ typedef Tile<64, 128, 1, 2, 2> T10;
 typedef Tile<256, 256, 2, 2, 4, true> T11;
 typedef Tile<256, 128, 2, 2, 4, true> T12;
 typedef Tile<128, 256, 2, 2, 4, true> T13;
-constexpr int kNumTiles = 14;
+typedef Tile<128, 128, 2, 2, 4, true> T14;
+constexpr int kNumTiles = 15;
 static_assert(kNumTiles == kConvTileConfigs, "launchers.hpp tile count");
 
 // fp32 operands run the split-bf16x3 loop (3 LDS images): 4-wave tiles only.
@@ -170,7 +174,9 @@ __device__ __forceinline__ void run_main_loop(char* smem, IA&& ia, IB&& ib, uint
 template <class T, class C>
 constexpr int conv_occ() {
   // (asking 5-6 blocks of the single-stage half-size tiles 9/10 spills: they need ~100 VGPRs)
-  return C::NW == 8 ? 1 : ((C::NS == 1 && !std::is_same<T, float>::value) ? 3 : 2);
+  // (8-wave tiles: one block per CU, two for the 64 KB 128x128 ping-pong tile)
+  return C::NW == 8 ? (C::BM * C::BN <= 128 * 128 ? 2 : 1)
+                    : ((C::NS == 1 && !std::is_same<T, float>::value) ? 3 : 2);
 }
 
 // DGRAD_EPI: the same im2col main loop run as a stride-1 data-grad (x = dy, w = the tap-flipped
@@ -320,6 +326,7 @@ inline void with_tile(int cfg, F&& f) {
       case 11: f(T11{}); break;
       case 12: f(T12{}); break;
       case 13: f(T13{}); break;
+      case 14: f(T14{}); break;
       default: f(T0{}); break;
     }
   }

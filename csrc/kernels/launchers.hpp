@@ -49,7 +49,7 @@ int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 // bias / relu: optional per-channel bias and ReLU in the epilogue (convs without BN: VGG, AlexNet)
 // cfg: tile config id (conv_common.hpp table; < 0 = heuristic default)
-constexpr int kConvTileConfigs = 14;
+constexpr int kConvTileConfigs = 15;
 //  det_rows > 0 (deterministic mode): st_sum / st_sq are [det_rows][Co] partial slabs, one row
 //  per M-tile (det_rows = conv_fwd_tiles_m(s, cfg)), written without atomics.
 // wflip (Ci*KH*KW*Co elements, w's dtype): when dgrad_preflip_ok(s), trailing blocks of the

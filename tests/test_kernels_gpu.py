@@ -661,7 +661,7 @@ TILE_CASES = [
 ]
 
 
-@pytest.mark.parametrize("cfg", list(range(14)))
+@pytest.mark.parametrize("cfg", list(range(15)))
 @pytest.mark.parametrize("case", TILE_CASES)
 @DTYPES
 def test_conv_every_tile_config(cfg, case, dt):
