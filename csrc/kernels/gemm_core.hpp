@@ -804,8 +804,12 @@ __device__ __forceinline__ void wait_vmcnt() {
 constexpr int kLoopRawBarrier = 1;  // lgkmcnt(0) + s_barrier instead of __syncthreads()
 constexpr int kLoopPrio = 2;        // s_setprio(1) around the MFMA block
 constexpr int kLoopSpread = 4;      // next stage's LDS-DMA pieces spread between MFMAs
+// single-stage tiles: the next k-step's LDS-DMA is issued as soon as every wave holds this
+// k-step's fragments in registers (a barrier after the reads), so it flies under this k-step's
+// MFMAs instead of after them
+constexpr int kLoopEarlyDma = 8;
 #ifndef MIPIPE_LOOP_DEFAULT
-#define MIPIPE_LOOP_DEFAULT 3
+#define MIPIPE_LOOP_DEFAULT 11
 #endif
 constexpr int kLoopDefault = MIPIPE_LOOP_DEFAULT;
 
@@ -916,6 +920,39 @@ struct MainLoop {
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   }
 
+  // NS == 1 with kLoopEarlyDma: fragments of k-step kt -> barrier (the single buffer is free)
+  // -> LDS-DMA of kt+1 -> MFMAs of kt
+  template <bool FIRST>
+  __device__ static void compute_then_refill(char* smem, f32x4 (&acc)[MT][NT], uint32_t arow0,
+                                             uint32_t bcol0, int lane, OpA& a, OpB& b, int kt_next,
+                                             int kt1, int wave) {
+    const char* aimg = smem;
+    const char* bimg = smem + A_BYTES;
+    bf16x8 af[2][MT], bfr[2][NT];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        af[ks][i] = FragLoader<OpA::KC, BM>::load(aimg, arow0 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        bfr[ks][j] = FragLoader<OpB::KC, BN>::load(bimg, bcol0 + j * 16, ks, lane);
+    }
+    barrier();  // this wave's reads retired (lgkmcnt 0) and every other wave's: buffer free
+    if (kt_next < kt1) stage(smem, a, b, kt_next, wave);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              bfr[ks][j], af[ks][i], (FIRST && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j],
+              0, 0, 0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  }
+
   __device__ static void run(char* smem, OpA& a, OpB& b, int kt0, int kt1,
                              f32x4 (&acc)[MT][NT], int wave, int lane) {
     if (kt0 >= kt1) {
@@ -927,7 +964,15 @@ struct MainLoop {
     }
     const int wr = wave / WN, wc = wave % WN;
     const uint32_t arow0 = wr * (BM / WM), bcol0 = wc * (BN / WN);
-    if constexpr (NS == 1) {
+    if constexpr (NS == 1 && (V & kLoopEarlyDma) != 0) {
+      stage(smem, a, b, kt0, wave);
+      for (int kt = kt0; kt < kt1; ++kt) {
+        wait_vmcnt<0>();
+        barrier();  // every wave's pieces of stage kt landed
+        if (kt == kt0) compute_then_refill<true>(smem, acc, arow0, bcol0, lane, a, b, kt + 1, kt1, wave);
+        else compute_then_refill<false>(smem, acc, arow0, bcol0, lane, a, b, kt + 1, kt1, wave);
+      }
+    } else if constexpr (NS == 1) {
       for (int kt = kt0; kt < kt1; ++kt) {
         if (kt > kt0) __syncthreads();  // every wave is done reading the single buffer
         stage(smem, a, b, kt, wave);
