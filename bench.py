@@ -177,6 +177,7 @@ def main() -> int:
         _heartbeat()
     r = _run(a, world, rank, local, dev, distributed, cpu)
     det = None
+    rd = None
     if _want_det_variant(a, cpu):
         # the headline again in the reference's own mode (task.py:25 cudnn.deterministic=True:
         # no float atomics, fixed-order reductions, shipped plan tables), same discipline
@@ -205,6 +206,8 @@ def main() -> int:
         b.batch = a.ref_batch
         b.emulate_ranks, b.dump_params, b.save_tune = 1, None, None
         r.pop("model", None)
+        if rd is not None:  # the deterministic variant's DDP model and buckets: gone too
+            rd.pop("model", None)
         if not cpu:
             torch.cuda.empty_cache()
         rr = _run(b, world, rank, local, dev, distributed, cpu)

@@ -57,6 +57,16 @@ float* fptr(const optional<Tensor>& t, int64_t n) {
   return t->data_ptr<float>();
 }
 
+// bf16 operands go through buffer descriptors with 32-bit byte offsets (gemm_core.hpp kOOB,
+// gk_rsrc clamps the range): a larger bf16 tensor would read zeros, so every conv entry point
+// (forward, data-grad, weight-grad) checks its input and output sizes here.
+void check_conv_buf_bytes(const mipipe::ConvShape& s, bool f32, const char* what) {
+  if (f32) return;
+  const int64_t lim = (1ll << 31) - (1ll << 24);
+  TORCH_CHECK((int64_t)s.N * s.H * s.W * s.Ci * 2 < lim && (int64_t)s.N * s.Ho * s.Wo * s.Co * 2 < lim,
+              "bf16 ", what, " tensors beyond 2 GiB are not supported");
+}
+
 mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int pad,
                              int stride_w = 0, int pad_w = -1) {
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv expects NHWC x and [Co,KH,KW,Ci] w");
@@ -79,11 +89,7 @@ mipipe::ConvShape conv_shape(const Tensor& x, const Tensor& w, int stride, int p
   TORCH_CHECK((int64_t)s.N * s.H * s.W * s.Ci < (1ll << 31) &&
                   (int64_t)s.N * s.Ho * s.Wo * s.Co < (1ll << 31),
               "conv tensors beyond 2^31 elements are not supported");
-  // bf16 operands go through buffer descriptors with 32-bit byte offsets (gemm_core.hpp kOOB)
-  const int64_t esz = x.scalar_type() == at::kFloat ? 4 : 2;
-  TORCH_CHECK(esz == 4 || ((int64_t)s.N * s.H * s.W * s.Ci * esz < (1ll << 31) - (1ll << 24) &&
-                           (int64_t)s.N * s.Ho * s.Wo * s.Co * esz < (1ll << 31) - (1ll << 24)),
-              "bf16 conv tensors beyond 2 GiB are not supported");
+  check_conv_buf_bytes(s, x.scalar_type() == at::kFloat, "conv");
   return s;
 }
 
@@ -302,6 +308,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
               "dy shape does not match the convolution");
   TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv dgrad needs Ci, Co % 8 == 0");
   TORCH_CHECK(dy.numel() < (1ll << 31), "conv dgrad dy too large for 32-bit gather offsets");
+  check_conv_buf_bytes(s, s.f32, "conv dgrad");
   TORCH_CHECK(s.pad < s.KH && pw < s.KW, "conv dgrad expects padding < kernel size");
   auto dx = torch::empty({s.N, s.H, s.W, s.Ci}, dy.options());
   // data-grads run as forward convolutions over tap-flipped (sub-)kernels, per stride-parity
@@ -444,6 +451,7 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
   TORCH_CHECK(x.numel() < (1ll << 31), "conv wgrad input too large for 32-bit gather offsets");
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo, "dy/x mismatch");
   TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv wgrad needs Ci, Co % 8 == 0");
+  check_conv_buf_bytes(s, s.f32, "conv wgrad");
   Tensor dw;
   if (out.has_value()) {  // accumulate straight into an existing gradient (flat DDP bucket view)
     check_f32(*out, "out");

@@ -393,6 +393,13 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
                              EpiOps<BM, BN, FUSE, T, WM, WN, TWO>* early = nullptr) {
   constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
   constexpr int kThreads = 64 * WM * WN;
+  // BN-backward Σg·x̂ as invstd·(Σg·y - mean·Σg): exact products for bf16 g, y only; the fp32
+  // path (and -DMIPIPE_BNR_CENTERED) accumulates the centred g·(y - mean)·invstd instead
+#ifdef MIPIPE_BNR_CENTERED
+  constexpr bool kBnrUncentered = false;
+#else
+  constexpr bool kBnrUncentered = !std::is_same<T, float>::value;
+#endif
   const int wr = wave / WN, wc = wave % WN;
   typedef AccMap<BM, BN, WM, WN, HALVES> Map;
   const uint32_t lr = lane & 15, lc = (lane >> 4) * 4;
@@ -606,27 +613,26 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
                                  : (zmask ? zv[q] : yv[q] * b_sc[q] + b_bi[q]);
           const float gq = zq > 0.f ? as_stored<T>(f[q]) : 0.f;  // stats of the stored g
           f[q] = gq;
-#ifndef MIPIPE_BNR_CENTERED
-          // Σg and Σg·y here (2 VALU); Σg·x̂ = invstd·(Σg·y - mean·Σg) once per thread below.
-          // bf16 g and y: each product is exact in fp32
-          const float gw = w * gq;
-          sg[q] += gw;
-          sgx[q] = fmaf(gw, yv[q], sgx[q]);
-#else
-          sg[q] += w * gq;
-          sgx[q] += w * gq * (yv[q] - b_mu[q]) * b_is[q];
-#endif
+          if constexpr (kBnrUncentered) {
+            // Σg and Σg·y here (2 VALU); Σg·x̂ = invstd·(Σg·y - mean·Σg) once per thread below.
+            // bf16 g and y: each product is exact in fp32
+            const float gw = w * gq;
+            sg[q] += gw;
+            sgx[q] = fmaf(gw, yv[q], sgx[q]);
+          } else {  // fp32 (the reference's precision): centred, no cancellation at |mean| >> std
+            sg[q] += w * gq;
+            sgx[q] += w * gq * (yv[q] - b_mu[q]) * b_is[q];
+          }
         }
         if constexpr (TWO) {
           float y2v[8];
           unpack_raw(ops.y2[it % PF], y2v);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-#ifndef MIPIPE_BNR_CENTERED
-            sgx2[q] = fmaf(w * f[q], y2v[q], sgx2[q]);
-#else
-            sgx2[q] += w * f[q] * (y2v[q] - b_mu2[q]) * b_is2[q];
-#endif
+            if constexpr (kBnrUncentered)
+              sgx2[q] = fmaf(w * f[q], y2v[q], sgx2[q]);
+            else
+              sgx2[q] += w * f[q] * (y2v[q] - b_mu2[q]) * b_is2[q];
           }
         }
       }
@@ -666,14 +672,14 @@ __device__ void epilogue_out(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
     }
   }
   if (FUSE && bnr) {
-#ifndef MIPIPE_BNR_CENTERED
-    // this thread's columns: Σg·x̂ = invstd·(Σg·y - mean·Σg) (linear: the sums below add these)
+    if constexpr (kBnrUncentered) {
+      // this thread's columns: Σg·x̂ = invstd·(Σg·y - mean·Σg) (linear: the sums below add these)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      sgx[q] = b_is[q] * (sgx[q] - b_mu[q] * sg[q]);
-      if constexpr (TWO) sgx2[q] = b_is2[q] * (sgx2[q] - b_mu2[q] * sg[q]);
+      for (int q = 0; q < 8; ++q) {
+        sgx[q] = b_is[q] * (sgx[q] - b_mu[q] * sg[q]);
+        if constexpr (TWO) sgx2[q] = b_is2[q] * (sgx2[q] - b_mu2[q] * sg[q]);
+      }
     }
-#endif
     // threads t, t+CPR, ... share a column chunk: reduce them through LDS, then one atomic
     // per column per block into replica row blockIdx % R
     lds_barrier();  // all staging-tile reads done (red overlaps it)

@@ -5,7 +5,8 @@ aiplatform ``CustomTrainingJob`` replicas, reference nb:181-188) and ``launch.lo
 (``bench.py --gpus N``, torchrun-style).  GPU visibility policy on one xGMI node — two modes:
 
 * ``"slice"`` (the launcher's default whenever a replica owns fewer GPUs than the node exposes):
-  each replica SEES only its own GPUs (``HIP_VISIBLE_DEVICES`` narrowed, offset 0), exactly what
+  each replica SEES only its own GPUs (``HIP_VISIBLE_DEVICES`` narrowed, offset 0 — or
+  ``ROCR_VISIBLE_DEVICES`` when that is where the ids came from), exactly what
   a Vertex VM with ``accelerator_count`` GPUs looks like.  Programs that count devices —
   the unmodified reference task.py (``ngpus_per_node = torch.cuda.device_count()``, task.py:102)
   or a non-distributed ``DataParallel(model)`` (task.py:201-208) — then stay on their slice.
@@ -56,11 +57,14 @@ def rank_env(base: Mapping[str, str], *, master_addr: str, master_port: int,
              local_rank: Optional[int] = None, local_world: Optional[int] = None,
              group_rank: Optional[int] = None, gpu_offset: int = 0,
              replica_gpus: Optional[int] = None, extra: Optional[Mapping[str, str]] = None,
-             rccl: bool = True, visible: Optional[str] = None) -> Dict[str, str]:
+             rccl: bool = True, visible: Optional[str] = None,
+             visible_var: str = "HIP_VISIBLE_DEVICES") -> Dict[str, str]:
     """Environment of one launched process.  ``replica_gpus``: GPUs owned by this process's
     replica (None: leave the GPU variables alone; 0: CPU-only replica).  ``visible``: the
     replica's own GPU ids ("slice" mode: HIP_VISIBLE_DEVICES narrowed to them, offset 0), or
-    None ("all" mode: visibility left as found, the slice named by the offset)."""
+    None ("all" mode: visibility left as found, the slice named by the offset).  ``visible_var``:
+    the variable the ids were read from — ``ROCR_VISIBLE_DEVICES`` ids are physical indices,
+    so that slice narrows ROCR itself (HIP would renumber them relative to the ROCR set)."""
     e = dict(base)
     if extra:
         e.update(extra)
@@ -83,7 +87,11 @@ def rank_env(base: Mapping[str, str], *, master_addr: str, master_port: int,
         else:
             e.pop("MIPIPE_FORCE_CPU", None)
             if visible is not None:
-                e["HIP_VISIBLE_DEVICES"] = visible
+                if visible_var == "ROCR_VISIBLE_DEVICES":
+                    e["ROCR_VISIBLE_DEVICES"] = visible
+                    e.pop("HIP_VISIBLE_DEVICES", None)
+                else:
+                    e["HIP_VISIBLE_DEVICES"] = visible
                 e.pop("CUDA_VISIBLE_DEVICES", None)
                 e["MIPIPE_DEVICE_OFFSET"] = "0"
             else:

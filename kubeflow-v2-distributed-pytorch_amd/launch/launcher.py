@@ -36,7 +36,8 @@ from typing import Dict, List, Optional, Sequence
 
 from .env import rank_env
 
-__all__ = ["LaunchSpec", "launch", "free_port", "visible_gpu_ids", "ReplicaResult"]
+__all__ = ["LaunchSpec", "launch", "free_port", "visible_gpu_ids", "visible_gpu_source",
+           "ReplicaResult"]
 
 
 def free_port() -> int:
@@ -45,14 +46,24 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def visible_gpu_ids() -> List[str]:
-    """GPU ids this launcher may hand out (honours an outer HIP/CUDA_VISIBLE_DEVICES)."""
+def visible_gpu_source(env=None):
+    """``(variable, ids)``: the GPU ids this launcher may hand out and the variable they came
+    from (None: no outer mask, ids are the node's device indices).  HIP numbers devices relative
+    to the ROCR-filtered set, so a slice must be written back into the SAME variable: ids read
+    from ``ROCR_VISIBLE_DEVICES`` (e.g. under Slurm) are physical and only mean something to
+    ROCR, ids read from ``HIP/CUDA_VISIBLE_DEVICES`` are relative to whatever ROCR exposes."""
+    env = os.environ if env is None else env
     for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
-        v = os.environ.get(var)
+        v = env.get(var)
         if v is not None and v.strip() != "":
-            return [x.strip() for x in v.split(",") if x.strip() != ""]
+            return var, [x.strip() for x in v.split(",") if x.strip() != ""]
     n = _count_gpus()
-    return [str(i) for i in range(n)]
+    return None, [str(i) for i in range(n)]
+
+
+def visible_gpu_ids() -> List[str]:
+    """GPU ids this launcher may hand out (honours an outer HIP/CUDA/ROCR_VISIBLE_DEVICES)."""
+    return visible_gpu_source()[1]
 
 
 def _count_gpus() -> int:
@@ -124,7 +135,9 @@ def _kill_group(p: subprocess.Popen, sig) -> None:
 
 def build_envs(spec: LaunchSpec) -> List[Dict[str, str]]:
     """Environment of every process the launch starts (exposed for tests)."""
-    gpus = visible_gpu_ids()
+    src_var, gpus = visible_gpu_source()
+    # a slice is written back into the variable the ids came from (ROCR ids are physical)
+    slice_var = "ROCR_VISIBLE_DEVICES" if src_var == "ROCR_VISIBLE_DEVICES" else "HIP_VISIBLE_DEVICES"
     per_replica = spec.accelerator_count
     nproc = spec.nproc_per_node
     total_needed = spec.replica_count * per_replica
@@ -155,7 +168,7 @@ def build_envs(spec: LaunchSpec) -> List[Dict[str, str]]:
             e = rank_env(os.environ, master_addr=spec.master_addr, master_port=port,
                          gpu_offset=r * per_replica, replica_gpus=per_replica, extra=spec.env,
                          visible=",".join(own) if (mode == "slice" and per_replica) else None,
-                         **ids)
+                         visible_var=slice_var, **ids)
             if spec.model_dir:
                 e["AIP_MODEL_DIR"] = spec.model_dir
             if spec.checkpoint_dir:

@@ -114,8 +114,14 @@ class _SparseRowExchange:
     capacity is agreed once (the largest first-step token count, one host exchange) and every
     later step pads its ids with -1 (skipped by the scatter) and its rows with zeros up to it.
     A ragged / dynamically padded batch with fewer tokens therefore still matches; a step with
-    MORE tokens than the capacity raises before issuing any collective.  The capacity is part of
-    the collective digest (``check_collectives``)."""
+    MORE tokens than the capacity raises on the rank that grew, before that rank issues any
+    collective.  Its peers have no way to know without a host round trip per step (which a
+    captured hipGraph step cannot make), so they block in the ids ``all_gather`` until the job
+    is torn down: mipipe's launchers are fail-fast (the raising rank's non-zero exit SIGTERMs
+    every other rank, launch/launcher.py), and otherwise the process group's timeout or the
+    transport's peer-closed error ends them — never a silently mismatched collective
+    (``tests/test_optim_ddp.py::test_ddp_sparse_capacity_one_rank_grows``).  The capacity is
+    part of the collective digest (``check_collectives``)."""
 
     def __init__(self, ddp: "DistributedDataParallel", param: tnn.Parameter):
         self.ddp = ddp

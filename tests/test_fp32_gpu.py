@@ -119,6 +119,29 @@ def test_conv_dgrad_fused_epilogue_fp32():
     assert rel_err(sgx, (gr * xhat).reshape(-1, Ci).sum(0)) < TOL
 
 
+def test_conv_dgrad_fused_bn_sums_fp32_large_mean():
+    """fp32 BN-backward sums at |mean| >> std (advice r5): the fp32 epilogue accumulates the
+    centred g·(y - mean)·invstd — the uncentred invstd·(Σg·y - mean·Σg) form the bf16 path uses
+    would cancel ~|mean|/std = 1e3 of its digits here."""
+    N, H, W, Ci, Co = 8, 8, 8, 64, 64
+    dy = f32(N, H, W, Co)
+    w = f32(Co, 1, 1, Ci, scale=1.0 / math.sqrt(Co))
+    y = 50.0 + 0.05 * f32(N, H, W, Ci)
+    mean = y.double().reshape(-1, Ci).mean(0).float()
+    invstd = (1.0 / y.double().reshape(-1, Ci).std(0, unbiased=False)).float()
+    gamma = torch.rand(Ci, device=dev) + 0.5
+    beta = torch.full((Ci,), 10.0, device=dev)  # z = γx̂ + β > 0: no ReLU decision near 0
+    scale, bias = gamma * invstd, beta - mean * gamma * invstd
+    rep = torch.zeros(3, native().STAT_REPLICAS, Ci, device=dev)
+    g = native().conv_dgrad(dy, w, [N, H, W, Ci], 1, 0, None, y, mean, invstd, scale, bias, rep)
+    sg, sgx = native().bn_bwd_collect(rep, Ci)
+    gr = _ref.conv_dgrad(d(dy), d(w), (N, H, W, Ci), 1, 0) * ((d(y) * d(scale) + d(bias)) > 0)
+    assert rel_err(g, gr) < TOL
+    xhat = (d(y) - d(mean)) * d(invstd)
+    assert rel_err(sg, gr.reshape(-1, Ci).sum(0)) < TOL
+    assert rel_err(sgx, (gr * xhat).reshape(-1, Ci).sum(0)) < TOL
+
+
 @pytest.mark.parametrize("M,N,K", [(1024, 512, 512), (300, 72, 200), (32, 1000, 512),
                                    (1024, 10, 512)])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])

@@ -316,3 +316,46 @@ def test_ddp_bert_lookup_ids_exchanged_during_forward():
         assert out[r]["cap"] == 4 * 32
         assert out[r]["ragged_ok"] and out[r]["same_on_all_ranks"], out[r]
         assert out[r]["grow_raises"], out[r]
+
+
+def _one_rank_grows_worker(rank, world, port, out):
+    import datetime
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=30))
+    from mipipe.models import create_model
+    from mipipe.parallel import DistributedDataParallel
+    torch.manual_seed(0)
+    m = create_model("bert_tiny", hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    d = DistributedDataParallel(m)
+    V = m.bert.embeddings.word_embeddings.weight.shape[0]
+
+    def batch(B, S=16):
+        g = torch.Generator().manual_seed(rank)
+        return (torch.randint(0, V, (B, S), generator=g), torch.ones(B, S, dtype=torch.int64),
+                torch.zeros(B, 2, dtype=torch.int64), torch.randint(0, V, (B, 2), generator=g))
+
+    ids, am, pos, lab = batch(2)
+    d(ids, am, masked_positions=pos, labels=lab).backward()
+    res = {"cap": d._sparse[0].cap}
+    # only rank 1 grows: it raises before issuing; rank 0 must not complete the step silently
+    ids, am, pos, lab = batch(3 if rank == 1 else 2)
+    try:
+        d(ids, am, masked_positions=pos, labels=lab).backward()
+        res["outcome"] = "completed"
+    except RuntimeError as e:
+        res["outcome"] = "capacity" if "capacity" in str(e) else "peer_error"
+    out[rank] = res
+    # no destroy_process_group: the group is broken by design here; the process exit closes it
+
+
+def test_ddp_sparse_capacity_one_rank_grows():
+    """Only ONE rank exceeds the agreed capacity (advice r5): that rank raises the capacity
+    error before any collective and its peer's pending ids all_gather fails (peer closed /
+    timeout) — neither rank completes a step with a mismatched collective."""
+    out = mp.Manager().dict()
+    mp.spawn(_one_rank_grows_worker, args=(2, 29800 + os.getpid() % 150, out), nprocs=2)
+    assert out[1]["outcome"] == "capacity", dict(out)
+    assert out[0]["outcome"] == "peer_error", dict(out)
+    assert out[0]["cap"] == out[1]["cap"] == 2 * 16

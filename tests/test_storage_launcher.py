@@ -76,6 +76,32 @@ def test_env_contract(monkeypatch):
                               gpu_visibility="some"))
 
 
+def test_env_slice_from_rocr_visible_devices(monkeypatch):
+    """Ids read from ROCR_VISIBLE_DEVICES (Slurm's mask) are physical: HIP renumbers the
+    ROCR-filtered set from 0, so HIP_VISIBLE_DEVICES=4,5 under ROCR=4,5,6,7 would name devices
+    that do not exist.  The slice narrows ROCR_VISIBLE_DEVICES itself; "all" mode keeps the mask
+    and names the slice by positional offsets."""
+    for v in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "MIPIPE_GPU_VISIBILITY"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "4,5,6,7")
+    envs = build_envs(LaunchSpec(command=["x"], replica_count=2, accelerator_count=1))
+    assert [e["ROCR_VISIBLE_DEVICES"] for e in envs] == ["4", "5"]
+    assert all("HIP_VISIBLE_DEVICES" not in e and "CUDA_VISIBLE_DEVICES" not in e for e in envs)
+    assert all(e["MIPIPE_DEVICE_OFFSET"] == "0" for e in envs)
+    envs = build_envs(LaunchSpec(command=["x"], replica_count=2, accelerator_count=2,
+                                 gpu_visibility="slice"))
+    assert [e["ROCR_VISIBLE_DEVICES"] for e in envs] == ["4,5", "6,7"]
+    envs = build_envs(LaunchSpec(command=["x"], replica_count=2, accelerator_count=2,
+                                 gpu_visibility="all"))
+    assert all(e["ROCR_VISIBLE_DEVICES"] == "4,5,6,7" for e in envs)
+    assert [e["MIPIPE_DEVICE_OFFSET"] for e in envs] == ["0", "2"]  # positional: cuda:0 / cuda:2
+    # HIP ids under a ROCR mask are already relative to it: the HIP variable is narrowed
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3")
+    envs = build_envs(LaunchSpec(command=["x"], replica_count=2, accelerator_count=1))
+    assert [e["HIP_VISIBLE_DEVICES"] for e in envs] == ["0", "1"]
+    assert all(e["ROCR_VISIBLE_DEVICES"] == "4,5,6,7" for e in envs)
+
+
 def test_device_count_worker_stays_on_its_slice(tmp_path, monkeypatch):
     """The unmodified reference task.py sizes its mp.spawn by torch.cuda.device_count()
     (task.py:102); under the default visibility every replica of the 3 x 2 topology must count
