@@ -180,12 +180,32 @@ int select(const std::string& k, bool f32, bool wgrad, F&& run) {
   return select_from(k, candidates(f32, wgrad), run);
 }
 
+// Conv forward / forward-style data-grad plans (launchers.hpp kConvSplitPlan): every tile, plus
+// split-K plans of the tiles whose output tiles alone leave the chip under-filled (fewer than
+// two blocks per CU; at least two k-steps per split).
+std::vector<int> conv_plan_candidates(bool f32, long M, long N, int nk) {
+  static const bool on = [] {  // MIPIPE_CONV_SPLIT=0: no split-K plans (A/B)
+    const char* v = getenv("MIPIPE_CONV_SPLIT");
+    return v == nullptr || atoi(v) != 0;
+  }();
+  std::vector<int> c;
+  for (int t : candidates(f32, false)) {
+    c.push_back(t);
+    if (!on) continue;
+    int bm = 128, bn = 128;
+    mipipe::conv_tile_dims(t, f32, &bm, &bn);
+    if (bm == 256 && bn == 256 && t != 11) continue;  // the 4-wave 256x256 tile never splits
+    const long tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+    if (tiles >= 512) continue;
+    for (int sp : {2, 3, 4, 6, 8})
+      if (nk >= 2 * sp && tiles * sp <= 4096) c.push_back(t + mipipe::kConvSplitPlan * sp);
+  }
+  return c;
+}
+
 // GEMM plans: tile id + 16 * split-K count (0 = heuristic split; accumulating GEMMs only)
 constexpr int kPlanSplit = 16;
 constexpr int kPlanWs = 1024;  // gemm plans: split-K through per-split workspace slices
-// deterministic conv forward: up to this many per-M-tile statistics rows go straight to
-// bn_finalize (summed there in row order) instead of through det_sum_rows first
-constexpr int kDetDirectRows = 128;
 std::vector<int> gemm_candidates(bool f32, bool accumulate) {
   std::vector<int> c;
   for (int t : candidates(f32, accumulate)) {
@@ -212,12 +232,26 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
                                                                 optional<Tensor> slab_sq,
                                                                 optional<Tensor> bias, bool relu,
                                                                 int stride_w, int pad_w, int cfg,
-                                                                optional<Tensor> wflip) {
+                                                                optional<Tensor> wflip,
+                                                                optional<Tensor> in_scale,
+                                                                optional<Tensor> in_bias) {
   check_act(x, "x");
   check_same(w, x, "w");
   c10::DeviceGuard g(x.device());
   auto s = conv_shape(x, w, stride, pad, stride_w, pad_w);
   s.f32 = is_f32(x);
+  // folded input BatchNorm: x holds y, the conv consumes relu(y*in_scale + in_bias)
+  const float* isc = nullptr;
+  const float* ibi = nullptr;
+  if (in_scale.has_value()) {
+    TORCH_CHECK(in_bias.has_value(), "in_scale needs in_bias");
+    TORCH_CHECK(!s.f32 && mipipe::conv_is_dense(s) && s.Ci <= mipipe::kConvBnInMaxK && !wflip.has_value(),
+                "folded input BN: bf16 dense 1x1 stride-1 convs with Ci <= ", mipipe::kConvBnInMaxK);
+    check_vec(*in_scale, s.Ci, "in_scale");
+    check_vec(*in_bias, s.Ci, "in_bias");
+    isc = in_scale->data_ptr<float>();
+    ibi = in_bias->data_ptr<float>();
+  }
   // wflip: the launch also writes the tap-flipped weight of this conv's stride-1 data-grad
   void* wfp = nullptr;
   if (wflip.has_value() && mipipe::dgrad_preflip_ok(s)) {
@@ -251,19 +285,36 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
     sh = shift->data_ptr<float>();
   }
   const float* bp = bias.has_value() ? bias->data_ptr<float>() : nullptr;
+  auto split_ws = [&](int plan) -> Tensor {  // fp32 workspace of a split-K plan (else empty)
+    const long n = mipipe::conv_fwd_split_ws_elems(s, plan);
+    return n > 0 ? torch::empty({n}, x.options().dtype(at::kFloat)) : Tensor();
+  };
+  auto wsp = [](const Tensor& t) { return t.defined() ? t.data_ptr<float>() : nullptr; };
   if (cfg < 0) {
-    cfg = tune::select(tune::key("fwd", s), s.f32, false, [&](int c) {
+    const long M = (long)s.N * s.Ho * s.Wo;
+    const int nk = (int)(((long)s.KH * s.KW * s.Ci + 63) / 64);
+    std::vector<int> cands = tune::conv_plan_candidates(s.f32, M, s.Co, nk);
+    if (isc != nullptr) {  // folded-BN variant: 4-wave tiles, no split
+      cands.clear();
+      for (int t : tune::candidates(false, false))
+        if (t < 11) cands.push_back(t);
+    }
+    cfg = tune::select_from(tune::key(isc != nullptr ? "fwdbn" : "fwd", s), cands, [&](int c) {
       auto ys = torch::empty_like(y);
       optional<Tensor> a, b;
       if (psp != nullptr) {
         a = torch::zeros_like(*ps);
         b = torch::zeros_like(*pss);
       }
+      Tensor ws = split_ws(c);
       mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), ys.data_ptr(),
                        a.has_value() ? a->data_ptr<float>() : nullptr,
-                       b.has_value() ? b->data_ptr<float>() : nullptr, sh, s, stream(), bp, relu, c);
+                       b.has_value() ? b->data_ptr<float>() : nullptr, sh, s, stream(), bp, relu, c,
+                       0, nullptr, wsp(ws), isc, ibi);
     });
   }
+  if (isc != nullptr && mipipe::conv_plan_tile(cfg) >= 11) cfg = -1;  // (a table from elsewhere)
+  Tensor ws = split_ws(cfg);
   if (mipipe::g_deterministic && psp != nullptr) {
     // per-M-tile partial rows (no atomics), then a fixed-order sum into slab row 0; the other
     // replica rows of the slabs stay zero
@@ -271,17 +322,14 @@ std::tuple<Tensor, optional<Tensor>, optional<Tensor>> conv_fwd(Tensor x, Tensor
     auto part = torch::empty({2, P, s.Co}, x.options().dtype(at::kFloat));
     float* p0 = part.data_ptr<float>();
     mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), p0, p0 + (long)P * s.Co, sh, s,
-                     stream(), bp, relu, cfg, P, wfp);
-    if (P <= tune::kDetDirectRows) {
-      // few M tiles (the small-spatial layers): hand the partial rows themselves to bn_finalize,
-      // which sums its P input rows in index order — no separate fixed-order sum launch
-      return {y, part[0], part[1]};
-    }
-    mipipe::det_sum_rows(p0, p0 + (long)P * s.Co, P, s.Co, psp, pssp, false, stream());
-    return {y, ps, pss};
+                     stream(), bp, relu, cfg, P, wfp, wsp(ws), isc, ibi);
+    // the partial rows themselves go to bn_finalize, which sums them in det_sum_rows' fixed
+    // order (chunk sums first for long columns) — no separate summing launch into the slab
+    (void)psp;
+    return {y, part[0], part[1]};
   }
   mipipe::conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), psp, pssp, sh, s, stream(), bp, relu,
-                   cfg, 0, wfp);
+                   cfg, 0, wfp, wsp(ws), isc, ibi);
   return {y, ps, pss};
 }
 
@@ -385,8 +433,18 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     }
     any = true;
   }
+  // split-K plans apply to the forward-style classes only (they need the flipped weight)
+  auto split_ws = [&](int plan) -> Tensor {
+    const long n = wfp != nullptr ? mipipe::conv_dgrad_split_ws_elems(s, plan) : 0;
+    return n > 0 ? torch::empty({n}, dy.options().dtype(at::kFloat)) : Tensor();
+  };
+  auto wsp = [](const Tensor& t) { return t.defined() ? t.data_ptr<float>() : nullptr; };
   if (cfg < 0) {
-    cfg = tune::select(tune::key("dgrad", s), s.f32, false, [&](int c) {
+    std::vector<int> cands = tune::candidates(s.f32, false);
+    if (wfp != nullptr && s.stride == 1)
+      cands = tune::conv_plan_candidates(s.f32, (long)s.N * s.H * s.W, s.Ci,
+                                         (int)(((long)s.KH * s.KW * s.Co + 63) / 64));
+    cfg = tune::select_from(tune::key("dgrad", s), cands, [&](int c) {
       auto dxs = torch::empty_like(dx);
       mipipe::DgradFusion f2 = fz;
       Tensor reps;
@@ -394,10 +452,12 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
         reps = torch::zeros_like(*bn_rep);
         f2.bn_rep = reps.data_ptr<float>();
       }
+      Tensor ws = split_ws(c);
       mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dxs.data_ptr(), s, stream(),
-                         any ? &f2 : nullptr, c, wfp, preflipped);
+                         any ? &f2 : nullptr, c, wfp, preflipped, wsp(ws));
     });
   }
+  Tensor ws = split_ws(cfg);
   if (mipipe::g_deterministic && fz.bn_rep != nullptr) {
     const int P = mipipe::conv_dgrad_tiles_m(s, cfg);
     const bool two = fz.bn_y2 != nullptr;
@@ -406,7 +466,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     fz.bn_rep = part.data_ptr<float>();
     fz.det_rows = P;
     mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), &fz, cfg, wfp,
-                       preflipped);
+                       preflipped, wsp(ws));
     const long rs = (long)mipipe::kStatReplicas * s.Ci, ps = (long)P * s.Ci;
     mipipe::det_sum_rows(fz.bn_rep, fz.bn_rep + ps, P, s.Ci, rep, rep + rs, false, stream());
     if (two)
@@ -415,7 +475,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, std::vector<int64_t> x_shape, int stride,
     return dx;
   }
   mipipe::conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s, stream(), any ? &fz : nullptr,
-                     cfg, wfp, preflipped);
+                     cfg, wfp, preflipped, wsp(ws));
   return dx;
 }
 
@@ -436,7 +496,8 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
                   int stride_w, int pad_w, int cfg, optional<Tensor> col_rep,
                   optional<Tensor> col_out, optional<Tensor> col_dgamma,
                   optional<Tensor> col_dbeta, bool col_two, optional<Tensor> col_dgamma2,
-                  optional<Tensor> col_dbeta2) {
+                  optional<Tensor> col_dbeta2, optional<Tensor> in_scale,
+                  optional<Tensor> in_bias) {
   check_act(dy, "dy");
   check_same(x, dy, "x");
   c10::DeviceGuard g(dy.device());
@@ -452,6 +513,16 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.Ho && dy.size(2) == s.Wo, "dy/x mismatch");
   TORCH_CHECK(s.Ci % 8 == 0 && s.Co % 8 == 0, "conv wgrad needs Ci, Co % 8 == 0");
   check_conv_buf_bytes(s, s.f32, "conv wgrad");
+  const float* isc = nullptr;  // folded input BN (see conv_fwd)
+  const float* ibi = nullptr;
+  if (in_scale.has_value()) {
+    TORCH_CHECK(in_bias.has_value(), "in_scale needs in_bias");
+    TORCH_CHECK(!s.f32 && mipipe::conv_is_dense(s), "folded input BN: bf16 dense 1x1 stride-1 convs");
+    check_vec(*in_scale, s.Ci, "in_scale");
+    check_vec(*in_bias, s.Ci, "in_bias");
+    isc = in_scale->data_ptr<float>();
+    ibi = in_bias->data_ptr<float>();
+  }
   Tensor dw;
   if (out.has_value()) {  // accumulate straight into an existing gradient (flat DDP bucket view)
     check_f32(*out, "out");
@@ -486,7 +557,7 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
   }
   // 3x3 / stride-1 convolutions: the patch-resident kernel (input patch in LDS shared by the
   // 9 taps, partial tiles summed in a fixed order: deterministic in both modes)
-  if (cfg < 0 && mipipe::g_wgrad3x3 && mipipe::conv_wgrad3x3_supported(s)) {
+  if (cfg < 0 && isc == nullptr && mipipe::g_wgrad3x3 && mipipe::conv_wgrad3x3_supported(s)) {
     const int S = mipipe::conv_wgrad3x3_splits(s);
     auto ws = torch::empty({S, (int64_t)s.Co * 9 * s.Ci}, dy.options().dtype(at::kFloat));
     mipipe::conv_wgrad3x3(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(),
@@ -500,16 +571,18 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
   auto run_ws = [&](float* out, int tile, int sp) {
     const int splits = mipipe::conv_wgrad_splits(s, tile, sp);
     if (splits == 1) {  // one writer per element: the plain read-modify-write is deterministic
-      mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), out, s, stream(), tile, nullptr, 1, colp);
+      mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), out, s, stream(), tile, nullptr, 1, colp, isc,
+                         ibi);
       return;
     }
     auto ws = torch::empty({splits, (int64_t)s.Co * kh * kw * s.Ci}, dy.options().dtype(at::kFloat));
     mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), out, s, stream(), tile, ws.data_ptr<float>(),
-                       sp, colp);
+                       sp, colp, isc, ibi);
   };
   if (plan < 0) {
     std::vector<int> cands;
     for (int t : tune::candidates(s.f32, true)) {
+      if (isc != nullptr && t >= 11) continue;  // folded-BN variant: 4-wave tiles
       // 3 / 6 / 12 / 24 as well: tiles x splits lands nearer a whole number of waves
       // (MIPIPE_WGRAD_WIDE_SPLITS=0: powers of two only, A/B)
       static const bool wide = [] {
@@ -526,7 +599,7 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
         for (int sp : {4, 6, 8, 12, 16, 24, 32})
           if (wide || (sp & (sp - 1)) == 0) cands.push_back((t + tune::kPlanSplit * sp) | tune::kPlanWs);
     }
-    plan = tune::select_from(tune::key("wgrad", s), cands, [&](int p) {
+    plan = tune::select_from(tune::key(isc != nullptr ? "wgradbn" : "wgrad", s), cands, [&](int p) {
       auto dws = torch::zeros_like(dw);
       const bool wsp = (p & tune::kPlanWs) != 0;
       p &= ~tune::kPlanWs;
@@ -536,11 +609,11 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
         auto ws = torch::empty({splits, (int64_t)s.Co * kh * kw * s.Ci},
                                dy.options().dtype(at::kFloat));
         mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dws.data_ptr<float>(), s, stream(),
-                           p % tune::kPlanSplit, ws.data_ptr<float>(), sp);
+                           p % tune::kPlanSplit, ws.data_ptr<float>(), sp, nullptr, isc, ibi);
         return;
       }
       mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dws.data_ptr<float>(), s, stream(),
-                         p % tune::kPlanSplit, nullptr, sp > 0 ? sp : -1);
+                         p % tune::kPlanSplit, nullptr, sp > 0 ? sp : -1, nullptr, isc, ibi);
     });
   }
   const bool ws_plan = plan >= 0 && (plan & tune::kPlanWs) != 0;
@@ -555,16 +628,16 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int kh, int kw, int stride, int pad, opti
     const int splits = mipipe::conv_wgrad_splits(s, tile, sp);
     if (splits == 1) {  // one writer per element: the plain read-modify-write is deterministic
       mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), tile,
-                         nullptr, 1, colp);
+                         nullptr, 1, colp, isc, ibi);
       return dw;
     }
     auto ws = torch::empty({splits, (int64_t)s.Co * kh * kw * s.Ci}, dy.options().dtype(at::kFloat));
     mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), tile,
-                       ws.data_ptr<float>(), sp, colp);
+                       ws.data_ptr<float>(), sp, colp, isc, ibi);
     return dw;
   }
   mipipe::conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), s, stream(), tile,
-                     nullptr, sp, colp);
+                     nullptr, sp, colp, isc, ibi);
   return dw;
 }
 
@@ -793,9 +866,18 @@ std::tuple<Tensor, Tensor, Tensor> pool_bn_bwd(Tensor dp, Tensor idx, Tensor pou
     mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), pout.data_ptr(), y.data_ptr(),
                                mean.data_ptr<float>(), invstd.data_ptr<float>(), N, H, W, C, Ho, Wo,
                                k, s, p, p0, G, stream(), f32);
-    float* r = rep.data_ptr<float>();
-    mipipe::det_sum_rows(p0, p0 + (long)G * C, G, C, r, r + (long)mipipe::kStatReplicas * C, false,
-                         stream());
+    // the G rows collected in det_sum_rows' order by one launch (rep stays zero)
+    auto o = rep.options();
+    auto sg = torch::empty({C}, o), sgx = torch::empty({C}, o);
+    mipipe::bn_bwd_collect_rows(p0, G, C, false, sg.data_ptr<float>(), sgx.data_ptr<float>(),
+                                nullptr, fptr(dgamma, C), fptr(dbeta, C), nullptr, nullptr, nullptr,
+                                stream());
+    auto dy = torch::empty_like(y);
+    mipipe::pool_bn_bwd_apply(dp.data_ptr(), idx.data_ptr<uint8_t>(), pout.data_ptr(), y.data_ptr(),
+                              mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                              gamma.data_ptr<float>(), sg.data_ptr<float>(), sgx.data_ptr<float>(),
+                              count, dy.data_ptr(), N, H, W, C, Ho, Wo, k, s, p, stream(), f32);
+    return {dy, sg, sgx};
   } else {
     mipipe::pool_bn_bwd_reduce(dp.data_ptr(), idx.data_ptr<uint8_t>(), pout.data_ptr(), y.data_ptr(),
                                mean.data_ptr<float>(), invstd.data_ptr<float>(), N, H, W, C, Ho, Wo,
@@ -858,7 +940,8 @@ std::tuple<Tensor, Tensor> stem_fwd_stats(Tensor xp, Tensor w, Tensor shift, Ten
     float* p0 = part.data_ptr<float>();
     mipipe::stem_fwd_stats(xp.data_ptr(), w.data_ptr(), g.N, g.Ho, g.Hp, shift.data_ptr<float>(), p0,
                            p0 + (long)G * 64, R, G, stream());
-    mipipe::det_sum_rows(p0, p0 + (long)G * 64, G, 64, s0, s1, false, stream());
+    // the partial rows go to bn_finalize (det_sum_rows' order there); the slabs stay zero
+    return {part[0], part[1]};
   } else {
     mipipe::stem_fwd_stats(xp.data_ptr(), w.data_ptr(), g.N, g.Ho, g.Hp, shift.data_ptr<float>(), s0,
                            s1, R, 0, stream());
@@ -1809,7 +1892,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("shift") = py::none(), py::arg("slab_sum") = py::none(),
         py::arg("slab_sq") = py::none(), py::arg("bias") = py::none(), py::arg("relu") = false,
         py::arg("stride_w") = 0, py::arg("pad_w") = -1, py::arg("cfg") = -1,
-        py::arg("wflip") = py::none());
+        py::arg("wflip") = py::none(), py::arg("in_scale") = py::none(),
+        py::arg("in_bias") = py::none());
   m.attr("STAT_REPLICAS") = mipipe::kStatReplicas;
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("x_shape"),
         py::arg("stride"), py::arg("pad"), py::arg("addend") = py::none(),
@@ -1836,7 +1920,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("pad_w") = -1, py::arg("cfg") = -1, py::arg("col_rep") = py::none(),
         py::arg("col_out") = py::none(), py::arg("col_dgamma") = py::none(),
         py::arg("col_dbeta") = py::none(), py::arg("col_two") = false,
-        py::arg("col_dgamma2") = py::none(), py::arg("col_dbeta2") = py::none());
+        py::arg("col_dgamma2") = py::none(), py::arg("col_dbeta2") = py::none(),
+        py::arg("in_scale") = py::none(), py::arg("in_bias") = py::none());
   m.attr("CONV_TILE_CONFIGS") = mipipe::kConvTileConfigs;
   m.def("set_benchmark", [](bool on, bool verbose, int reps) {
     tune::g_benchmark = on;

@@ -102,20 +102,105 @@ __global__ void bn_finalize_kernel(float* __restrict__ s1, float* __restrict__ s
   }
 }
 
+// Sum of P rows (row p at in[k][p * rs + c]) in det_sum_rows' fixed order: 16 row groups per
+// channel (group g: rows g, g+16, ... with 8 rows of loads in flight, added in row order), the
+// caller then adds the 16 group sums in index order.  One memory latency per 8 rows instead of
+// one per row: a one-thread-per-channel loop over 128 rows cost 34-36 us per call.
+template <int NA>
+__device__ __forceinline__ void rows_sum16(float* const (&in)[NA], int P, long rs, int c, int g,
+                                           float (&a)[NA]) {
+#pragma unroll
+  for (int k = 0; k < NA; ++k) a[k] = 0.f;
+  int p = g;
+  for (; p + 7 * 16 < P; p += 8 * 16) {
+    float v[NA][8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int k = 0; k < NA; ++k) v[k][u] = in[k][(long)(p + u * 16) * rs + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int k = 0; k < NA; ++k) a[k] += v[k][u];
+  }
+  for (; p < P; p += 16)
+#pragma unroll
+    for (int k = 0; k < NA; ++k) a[k] += in[k][(long)p * rs + c];
+}
+
+// bn_finalize of P partial rows that are NOT a replica slab (the deterministic mode's one row
+// per M-tile of the producing conv): 64 channels x 16 row groups per 1024-thread block, the
+// rows summed in det_sum_rows' order — the same bits as det_sum_rows into a zeroed replica slab
+// followed by the replica finalize, in one launch.  stride: rows are every stride-th row of the
+// [rows][C] array (the chunk sums det_chunk_sums leaves in place for P > 256).
+__global__ __launch_bounds__(1024) void bn_finalize_rows_kernel(
+    float* __restrict__ s1, float* __restrict__ s2, int P, int C, int stride, float inv_count,
+    float unbias, const float* shift, const float* gamma, const float* beta, float* run_mean,
+    float* run_var, float momentum, float eps, float* mean, float* invstd, float* scale,
+    float* bias, bool zero_after, long long* nbt) {
+  __shared__ float part[2][16][65];
+  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  if (nbt != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+  float a[2] = {0.f, 0.f};
+  const long rs = (long)stride * C;
+  if (c < C) {
+    float* const in[2] = {s1, s2};
+    rows_sum16<2>(in, P, rs, c, g, a);
+    if (zero_after)  // (every row this thread read; its own loads retired above)
+      for (int p = g; p < P; p += 16) {
+        s1[(long)p * rs + c] = 0.f;
+        s2[(long)p * rs + c] = 0.f;
+      }
+  }
+  part[0][g][lc] = a[0];
+  part[1][g][lc] = a[1];
+  __syncthreads();
+  if (g != 0 || c >= C) return;
+  float sa = 0.f, sb = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    sa += part[0][k][lc];
+    sb += part[1][k][lc];
+  }
+  float ms = sa * inv_count;
+  float var = fmaxf(sb * inv_count - ms * ms, 0.f);
+  float mu = ms + shift[c];
+  float is = rsqrtf(var + eps);
+  float sc = gamma[c] * is;
+  mean[c] = mu;
+  invstd[c] = is;
+  scale[c] = sc;
+  bias[c] = beta[c] - mu * sc;
+  if (run_mean != nullptr) {
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * unbias;
+  }
+}
+
 void bn_finalize(float* psum, float* psq, int P, int C, long count, const float* shift,
                  const float* gamma, const float* beta, float* run_mean, float* run_var,
                  float momentum, float eps, float* mean, float* invstd, float* scale, float* bias,
                  bool zero_after, long long* nbt, hipStream_t st) {
   float unbias = count > 1 ? (float)count / (float)(count - 1) : 1.f;
-  dim3 grid((C + 255) / 256);
-  if (P == kStatReplicas)
+  if (P == kStatReplicas) {
+    dim3 grid((C + 255) / 256);
     hipLaunchKernelGGL(bn_finalize_kernel<kStatReplicas>, grid, dim3(256), 0, st, psum, psq, P, C,
                        1.f / (float)count, unbias, shift, gamma, beta, run_mean, run_var, momentum,
                        eps, mean, invstd, scale, bias, zero_after, nbt);
-  else
-    hipLaunchKernelGGL(bn_finalize_kernel<0>, grid, dim3(256), 0, st, psum, psq, P, C,
-                       1.f / (float)count, unbias, shift, gamma, beta, run_mean, run_var, momentum,
-                       eps, mean, invstd, scale, bias, zero_after, nbt);
+    return;
+  }
+  // partial rows (deterministic mode): long columns are chunk-summed in place first, exactly as
+  // det_sum_rows does (so the result is det_sum_rows' bits)
+  int stride = 1;
+  if (P > 4 * kDetChunkRows) {
+    P = det_chunk_sums(psum, psq, nullptr, P, C, st);
+    stride = kDetChunkRows;
+    zero_after = false;  // scratch rows, now partly overwritten by the chunk sums
+  }
+  hipLaunchKernelGGL(bn_finalize_rows_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, psum, psq,
+                     P, C, stride, 1.f / (float)count, unbias, shift, gamma, beta, run_mean,
+                     run_var, momentum, eps, mean, invstd, scale, bias, zero_after, nbt);
 }
 
 // ----------------------------------------------------------------------------- forward apply
@@ -388,6 +473,73 @@ __global__ void bn_bwd_collect_kernel(float* __restrict__ rep, int C, float* og,
   }
 }
 
+// bn_bwd_collect of P partial rows ([2|3][P][C], the deterministic mode's one row per block of
+// the producing reduction) instead of a replica slab: rows summed in det_sum_rows' order
+// (rows_sum16, chunk sums in place first for P > 256) — the bits of det_sum_rows into a zeroed
+// slab followed by bn_bwd_collect_kernel, without the extra launches.
+__global__ __launch_bounds__(1024) void bn_bwd_collect_rows_kernel(
+    float* __restrict__ in, int P, int C, int stride, long as, bool two, float* og, float* ogx,
+    float* ogx2, float* dgamma, float* dbeta, float* dgamma2, float* dbeta2, const float* gx_div) {
+  __shared__ float part[3][16][65];
+  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  float a[3] = {0.f, 0.f, 0.f};
+  const long rs = (long)stride * C;
+  if (c < C) {
+    if (two) {
+      float* const src[3] = {in, in + as, in + 2 * as};
+      rows_sum16<3>(src, P, rs, c, g, a);
+    } else {
+      float* const src[2] = {in, in + as};
+      float a2[2];
+      rows_sum16<2>(src, P, rs, c, g, a2);
+      a[0] = a2[0];
+      a[1] = a2[1];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) part[k][g][lc] = a[k];
+  __syncthreads();
+  if (g != 0 || c >= C) return;
+  float sa = 0.f, sb = 0.f, sd = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    sa += part[0][k][lc];
+    sb += part[1][k][lc];
+    sd += part[2][k][lc];
+  }
+  if (gx_div != nullptr) {  // Σg·(z-β) -> Σg·x̂ = Σg·(z-β)/γ (as bn_bwd_collect_kernel)
+    const float gd = gx_div[c];
+    sb = fabsf(gd) > 1e-30f ? sb / gd : 0.f;
+  }
+  og[c] = sa;
+  ogx[c] = sb;
+  if (ogx2 != nullptr) ogx2[c] = sd;
+  if (dgamma != nullptr) {
+    dgamma[c] += sb;
+    dbeta[c] += sa;
+  }
+  if (dgamma2 != nullptr) {
+    dgamma2[c] += sd;
+    dbeta2[c] += sa;
+  }
+}
+
+void bn_bwd_collect_rows(float* rows, int P, int C, bool two, float* out_g, float* out_gx,
+                         float* out_gx2, float* dgamma, float* dbeta, float* dgamma2,
+                         float* dbeta2, const float* gx_div, hipStream_t st) {
+  const long as = (long)P * C;  // array stride of the [2|3][P][C] rows
+  int stride = 1;
+  if (P > 4 * kDetChunkRows) {
+    const int n = det_chunk_sums(rows, rows + as, two ? rows + 2 * as : nullptr, P, C, st);
+    P = n;
+    stride = kDetChunkRows;
+  }
+  hipLaunchKernelGGL(bn_bwd_collect_rows_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, rows, P,
+                     C, stride, as, two, out_g, out_gx, out_gx2, dgamma, dbeta, dgamma2, dbeta2,
+                     gx_div);
+}
+
 int bn_bwd_reduce_blocks(long M, int C) {
   RowMap mp = row_map(C);
   // >= 16 row-iterations per thread, and at most ~1M atomic adds in total
@@ -416,11 +568,11 @@ void bn_act_bwd_reduce(const void* dz, const void* z, const void* y, const float
   if (f32) launch(float{});
   else launch(__bf16{});
   if (det_ws != nullptr) {
-    // fixed-order sum of the G per-block rows into replica row 0 (the rest of rep stays zero),
-    // then the usual collect
-    const long rs = (long)kStatReplicas * C, ds = (long)G * C;
-    det_sum_rows(det_ws, det_ws + ds, G, C, rep, rep + rs, false, st);
-    if (y2 != nullptr) det_sum_rows(det_ws + 2 * ds, nullptr, G, C, rep + 2 * rs, nullptr, false, st);
+    // the G per-block rows collected in det_sum_rows' fixed order by one launch (the replica
+    // slab is not touched)
+    bn_bwd_collect_rows(det_ws, G, C, y2 != nullptr, out_g, out_gx, y2 ? out_gx2 : nullptr,
+                        dgamma, dbeta, y2 ? dgamma2 : nullptr, y2 ? dbeta2 : nullptr, gx_div, st);
+    return;
   }
   hipLaunchKernelGGL(bn_bwd_collect_kernel, dim3((C + 255) / 256), dim3(256), 0, st, rep, C, out_g,
                      out_gx, y2 ? out_gx2 : nullptr, dgamma, dbeta, y2 ? dgamma2 : nullptr,

@@ -135,6 +135,17 @@ template <bool AL, class T> struct PolMCDgradW {
   using type = typename std::conditional<AL && use_buf<T>(), MCDgradWBuf<R, T, NW>,
                                          MCDgradW<R, T, NW>>::type;
 };
+// folded BatchNorm on the input (bf16 dense convs only: the buffer policies + fragment transform)
+template <class T> struct PolKCDenseBN {
+  template <int R, int NW>
+  using type = KCDenseBufBN<R, T, NW>;
+};
+template <class T> struct PolMCDenseBN {
+  template <int R, int NW>
+  using type = MCDenseBufBN<R, T, NW>;
+};
+// channels of the folded-BN (scale, bias) LDS table (float2 each) of a BNIN forward
+constexpr int kBnInMaxK = kConvBnInMaxK;
 template <class T> struct PolMCIm2colT {
   template <int R, int NW>
   using type = typename std::conditional<use_buf<T>(), MCIm2colTBuf<R, T, NW>, MCIm2colT<R, T, NW>>::type;
@@ -180,20 +191,42 @@ constexpr int conv_occ() {
 }
 
 // DGRAD_EPI: the same im2col main loop run as a stride-1 data-grad (x = dy, w = the tap-flipped
-// [Ci][KH][KW][Co] weight, pad = K-1-pad) with the data-grad epilogue and its fusions
-template <class C, bool DENSE, bool ALIGNED, class T, bool DGRAD_EPI = false>
+// [Ci][KH][KW][Co] weight, pad = K-1-pad) with the data-grad epilogue and its fusions.
+// SPLIT: split-K plan — blockIdx.y runs k-steps [y*e.split_kt, (y+1)*e.split_kt) and writes its
+// fp32 partial tile to slice y of e.split_ws; conv_splitk_finish_kernel runs the epilogue.
+template <class T, class C, bool SPLIT>
+constexpr int conv_fwd_lds_bytes() {
+  return SPLIT && lds_bytes_f32out<T, C>() > lds_bytes_out<T, C>() ? lds_bytes_f32out<T, C>()
+                                                                   : lds_bytes_out<T, C>();
+}
+// BNIN: folded BatchNorm on the input (dense bf16, non-ping-pong tiles, K <= kBnInMaxK): x holds
+// y and the A fragments are transformed to relu(y*e.in_scale + e.in_bias) after their LDS read
+// (the (scale, bias) table sits in LDS behind the stage buffers).
+template <class T, class C, bool BNIN>
+constexpr int bnin_lds_bytes() {
+  return BNIN ? main_lds_bytes<T, C>() + kBnInMaxK * 8 : 0;
+}
+template <class C, bool DENSE, bool ALIGNED, class T, bool DGRAD_EPI = false, bool SPLIT = false,
+          bool BNIN = false>
 __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_fwd_kernel(
     const T* __restrict__ x, const T* __restrict__ w, ConvGeom g, uint32_t M,
     uint32_t tilesN, EpiParams e) {
   constexpr int BM = C::BM, BN = C::BN;
-  typedef typename std::conditional<DENSE, PolKCDense<T>, PolKCIm2col<ALIGNED, T>>::type PA;
-  __shared__ __attribute__((aligned(16))) char smem[lds_bytes_out<T, C>()];
+  static_assert(!BNIN || (DENSE && !C::PP && !SPLIT && !DGRAD_EPI), "folded-BN forward variant");
+  typedef typename std::conditional<
+      BNIN, PolKCDenseBN<T>,
+      typename std::conditional<DENSE, PolKCDense<T>, PolKCIm2col<ALIGNED, T>>::type>::type PA;
+  constexpr int kLds = conv_fwd_lds_bytes<T, C, SPLIT>() > bnin_lds_bytes<T, C, BNIN>()
+                           ? conv_fwd_lds_bytes<T, C, SPLIT>()
+                           : bnin_lds_bytes<T, C, BNIN>();
+  __shared__ __attribute__((aligned(16))) char smem[kLds];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   uint32_t ntile = gridDim.x;
   if constexpr (!DGRAD_EPI) {
     if (e.fl_wt != nullptr) {  // trailing blocks: the data-grad's flipped weight
       if (blockIdx.x >= e.fl_tiles) {
+        if (SPLIT && blockIdx.y != 0) return;  // once, not per split
         flip_block<T, C::THREADS>(e, blockIdx.x - e.fl_tiles, smem);
         return;
       }
@@ -205,15 +238,91 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_fwd_kerne
   const uint32_t m0 = tm * BM, n0 = tn * BN;
   const uint32_t K = (uint32_t)(g.KH * g.KW * g.C);
   const int nk = (int)((K + BK - 1) / BK);
+  int kt0 = 0, kt1 = nk;
+  if constexpr (SPLIT) {
+    kt0 = (int)blockIdx.y * e.split_kt;
+    kt1 = min(nk, kt0 + e.split_kt);
+  }
+  char* bn_tab = smem + main_lds_bytes<T, C>();
+  if constexpr (BNIN) {  // (ordered before the first fragment read by the main loop's barrier)
+    float2* tab = reinterpret_cast<float2*>(bn_tab);
+    for (int c = threadIdx.x; c < nk * BK; c += C::THREADS)
+      tab[c] = (uint32_t)c < K ? make_float2(e.in_scale[c], e.in_bias[c]) : make_float2(0.f, 0.f);
+  }
   auto ia = [&](auto& a, uint32_t origin) {
     if constexpr (DENSE) a.init(x, g.C, M, K, origin, wave, lane, g_conv_zero);
     else a.init(x, g, M, origin, wave, lane, g_conv_zero);
+    if constexpr (BNIN) a.tab = bn_tab;
   };
   auto ib = [&](auto& b, uint32_t origin) { b.init(w, K, e.N, K, origin, wave, lane, g_conv_zero); };
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
-  run_main_loop<T, C, PA, PolKCDense<T>>(smem, ia, ib, m0, n0, 0, nk, acc, wave, lane);
-  epilogue_out<BM, BN, DGRAD_EPI, T, C::WM, C::WN, false, C::PP>(smem, acc, e, m0, n0, 0, wave,
-                                                                 lane);
+  run_main_loop<T, C, PA, PolKCDense<T>>(smem, ia, ib, m0, n0, kt0, kt1, acc, wave, lane);
+  if constexpr (SPLIT) {
+    EpiParams ws{};  // this split's partial tile -> slice blockIdx.y ([splits][M][N], pitch N)
+    ws.C = e.split_ws;
+    ws.ldc = e.N;
+    ws.M = M;
+    ws.N = e.N;
+    ws.det_rows = 1;
+    epilogue_f32<BM, BN, true, C::WM, C::WN, C::PP>(smem, acc, ws, m0, n0, wave, lane);
+  } else {
+    epilogue_out<BM, BN, DGRAD_EPI, T, C::WM, C::WN, false, C::PP>(smem, acc, e, m0, n0, 0, wave,
+                                                                   lane);
+  }
+}
+
+// Finish of a split-K conv plan: each lane sums its accumulator positions over the splits in
+// slice order (every slice's loads of a position issued together), then the block runs the
+// regular output epilogue on the sum — BatchNorm statistics, bias / ReLU, the data-grad row remap
+// and BN-backward fusions — exactly as the unsplit kernel would have on its accumulators.
+template <class T, class C>
+constexpr int finish_lds_bytes() {
+  constexpr int a = kEpiLdsBytes<C::BM, C::BN, T, C::WM>();
+  constexpr int b = 16 * (C::THREADS + 8) * 4;  // the BN-backward column-sum rows
+  return a > b ? a : b;
+}
+template <class C, class T, bool FUSE>
+__global__ __launch_bounds__(C::THREADS) void conv_splitk_finish_kernel(
+    const float* __restrict__ ws, int S, uint32_t tilesN, EpiParams e) {
+  constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN;
+  constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
+  __shared__ __attribute__((aligned(16))) char smem[finish_lds_bytes<T, C>()];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const uint32_t tm = blockIdx.x / tilesN, tn = blockIdx.x % tilesN;
+  const uint32_t m0 = tm * BM, n0 = tn * BN;
+  const int wr = wave / WN, wc = wave % WN;
+  typedef AccMap<BM, BN, WM, WN, false> Map;
+  const uint32_t lr = lane & 15, lc = (lane >> 4) * 4;
+  const long slice = (long)e.M * e.N;
+  long off[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const uint32_t m = min(m0 + Map::row(wr, i) + lr, e.M - 1);  // clamped: masked later
+      const uint32_t n = n0 + Map::col(wc, j) + lc;
+      off[i][j] = (long)m * e.N + (n < e.N ? n : 0);
+    }
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const float4 v = *reinterpret_cast<const float4*>(ws + off[i][j]);
+      acc[i][j] = f32x4{v.x, v.y, v.z, v.w};
+    }
+  for (int s = 1; s < S; ++s) {  // slice order: deterministic
+    const float* wsl = ws + s * slice;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const float4 v = *reinterpret_cast<const float4*>(wsl + off[i][j]);
+        acc[i][j] += f32x4{v.x, v.y, v.z, v.w};
+      }
+  }
+  epilogue_out<BM, BN, FUSE, T, WM, WN, false, false>(smem, acc, e, m0, n0, 0, wave, lane);
 }
 
 // TWO: BN-backward fusion of a two-branch block output (dense bf16 data-grads only)
@@ -247,13 +356,18 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_dgrad_ker
 }
 
 // ATOMIC: split-K partial tiles added with fp32 atomics; else the block owns its output tile
-// (no split) and adds it with a plain read-modify-write (e.rmw) or writes a workspace slice
-template <class C, bool DENSE, class T, bool ATOMIC = true>
+// (no split) and adds it with a plain read-modify-write (e.rmw) or writes a workspace slice.
+// BNIN: folded BatchNorm on the input (dense bf16, 4-wave tiles): x holds y and the B fragments
+// are transformed to relu(y*e.in_scale + e.in_bias) after their LDS read.
+template <class C, bool DENSE, class T, bool ATOMIC = true, bool BNIN = false>
 __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_wgrad_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, ConvGeom g, uint32_t tilesN,
     int kt_per_split, EpiParams e) {
   constexpr int BM = C::BM, BN = C::BN;
-  typedef typename std::conditional<DENSE, PolMCDense<T>, PolMCIm2colT<T>>::type PB;
+  static_assert(!BNIN || (DENSE && !C::PP), "folded-BN weight-grad variant");
+  typedef typename std::conditional<
+      BNIN, PolMCDenseBN<T>,
+      typename std::conditional<DENSE, PolMCDense<T>, PolMCIm2colT<T>>::type>::type PB;
   __shared__ __attribute__((aligned(16))) char smem[lds_bytes_f32out<T, C>()];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -270,6 +384,12 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void conv_wgrad_ker
   auto ib = [&](auto& b, uint32_t origin) {
     if constexpr (DENSE) b.init(x, g.C, g.C, K, origin, wave, lane, g_conv_zero);
     else b.init(x, g, origin, wave, lane, g_conv_zero, kt0);  // (the buffer policy starts at kt0)
+    if constexpr (BNIN) {
+      b.g_sc = e.in_scale;
+      b.g_bi = e.in_bias;
+      b.origin = origin;
+      b.ncols = (uint32_t)g.C;
+    }
   };
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
   run_main_loop<T, C, PolMCDense<T>, PB>(smem, ia, ib, m0, n0, kt0, kt1, acc, wave, lane);
@@ -294,10 +414,7 @@ inline gk::ConvGeom make_geom(const ConvShape& s) {
 
 inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-inline bool is_dense(const ConvShape& s) {
-  return s.KH == 1 && s.KW == 1 && s.stride == 1 && s.pad == 0 && s.pad_w <= 0 &&
-         (s.stride_w == 0 || s.stride_w == 1);
-}
+inline bool is_dense(const ConvShape& s) { return conv_is_dense(s); }
 
 // Dispatch a runtime config id to a compile-time tile: f(Tile) for valid ids.
 // NO_WIDE: the op cannot stage a 256x256 fp32 tile in LDS (weight-grad): id 6 runs as 3.

@@ -45,6 +45,7 @@ static void for_each_class(const ConvShape& s, F&& f) {
 }
 
 static int resolve_dgrad_cfg(const ConvShape& s, int cfg, long K_class) {
+  cfg = conv_plan_tile(cfg);
   const bool ok = s.f32 ? tile_ok_for<float>(cfg) : tile_ok_for<__bf16>(cfg);
   return ok ? cfg : default_dgrad_cfg(s, K_class);
 }
@@ -84,6 +85,23 @@ int dgrad_fwd_style_mode() {
     return v == nullptr ? 1 : atoi(v);
   }();
   return mode;
+}
+
+// workspace of a split plan: the largest forward-style class's splits x rows x Ci (classes run
+// one after another on the stream and reuse it)
+long conv_dgrad_split_ws_elems(const ConvShape& s, int cfg) {
+  if (conv_plan_splits(cfg) <= 1 || dgrad_fwd_style_mode() <= 0 ||
+      !conv_dgrad_fwd_style(s, dgrad_fwd_style_mode() >= 2))
+    return 0;
+  long need = 0;
+  for_each_class(s, [&](const DgradClass& c, uint32_t M) {
+    if (c.ntaps <= 0) return;
+    const int nk = (int)cdiv((uint64_t)c.ntaps * s.Co, BK);
+    int S, kps;
+    conv_split_geometry(nk, conv_plan_splits(cfg), &S, &kps);
+    if (S > 1) need = std::max(need, (long)S * M * s.Ci);
+  });
+  return need;
 }
 
 bool dgrad_preflip_ok(const ConvShape& s) {
@@ -150,7 +168,7 @@ static void weight_flip(const T* w, T* wt, const ConvShape& s, const DgradClass&
 template <class T>
 static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShape& s,
                          hipStream_t st, const DgradFusion* fz, int cfg_in, void* wflip,
-                         bool preflipped) {
+                         bool preflipped, float* split_ws) {
   const bool dense = is_dense(s);
   long flip_off = 0;  // this class's slice of the flipped-weight workspace
   const bool aligned = s.Co % BK == 0;
@@ -200,11 +218,30 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
         s2.pad_w = c.nkw - 1 - c.dw0;
         const ConvGeom g2 = make_geom(s2);
         const bool dense2 = dense && S == 1;
+        int SK = 1, kps = 0;
+        conv_split_geometry((int)cdiv((uint64_t)c.ntaps * s.Co, BK),
+                            split_ws != nullptr ? conv_plan_splits(cfg_in) : 1, &SK, &kps);
         with_tile<T>(cfg, [&](auto tile) {
           typedef decltype(tile) C;
           const uint32_t tN = cdiv(s.Ci, C::BN), tiles = cdiv(M, C::BM) * tN;
           row0 += (int)cdiv(M, C::BM);
           const dim3 grid(tiles), block(C::THREADS);
+          constexpr bool kSplitOk = !(C::BM == 256 && C::BN == 256 && !C::PP);  // (see conv_fwd)
+          if constexpr (kSplitOk) if (SK > 1) {  // split-K plan (see conv_fwd): partial tiles, then the finish launch
+            EpiParams es = e;
+            es.split_kt = kps;
+            es.split_ws = split_ws;
+            const dim3 g2d(tiles, SK);
+            if (dense2)
+              hipLaunchKernelGGL((conv_fwd_kernel<C, true, false, T, true, true>), g2d, block, 0, st, dyp, wt, g2, M, tN, es);
+            else if (aligned && (s.f32 || nkh * c.nkw <= 32))
+              hipLaunchKernelGGL((conv_fwd_kernel<C, false, true, T, true, true>), g2d, block, 0, st, dyp, wt, g2, M, tN, es);
+            else
+              hipLaunchKernelGGL((conv_fwd_kernel<C, false, false, T, true, true>), g2d, block, 0, st, dyp, wt, g2, M, tN, es);
+            hipLaunchKernelGGL((conv_splitk_finish_kernel<C, T, true>), dim3(tiles), block, 0, st,
+                               (const float*)split_ws, SK, tN, e);
+            return;
+          }
           if (dense2)
             hipLaunchKernelGGL((conv_fwd_kernel<C, true, false, T, true>), grid, block, 0, st, dyp, wt, g2, M, tN, e);
           else if (aligned && (s.f32 || nkh * c.nkw <= 32))  // bf16: buffer im2col tap mask
@@ -234,10 +271,10 @@ static void conv_dgrad_t(const void* dy, const void* w, void* dx, const ConvShap
 }
 
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
-                const DgradFusion* fz, int cfg, void* w_flip, bool preflipped) {
+                const DgradFusion* fz, int cfg, void* w_flip, bool preflipped, float* split_ws) {
   preflipped = preflipped && w_flip != nullptr && dgrad_preflip_ok(s);
-  if (s.f32) conv_dgrad_t<float>(dy, w, dx, s, st, fz, cfg, w_flip, preflipped);
-  else conv_dgrad_t<__bf16>(dy, w, dx, s, st, fz, cfg, w_flip, preflipped);
+  if (s.f32) conv_dgrad_t<float>(dy, w, dx, s, st, fz, cfg, w_flip, preflipped, split_ws);
+  else conv_dgrad_t<__bf16>(dy, w, dx, s, st, fz, cfg, w_flip, preflipped, split_ws);
 }
 
 }  // namespace mipipe

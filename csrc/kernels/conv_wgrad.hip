@@ -50,7 +50,7 @@ int conv_wgrad_splits(const ConvShape& s, int cfg, int splits_req) {
 template <class T>
 static void conv_wgrad_t(const void* dy, const void* x, float* dw, const ConvShape& s,
                          hipStream_t st, int cfg, float* ws, int splits_req,
-                         const BnCollect* col) {
+                         const BnCollect* col, const float* in_scale, const float* in_bias) {
   ConvGeom g = make_geom(s);
   const uint32_t Ntot = (uint32_t)(s.KH * s.KW * s.Ci);
   EpiParams e{};
@@ -60,6 +60,11 @@ static void conv_wgrad_t(const void* dy, const void* x, float* dw, const ConvSha
   const T* dyp = (const T*)dy;
   const T* xp = (const T*)x;
   cfg = resolve_wgrad_cfg(s, cfg);
+  if (in_scale != nullptr) {  // folded input BN: dense bf16, 4-wave tiles
+    e.in_scale = in_scale;
+    e.in_bias = in_bias;
+    if (cfg >= 11) cfg = default_wgrad_cfg(s);
+  }
   int splits_used = 1;
   if (ws != nullptr) {  // deterministic: partial tiles to the workspace, summed in split order
     e.C = ws;
@@ -77,6 +82,13 @@ static void conv_wgrad_t(const void* dy, const void* x, float* dw, const ConvSha
     // non-atomic read-modify-write; the ATOMIC template also carries the workspace-slice store
     const bool atomic = splits > 1 || ws != nullptr;
     if (!atomic) ee.rmw = 1;
+    if constexpr (!C::PP && std::is_same<T, __bf16>::value) {
+      if (in_scale != nullptr) {  // (host checks: dense)
+        if (atomic) hipLaunchKernelGGL((conv_wgrad_kernel<C, true, T, true, true>), grid, block, 0, st, dyp, xp, g, tN, per, ee);
+        else hipLaunchKernelGGL((conv_wgrad_kernel<C, true, T, false, true>), grid, block, 0, st, dyp, xp, g, tN, per, ee);
+        return;
+      }
+    }
     if (dense) {
       if (atomic) hipLaunchKernelGGL((conv_wgrad_kernel<C, true, T, true>), grid, block, 0, st, dyp, xp, g, tN, per, ee);
       else hipLaunchKernelGGL((conv_wgrad_kernel<C, true, T, false>), grid, block, 0, st, dyp, xp, g, tN, per, ee);
@@ -89,9 +101,10 @@ static void conv_wgrad_t(const void* dy, const void* x, float* dw, const ConvSha
 }
 
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
-                int cfg, float* ws, int splits, const BnCollect* col) {
-  if (s.f32) conv_wgrad_t<float>(dy, x, dw, s, st, cfg, ws, splits, col);
-  else conv_wgrad_t<__bf16>(dy, x, dw, s, st, cfg, ws, splits, col);
+                int cfg, float* ws, int splits, const BnCollect* col, const float* in_scale,
+                const float* in_bias) {
+  if (s.f32) conv_wgrad_t<float>(dy, x, dw, s, st, cfg, ws, splits, col, nullptr, nullptr);
+  else conv_wgrad_t<__bf16>(dy, x, dw, s, st, cfg, ws, splits, col, in_scale, in_bias);
 }
 
 }  // namespace mipipe

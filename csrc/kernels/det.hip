@@ -54,7 +54,6 @@ __global__ __launch_bounds__(1024) void det_sum_rows_kernel(const float* __restr
 // fixed order and writes the chunk sum over the chunk's FIRST row (the partial rows are scratch;
 // only this block reads its chunk).  The one-level kernel ran such a sum on C/64 blocks — two
 // CUs for C = 64 — and cost ~11 us per call, 1.2 ms per deterministic ResNet-50 step.
-constexpr int kDetChunkRows = 64;
 __global__ __launch_bounds__(256) void det_chunk_sum_kernel(float* __restrict__ in0,
                                                             float* __restrict__ in1,
                                                             float* __restrict__ in2, int P,
@@ -79,6 +78,14 @@ __global__ __launch_bounds__(256) void det_chunk_sum_kernel(float* __restrict__ 
   part[g][lc] = a;
   __syncthreads();  // every row of the chunk has been read before its first row is overwritten
   if (g == 0 && c < C) in[(long)r0 * C + c] = ((part[0][lc] + part[1][lc]) + part[2][lc]) + part[3][lc];
+}
+
+int det_chunk_sums(float* in0, float* in1, float* in2, int P, int C, hipStream_t st) {
+  const int arrays = in1 == nullptr ? 1 : in2 == nullptr ? 2 : 3;
+  const int nch = (P + kDetChunkRows - 1) / kDetChunkRows;
+  hipLaunchKernelGGL(det_chunk_sum_kernel, dim3((C + 63) / 64, nch, arrays), dim3(256), 0, st,
+                     in0, in1, in2, P, C);
+  return nch;
 }
 
 void det_sum_rows(float* in0, float* in1, int P, int C, float* out0, float* out1,

@@ -64,6 +64,17 @@ struct EpiParams {
   int fl_Co, fl_KH, fl_KW, fl_Ci;
   uint32_t fl_tiles;
   FlipPlan fl;
+  // split-K conv forward / forward-style data-grad (conv_common.hpp): split blockIdx.y runs
+  // k-steps [y*split_kt, (y+1)*split_kt) and stores its fp32 partial tile in slice y of
+  // split_ws [splits][M][N]; conv_splitk_finish_kernel sums the slices in order and runs the
+  // regular epilogue (statistics / BN-backward fusions) on the sum
+  int split_kt;
+  float* split_ws;
+  // folded BatchNorm on the conv INPUT (dense 1x1 bf16 forward / weight-grad, BNIN kernels): the
+  // operand is y and the conv consumes relu(y*in_scale + in_bias) (gemm_core.hpp KCDenseBufBN /
+  // MCDenseBufBN)
+  const float* in_scale;
+  const float* in_bias;
 };
 
 // One 64 x 64 (co x ci) transpose of one tap of one parity class's flipped sub-kernel, riding in

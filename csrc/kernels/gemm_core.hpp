@@ -231,6 +231,82 @@ struct MCDenseBuf {
   }
 };
 
+// ---------------------------------------------------------------------------------------------
+// Folded BatchNorm on an operand (the producing BN's apply + ReLU moved into its consumer's
+// operand path, so the normalised activation is never written): policies with XFORM = true
+// transform each bf16 fragment after its LDS read, v -> bf16(max(v*scale[c] + bias[c], 0)) —
+// the bits bn_act_fwd would have stored (same fused multiply-add, ReLU, round-to-nearest).
+template <class Op, class = void>
+struct HasXform : std::false_type {};
+template <class Op>
+struct HasXform<Op, std::void_t<decltype(Op::XFORM)>> : std::integral_constant<bool, Op::XFORM> {};
+
+__device__ __forceinline__ bf16x8 bn_relu_frag(bf16x8 v, const float (&sc)[8], const float (&bi)[8]) {
+  const uint4 u = __builtin_bit_cast(uint4, v);
+  float f[8];
+  unpack8(u, f);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) f[q] = fmaxf(f[q] * sc[q] + bi[q], 0.f);
+  return __builtin_bit_cast(bf16x8, pack8(f));
+}
+
+// A operand of a dense 1x1 conv whose input is relu(bn(y)) (x = y in memory): k = input
+// channel.  The per-channel (scale, bias) pairs sit in an LDS table the kernel fills before the
+// main loop (tab: float2 per channel, zeros past K so padded channels stay 0); a lane's fragment
+// covers channels kt*64 + ks*32 + 8*(lane>>4) .. +7: four ds_read_b128 per k-substep.
+template <int R, class T = __bf16, int NW = 4>
+struct KCDenseBufBN : KCDenseBuf<R, T, NW> {
+  static constexpr bool XFORM = true;
+  const char* tab;
+  __device__ void xform(bf16x8& f, int kt, int ks, int lane) const {
+    const uint32_t c0 = (uint32_t)kt * BK + (uint32_t)ks * 32 + ((uint32_t)lane >> 4) * 8;
+    const float4* t = reinterpret_cast<const float4*>(tab + c0 * 8);
+    const float4 t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
+    const float sc[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
+    const float bi[8] = {t0.y, t0.w, t1.y, t1.w, t2.y, t2.w, t3.y, t3.w};
+    f = bn_relu_frag(f, sc, bi);
+  }
+};
+
+// B operand of a dense 1x1 conv's weight-grad whose input was relu(bn(y)): B(k = pixel, n =
+// input channel) = y (MN-contiguous).  A lane's fragment is 8 consecutive pixels of ONE column
+// (col0 + (lane & 15)), so its (scale, bias) is fixed for the whole k-loop: one register pair per
+// fragment column, loaded by xform_setup.  The tail k-step (K % 64 != 0) zeroes pixels past K
+// after the transform (the range check reads zeros, which would become relu(bias)).
+template <int W, class T = __bf16, int NW = 4>
+struct MCDenseBufBN : MCDenseBuf<W, T, NW> {
+  static constexpr bool XFORM = true;
+  static constexpr int NJ = 8;  // fragment columns per wave supported (BN / WN / 16)
+  const float* g_sc;
+  const float* g_bi;
+  uint32_t origin, ncols;
+  float sc[NJ], bi[NJ];
+  __device__ void xform_setup(uint32_t col0, int nt, int lane) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const uint32_t n = origin + col0 + (uint32_t)j * 16 + ((uint32_t)lane & 15);
+      const bool ok = j < nt && n < ncols;
+      sc[j] = ok ? g_sc[n] : 0.f;
+      bi[j] = ok ? g_bi[n] : 0.f;
+    }
+  }
+  __device__ void xform(bf16x8& f, int kt, int ks, int lane, int j) const {
+    float s8[8], b8[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      s8[q] = sc[j];
+      b8[q] = bi[j];
+    }
+    f = bn_relu_frag(f, s8, b8);
+    if (kt == this->kt_tail) {  // wave-uniform: the one k-step whose rows may pass K
+      const uint32_t k0 = (uint32_t)kt * BK + (uint32_t)ks * 32 + ((uint32_t)lane >> 4) * 8;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (k0 + (uint32_t)q >= this->K) f[q] = (__bf16)0.0f;
+    }
+  }
+};
+
 // Conv forward A operand: im2col of NHWC x.  row m -> (img, ho, wo); k -> (kh, kw, ci).
 struct ConvGeom {
   int N, H, W, C;        // input
@@ -876,10 +952,28 @@ struct MainLoop {
   // (nbuf != nullptr) are issued between MFMA groups instead of in one burst before them.
   // FIRST: the k-step that starts the accumulation — its first MFMA of each tile takes C = 0
   // (an inline constant) instead of 64 zeroed accumulator registers
+  // folded-BN operands (HasXform): fragments of k-step kt transformed after their LDS read
+  __device__ static void xform(bf16x8 (&af)[2][MT], bf16x8 (&bfr)[2][NT], const OpA& a,
+                               const OpB& b, int kt, int lane) {
+    if constexpr (HasXform<OpA>::value) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) a.xform(af[ks][i], kt, ks, lane);
+    }
+    if constexpr (HasXform<OpB>::value) {
+      static_assert(NT <= OpB::NJ, "folded-BN B operand: fragment columns per wave");
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) b.xform(bfr[ks][j], kt, ks, lane, j);
+    }
+  }
+
   template <bool FIRST = false>
   __device__ static void compute(const char* cbuf, f32x4 (&acc)[MT][NT], uint32_t arow0,
                                  uint32_t bcol0, int lane, char* nbuf, OpA& a, OpB& b, int nkt,
-                                 int wave) {
+                                 int wave, int kt) {
     const char* aimg = cbuf;
     const char* bimg = cbuf + A_BYTES;
     // both k-substeps' fragments are requested up front, so the second substep's LDS reads
@@ -894,6 +988,7 @@ struct MainLoop {
       for (int j = 0; j < NT; ++j)
         bfr[ks][j] = FragLoader<OpB::KC, BN>::load(bimg, bcol0 + j * 16, ks, lane);
     }
+    xform(af, bfr, a, b, kt, lane);
     if constexpr (SPREAD) {
       if (nbuf != nullptr) {
         a.prep(nkt);
@@ -938,6 +1033,7 @@ struct MainLoop {
       for (int j = 0; j < NT; ++j)
         bfr[ks][j] = FragLoader<OpB::KC, BN>::load(bimg, bcol0 + j * 16, ks, lane);
     }
+    xform(af, bfr, a, b, kt_next - 1, lane);  // (the A table lives outside the stage buffer)
     barrier();  // this wave's reads retired (lgkmcnt 0) and every other wave's: buffer free
     if (kt_next < kt1) stage(smem, a, b, kt_next, wave);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
@@ -964,6 +1060,7 @@ struct MainLoop {
     }
     const int wr = wave / WN, wc = wave % WN;
     const uint32_t arow0 = wr * (BM / WM), bcol0 = wc * (BN / WN);
+    if constexpr (HasXform<OpB>::value) b.xform_setup(bcol0, NT, lane);
     if constexpr (NS == 1 && (V & kLoopEarlyDma) != 0) {
       stage(smem, a, b, kt0, wave);
       for (int kt = kt0; kt < kt1; ++kt) {
@@ -978,8 +1075,8 @@ struct MainLoop {
         stage(smem, a, b, kt, wave);
         wait_vmcnt<0>();
         __syncthreads();
-        if (kt == kt0) compute<true>(smem, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave);
-        else compute(smem, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave);
+        if (kt == kt0) compute<true>(smem, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave, kt);
+        else compute(smem, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave, kt);
       }
     } else {
 #pragma unroll
@@ -1003,10 +1100,10 @@ struct MainLoop {
         }
         if (kt == kt0)
           compute<true>(smem + cur * STAGE_BYTES, acc, arow0, bcol0, lane, nb, a, b,
-                        kt + NS - 1, wave);
+                        kt + NS - 1, wave, kt);
         else
           compute(smem + cur * STAGE_BYTES, acc, arow0, bcol0, lane, nb, a, b, kt + NS - 1,
-                  wave);
+                  wave, kt);
         cur = cur + 1 == NS ? 0 : cur + 1;
         nxt = nxt + 1 == NS ? 0 : nxt + 1;
       }
@@ -1033,6 +1130,7 @@ struct MainLoop {
 // k's MFMAs.
 template <int BM, int BN, class OpA, class OpB, int WM = 2, int WN = 2>
 struct MainLoopF32 {
+  static_assert(!HasXform<OpA>::value && !HasXform<OpB>::value, "folded BN: bf16 loops only");
   static constexpr int MT = BM / WM / 16;
   static constexpr int NT = BN / WN / 16;
   static constexpr int PARTS = 3;

@@ -81,6 +81,7 @@ struct MainLoopPP {
   static_assert(OpA::NI * 8 * NW == HM || !OpA::KC, "A half policy: R = BM/2 rows, 8 waves");
   static_assert(OpB::NI * 8 * NW == HN || !OpB::KC, "B half policy: R = BN/2 rows, 8 waves");
   static_assert(QM >= 1 && QN >= 1, "tile too small for the wave grid");
+  static_assert(!HasXform<OpA>::value && !HasXform<OpB>::value, "folded BN: 4-wave loops only");
 
   // tile-local row / column of accumulator (i, j) of wave (wr, wc), before the lane offset
   __device__ static uint32_t row(int wr, int i) {

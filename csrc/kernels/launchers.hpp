@@ -40,6 +40,15 @@ extern int g_deterministic;
 // SCRATCH: long sums (P > 256) are done in two levels, the first writing chunk sums in place.
 void det_sum_rows(float* in0, float* in1, int P, int C, float* out0, float* out1,
                   bool accumulate, hipStream_t st, float* in2 = nullptr, float* out2 = nullptr);
+// First level of a long fixed-order column sum: rows [k*kDetChunkRows, (k+1)*kDetChunkRows) of
+// each array summed in place into row k*kDetChunkRows (arrays in order: in2 only with in1).
+// Returns the number of chunk rows (every kDetChunkRows-th row) the second level sums.
+constexpr int kDetChunkRows = 64;
+int det_chunk_sums(float* in0, float* in1, float* in2, int P, int C, hipStream_t st);
+// bn_bwd_collect of [2|3][P][C] deterministic partial rows (det_sum_rows' order; rows scratch)
+void bn_bwd_collect_rows(float* rows, int P, int C, bool two, float* out_g, float* out_gx,
+                         float* out_gx2, float* dgamma, float* dbeta, float* dgamma2,
+                         float* dbeta2, const float* gx_div, hipStream_t st);
 // out[i] += sum_s ws[s][i] over splits in order.
 void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st);
 // out[m][n] (bf16, row pitch ldc) = sum_s ws[s][m][n] + bias[n] (bias may be null); N % 8 == 0
@@ -55,10 +64,41 @@ constexpr int kConvTileConfigs = 15;
 // wflip (Ci*KH*KW*Co elements, w's dtype): when dgrad_preflip_ok(s), trailing blocks of the
 // launch also write the tap-flipped weight the stride-1 data-grad reads (conv_dgrad's
 // `preflipped`) — no flip kernel in the backward.
+// split_ws: fp32 workspace of conv_fwd_split_ws_elems(s, cfg) elements when the plan splits K
 void conv_fwd(const void* x, const void* w, void* y, float* st_sum, float* st_sq,
               const float* st_shift, const ConvShape& s, hipStream_t st,
               const float* bias = nullptr, bool relu = false, int cfg = -1, int det_rows = 0,
-              void* wflip = nullptr);
+              void* wflip = nullptr, float* split_ws = nullptr,
+              const float* in_scale = nullptr, const float* in_bias = nullptr);
+constexpr int kConvBnInMaxK = 1024;  // input channels of a folded-BN forward (LDS table)
+inline bool conv_is_dense(const ConvShape& s) {  // 1x1, stride 1, no padding
+  return s.KH == 1 && s.KW == 1 && s.stride == 1 && s.pad == 0 && s.pad_w <= 0 &&
+         (s.stride_w == 0 || s.stride_w == 1);
+}
+// in_scale / in_bias (bf16 dense 1x1, Ci <= 1024): x holds y of a BatchNorm + ReLU whose apply is
+// FOLDED into this conv — the conv consumes relu(y*in_scale + in_bias) (per input channel),
+// transformed after each operand fragment's LDS read; the normalised tensor never exists.
+// Conv forward / forward-style data-grad PLANS: tile id + kConvSplitPlan * splits.  A split plan
+// (splits >= 2) runs the k-steps in `splits` slices (grid.y) into an fp32 workspace and a finish
+// launch sums the slices in slice order (deterministic) and runs the regular epilogue — for the
+// small-spatial layers whose tiles alone cannot fill 256 CUs (ResNet-18 32x32 layer 3 / 4: 64-128
+// tiles of 36 k-steps each).
+constexpr int kConvSplitPlan = 16;
+inline int conv_plan_tile(int plan) { return plan < 0 ? plan : plan % kConvSplitPlan; }
+inline int conv_plan_splits(int plan) { return plan < kConvSplitPlan ? 1 : plan / kConvSplitPlan; }
+// (effective splits, k-steps per split) of nk k-steps under a plan's split request
+inline void conv_split_geometry(int nk, int req, int* splits, int* kps) {
+  if (req <= 1 || nk < 2) {
+    *splits = 1;
+    *kps = nk;
+    return;
+  }
+  *kps = (nk + req - 1) / req;
+  *splits = (nk + *kps - 1) / *kps;
+}
+long conv_fwd_split_ws_elems(const ConvShape& s, int cfg);
+void conv_tile_dims(int cfg, bool f32, int* bm, int* bn);  // block tile of a plan's tile id
+long conv_dgrad_split_ws_elems(const ConvShape& s, int cfg);
 // The data-grad of s runs as forward-style parity classes over tap-flipped sub-kernels (see
 // conv_dgrad_fwd_style; stride <= 2), so a forward launch can produce those weights.
 bool dgrad_preflip_ok(const ConvShape& s);
@@ -98,9 +138,11 @@ struct DgradFusion {
 // runs as a stride-1 FORWARD im2col convolution of dy over its tap-flipped sub-kernel (written
 // into the workspace by this call); allocate it only when conv_dgrad_fwd_style(s, ...) holds
 // preflipped: w_flip already holds the flipped weight (conv_fwd's wflip, dgrad_preflip_ok(s))
+// split_ws: conv_dgrad_split_ws_elems(s, cfg) fp32 elements when the plan splits K (the
+// forward-style classes only; the other data-grad kernels ignore the split)
 void conv_dgrad(const void* dy, const void* w, void* dx, const ConvShape& s, hipStream_t st,
                 const DgradFusion* fz = nullptr, int cfg = -1, void* w_flip = nullptr,
-                bool preflipped = false);
+                bool preflipped = false, float* split_ws = nullptr);
 bool conv_dgrad_fwd_style(const ConvShape& s, bool dense_too);
 int conv_dgrad_tiles_m(const ConvShape& s, int cfg);  // M-tiles over all stride classes
 // dw is ACCUMULATED into (split-K fp32 atomics, or a plain read-modify-write when unsplit): pass
@@ -137,8 +179,11 @@ struct WsFinish {
   int bf16 = 0;
 };
 // col: optional collect riding in this launch (see BnCollect)
+// in_scale / in_bias: folded input BatchNorm (see conv_fwd; bf16 dense): x holds y and the
+// weight-grad reads relu(y*in_scale + in_bias)
 void conv_wgrad(const void* dy, const void* x, float* dw, const ConvShape& s, hipStream_t st,
-                int cfg = -1, float* ws = nullptr, int splits = -1, const BnCollect* col = nullptr);
+                int cfg = -1, float* ws = nullptr, int splits = -1, const BnCollect* col = nullptr,
+                const float* in_scale = nullptr, const float* in_bias = nullptr);
 int conv_wgrad_splits(const ConvShape& s, int cfg, int splits = -1);
 // 3x3 / stride 1 / pad 1 bf16 weight-grad with the input patch resident in LDS (wgrad3x3.hip):
 // partial tiles per split go to ws [splits][Co*9*Ci] and are added to dw in a fixed order

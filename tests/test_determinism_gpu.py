@@ -99,3 +99,65 @@ def test_identical_runs_with_benchmark_mode_on():
         tuning.clear()
     assert torch.equal(la, lb), (la, lb)
     assert torch.equal(a, b), f"{(a != b).sum().item()} of {a.numel()} values differ"
+
+
+def _det_rows_sum(rows):
+    """det_sum_rows' fixed order on the CPU in fp32 (IEEE adds, no FMA): long columns (> 256
+    rows) as 64-row chunk sums first (4 interleaved groups, then ((g0+g1)+g2)+g3), then 16
+    interleaved row groups each summed in row order, then the 16 group sums in index order."""
+    rows = rows.float().cpu()
+    if rows.shape[0] > 256:
+        chunks = []
+        for r0 in range(0, rows.shape[0], 64):
+            ch = rows[r0:r0 + 64]
+            gs = []
+            for g in range(4):
+                a = torch.zeros(rows.shape[1])
+                for p in range(g, ch.shape[0], 4):
+                    a = a + ch[p]
+                gs.append(a)
+            chunks.append(((gs[0] + gs[1]) + gs[2]) + gs[3])
+        rows = torch.stack(chunks)
+    parts = []
+    for g in range(16):
+        a = torch.zeros(rows.shape[1])
+        for p in range(g, rows.shape[0], 16):
+            a = a + rows[p]
+        parts.append(a)
+    s = torch.zeros(rows.shape[1])
+    for a in parts:
+        s = s + a
+    return s
+
+
+@pytest.mark.parametrize("P", [5, 16 * 8 + 3, 128, 300, 2048])
+@pytest.mark.parametrize("C", [64, 200])
+def test_bn_finalize_partial_rows_fixed_order(P, C):
+    """Deterministic-mode bn_finalize of P per-tile partial rows (one launch, no det_sum_rows
+    into the slab first): the same bits as the slab route — the rows summed in det_sum_rows'
+    order into replica row 0 of a zeroed [16, C] slab, then the replica finalize — and within
+    fp32 rounding of a float64 evaluation."""
+    torch.manual_seed(P + C)
+    count = 4096
+    s1 = torch.randn(P, C, device=dev) * 3.0
+    s2 = torch.rand(P, C, device=dev) * 20.0 + 40.0
+    shift = torch.randn(C, device=dev) * 0.1
+    gamma, beta = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    outs = []
+    for route in ("rows", "slab"):
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        if route == "rows":
+            a, b = s1.clone(), s2.clone()
+        else:
+            R = native().STAT_REPLICAS
+            a, b = torch.zeros(R, C, device=dev), torch.zeros(R, C, device=dev)
+            a[0], b[0] = _det_rows_sum(s1).to(dev), _det_rows_sum(s2).to(dev)
+        outs.append(native().bn_finalize(a, b, count, shift, gamma, beta, rm, rv, 0.1, 1e-5, True,
+                                         None) + (rm, rv))
+    for x, y in zip(outs[0], outs[1]):
+        assert torch.equal(x, y), (x - y).abs().max()
+    mean, invstd = outs[0][0].double(), outs[0][1].double()
+    ms = s1.double().sum(0) / count
+    var = s2.double().sum(0) / count - ms * ms
+    assert torch.allclose(mean, ms + shift.double(), rtol=1e-5, atol=1e-5)
+    assert torch.allclose(invstd, torch.rsqrt(var + 1e-5), rtol=1e-5)

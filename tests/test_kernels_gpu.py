@@ -661,6 +661,80 @@ TILE_CASES = [
 ]
 
 
+SPLIT_CASES = [
+    # N, H, W, Ci, Co, k, s, p — small-spatial layers (ResNet-18 32x32 layer 3 / 4 shapes), the
+    # dense 1x1, a strided conv (split forward; its data-grad classes are not forward-style) and
+    # odd channel counts (unaligned im2col, rows past M, columns past N)
+    (16, 2, 2, 256, 256, 3, 1, 1),
+    (32, 1, 1, 512, 512, 1, 1, 0),
+    (8, 4, 4, 128, 256, 3, 2, 1),
+    (3, 7, 5, 40, 72, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("splits", [2, 3, 4, 8])
+@pytest.mark.parametrize("tile", [0, 2, 8, 1, 9, 11, 14])
+@pytest.mark.parametrize("case", SPLIT_CASES)
+@DTYPES
+def test_conv_split_k_plans(splits, tile, case, dt):
+    """Split-K conv plans (plan = tile + 16 x splits): the k-steps run in `splits` slices into an
+    fp32 workspace and a finish launch sums the slices in order and runs the regular epilogue —
+    forward (+BN statistics, +bias/ReLU) and the forward-style data-grad (+residual addend,
+    +BN-backward sums) equal the reference; deterministic mode (statistics as per-tile rows) gives
+    bit-identical reruns."""
+    f32 = dt == torch.float32
+    if f32 and tile not in (0, 2, 8):
+        pytest.skip("fp32 runs the 4-wave split-bf16x3 tiles")
+    from mipipe.ops import determinism
+    N, H, W, Ci, Co, k, s, p = case
+    cfg = tile + 16 * splits
+    R = (lambda t: t.detach().double().cpu()) if f32 else (lambda t: t.float())
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    x = rnd(dt, N, H, W, Ci)
+    w = rnd(dt, Co, k, k, Ci, scale=1.0 / math.sqrt(Ci * k * k))
+    shift = torch.randn(Co, device=dev) * 0.1
+    y, ps, pss = native().conv_fwd(x, w, s, p, shift, cfg=cfg)
+    yr, psr, pssr = _ref.conv_fwd(R(x), R(w), s, p, R(shift))
+    assert rel_err(y, yr) < TOL_OUT[dt]
+    # bf16: statistics of the stored (bf16-rounded) outputs over as few as 32 rows
+    tol_st = TOL_ACC[dt] if f32 else 5e-3
+    assert rel_err(ps.sum(0), psr[0]) < tol_st and rel_err(pss.sum(0), pssr[0]) < tol_st
+    bias = torch.randn(Co, device=dev) * 0.1
+    yb = native().conv_fwd(x, w, s, p, None, bias=bias, relu=True, cfg=cfg)[0]
+    assert rel_err(yb, torch.relu(yr + R(bias))) < TOL_OUT[dt]
+    dy = rnd(dt, N, Ho, Wo, Co)
+    dxr = _ref.conv_dgrad(R(dy), R(w), (N, H, W, Ci), s, p)
+    dx = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, cfg=cfg)
+    assert rel_err(dx, dxr) < TOL_OUT[dt]
+    yin, add = rnd(dt, N, H, W, Ci), rnd(dt, N, H, W, Ci)
+    mean = torch.randn(Ci, device=dev) * 0.1
+    invstd = torch.rand(Ci, device=dev) + 0.5
+    scale = torch.rand(Ci, device=dev) + 0.5
+    bb = torch.randn(Ci, device=dev) * 0.1
+    rep = torch.zeros(3, native().STAT_REPLICAS, Ci, device=dev)
+    g = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, add, yin, mean, invstd, scale, bb, rep,
+                            cfg=cfg)
+    sg, sgx = native().bn_bwd_collect(rep, Ci)
+    gr = (dxr + R(add)) * ((R(yin) * R(scale) + R(bb)) > 0)
+    assert rel_err(g, gr) < TOL_OUT[dt]
+    grb = gr if f32 else gr.to(torch.bfloat16).float()
+    tol_sum = 1e-4 if f32 else 8e-3
+    assert rel_err(sg, grb.reshape(-1, Ci).sum(0)) < tol_sum
+    assert rel_err(sgx, (grb * (R(yin) - R(mean)) * R(invstd)).reshape(-1, Ci).sum(0)) < tol_sum
+    with determinism.deterministic(True):
+        outs = []
+        for _ in range(2):
+            y1, a1, b1 = native().conv_fwd(x, w, s, p, shift, cfg=cfg)
+            rep1 = torch.zeros(3, native().STAT_REPLICAS, Ci, device=dev)
+            g1 = native().conv_dgrad(dy, w, [N, H, W, Ci], s, p, add, yin, mean, invstd, scale, bb,
+                                     rep1, cfg=cfg)
+            outs.append((y1, a1, b1, g1, rep1))
+        for u, v in zip(*outs):
+            assert torch.equal(u, v)
+        assert rel_err(outs[0][0], yr) < TOL_OUT[dt]
+        assert rel_err(outs[0][1].sum(0), psr[0]) < tol_st
+
+
 @pytest.mark.parametrize("cfg", list(range(15)))
 @pytest.mark.parametrize("case", TILE_CASES)
 @DTYPES
