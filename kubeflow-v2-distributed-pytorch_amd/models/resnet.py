@@ -88,7 +88,9 @@ class Bottleneck(tnn.Module):
         if isinstance(self.conv2, mnn.XConv2d):  # grouped: direct kernel + any-C BN/ReLU pass
             out = MF.bn_act(self.conv2.run(out), self.bn2, "relu")
         else:
-            out = mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, fuse_prev=True)
+            # conv3 (dense 1x1) is the only consumer: BN2's apply + ReLU folds into it
+            out = mnn.conv_bn_act(out, self.conv2, self.bn2, relu=True, fuse_prev=True,
+                                  fold_next=True)
         if self.downsample is not None:
             ds_conv, ds_bn = self.downsample[0], self.downsample[1]
             return mnn.conv_bn_act(out, self.conv3, self.bn3, relu=True, fuse_prev=True,

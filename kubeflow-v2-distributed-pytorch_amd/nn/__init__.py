@@ -13,6 +13,7 @@ saves ``model.state_dict()``, task.py:282-294).  Differences in *execution*:
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -88,11 +89,12 @@ class Conv2d(ShadowMixin, tnn.Module):
         return r
 
     def forward(self, x: torch.Tensor, stats_shift: Optional[torch.Tensor] = None, slabs=None,
-                prev=None, res_take=None, res_give=None):
-        """x: NHWC.  Returns y, or (y, psum, psumsq) when ``stats_shift`` is given."""
+                prev=None, res_take=None, res_give=None, in_bn=None):
+        """x: NHWC.  Returns y, or (y, psum, psumsq) when ``stats_shift`` is given.  ``in_bn``:
+        (scale, bias) of a BatchNorm + ReLU folded into this conv (x holds its input y)."""
         w_c = self.compute_weight(x.dtype)
         y, ps, pss = MF.conv2d(x, self.weight, w_c, self.stride[0], self.padding[0], stats_shift,
-                               slabs, prev, res_take, res_give)
+                               slabs, prev, res_take, res_give, in_bn)
         if self.bias is not None:
             y = y + self.bias.to(y.dtype)
         return y if stats_shift is None else (y, ps, pss)
@@ -183,11 +185,26 @@ class BatchNorm2d(tnn.BatchNorm2d):
         return MF.batchnorm_act(y, st, self, relu=False)
 
 
+# Measured a net LOSS on ResNet-50 b256 (profiles/r6_bn_fold_negative.txt): the per-fragment
+# transform (28 VALU per 8 values, redone by every wave and N-tile that reads the fragment, ahead
+# of the MFMAs) costs the conv3 forwards 30-60 % and the weight-grads 5-40 %, more than the
+# bn_act_fwd pass it removes (-280 us): 12,700 vs 13,150 img/s.  Kept opt-in (MIPIPE_BN_FOLD=1).
+_BN_FOLD = os.environ.get("MIPIPE_BN_FOLD", "0") == "1"
+
+
+def _foldable_into_1x1(y: torch.Tensor) -> bool:
+    """A BN + ReLU output the next dense 1x1 conv can consume folded (bf16 GPU, C <= 1024)."""
+    from mipipe.ops import kernels as K
+    return (_BN_FOLD and y.is_cuda and y.dtype == torch.bfloat16 and K.use_native(y)
+            and y.shape[-1] <= 1024 and y.shape[-1] % 8 == 0)
+
+
 def conv_bn_act(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d, relu: bool = True,
                 residual: Optional[torch.Tensor] = None,
                 branch: Optional[tuple] = None, fuse_prev: bool = False,
                 res_take: Optional[MF.ResidualSlot] = None,
-                res_give: Optional[MF.ResidualSlot] = None) -> torch.Tensor:
+                res_give: Optional[MF.ResidualSlot] = None,
+                fold_next: bool = False) -> torch.Tensor:
     """Fused conv -> BN -> [+residual | +BN(conv(branch_x))] -> ReLU on NHWC activations.
 
     ``branch`` = (x_b, conv_b, bn_b): the ResNet downsample path, normalised and added in the
@@ -196,15 +213,25 @@ def conv_bn_act(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d, relu: bool = Tru
     a previous relu-only conv_bn_act) -> that BN's backward reductions run in this conv's
     dgrad epilogue.  ``res_take`` / ``res_give``: residual-gradient hand-off (the conv that
     also reads the block input adds the identity/downsample gradient in its dgrad epilogue).
+    ``fold_next``: the caller guarantees the returned tensor's ONLY consumer is a dense 1x1
+    stride-1 conv reached through ``conv_bn_act(fuse_prev=True)`` (ResNet Bottleneck conv3): this
+    BN's apply + ReLU is then folded into that conv — its forward and weight-grad read y and
+    transform their operand fragments (gemm_core.hpp KCDenseBufBN / MCDenseBufBN), so the
+    normalised activation is never written (saves a read and a write of the tensor per step; opt-in
+    with MIPIPE_BN_FOLD=1 — measured slower end to end, see _BN_FOLD).  The returned tensor is then
+    an alias of y.
     """
     use_batch = bn.training
     prev = getattr(x, "_mipipe_bnact", None) if fuse_prev else None
+    in_bn = getattr(x, "_mipipe_lazy_bn", None) if fuse_prev else None
+    if in_bn is not None and prev is None:
+        raise RuntimeError("a folded BN output reached a conv without its BN token")
     if use_batch:
         ws = MF.bn_workspace(bn, "fwd", x.device)
         y, ps, pss = conv(x, bn.running_mean, None if ws is None else (ws[0], ws[1]), prev=prev,
-                          res_take=res_take)
+                          res_take=res_take, in_bn=in_bn)
     else:
-        y, ps, pss = conv(x, prev=prev, res_take=res_take), None, None
+        y, ps, pss = conv(x, prev=prev, res_take=res_take, in_bn=in_bn), None, None
     count = y.numel() // y.shape[-1]
     st = MF.bn_stats_from_partials(ps, pss, count, bn, use_batch)
     if branch is not None:
@@ -230,12 +257,16 @@ def conv_bn_act(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d, relu: bool = Tru
     token = None
     if relu and use_batch:
         token = MF.BNActToken(bn, st, y)
+    lazy = (fold_next and token is not None and residual is None and torch.is_grad_enabled()
+            and _foldable_into_1x1(y))
     z = MF.batchnorm_act(y, st, bn, relu, residual=residual, token=token,
-                         res_give=res_give if residual is not None else None)
+                         res_give=res_give if residual is not None else None, lazy=lazy)
     if token is not None:
         if residual is not None:
             token.z = z  # mask source for the (multi-consumer) block-output fusion
         z._mipipe_bnact = token
+    if lazy:
+        z._mipipe_lazy_bn = (st.scale, st.bias)
     return z
 
 

@@ -490,3 +490,9 @@ def synthetic_images(indices: Tensor, num_classes: int, shape, seed: int,
         noise[i] = torch.randn(H, W, C, generator=gi, device=indices.device)
     x = 0.5 * templates[labels] + noise
     return x.to(dtype), labels
+
+
+def bn_relu_fold(y: Tensor, scale: Tensor, bias: Tensor) -> Tensor:
+    """The operand a folded input BatchNorm hands its consumer conv: relu(y*scale + bias) per
+    channel (NHWC), in y's dtype — the values bn_act_fwd would have stored."""
+    return torch.relu(y.float() * scale.float() + bias.float()).to(y.dtype)

@@ -190,11 +190,14 @@ def tap_crop(x_shape, w_shape, stride, pad):
 class _ConvFn(Function):
     @staticmethod
     def forward(ctx, x, weight, w_c, stride, pad, shift, slabs=None, prev=None, res_take=None,
-                res_give=None):
+                res_give=None, in_bn=None):
+        # in_bn = (scale, bias): x holds y of a BatchNorm + ReLU folded into this conv (dense 1x1,
+        # see conv_bn_act(fold_next=)): the forward and the weight-grad transform their operand
+        ctx.in_bn = in_bn
         # taps that never touch the image are cropped away (forward, data-grad and weight-grad
         # all run the smaller filter; the weight-grad lands in its slice of the full gradient)
         crop = (tap_crop(tuple(x.shape), tuple(w_c.shape), stride, pad)
-                if getattr(weight, "_mipipe_wgrad_map", None) is None else None)
+                if getattr(weight, "_mipipe_wgrad_map", None) is None and in_bn is None else None)
         if crop is not None:
             kh0, kh1, kw0, kw1, pad = crop
             w_c = w_c[:, kh0:kh1, kw0:kw1, :].contiguous()
@@ -205,7 +208,7 @@ class _ConvFn(Function):
         # per stride-parity class (ResNet-18 layer 4's stride-2 conv on its 2x2 map)
         ctx.flat = None
         if (_TAP_CROP and _CONV_FLATTEN and isinstance(stride, int) and isinstance(pad, int)
-                and pad == 0
+                and pad == 0 and in_bn is None
                 and getattr(weight, "_mipipe_wgrad_map", None) is None
                 and w_c.shape[1] == x.shape[1] and w_c.shape[2] == x.shape[2]
                 and w_c.shape[3] == x.shape[3] and x.shape[1] * x.shape[2] > 1):
@@ -227,7 +230,7 @@ class _ConvFn(Function):
                     or wflip.device != w_c.device):
                 wflip = torch.empty(w_c.numel(), dtype=w_c.dtype, device=w_c.device)
                 weight.__dict__["_mipipe_wflip"] = wflip
-        y, psum, psumsq = K.conv_fwd(x, w_c, stride, pad, shift, slabs, wflip=wflip)
+        y, psum, psumsq = K.conv_fwd(x, w_c, stride, pad, shift, slabs, wflip=wflip, in_bn=in_bn)
         ctx.wflip = wflip
         ctx.set_materialize_grads(False)  # stats outputs never get gradients: no zero fills
         ctx.save_for_backward(x, w_c)
@@ -244,7 +247,8 @@ class _ConvFn(Function):
     def backward(ctx, dy, _g1, _g2):
         x, w_c = ctx.saved_tensors
         if dy is None:
-            return (None,) * 10
+            return (None,) * 11
+        in_bn = ctx.in_bn
         stride, pad, kh, kw, ci = ctx.conf
         dy = dy.contiguous()
         dx = dw = None
@@ -315,7 +319,8 @@ class _ConvFn(Function):
                 main = torch.cuda.current_stream(dy.device)
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
-                    K.conv_wgrad(dy, x, kh, kw, stride, pad, out=g.permute(0, 2, 3, 1))
+                    K.conv_wgrad(dy, x, kh, kw, stride, pad, out=g.permute(0, 2, 3, 1),
+                                 in_bn=in_bn)
                 dy.record_stream(side)
                 x.record_stream(side)
                 _queue_side_join(main, side)
@@ -331,10 +336,10 @@ class _ConvFn(Function):
                         part.reshape(part.shape[0], kh1 - kh0, kw1 - kw0, -1))
                 else:
                     K.conv_wgrad(dy, x, kh, kw, stride, pad, out=g.permute(0, 2, 3, 1),
-                                 collect=collect)
+                                 collect=collect, in_bn=in_bn)
                 fs.grad_ready(weight)
             else:
-                dw = K.conv_wgrad(dy, x, kh, kw, stride, pad, collect=collect)
+                dw = K.conv_wgrad(dy, x, kh, kw, stride, pad, collect=collect, in_bn=in_bn)
                 if ctx.crop is not None:
                     kh0, kh1, kw0, kw1, _ = ctx.crop
                     dw = dw.reshape(dw.shape[0], kh1 - kh0, kw1 - kw0, -1)
@@ -347,18 +352,20 @@ class _ConvFn(Function):
                     if dw.shape[-1] != ci:  # input channels were zero-padded for the kernel
                         dw = dw[..., :ci]
                     dw = dw.permute(0, 3, 1, 2)
-        return dx, dw, None, None, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None, None, None
 
 
 def conv2d(x: Tensor, weight: Tensor, w_c: Tensor, stride: int, pad: int,
            stats_shift: Optional[Tensor] = None, slabs=None, prev: Optional[BNActToken] = None,
-           res_take: Optional[ResidualSlot] = None, res_give: Optional[ResidualSlot] = None):
+           res_take: Optional[ResidualSlot] = None, res_give: Optional[ResidualSlot] = None,
+           in_bn=None):
     """NHWC conv.  Returns (y, psum, psumsq); the partials are None unless ``stats_shift``.
     ``prev``: token of the BN(+ReLU) that produced x (x has no other consumer) -> BN-backward
     reductions fused into this conv's dgrad.  ``res_take`` / ``res_give``: residual-gradient
-    slot this conv's dgrad adds / hands over (see :class:`ResidualSlot`)."""
+    slot this conv's dgrad adds / hands over (see :class:`ResidualSlot`).  ``in_bn = (scale,
+    bias)``: x holds y of a BatchNorm + ReLU folded into this conv (bf16 dense 1x1)."""
     return _ConvFn.apply(x, weight, w_c, stride, pad, stats_shift, slabs, prev, res_take,
-                         res_give)
+                         res_give, in_bn)
 
 
 class _ConvBiasActFn(Function):
@@ -592,7 +599,20 @@ def bn_stats_from_partials(psum, psumsq, count, bn, training: bool) -> BNStats:
 class _BNActFn(Function):
     @staticmethod
     def forward(ctx, y, gamma, beta, residual, y2, gamma2, beta2, st, st2, relu, bn=None,
-                token=None, res_give=None):
+                token=None, res_give=None, lazy=False):
+        ctx.lazy = lazy
+        if lazy:
+            # folded into the single consuming 1x1 conv (conv_bn_act(fold_next=)): that conv reads
+            # y and applies relu(y*scale + bias) to its operand fragments; nothing is written here.
+            # The returned alias of y carries the pending transform for the consumer.
+            z = y.view_as(y)
+            ctx.save_for_backward(y, None, y2, gamma, gamma2)
+            ctx.st, ctx.st2, ctx.relu = st, st2, relu
+            ctx.has_res = False
+            ctx.bn = bn
+            ctx.beta, ctx.beta2 = beta, beta2
+            ctx.token, ctx.res_give = token, res_give
+            return z
         mask = None
         if (_RELU_BITMASK and token is not None and relu
                 and (residual is not None or y2 is not None) and K.use_native(y)):
@@ -618,7 +638,9 @@ class _BNActFn(Function):
         dz = dz.contiguous()
         tok = ctx.token
         if tok is not None and tok.pre_reduced:
-            return _BNActFn._backward_pre_reduced(ctx, dz, y, gamma, y2, gamma2)
+            return _BNActFn._backward_pre_reduced(ctx, dz, y, gamma, y2, gamma2) + (None,)
+        if ctx.lazy:  # the consumer did not reduce (no fused dgrad ran): materialise z here
+            z = K.bn_act_fwd(y, st.scale, st.bias, relu)
         rep = bn_workspace(ctx.bn, "bwd", dz.device) if ctx.bn is not None else None
         # BN affine grads accumulate straight into the flat gradient buffer when possible
         direct = None
@@ -659,13 +681,13 @@ class _BNActFn(Function):
             dres = ctx.res_give.produce(dres)
         dy2 = other if y2 is not None else None
         if direct is not None:
-            return dy, None, None, dres, dy2, None, None, None, None, None, None, None, None
+            return dy, None, None, dres, dy2, None, None, None, None, None, None, None, None, None
         dgamma2 = sgx2 if y2 is not None else None
         dbeta2 = sg if y2 is not None else None
         return (dy, sgx.to(gamma.dtype), sg.to(gamma.dtype), dres, dy2,
                 None if dgamma2 is None else dgamma2.to(gamma2.dtype),
                 None if dbeta2 is None else dbeta2.to(gamma2.dtype), None, None, None, None,
-                None, None)
+                None, None, None)
 
     @staticmethod
     def _backward_pre_reduced(ctx, g, y, gamma, y2=None, gamma2=None):
@@ -727,12 +749,15 @@ class _BNActFn(Function):
 def batchnorm_act(y: Tensor, st: BNStats, bn, relu: bool, residual: Optional[Tensor] = None,
                   y2: Optional[Tensor] = None, st2: Optional[BNStats] = None, bn2=None,
                   token: Optional[BNActToken] = None,
-                  res_give: Optional[ResidualSlot] = None) -> Tensor:
+                  res_give: Optional[ResidualSlot] = None, lazy: bool = False) -> Tensor:
     """z = relu?( bn(y) [+ residual | + bn2(y2)] ).  ``token``: z's single consumer will fuse
-    this BN's backward reductions; ``res_give``: slot receiving the residual's gradient."""
+    this BN's backward reductions; ``res_give``: slot receiving the residual's gradient.
+    ``lazy``: the apply is folded into z's single consuming 1x1 conv — the returned tensor is an
+    alias of y (see nn.conv_bn_act(fold_next=))."""
     return _BNActFn.apply(y, bn.weight, bn.bias, residual, y2,
                           None if bn2 is None else bn2.weight,
-                          None if bn2 is None else bn2.bias, st, st2, relu, bn, token, res_give)
+                          None if bn2 is None else bn2.bias, st, st2, relu, bn, token, res_give,
+                          lazy)
 
 
 def channel_partials(y: Tensor, shift: Tensor) -> Tuple[Tensor, Tensor]:

@@ -46,18 +46,23 @@ def _pads(pad):
 
 
 def conv_fwd(x, w, stride, pad, stats_shift=None, slabs=None, bias=None, relu=False,
-             wflip=None):
+             wflip=None, in_bn=None):
     """``slabs``: persistent zeroed (sum, sumsq) replica slabs the GPU epilogue accumulates BN
     statistics into (re-zeroed by :func:`bn_finalize`).  ``bias`` / ``relu``: epilogue bias and
     ReLU for convolutions without BatchNorm (exclusive with the statistics epilogue).
     ``wflip`` (native, :func:`dgrad_preflip_ok` shapes): extra blocks of the same launch write
-    the tap-flipped weight the data-grad reads — pass it to :func:`conv_dgrad` as ``wflip``."""
+    the tap-flipped weight the data-grad reads — pass it to :func:`conv_dgrad` as ``wflip``.
+    ``in_bn = (scale, bias)``: folded input BatchNorm (bf16 dense 1x1): ``x`` holds y and the conv
+    consumes relu(y*scale + bias), the normalised tensor is never written."""
     sh, sw = (stride, 0) if isinstance(stride, int) else (stride[0], stride[1])
     ph, pw = _pads(pad)
     if use_native(x):
         s1, s2 = slabs if slabs is not None else (None, None)
+        isc, ibi = in_bn if in_bn is not None else (None, None)
         return native().conv_fwd(x, w, sh, ph, stats_shift, s1, s2, bias, relu, sw, pw,
-                                 wflip=wflip)
+                                 wflip=wflip, in_scale=isc, in_bias=ibi)
+    if in_bn is not None:
+        x = _ref.bn_relu_fold(x, *in_bn)
     y, a, b = _ref.conv_fwd(x, w, stride if isinstance(stride, int) else tuple(stride),
                             pad if isinstance(pad, int) else tuple(pad), stats_shift)
     if bias is not None or relu:
@@ -106,21 +111,25 @@ def bn_bwd_collect(rep, C, acc=None):
     return native().bn_bwd_collect(rep, C, *a)
 
 
-def conv_wgrad(dy, x, kh, kw, stride, pad, out=None, collect=None):
+def conv_wgrad(dy, x, kh, kw, stride, pad, out=None, collect=None, in_bn=None):
     """``out``: accumulate into this fp32 [Co,KH,KW,Ci] buffer (the parameter's flat gradient).
     ``stride``: int or (vertical, horizontal).  ``collect = (rep, out2, dgamma, dbeta[, True,
     dgamma2, dbeta2])`` (native): one block of the launch also does :func:`bn_bwd_collect` of
     ``rep`` into ``out2`` [2, C] (Σg, Σg·x̂; dgamma / dbeta accumulators or None) — the slab a
-    fused dgrad just filled; the 7-tuple form also collects Σg·x̂₂ (out2 [3, C])."""
+    fused dgrad just filled; the 7-tuple form also collects Σg·x̂₂ (out2 [3, C]).
+    ``in_bn``: folded input BatchNorm (see :func:`conv_fwd`)."""
     sh, sw = (stride, 0) if isinstance(stride, int) else (stride[0], stride[1])
     if use_native(dy):
         ph, pw = _pads(pad)
         c = tuple(collect) if collect is not None else (None, None, None, None)
         if len(c) == 4:
             c = c + (False, None, None)
-        return native().conv_wgrad(dy, x, kh, kw, sh, ph, out, sw, pw, -1, *c)
+        isc, ibi = in_bn if in_bn is not None else (None, None)
+        return native().conv_wgrad(dy, x, kh, kw, sh, ph, out, sw, pw, -1, *c, isc, ibi)
     if collect is not None:
         raise RuntimeError("collect-in-wgrad is a native-kernel path")
+    if in_bn is not None:
+        x = _ref.bn_relu_fold(x, *in_bn)
     dw = _ref.conv_wgrad(dy, x, kh, kw, stride if isinstance(stride, int) else tuple(stride),
                          pad if isinstance(pad, int) else tuple(pad))
     if out is not None:
