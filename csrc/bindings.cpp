@@ -1565,17 +1565,43 @@ Tensor colsum(Tensor x, optional<Tensor> out, bool two_pass) {
   return o;
 }
 
-Tensor stem_pack(Tensor x, int64_t pad, int64_t Hp, int64_t Wsp, at::ScalarType dtype) {
+std::tuple<Tensor, optional<Tensor>> stem_pack(Tensor x, int64_t pad, int64_t Hp, int64_t Wsp,
+                                               at::ScalarType dtype, optional<Tensor> w) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
   TORCH_CHECK(x.dim() == 4 && x.size(1) <= 4, "stem_pack expects NCHW with C <= 4");
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x dtype");
   TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "stem_pack produces bf16 / fp32");
   auto y = torch::empty({x.size(0), Hp, Wsp, 8}, x.options().dtype(dtype));
+  optional<Tensor> wp;
+  long ws[4] = {0, 0, 0, 0};
+  if (w.has_value()) {  // the stem filter packed by the same launch
+    // (any strides: the parameter is channels_last)
+    TORCH_CHECK(w->is_cuda() && w->scalar_type() == at::kFloat && w->device() == x.device(),
+                "stem filter: fp32 on x's device");
+    TORCH_CHECK(w->dim() == 4 && w->size(1) == x.size(1) && w->size(2) == w->size(3),
+                "stem filter must be [Co, C, K, K]");
+    for (int d = 0; d < 4; ++d) ws[d] = (long)w->stride(d);
+    wp = torch::empty({w->size(0), w->size(2), (w->size(3) + 1) / 2, 8}, x.options().dtype(dtype));
+  }
   mipipe::stem_pack(x.data_ptr(), x.scalar_type() == at::kBFloat16, y.data_ptr(), (int)x.size(0),
                     (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)pad, (int)Hp, (int)Wsp,
-                    stream(), dtype == at::kFloat);
-  return y;
+                    stream(), dtype == at::kFloat, w.has_value() ? w->data_ptr<float>() : nullptr,
+                    wp.has_value() ? wp->data_ptr() : nullptr,
+                    w.has_value() ? (int)w->size(0) : 0, w.has_value() ? (int)w->size(2) : 0, ws);
+  return {y, wp};
+}
+
+void stem_wgrad_unpack(Tensor dwp, Tensor g) {
+  check_f32(dwp, "dwp");
+  TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat && g.dim() == 4, "g: fp32 [Co,C,K,K]");
+  c10::DeviceGuard dg(g.device());
+  const int Co = (int)g.size(0), C = (int)g.size(1), K = (int)g.size(2);
+  TORCH_CHECK(C <= 4 && g.size(3) == K && dwp.numel() == (int64_t)Co * K * ((K + 1) / 2) * 8,
+              "dwp must be the packed [Co, K, ceil(K/2), 8] stem filter gradient");
+  long gs[4];
+  for (int d = 0; d < 4; ++d) gs[d] = (long)g.stride(d);
+  mipipe::stem_wgrad_unpack(dwp.data_ptr<float>(), g.data_ptr<float>(), Co, C, K, gs, stream());
 }
 
 void check_attn(const Tensor& qkv, int64_t B, int64_t S, int64_t H) {
@@ -2036,7 +2062,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("dropout_fwd", &dropout_fwd, py::arg("x"), py::arg("p"), py::arg("seed"),
         py::arg("seed_dev") = py::none());
   m.def("stem_pack", &stem_pack, py::arg("x"), py::arg("pad"), py::arg("Hp"), py::arg("Wsp"),
-        py::arg("dtype") = at::kBFloat16);
+        py::arg("dtype") = at::kBFloat16, py::arg("w") = py::none());
+  m.def("stem_wgrad_unpack", &stem_wgrad_unpack, py::arg("dwp"), py::arg("g"));
   m.def("top1_correct", &top1_correct, py::arg("logits"), py::arg("labels"),
         py::arg("out") = py::none());
   m.def("set_splitk_target", [](int v) { mipipe::g_splitk_target = std::max(1, v); });

@@ -353,8 +353,14 @@ void nchw_to_nhwc(const void* x, bool x_is_bf16, void* y, int N, int C, int H, i
 // outside), h' < Hp, j < Wsp.  A KxK stride-2 conv on x becomes a K x ceil(K/2) conv with
 // vertical stride 2 and horizontal stride 1 on 8-channel super-pixels: 16-byte operand rows with
 // 3 of 8 lanes padding instead of 5 of 8 (the reduction shrinks from K*K*8 to K*ceil(K/2)*8).
+// w (fp32 [Co][C][K][K], strides ws[4]) given: the same launch also writes the packed filter
+// wp [Co][K][ceil(K/2)][8] in y's dtype.
 void stem_pack(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int pad,
-               int Hp, int Wsp, hipStream_t st, bool y_f32 = false);
+               int Hp, int Wsp, hipStream_t st, bool y_f32 = false, const float* w = nullptr,
+               void* wp = nullptr, int Co = 0, int K = 0, const long* ws = nullptr);
+// g[co][c][kh][kw] (strides gs[4]) += dwp[co][kh][kw/2][(kw%2)*4 + c] (packed stem filter grad)
+void stem_wgrad_unpack(const float* dwp, float* g, int Co, int C, int K, const long* gs,
+                       hipStream_t st);
 void synthetic_batch(const int64_t* idx, int n, int C, int H, int W, int classes, int seed,
                      void* x, bool bf16_out, int64_t* labels, hipStream_t st);
 // Fused ResNet stem on the packed input (stem.hip): conv 7x7/2 (packed K = 224, 64 channels,

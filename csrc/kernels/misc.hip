@@ -1238,10 +1238,36 @@ void dropout_fwd(const void* x, void* y, long n, float p, uint32_t seed, hipStre
 
 // ------------------------------------------------------------------------------ stem packing
 // One thread per output super-pixel: 2 horizontally adjacent padded pixels x 4 channels.
+// The same launch also packs the stem FILTER (w != nullptr): wp[co][kh][j][p*4 + c] =
+// w[co][c][kh][2j + p] (zero for kw = 7 and c >= C), from the fp32 parameter with any strides
+// (channels_last), in the activation dtype — the work of a zero-fill, a strided copy and a cast
+// in separate launches.
+struct StemWPack {
+  const float* w = nullptr;
+  void* wp = nullptr;
+  int Co = 0, K = 0;
+  long s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+};
+template <class T>
+__device__ void stem_wpack(const StemWPack& k, int C) {
+  const int K2 = (k.K + 1) / 2;
+  const long total = (long)k.Co * k.K * K2 * 8;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long)gridDim.x * blockDim.x) {
+    const int q = (int)(t % 8), j = (int)((t / 8) % K2), kh = (int)((t / 8 / K2) % k.K);
+    const int co = (int)(t / 8 / K2 / k.K);
+    const int p = q / 4, c = q % 4, kw = 2 * j + p;
+    const float v = (kw < k.K && c < C) ? k.w[co * k.s0 + c * k.s1 + kh * k.s2 + kw * k.s3] : 0.f;
+    reinterpret_cast<T*>(k.wp)[t] = from_f32<T>(v);
+  }
+}
+
 template <bool IN_BF16, class T>
 __global__ __launch_bounds__(256) void stem_pack_kernel(const void* __restrict__ xin,
                                                         T* __restrict__ y, int N, int C,
-                                                        int H, int W, int pad, int Hp, int Wsp) {
+                                                        int H, int W, int pad, int Hp, int Wsp,
+                                                        StemWPack wk) {
+  if (wk.w != nullptr) stem_wpack<T>(wk, C);
   const long total = (long)N * Hp * Wsp;
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (long)gridDim.x * blockDim.x) {
@@ -1275,16 +1301,47 @@ __global__ __launch_bounds__(256) void stem_pack_kernel(const void* __restrict__
 }
 
 void stem_pack(const void* x, bool x_is_bf16, void* y, int N, int C, int H, int W, int pad,
-               int Hp, int Wsp, hipStream_t st, bool y_f32) {
+               int Hp, int Wsp, hipStream_t st, bool y_f32, const float* w, void* wp, int Co,
+               int K, const long* ws) {
   const long total = (long)N * Hp * Wsp;
   dim3 g(grid1d(total));
-  if (y_f32) {
-    if (x_is_bf16) hipLaunchKernelGGL((stem_pack_kernel<true, float>), g, dim3(256), 0, st, x, (float*)y, N, C, H, W, pad, Hp, Wsp);
-    else hipLaunchKernelGGL((stem_pack_kernel<false, float>), g, dim3(256), 0, st, x, (float*)y, N, C, H, W, pad, Hp, Wsp);
-  } else {
-    if (x_is_bf16) hipLaunchKernelGGL((stem_pack_kernel<true, __bf16>), g, dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, pad, Hp, Wsp);
-    else hipLaunchKernelGGL((stem_pack_kernel<false, __bf16>), g, dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, pad, Hp, Wsp);
+  StemWPack wk;
+  if (w != nullptr) {
+    wk.w = w; wk.wp = wp; wk.Co = Co; wk.K = K;
+    wk.s0 = ws[0]; wk.s1 = ws[1]; wk.s2 = ws[2]; wk.s3 = ws[3];
   }
+  if (y_f32) {
+    if (x_is_bf16) hipLaunchKernelGGL((stem_pack_kernel<true, float>), g, dim3(256), 0, st, x, (float*)y, N, C, H, W, pad, Hp, Wsp, wk);
+    else hipLaunchKernelGGL((stem_pack_kernel<false, float>), g, dim3(256), 0, st, x, (float*)y, N, C, H, W, pad, Hp, Wsp, wk);
+  } else {
+    if (x_is_bf16) hipLaunchKernelGGL((stem_pack_kernel<true, __bf16>), g, dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, pad, Hp, Wsp, wk);
+    else hipLaunchKernelGGL((stem_pack_kernel<false, __bf16>), g, dim3(256), 0, st, x, (__bf16*)y, N, C, H, W, pad, Hp, Wsp, wk);
+  }
+}
+
+// Stem filter gradient, kernel layout [Co][K][K2][8] -> ACCUMULATED into the parameter's
+// gradient [Co][C][K][K] (any strides: the flat DDP bucket view), one launch instead of a
+// strided copy + autograd's accumulate.
+__global__ __launch_bounds__(256) void stem_wgrad_unpack_kernel(const float* __restrict__ dwp,
+                                                                float* __restrict__ g, int Co,
+                                                                int C, int K, long s0, long s1,
+                                                                long s2, long s3) {
+  const int K2 = (K + 1) / 2;
+  const long total = (long)Co * C * K * K;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long)gridDim.x * blockDim.x) {
+    const int kw = (int)(t % K), kh = (int)((t / K) % K), c = (int)((t / K / K) % C);
+    const int co = (int)(t / K / K / C);
+    const float v = dwp[(((long)co * K + kh) * K2 + kw / 2) * 8 + (kw % 2) * 4 + c];
+    g[co * s0 + c * s1 + kh * s2 + kw * s3] += v;
+  }
+}
+
+void stem_wgrad_unpack(const float* dwp, float* g, int Co, int C, int K, const long* gs,
+                       hipStream_t st) {
+  const long total = (long)Co * C * K * K;
+  hipLaunchKernelGGL(stem_wgrad_unpack_kernel, dim3(grid1d(total)), dim3(256), 0, st, dwp, g, Co,
+                     C, K, gs[0], gs[1], gs[2], gs[3]);
 }
 
 }  // namespace mipipe

@@ -120,9 +120,18 @@ class _StemConv(mnn.Conv2d):
 
     def pack_input(self, x: torch.Tensor, dtype) -> torch.Tensor:
         _, _, Hp, Wsp = self.packed_geometry(x.shape[2], x.shape[3])
+        w = self.weight.detach()
+        if K.use_native(x) and w.is_cuda and w.dtype == torch.float32:
+            # the packing launch also packs this step's filter (consumed once by compute_weight)
+            xp, wp = K.stem_pack(x, dtype, self.padding[0], Hp, Wsp, w=w)
+            self.__dict__["_mipipe_wpack"] = wp
+            return xp
         return K.stem_pack(x, dtype, self.padding[0], Hp, Wsp)
 
     def compute_weight(self, dtype):
+        wp = self.__dict__.pop("_mipipe_wpack", None)
+        if wp is not None and wp.dtype == dtype:
+            return wp
         w = self.weight.detach()
         Co, C, k, _ = w.shape
         kw2 = (k + 1) // 2
@@ -139,6 +148,13 @@ class _StemConv(mnn.Conv2d):
                 Co = dw.shape[0]
                 d = dw.reshape(Co, k, -1, 4)[:, :, :k, :C]
                 return d.permute(0, 3, 1, 2).contiguous()
+
+            def unpack_into(dw, g):  # native: accumulate straight into g (the flat grad view)
+                if dw.is_cuda and dw.dtype == torch.float32 and g.dtype == torch.float32:
+                    K.stem_wgrad_unpack(dw.contiguous(), g)
+                    return True
+                return False
+            unpack.accumulate_into = unpack_into
             self.weight._mipipe_wgrad_map = unpack
 
     def forward(self, x, stats_shift=None, slabs=None, prev=None, res_take=None, res_give=None):

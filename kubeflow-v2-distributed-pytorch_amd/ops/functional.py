@@ -85,6 +85,18 @@ def _direct_grad_target(p: Tensor, rows: Optional[int] = None):
     return fs, g
 
 
+def _wgrad_map_into_grad(wmap, dw, weight):
+    """A kernel-layout weight gradient (packed stem filter) for ``weight``: accumulated straight
+    into its flat-buffer gradient by one native launch when the map supports it (returns None:
+    nothing left for autograd to add), else mapped to the parameter layout and returned."""
+    acc = getattr(wmap, "accumulate_into", None)
+    tgt = _direct_grad_target(weight) if acc is not None else None
+    if tgt is not None and acc(dw, tgt[1]):
+        tgt[0].grad_ready(weight)
+        return None
+    return wmap(dw).to(weight.dtype)
+
+
 class ResidualSlot:
     """Hands a block input's second gradient (identity / downsample path) to the conv that
     also consumes that input, so its dgrad epilogue adds it (no separate elementwise add).
@@ -347,7 +359,7 @@ class _ConvFn(Function):
                     full[:, kh0:kh1, kw0:kw1, :] = dw
                     dw = full
                 if ctx.wmap is not None:  # kernel layout -> parameter layout (packed stem)
-                    dw = ctx.wmap(dw)
+                    dw = _wgrad_map_into_grad(ctx.wmap, dw, weight)
                 else:
                     if dw.shape[-1] != ci:  # input channels were zero-padded for the kernel
                         dw = dw[..., :ci]
@@ -927,7 +939,7 @@ class _StemFusedFn(Function):
         _ws_done(bn, "bwd")
         dw = None
         if ctx.needs_input_grad[1]:
-            dw = ctx.weight._mipipe_wgrad_map(dwp).to(ctx.weight.dtype)
+            dw = _wgrad_map_into_grad(ctx.weight._mipipe_wgrad_map, dwp, ctx.weight)
         if direct is not None:
             fs = _direct_grad_target(gamma)[0]
             fs.grad_ready(gamma)

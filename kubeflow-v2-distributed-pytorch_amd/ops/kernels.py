@@ -232,6 +232,11 @@ def stem_fused_supported(xp, w) -> bool:
     return use_native(xp) and bool(native().stem_fused_supported(xp, w))
 
 
+def stem_wgrad_unpack(dwp, g) -> None:
+    """g[co][c][kh][kw] += dwp[co][kh][kw // 2][(kw % 2) * 4 + c] (native; g fp32, any strides)."""
+    native().stem_wgrad_unpack(dwp, g)
+
+
 def stem_fwd_stats(xp, w, shift, slab_sum, slab_sq):
     """Shifted Σ, Σ² of the packed stem conv's bf16 output into zeroed replica slabs [R, 64]
     (native; the conv output is recomputed, not stored)."""
@@ -533,11 +538,16 @@ def gelu_bwd_colsum(dy, x, bias):
     return dx
 
 
-def stem_pack(x, dtype, pad: int, Hp: int, Wsp: int):
+def stem_pack(x, dtype, pad: int, Hp: int, Wsp: int, w=None):
     """NCHW image (C <= 4) -> bf16/``dtype`` super-pixels [N, Hp, Wsp, 8]: channel p*4 + c of
-    super-pixel (h', j) is x[c, h'-pad, 2j+p-pad] (zero outside the image)."""
+    super-pixel (h', j) is x[c, h'-pad, 2j+p-pad] (zero outside the image).  ``w`` (native, fp32
+    [Co, C, K, K]): the same launch also packs the filter -> returns (x_packed, w_packed
+    [Co, K, ceil(K/2), 8]) with w_packed[co][kh][j][p*4 + c] = w[co][c][kh][2j + p]."""
     if use_native(x) and dtype in (torch.bfloat16, torch.float32):
-        return native().stem_pack(x.contiguous(), pad, Hp, Wsp, dtype)
+        y, wp = native().stem_pack(x.contiguous(), pad, Hp, Wsp, dtype, w)
+        return (y, wp) if w is not None else y
+    if w is not None:
+        raise RuntimeError("stem_pack with the filter is a native-kernel path")
     N, C, H, W = x.shape
     P = x.new_zeros(N, 4, Hp, 2 * Wsp, dtype=torch.float64 if x.dtype == torch.float64 else torch.float32)
     hh, ww = min(H, Hp - pad), min(W, 2 * Wsp - pad)

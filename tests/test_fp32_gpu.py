@@ -233,8 +233,8 @@ def test_layout_kernels_fp32():
     y = native().nchw_to_nhwc(x, torch.float32, 8)
     assert y.dtype == torch.float32 and torch.equal(y[..., :3], x.permute(0, 2, 3, 1))
     assert torch.count_nonzero(y[..., 3:]) == 0
-    p = native().stem_pack(x, 3, 37, 19, torch.float32)
-    pb = native().stem_pack(x, 3, 37, 19, torch.bfloat16)
+    p = native().stem_pack(x, 3, 37, 19, torch.float32)[0]
+    pb = native().stem_pack(x, 3, 37, 19, torch.bfloat16)[0]
     assert p.dtype == torch.float32 and rel_err(p, pb.float()) < 1e-2
 
 

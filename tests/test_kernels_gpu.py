@@ -633,7 +633,15 @@ def test_stem_superpixel_conv_matches_direct():
     assert xp.shape == (N, Hp, Wsp, 8)
     xr = Kx.stem_pack(x.cpu(), torch.float32, 3, Hp, Wsp)
     assert torch.equal(xp.float().cpu(), xr.to(torch.bfloat16).float())
-    wk = conv.compute_weight(torch.bfloat16)
+    wk = conv.compute_weight(torch.bfloat16)  # packed by the pack_input launch
+    assert torch.equal(wk, conv.compute_weight(torch.bfloat16))  # == the torch-built packing
+    # the packed filter gradient accumulates straight into a strided (channels_last) gradient
+    conv._ensure_wgrad_map()
+    dwp = torch.randn(64, 7, 4, 8, device=dev)
+    g0 = torch.randn(64, 3, 7, 7, device=dev).to(memory_format=torch.channels_last)
+    g = g0.clone()
+    assert conv.weight._mipipe_wgrad_map.accumulate_into(dwp, g)
+    assert torch.equal(g, g0 + conv.weight._mipipe_wgrad_map(dwp))
     y, _, _ = native().conv_fwd(xp, wk, 2, 0, None, None, None, None, False, 1)
     ref = torch.nn.functional.conv2d(x.to(torch.bfloat16).float(),
                                      conv.weight.detach().to(torch.bfloat16).float(), stride=2,
@@ -801,7 +809,9 @@ def test_tile_benchmark_mode_picks_and_caches():
         w = bf(256, 3, 3, 256, scale=1 / 48)
         y, _, _ = C.conv_fwd(x, w, 1, 1)
         tab = C.tune_table()
-        assert len(tab) == 1 and 0 <= next(iter(tab.values())) < C.CONV_TILE_CONFIGS
+        # a plan: tile id + 16 x split-K count (split plans are candidates for small grids)
+        plan = next(iter(tab.values()))
+        assert len(tab) == 1 and 0 <= plan % 16 < C.CONV_TILE_CONFIGS and plan // 16 <= 8
         y2, _, _ = C.conv_fwd(x, w, 1, 1)
         assert torch.equal(y, y2) and len(C.tune_table()) == 1
     finally:
