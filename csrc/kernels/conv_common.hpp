@@ -81,8 +81,9 @@ constexpr bool tile_ok_for(int cfg) {
 
 template <class T, class C>
 constexpr int main_lds_bytes() {
-  return std::is_same<T, float>::value ? 3 * (C::BM + C::BN) * BK * 2  // split-bf16x3 images
-                                       : C::NS * (C::BM + C::BN) * BK * 2;
+  return std::is_same<T, float>::value  // split-bf16x3 images, one or two stages
+             ? f32_stages<C::BM, C::BN>() * 3 * (C::BM + C::BN) * BK * 2
+             : C::NS * (C::BM + C::BN) * BK * 2;
 }
 template <class T, class C>
 constexpr int lds_bytes_out() {
@@ -186,6 +187,8 @@ template <class T, class C>
 constexpr int conv_occ() {
   // (asking 5-6 blocks of the single-stage half-size tiles 9/10 spills: they need ~100 VGPRs)
   // (8-wave tiles: one block per CU, two for the 64 KB 128x128 ping-pong tile)
+  // (two-stage fp32 tiles: 144 KB of LDS, one block per CU -> the register budget of one)
+  if (std::is_same<T, float>::value && f32_stages<C::BM, C::BN>() == 2) return 1;
   return C::NW == 8 ? (C::BM * C::BN <= 128 * 128 ? 2 : 1)
                     : ((C::NS == 1 && !std::is_same<T, float>::value) ? 3 : 2);
 }

@@ -1126,18 +1126,25 @@ struct MainLoop {
 // error (~1e-7 relative; measured against float64 in tests/test_fp32_gpu.py) at 1/6 of the bf16
 // MFMA rate — still ~2.6x the v_mfma_f32_16x16x4_f32 peak.  (A two-part split would lose 8 bits
 // per operand: ~1e-5 errors, enough to flip near-zero ReLU decisions the float64 model makes.)
-// One LDS stage: the register prefetch of step k+1 is what overlaps global latency with step
-// k's MFMAs.
-template <int BM, int BN, class OpA, class OpB, int WM = 2, int WN = 2>
+// STAGES = 1: one LDS stage; the register prefetch of step k+1 overlaps global latency with
+// step k's MFMAs, and the split + store of k+1 waits behind a barrier for every wave to finish
+// reading step k (two barriers per k-step, the split VALU never beside the MFMAs).
+// STAGES = 2 (tiles with BM + BN <= 192: 144 KB of images, one block per CU): two image sets;
+// registers hold steps k+1 and k+2, and the split + store of step k+1 into the OTHER stage
+// follows step k's MFMAs in the same basic block (independent: the scheduler interleaves the
+// split VALU with the MFMAs), one barrier per k-step.
+template <int BM, int BN, class OpA, class OpB, int WM = 2, int WN = 2, int STAGES = 1>
 struct MainLoopF32 {
   static_assert(!HasXform<OpA>::value && !HasXform<OpB>::value, "folded BN: bf16 loops only");
+  static_assert(STAGES == 1 || STAGES == 2, "fp32 loop stages");
   static constexpr int MT = BM / WM / 16;
   static constexpr int NT = BN / WN / 16;
   static constexpr int PARTS = 3;
   static constexpr int A_BYTES = BM * BK * 2;
   static constexpr int B_BYTES = BN * BK * 2;
   static constexpr int IMG_BYTES = A_BYTES + B_BYTES;      // one part's image (A | B)
-  static constexpr int LDS_BYTES = PARTS * IMG_BYTES;      // part 0 | part 1 | part 2
+  static constexpr int STAGE_BYTES = PARTS * IMG_BYTES;    // part 0 | part 1 | part 2
+  static constexpr int LDS_BYTES = STAGES * STAGE_BYTES;
   struct Regs {
     float4 a[OpA::NI][2];
     float4 b[OpB::NI][2];
@@ -1187,6 +1194,50 @@ struct MainLoopF32 {
       split_store(smem + A_BYTES + (wave * OpB::NI + i) * 1024 + lane * 16, r.b[i]);
   }
 
+  // fragments + the 6 MFMAs per 16x16x32 tile of the stage at `img` (both k-substeps)
+  __device__ static void mfmas(const char* img, f32x4 (&acc)[MT][NT], uint32_t arow0,
+                               uint32_t bcol0, int lane) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[PARTS][MT], bfr[PARTS][NT];
+#pragma unroll
+      for (int p = 0; p < PARTS; ++p) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          af[p][i] = FragLoader<OpA::KC, BM>::load(img + p * IMG_BYTES, arow0 + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          bfr[p][j] = FragLoader<OpB::KC, BN>::load(img + p * IMG_BYTES + A_BYTES,
+                                                    bcol0 + j * 16, ks, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          f32x4 c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[2][j], af[0][i], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[2][i], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[0][i], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[1][i], c, 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[0][i], c, 0, 0, 0);
+        }
+    }
+  }
+
+  // STAGES = 2, step k (stage CUR): registers r[CUR] held step k (already in LDS) and take step
+  // k+2 now; step k's MFMAs; then step k+1 (registers r[1-CUR], loaded one step ago) is split
+  // into the other stage; one barrier.
+  template <int CUR>
+  __device__ static void step2(char* smem, Regs (&r)[2], OpA& a, OpB& b, int kt, int kt1,
+                               f32x4 (&acc)[MT][NT], uint32_t arow0, uint32_t bcol0, int wave,
+                               int lane) {
+    if (kt + 2 < kt1) load(r[CUR], a, b, kt + 2);
+    mfmas(smem + CUR * STAGE_BYTES, acc, arow0, bcol0, lane);
+    if (kt + 1 < kt1) store(smem + (1 - CUR) * STAGE_BYTES, r[1 - CUR], wave, lane);
+    __syncthreads();  // stage 1-CUR written; every wave done reading stage CUR
+  }
+
   __device__ static void run(char* smem, OpA& a, OpB& b, int kt0, int kt1,
                              f32x4 (&acc)[MT][NT], int wave, int lane) {
 #pragma unroll
@@ -1196,6 +1247,18 @@ struct MainLoopF32 {
     if (kt0 >= kt1) return;
     const int wr = wave / WN, wc = wave % WN;
     const uint32_t arow0 = wr * (BM / WM), bcol0 = wc * (BN / WN);
+    if constexpr (STAGES == 2) {
+      Regs r[2];
+      load(r[0], a, b, kt0);
+      if (kt0 + 1 < kt1) load(r[1], a, b, kt0 + 1);
+      store(smem, r[0], wave, lane);
+      __syncthreads();
+      for (int kt = kt0; kt < kt1; kt += 2) {  // unrolled by two: the register sets stay static
+        step2<0>(smem, r, a, b, kt, kt1, acc, arow0, bcol0, wave, lane);
+        if (kt + 1 < kt1) step2<1>(smem, r, a, b, kt + 1, kt1, acc, arow0, bcol0, wave, lane);
+      }
+      return;  // (the last step's barrier: every wave is done reading before the epilogue)
+    }
     Regs r;
     load(r, a, b, kt0);
     store(smem, r, wave, lane);
@@ -1203,32 +1266,7 @@ struct MainLoopF32 {
     for (int kt = kt0; kt < kt1; ++kt) {
       const bool more = kt + 1 < kt1;
       if (more) load(r, a, b, kt + 1);  // in flight under this step's MFMAs
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 af[PARTS][MT], bfr[PARTS][NT];
-#pragma unroll
-        for (int p = 0; p < PARTS; ++p) {
-#pragma unroll
-          for (int i = 0; i < MT; ++i)
-            af[p][i] = FragLoader<OpA::KC, BM>::load(smem + p * IMG_BYTES, arow0 + i * 16, ks, lane);
-#pragma unroll
-          for (int j = 0; j < NT; ++j)
-            bfr[p][j] = FragLoader<OpB::KC, BN>::load(smem + p * IMG_BYTES + A_BYTES,
-                                                      bcol0 + j * 16, ks, lane);
-        }
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-          for (int j = 0; j < NT; ++j) {
-            f32x4 c = acc[i][j];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[2][j], af[0][i], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[2][i], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[0][i], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[1][i], c, 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[0][i], c, 0, 0, 0);
-          }
-      }
+      mfmas(smem, acc, arow0, bcol0, lane);
       if (more) {
         __syncthreads();  // every wave is done reading this step's images
         store(smem, r, wave, lane);
@@ -1239,6 +1277,18 @@ struct MainLoopF32 {
   }
 };
 
+// Two fp32 image stages (-DMIPIPE_F32_TWO_STAGE; tiles with BM + BN <= 192) measured SLOWER on
+// the reference config: 291k vs 339k img/s, the 128x64 forwards 1,173 vs 883 us per step — one
+// block per CU interleaving split VALU and MFMAs inside each wave loses to two single-stage
+// blocks per CU interleaving them across blocks (profiles/r6_f32_two_stage_negative.txt).
+#ifdef MIPIPE_F32_TWO_STAGE
+constexpr bool kF32TwoStage = true;
+#else
+constexpr bool kF32TwoStage = false;
+#endif
+template <int BM, int BN>
+constexpr int f32_stages() { return (kF32TwoStage && BM + BN <= 192) ? 2 : 1; }
+
 // Selects the main loop for the operand element type.
 template <class T, int BM, int BN, class OpA, class OpB, int NS = 2, int WM = 2, int WN = 2,
           int V = kLoopDefault>
@@ -1248,8 +1298,8 @@ struct MainLoopFor {
 };
 template <int BM, int BN, class OpA, class OpB, int NS, int WM, int WN, int V>
 struct MainLoopFor<float, BM, BN, OpA, OpB, NS, WM, WN, V> {
-  typedef MainLoopF32<BM, BN, OpA, OpB, WM, WN> type;
-  static constexpr int LDS_BYTES = MainLoopF32<BM, BN, OpA, OpB, WM, WN>::LDS_BYTES;
+  typedef MainLoopF32<BM, BN, OpA, OpB, WM, WN, f32_stages<BM, BN>()> type;
+  static constexpr int LDS_BYTES = type::LDS_BYTES;
 };
 
 // Row/col of acc element: lane holds C[m][n + e], e = 0..3, for tile (i, j):
