@@ -252,57 +252,58 @@ __device__ __forceinline__ bf16x8 bn_relu_frag(bf16x8 v, const float (&sc)[8], c
 
 // A operand of a dense 1x1 conv whose input is relu(bn(y)) (x = y in memory): k = input
 // channel.  The per-channel (scale, bias) pairs sit in an LDS table the kernel fills before the
-// main loop (tab: float2 per channel, zeros past K so padded channels stay 0); a lane's fragment
-// covers channels kt*64 + ks*32 + 8*(lane>>4) .. +7: four ds_read_b128 per k-substep.
+// main loop (tab: float2 per channel, zeros past K so padded channels stay 0).  Each k-step's
+// landed A image is transformed IN PLACE once per block (xform_lds), before any wave reads a
+// fragment: a thread owns one 8-channel chunk slot (t & 7) for every row it visits, so its 16
+// coefficients are four ds_read_b128 per k-step, and each element is transformed once per block
+// (a per-fragment transform redid it in every wave that reads the fragment, in front of the
+// MFMAs: profiles/r6_bn_fold_negative.txt).
 template <int R, class T = __bf16, int NW = 4>
 struct KCDenseBufBN : KCDenseBuf<R, T, NW> {
   static constexpr bool XFORM = true;
   const char* tab;
-  __device__ void xform(bf16x8& f, int kt, int ks, int lane) const {
-    const uint32_t c0 = (uint32_t)kt * BK + (uint32_t)ks * 32 + ((uint32_t)lane >> 4) * 8;
-    const float4* t = reinterpret_cast<const float4*>(tab + c0 * 8);
+  __device__ void xform_lds(char* img, int kt, int tid, int nthreads) const {
+    const uint32_t c = (uint32_t)tid & 7u;
+    const float4* t = reinterpret_cast<const float4*>(tab + ((uint32_t)kt * BK + c * 8) * 8);
     const float4 t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3];
     const float sc[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
     const float bi[8] = {t0.y, t0.w, t1.y, t1.w, t2.y, t2.w, t3.y, t3.w};
-    f = bn_relu_frag(f, sc, bi);
+    for (uint32_t r = (uint32_t)tid >> 3; r < (uint32_t)R; r += (uint32_t)nthreads >> 3) {
+      bf16x8* p = reinterpret_cast<bf16x8*>(img + kc_off(r, c));
+      *p = bn_relu_frag(*p, sc, bi);
+    }
   }
 };
 
 // B operand of a dense 1x1 conv's weight-grad whose input was relu(bn(y)): B(k = pixel, n =
-// input channel) = y (MN-contiguous).  A lane's fragment is 8 consecutive pixels of ONE column
-// (col0 + (lane & 15)), so its (scale, bias) is fixed for the whole k-loop: one register pair per
-// fragment column, loaded by xform_setup.  The tail k-step (K % 64 != 0) zeroes pixels past K
-// after the transform (the range check reads zeros, which would become relu(bias)).
+// input channel) = y (MN-contiguous image [64 k][W cols]).  Transformed in place once per block
+// and k-step like KCDenseBufBN: a thread owns one 8-column chunk (t % (W/8)) — its 16
+// coefficients are loaded once per tile (xform_setup) — and visits rows t / (W/8), +nthreads/(W/8)...
+// Rows past K (the tail k-step) stay the range check's zeros (relu(bias) otherwise).
 template <int W, class T = __bf16, int NW = 4>
 struct MCDenseBufBN : MCDenseBuf<W, T, NW> {
   static constexpr bool XFORM = true;
-  static constexpr int NJ = 8;  // fragment columns per wave supported (BN / WN / 16)
+  static constexpr int CPR = W / 8;  // 8-column chunks per image row
   const float* g_sc;
   const float* g_bi;
   uint32_t origin, ncols;
-  float sc[NJ], bi[NJ];
-  __device__ void xform_setup(uint32_t col0, int nt, int lane) {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const uint32_t n = origin + col0 + (uint32_t)j * 16 + ((uint32_t)lane & 15);
-      const bool ok = j < nt && n < ncols;
-      sc[j] = ok ? g_sc[n] : 0.f;
-      bi[j] = ok ? g_bi[n] : 0.f;
-    }
-  }
-  __device__ void xform(bf16x8& f, int kt, int ks, int lane, int j) const {
-    float s8[8], b8[8];
+  float sc[8], bi[8];
+  __device__ void xform_setup(int tid) {
+    const uint32_t n0 = origin + ((uint32_t)tid % CPR) * 8;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      s8[q] = sc[j];
-      b8[q] = bi[j];
+      const bool ok = n0 + q < ncols;
+      sc[q] = ok ? g_sc[n0 + q] : 0.f;
+      bi[q] = ok ? g_bi[n0 + q] : 0.f;
     }
-    f = bn_relu_frag(f, s8, b8);
-    if (kt == this->kt_tail) {  // wave-uniform: the one k-step whose rows may pass K
-      const uint32_t k0 = (uint32_t)kt * BK + (uint32_t)ks * 32 + ((uint32_t)lane >> 4) * 8;
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (k0 + (uint32_t)q >= this->K) f[q] = (__bf16)0.0f;
+  }
+  __device__ void xform_lds(char* img, int kt, int tid, int nthreads) const {
+    const uint32_t cc = (uint32_t)tid % CPR;
+    uint32_t rows = (uint32_t)BK;
+    if (kt == this->kt_tail) rows = this->K - (uint32_t)kt * BK;  // wave-uniform
+    for (uint32_t r = (uint32_t)tid / CPR; r < rows; r += (uint32_t)nthreads / CPR) {
+      bf16x8* p = reinterpret_cast<bf16x8*>(img + mc_off<W>(r, cc));
+      *p = bn_relu_frag(*p, sc, bi);
     }
   }
 };
@@ -952,23 +953,14 @@ struct MainLoop {
   // (nbuf != nullptr) are issued between MFMA groups instead of in one burst before them.
   // FIRST: the k-step that starts the accumulation — its first MFMA of each tile takes C = 0
   // (an inline constant) instead of 64 zeroed accumulator registers
-  // folded-BN operands (HasXform): fragments of k-step kt transformed after their LDS read
-  __device__ static void xform(bf16x8 (&af)[2][MT], bf16x8 (&bfr)[2][NT], const OpA& a,
-                               const OpB& b, int kt, int lane) {
-    if constexpr (HasXform<OpA>::value) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < MT; ++i) a.xform(af[ks][i], kt, ks, lane);
-    }
-    if constexpr (HasXform<OpB>::value) {
-      static_assert(NT <= OpB::NJ, "folded-BN B operand: fragment columns per wave");
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) b.xform(bfr[ks][j], kt, ks, lane, j);
-    }
+  // folded-BN operands (HasXform): the landed images of k-step kt transformed in place by the
+  // whole block (every thread's chunks), between the "stage landed" barrier and the fragment
+  // reads (the caller's next barrier orders the writes)
+  __device__ static void xform_pass(char* buf, const OpA& a, const OpB& b, int kt) {
+    if constexpr (HasXform<OpA>::value) a.xform_lds(buf, kt, (int)threadIdx.x, NW * 64);
+    if constexpr (HasXform<OpB>::value) b.xform_lds(buf + A_BYTES, kt, (int)threadIdx.x, NW * 64);
   }
+  static constexpr bool XF = HasXform<OpA>::value || HasXform<OpB>::value;
 
   template <bool FIRST = false>
   __device__ static void compute(const char* cbuf, f32x4 (&acc)[MT][NT], uint32_t arow0,
@@ -988,7 +980,6 @@ struct MainLoop {
       for (int j = 0; j < NT; ++j)
         bfr[ks][j] = FragLoader<OpB::KC, BN>::load(bimg, bcol0 + j * 16, ks, lane);
     }
-    xform(af, bfr, a, b, kt, lane);
     if constexpr (SPREAD) {
       if (nbuf != nullptr) {
         a.prep(nkt);
@@ -1033,7 +1024,6 @@ struct MainLoop {
       for (int j = 0; j < NT; ++j)
         bfr[ks][j] = FragLoader<OpB::KC, BN>::load(bimg, bcol0 + j * 16, ks, lane);
     }
-    xform(af, bfr, a, b, kt_next - 1, lane);  // (the A table lives outside the stage buffer)
     barrier();  // this wave's reads retired (lgkmcnt 0) and every other wave's: buffer free
     if (kt_next < kt1) stage(smem, a, b, kt_next, wave);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
@@ -1060,12 +1050,16 @@ struct MainLoop {
     }
     const int wr = wave / WN, wc = wave % WN;
     const uint32_t arow0 = wr * (BM / WM), bcol0 = wc * (BN / WN);
-    if constexpr (HasXform<OpB>::value) b.xform_setup(bcol0, NT, lane);
+    if constexpr (HasXform<OpB>::value) b.xform_setup((int)threadIdx.x);
     if constexpr (NS == 1 && (V & kLoopEarlyDma) != 0) {
       stage(smem, a, b, kt0, wave);
       for (int kt = kt0; kt < kt1; ++kt) {
         wait_vmcnt<0>();
         barrier();  // every wave's pieces of stage kt landed
+        if constexpr (XF) {
+          xform_pass(smem, a, b, kt);
+          barrier();
+        }
         if (kt == kt0) compute_then_refill<true>(smem, acc, arow0, bcol0, lane, a, b, kt + 1, kt1, wave);
         else compute_then_refill<false>(smem, acc, arow0, bcol0, lane, a, b, kt + 1, kt1, wave);
       }
@@ -1075,6 +1069,10 @@ struct MainLoop {
         stage(smem, a, b, kt, wave);
         wait_vmcnt<0>();
         __syncthreads();
+        if constexpr (XF) {
+          xform_pass(smem, a, b, kt);
+          __syncthreads();
+        }
         if (kt == kt0) compute<true>(smem, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave, kt);
         else compute(smem, acc, arow0, bcol0, lane, nullptr, a, b, 0, wave, kt);
       }
@@ -1092,6 +1090,10 @@ struct MainLoop {
           wait_vmcnt<0>();
         }
         barrier();
+        if constexpr (XF) {
+          xform_pass(smem + cur * STAGE_BYTES, a, b, kt);
+          barrier();
+        }
         const bool more = kt + NS - 1 < kt1;
         char* nb = more ? smem + nxt * STAGE_BYTES : nullptr;
         if constexpr (!SPREAD) {

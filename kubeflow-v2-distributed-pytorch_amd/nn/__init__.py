@@ -185,18 +185,24 @@ class BatchNorm2d(tnn.BatchNorm2d):
         return MF.batchnorm_act(y, st, self, relu=False)
 
 
-# Measured a net LOSS on ResNet-50 b256 (profiles/r6_bn_fold_negative.txt): the per-fragment
-# transform (28 VALU per 8 values, redone by every wave and N-tile that reads the fragment, ahead
-# of the MFMAs) costs the conv3 forwards 30-60 % and the weight-grads 5-40 %, more than the
-# bn_act_fwd pass it removes (-280 us): 12,700 vs 13,150 img/s.  Kept opt-in (MIPIPE_BN_FOLD=1).
-_BN_FOLD = os.environ.get("MIPIPE_BN_FOLD", "0") == "1"
+# Folding BN2 into conv3 saves a read + write of the BN output but costs the conv3 forward /
+# weight-grad an in-place LDS transform pass per k-step (+ a barrier and the coefficient table).
+# Measured (profiles/r6_bn_fold_negative.txt): per kernel it pays only on ResNet-50 layer 1, and
+# end to end it LOSES in every mode — per-fragment transform 12,700 vs 13,150 img/s, LDS-pass
+# transform 13,130 vs 13,275 ("1"), size-gated 13,209 vs 13,270 ("auto": tensors of at least
+# MIPIPE_BN_FOLD_MIN_ELEMS = 2^25 elements) — so it is off by default ("0").
+_BN_FOLD_MODE = os.environ.get("MIPIPE_BN_FOLD", "0")
+_BN_FOLD = _BN_FOLD_MODE != "0"
+_BN_FOLD_MIN = int(os.environ.get("MIPIPE_BN_FOLD_MIN_ELEMS", str(1 << 25)))
 
 
 def _foldable_into_1x1(y: torch.Tensor) -> bool:
     """A BN + ReLU output the next dense 1x1 conv can consume folded (bf16 GPU, C <= 1024)."""
     from mipipe.ops import kernels as K
-    return (_BN_FOLD and y.is_cuda and y.dtype == torch.bfloat16 and K.use_native(y)
-            and y.shape[-1] <= 1024 and y.shape[-1] % 8 == 0)
+    if not (_BN_FOLD and y.is_cuda and y.dtype == torch.bfloat16 and K.use_native(y)
+            and y.shape[-1] <= 1024 and y.shape[-1] % 8 == 0):
+        return False
+    return _BN_FOLD_MODE == "1" or y.numel() >= _BN_FOLD_MIN
 
 
 def conv_bn_act(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d, relu: bool = True,
@@ -217,9 +223,8 @@ def conv_bn_act(x: torch.Tensor, conv: Conv2d, bn: BatchNorm2d, relu: bool = Tru
     stride-1 conv reached through ``conv_bn_act(fuse_prev=True)`` (ResNet Bottleneck conv3): this
     BN's apply + ReLU is then folded into that conv — its forward and weight-grad read y and
     transform their operand fragments (gemm_core.hpp KCDenseBufBN / MCDenseBufBN), so the
-    normalised activation is never written (saves a read and a write of the tensor per step; opt-in
-    with MIPIPE_BN_FOLD=1 — measured slower end to end, see _BN_FOLD).  The returned tensor is then
-    an alias of y.
+    normalised activation is never written (saves a read and a write of the tensor per step; large
+    tensors only by default, see _BN_FOLD_MODE).  The returned tensor is then an alias of y.
     """
     use_batch = bn.training
     prev = getattr(x, "_mipipe_bnact", None) if fuse_prev else None

@@ -85,8 +85,8 @@ def _bottleneck_step(fold, det, steps=2):
     from mipipe.models import create_model
     from mipipe.optim import SGD
     from mipipe.ops.functional import cross_entropy
-    old = mnn._BN_FOLD
-    mnn._BN_FOLD = fold
+    old = (mnn._BN_FOLD, mnn._BN_FOLD_MODE)
+    mnn._BN_FOLD, mnn._BN_FOLD_MODE = fold, ("1" if fold else "0")  # every size (small model)
     try:
         with determinism.deterministic(det):
             torch.manual_seed(0)
@@ -107,7 +107,7 @@ def _bottleneck_step(fold, det, steps=2):
             state = [v.detach().float().clone() for v in m.state_dict().values()]
             return torch.stack(losses), grads, state
     finally:
-        mnn._BN_FOLD = old
+        mnn._BN_FOLD, mnn._BN_FOLD_MODE = old
 
 
 def test_resnet50_step_folded_equals_unfolded_deterministic():
