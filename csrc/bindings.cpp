@@ -1160,7 +1160,7 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
   // number of waves over the 256 CUs.
   // Plans with kPlanWs set.  (Round 3 also timed a hipBLASLt "library plan" here; it is gone:
   // every GEMM of the training step runs on the MFMA kernels, tools/gemm_plans.py.)
-  const bool ws_out0 = mode == 0 && act_i == 0 && !f32 && N % 8 == 0;
+  const bool ws_out0 = mode == 0 && act_i == 0 && N % 8 == 0;
   auto launch = [&](void* C, int p) {
     if (p >= 4096) p = -1;  // a round-3 table's library plan: the heuristic MFMA plan
     const bool ws_plan = p >= 0 && (p & tune::kPlanWs) != 0;
@@ -1171,7 +1171,10 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
       const int ns = mipipe::gemm_ws_splits((int)K, sp);
       Tensor ws = torch::empty({(int64_t)ns, M, N}, a.options().dtype(at::kFloat));
       mipipe::WsFinish fin;
-      fin.ticket = ns > 1 && N % 4 == 0 ? ws_tickets(a, mipipe::gemm_max_tiles(M, N)) : nullptr;
+      // (an fp32 activation output is finished by the separate ordered sum: ws_finish adds into
+      // fp32 targets)
+      fin.ticket = ns > 1 && N % 4 == 0 && (mode == 2 || !f32)
+                       ? ws_tickets(a, mipipe::gemm_max_tiles(M, N)) : nullptr;
       fin.out = C;
       fin.ldo = N;
       fin.bias = bias_p;
@@ -1183,6 +1186,9 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
       if (fin.ticket != nullptr) return;  // the GEMM's last split per tile summed the slices
       if (mode == 2)
         mipipe::splitk_sum(ws.data_ptr<float>(), ns, M * N, static_cast<float*>(C), stream());
+      else if (f32)
+        mipipe::splitk_sum_f32out(ws.data_ptr<float>(), ns, M, (int)N, bias_p, static_cast<float*>(C),
+                                  N, stream(), static_cast<const float*>(add_p));
       else
         mipipe::splitk_sum_bf16(ws.data_ptr<float>(), ns, M, (int)N, bias_p, C, N, stream(),
                                 add_p);
@@ -1193,7 +1199,10 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
   };
   if (plan < 0) {
     std::vector<int> cands = tune::gemm_candidates(f32, mode == 2);
-    if ((mode == 2 && K >= 1024) || (ws_out0 && K >= 2048)) {
+    // (fp32 activation outputs: small grids too — the reference config's fc layer, 64-128 output
+    // tiles of 8-16 k-steps)
+    const bool small_f32 = ws_out0 && f32 && K >= 256 && ((M + 127) / 128) * ((N + 63) / 64) < 256;
+    if ((mode == 2 && K >= 1024) || (ws_out0 && K >= 2048) || small_f32) {
       for (int t : tune::candidates(f32, mode == 2))
         for (int sp : {2, 3, 4, 6, 8}) cands.push_back((t + tune::kPlanSplit * sp) | tune::kPlanWs);
     }

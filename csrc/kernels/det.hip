@@ -185,14 +185,17 @@ __global__ __launch_bounds__(256) void splitk_sum_wide_kernel(const float* __res
   }
 }
 
-// out[m][n] = bf16(sum_s ws[s][m][n] + bias[n] + addend[m][n]), s in order: the finishing pass of
+// out[m][n] = T(sum_s ws[s][m][n] + bias[n] + addend[m][n]), s in order: the finishing pass of
 // a split-K GEMM with an activation-dtype output (M x N, N % 8 == 0; ws slices are [M][N]
-// contiguous; addend: the data-grad's second gradient, [M][N] bf16, as the GEMM epilogue adds it).
-__global__ __launch_bounds__(256) void splitk_sum_bf16_kernel(const float* __restrict__ ws,
-                                                              int splits, long M, int N,
-                                                              const float* __restrict__ bias,
-                                                              const __bf16* __restrict__ addend,
-                                                              __bf16* __restrict__ out, long ldc) {
+// contiguous; addend: the data-grad's second gradient, [M][N] in T, as the GEMM epilogue adds it).
+// T = bf16, or fp32 on the reference-precision path (the fc layer of ResNet-18 at 32x32: 64-128
+// output tiles of 128x64 for 256 CUs).
+template <class T>
+__global__ __launch_bounds__(256) void splitk_sum_out_kernel(const float* __restrict__ ws,
+                                                             int splits, long M, int N,
+                                                             const float* __restrict__ bias,
+                                                             const T* __restrict__ addend,
+                                                             T* __restrict__ out, long ldc) {
   const long n8 = (long)N / 8;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-column chunk
   if (i >= M * n8) return;
@@ -212,20 +215,28 @@ __global__ __launch_bounds__(256) void splitk_sum_bf16_kernel(const float* __res
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] += b[e];
   }
-  if (addend != nullptr) {  // the GEMM epilogue's order: bf16(acc + float(addend))
+  if (addend != nullptr) {  // the GEMM epilogue's order: T(acc + float(addend))
     float a[8];
-    unpack8(*reinterpret_cast<const uint4*>(addend + m * (long)N + c), a);
+    load8(addend + m * (long)N + c, a);
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] += a[e];
   }
-  *reinterpret_cast<uint4*>(out + m * ldc + c) = pack8(f);
+  store8(out + m * ldc + c, f);
 }
 
 void splitk_sum_bf16(const float* ws, int splits, long M, int N, const float* bias, void* out,
                      long ldc, hipStream_t st, const void* addend) {
   const long chunks = M * (N / 8);
-  hipLaunchKernelGGL(splitk_sum_bf16_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
-                     st, ws, splits, M, N, bias, (const __bf16*)addend, (__bf16*)out, ldc);
+  hipLaunchKernelGGL(splitk_sum_out_kernel<__bf16>, dim3((unsigned)((chunks + 255) / 256)),
+                     dim3(256), 0, st, ws, splits, M, N, bias, (const __bf16*)addend,
+                     (__bf16*)out, ldc);
+}
+
+void splitk_sum_f32out(const float* ws, int splits, long M, int N, const float* bias, float* out,
+                       long ldc, hipStream_t st, const float* addend) {
+  const long chunks = M * (N / 8);
+  hipLaunchKernelGGL(splitk_sum_out_kernel<float>, dim3((unsigned)((chunks + 255) / 256)),
+                     dim3(256), 0, st, ws, splits, M, N, bias, addend, out, ldc);
 }
 
 void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st) {

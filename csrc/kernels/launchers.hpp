@@ -54,6 +54,9 @@ void splitk_sum(const float* ws, int splits, long n, float* out, hipStream_t st)
 // out[m][n] (bf16, row pitch ldc) = sum_s ws[s][m][n] + bias[n] (bias may be null); N % 8 == 0
 void splitk_sum_bf16(const float* ws, int splits, long M, int N, const float* bias, void* out,
                      long ldc, hipStream_t st, const void* addend = nullptr);
+// the same with an fp32 output (the reference-precision path)
+void splitk_sum_f32out(const float* ws, int splits, long M, int N, const float* bias, float* out,
+                       long ldc, hipStream_t st, const float* addend = nullptr);
 int conv_fwd_stat_rows(const ConvShape& s);
 // st_sum / st_sq: zeroed [kStatReplicas][Co] slabs (accumulated into)
 // bias / relu: optional per-channel bias and ReLU in the epilogue (convs without BN: VGG, AlexNet)

@@ -235,6 +235,28 @@ def test_gemm_every_plan(M, N, K, ta, tb, dt):
             assert torch.equal(acc, acc2), (cfg, sp, "ws split-K must be deterministic")
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 1000, 512), (1024, 512, 1000), (200, 136, 264)])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False)])
+def test_gemm_splitk_fp32_output(M, N, K, ta, tb):
+    """Workspace split-K plans of an fp32-output GEMM (the reference config's fc layer: 64-128
+    output tiles for 256 CUs): slices summed in order with the bias by one pass — every fp32 tile
+    at 2/3/4/8 splits against a float64 reference at 1e-4, bit-identical reruns."""
+    if N % 8:
+        pytest.skip("layout constraint")
+    a = torch.randn(M, K, device=dev)
+    b = torch.randn(N, K, device=dev) if tb else torch.randn(K, N, device=dev)
+    bias = torch.randn(N, device=dev)
+    ref = _ref.gemm(a.double().cpu(), b.double().cpu(), ta, tb, bias.double().cpu(), "none",
+                    torch.float64)
+    for cfg in (0, 2, 8):
+        for sp in (2, 3, 4, 8):
+            plan = (cfg + 16 * sp) | 1024
+            out = native().gemm(a, b, ta, tb, bias, "none", torch.float32, None, 0.0, plan)
+            assert out.dtype == torch.float32 and rel_err(out, ref) < 1e-4, (cfg, sp)
+            out2 = native().gemm(a, b, ta, tb, bias, "none", torch.float32, None, 0.0, plan)
+            assert torch.equal(out, out2), (cfg, sp)
+
+
 @pytest.mark.parametrize("M,N,K", [(512, 768, 8192), (200, 136, 4104), (640, 768, 30528)])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False)])
 def test_gemm_splitk_bf16_output(M, N, K, ta, tb):
