@@ -1253,6 +1253,49 @@ std::tuple<Tensor, Tensor> gemm_gelu(Tensor a, Tensor b, optional<Tensor> bias, 
 }
 
 // ------------------------------------------------------------------------------- loss / optim
+// Split cross-entropy (training step): forward -> (loss, work = [count | row losses | row lse]),
+// backward -> grad from the saved logits and the upstream gradient (a device scalar).
+std::tuple<Tensor, Tensor> cross_entropy_fwd(Tensor logits, Tensor labels, double smoothing,
+                                             int64_t ignore_index, int64_t valid_cols) {
+  check_act(logits, "logits");
+  check_cuda(labels, "labels");
+  c10::DeviceGuard g(logits.device());
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  TORCH_CHECK(logits.dim() == 2 && labels.numel() == logits.size(0) && logits.is_contiguous(),
+              "CE shape mismatch");
+  const int R = logits.size(0), V = logits.size(1);
+  auto loss = torch::empty({}, logits.options().dtype(at::kFloat));
+  auto work = torch::empty({4 + 2 * (int64_t)R}, logits.options().dtype(at::kInt));
+  mipipe::cross_entropy_fwd(logits.data_ptr(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                            R, V, (float)smoothing, ignore_index, work.data_ptr<int>(), stream(),
+                            is_f32(logits), (int)std::min<int64_t>(valid_cols > 0 ? valid_cols : V, V));
+  return {loss, work};
+}
+
+Tensor cross_entropy_bwd(Tensor logits, Tensor labels, Tensor work, Tensor gout, double smoothing,
+                         int64_t ignore_index, int64_t valid_cols) {
+  check_act(logits, "logits");
+  c10::DeviceGuard g(logits.device());
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous() && labels.numel() == logits.size(0),
+              "CE shape mismatch");
+  const int R = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(work.scalar_type() == at::kInt && work.numel() == 4 + 2 * (int64_t)R,
+              "CE work buffer mismatch");
+  check_cuda(labels, "labels");
+  check_cuda(work, "work");
+  check_f32(gout, "gout");
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels must be int64");
+  TORCH_CHECK(gout.numel() == 1 && gout.device() == logits.device() &&
+              labels.device() == logits.device() && work.device() == logits.device(),
+              "gout must be one value; every operand on the logits' device");
+  auto grad = torch::empty_like(logits);
+  mipipe::cross_entropy_bwd(logits.data_ptr(), labels.data_ptr<int64_t>(), work.data_ptr<int>(),
+                            gout.data_ptr<float>(), grad.data_ptr(), R, V, (float)smoothing,
+                            ignore_index, stream(), is_f32(logits),
+                            (int)std::min<int64_t>(valid_cols > 0 ? valid_cols : V, V));
+  return grad;
+}
+
 std::tuple<Tensor, Tensor> cross_entropy_fwd_bwd(Tensor logits, Tensor labels, double smoothing,
                                                  int64_t ignore_index, int64_t valid_cols) {
   check_act(logits, "logits");
@@ -1973,6 +2016,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("get_nt_store", []() { return mipipe::g_nt_store; });
   m.def("set_ws_finish", [](bool on) { g_ws_finish = on; });
   m.def("get_ws_finish", []() { return g_ws_finish; });
+  m.def("set_layernorm_mode", [](int64_t m) { mipipe::set_layernorm_mode((int)m); });
+  m.def("get_layernorm_mode", []() { return mipipe::get_layernorm_mode(); });
   m.def("set_deterministic", [](bool on) { mipipe::g_deterministic = on ? 1 : 0; });
   m.def("get_deterministic", []() { return mipipe::g_deterministic != 0; });
   m.def("tune_table", []() { return tune::g_table; });
@@ -2034,6 +2079,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("trans_a"), py::arg("trans_b"),
         py::arg("bias"), py::arg("act"), py::arg("out_dtype"), py::arg("c"), py::arg("beta"),
         py::arg("plan") = -1, py::arg("addend") = py::none());
+  m.def("cross_entropy_fwd", &cross_entropy_fwd, py::arg("logits"), py::arg("labels"),
+        py::arg("smoothing") = 0.0, py::arg("ignore_index") = -100, py::arg("valid_cols") = -1);
+  m.def("cross_entropy_bwd", &cross_entropy_bwd, py::arg("logits"), py::arg("labels"),
+        py::arg("work"), py::arg("gout"), py::arg("smoothing") = 0.0,
+        py::arg("ignore_index") = -100, py::arg("valid_cols") = -1);
   m.def("cross_entropy_fwd_bwd", &cross_entropy_fwd_bwd, py::arg("logits"), py::arg("labels"),
         py::arg("smoothing"), py::arg("ignore_index"), py::arg("valid_cols") = -1);
   m.def("sgd_step", &sgd_step);

@@ -152,6 +152,34 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Whole-wave sum without the LDS crossbar (each __shfl_xor step above is a ds_bpermute round
+// trip): DPP within each 16-lane row, then the four row totals read lane by lane (v_readlane)
+// and added in a fixed order; every lane gets the total.  All 64 lanes must be active.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  const int b = __builtin_bit_cast(int, row16_sum(v));
+  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
+         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
+}
+
+// 4 bf16 held in a uint2 <-> floats (the 8-byte twins of unpack8 / pack8)
+__device__ __forceinline__ void unpack4(const uint2& u, float* f) {
+  f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+__device__ __forceinline__ uint2 pack4(const float* f) {
+  return make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3]));
+}
+__device__ __forceinline__ void unpackv(const uint4& u, float* f) { unpack8(u, f); }
+__device__ __forceinline__ void unpackv(const uint2& u, float* f) { unpack4(u, f); }
+template <class VT>
+__device__ __forceinline__ VT packv(const float* f);
+template <>
+__device__ __forceinline__ uint4 packv<uint4>(const float* f) { return pack8(f); }
+template <>
+__device__ __forceinline__ uint2 packv<uint2>(const float* f) { return pack4(f); }
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));

@@ -328,6 +328,15 @@ void avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st,
 void cross_entropy_fwd_bwd(const void* logits, const int64_t* labels, float* loss, void* grad,
                            int R, int V, float smoothing, int64_t ignore_index, int* work,
                            hipStream_t st, bool f32 = false, int valid_cols = 0);
+// The training-step split of the same loss: cross_entropy_fwd writes the loss, the valid-row count
+// (work[0]) and per-row losses / log-sum-exps (work + 4: [2][R] floats; work holds 4 + 2R ints);
+// cross_entropy_bwd then writes grad = (softmax - target) * gout[0] / count from the logits.
+void cross_entropy_fwd(const void* logits, const int64_t* labels, float* loss, int R, int V,
+                       float smoothing, int64_t ignore_index, int* work, hipStream_t st, bool f32,
+                       int Vv);
+void cross_entropy_bwd(const void* logits, const int64_t* labels, const int* work,
+                       const float* gout, void* grad, int R, int V, float smoothing,
+                       int64_t ignore_index, hipStream_t st, bool f32, int Vv);
 // *correct += #rows whose first maximal logit is at the label (torch.argmax tie rule)
 void top1_correct(const void* logits, const int64_t* labels, int R, int V, int* correct,
                   hipStream_t st, bool f32 = false);
@@ -404,6 +413,12 @@ void layernorm_bwd(const void* dy, const void* x, const float* mean, const float
                    long rows, int H, hipStream_t st, void* dxd = nullptr,
                    const DropSpec* drop = nullptr, float* dbias = nullptr);
 int layernorm_bwd_blocks(long rows);  // partial rows of layernorm_bwd's work
+// LayerNorm kernel family: 0 = the generic one-row-per-wave kernels (16-B chunks, any H % 8 == 0),
+// 4 / 8 (default) / 16 = the exact-width kernels (chunk width picked so every lane holds whole
+// chunks, DPP wave sums) with that many waves per backward block; the generic kernels still
+// serve the widths the exact ones do not cover (and the 8-wide forward).  MIPIPE_LN_MODE.
+void set_layernorm_mode(int mode);
+int get_layernorm_mode();
 void gelu_fwd(const void* x, void* y, long n, hipStream_t st);
 void gelu_bwd(const void* dy, const void* x, void* dx, long n, hipStream_t st);
 // gelu_bwd of a [rows, cols] tensor that also accumulates out[c] += Σ_rows dx[:, c] (the GELU

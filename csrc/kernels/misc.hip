@@ -153,6 +153,156 @@ void cross_entropy_fwd_bwd(const void* logits, const int64_t* labels, float* los
   hipLaunchKernelGGL(ce_sum_kernel, dim3(1), dim3(256), 0, st, rowloss, R, loss);
 }
 
+// Split form for the training step: the forward keeps only the per-row log-sum-exp (one pass
+// over the logits: running max and rescaled exp-sum per thread, merged per wave and block), the
+// backward writes grad = (softmax - target) * g / n straight from the logits with the upstream
+// gradient g read on the device — so no [R][V] gradient is written in the forward and then
+// rescaled by a separate elementwise pass (BERT-base MLM: 640 x 30528 logits).
+__device__ __forceinline__ void lse_merge(float& m, float& s, float mo, float so) {
+  const float mn = fmaxf(m, mo);
+  if (mn == -INFINITY) return;  // both empty
+  s = s * __expf(m - mn) + so * __expf(mo - mn);
+  m = mn;
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const T* __restrict__ logits,
+                                                     const int64_t* __restrict__ labels, int V,
+                                                     int Vv, float eps, int64_t ignore,
+                                                     const int* __restrict__ nvalid,
+                                                     float* __restrict__ rowloss,
+                                                     float* __restrict__ lse_out) {
+  __shared__ float sh[3][4];
+  const long row = blockIdx.x;
+  const T* x = logits + row * V;
+  float m = -INFINITY, s = 0.f, sx = 0.f;
+  if ((V % 8) == 0) {
+    for (int c = threadIdx.x; c < V / 8; c += 256) {
+      float v[8];
+      load8(x + c * 8, v);
+      float m8 = -INFINITY;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (c * 8 + q < Vv) {
+          m8 = fmaxf(m8, v[q]);
+          sx += v[q];
+        }
+      const float mn = fmaxf(m, m8);
+      if (mn == -INFINITY) continue;
+      float e = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (c * 8 + q < Vv) e += __expf(v[q] - mn);
+      s = s * __expf(m - mn) + e;
+      m = mn;
+    }
+  } else {
+    for (int c = threadIdx.x; c < Vv; c += 256) {
+      const float v = (float)x[c];
+      sx += v;
+      lse_merge(m, s, v, 1.f);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float mo = __shfl_xor(m, o), so = __shfl_xor(s, o);
+    lse_merge(m, s, mo, so);
+    sx += __shfl_xor(sx, o);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][w] = m;
+    sh[1][w] = s;
+    sh[2][w] = sx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sh[0][0], S = sh[1][0], SX = sh[2][0];
+    for (int i = 1; i < 4; ++i) {
+      lse_merge(M, S, sh[0][i], sh[1][i]);
+      SX += sh[2][i];
+    }
+    const float lse = M + __logf(S);
+    const int64_t lab = labels[row];
+    float l = 0.f;
+    if (lab != ignore)
+      l = (1.f - eps) * (lse - (float)x[lab]) + eps * (lse - SX / (float)Vv);
+    rowloss[row] = l / (float)max(1, nvalid[0]);
+    lse_out[row] = lse;
+  }
+}
+
+// grid (column blocks, rows): 8 columns per thread (V % 8 == 0) or 1
+template <class T, bool VEC>
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const T* __restrict__ logits,
+                                                     const int64_t* __restrict__ labels,
+                                                     const float* __restrict__ lse,
+                                                     const int* __restrict__ nvalid,
+                                                     const float* __restrict__ gout,
+                                                     T* __restrict__ grad, int R, int V, int Vv,
+                                                     float eps, int64_t ignore) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= (VEC ? V / 8 : V)) return;
+  const float gs = gout[0] / (float)max(1, nvalid[0]), base_t = eps / (float)Vv;
+  for (long row = blockIdx.y; row < R; row += gridDim.y) {  // (grid.y is capped at 65535)
+  const int64_t lab = labels[row];
+  const float scale = lab != ignore ? gs : 0.f;
+  const float l = lse[row];
+  if constexpr (VEC) {
+    float v[8];
+    load8(logits + row * V + c * 8, v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int col = c * 8 + q;
+      const float t = base_t + (col == lab ? 1.f - eps : 0.f);
+      v[q] = col < Vv ? (__expf(v[q] - l) - t) * scale : 0.f;
+    }
+    store8(grad + row * V + c * 8, v);
+  } else {
+    const float t = base_t + (c == lab ? 1.f - eps : 0.f);
+    grad[row * V + c] = (T)(c < Vv ? (__expf((float)logits[row * V + c] - l) - t) * scale : 0.f);
+  }
+  }
+}
+
+void cross_entropy_fwd(const void* logits, const int64_t* labels, float* loss, int R, int V,
+                       float smoothing, int64_t ignore_index, int* work, hipStream_t st, bool f32,
+                       int Vv) {
+  if (Vv <= 0 || Vv > V) Vv = V;
+  float* rowloss = reinterpret_cast<float*>(work + 4);
+  float* lse = rowloss + R;
+  hipLaunchKernelGGL(ce_count_kernel, dim3(1), dim3(256), 0, st, labels, R, ignore_index, work);
+  if (f32)
+    hipLaunchKernelGGL(ce_fwd_kernel<float>, dim3(R), dim3(256), 0, st, (const float*)logits,
+                       labels, V, Vv, smoothing, ignore_index, (const int*)work, rowloss, lse);
+  else
+    hipLaunchKernelGGL(ce_fwd_kernel<__bf16>, dim3(R), dim3(256), 0, st, (const __bf16*)logits,
+                       labels, V, Vv, smoothing, ignore_index, (const int*)work, rowloss, lse);
+  hipLaunchKernelGGL(ce_sum_kernel, dim3(1), dim3(256), 0, st, rowloss, R, loss);
+}
+
+void cross_entropy_bwd(const void* logits, const int64_t* labels, const int* work,
+                       const float* gout, void* grad, int R, int V, float smoothing,
+                       int64_t ignore_index, hipStream_t st, bool f32, int Vv) {
+  if (Vv <= 0 || Vv > V) Vv = V;
+  const float* lse = reinterpret_cast<const float*>(work + 4) + R;
+  const bool vec = V % 8 == 0;
+  const dim3 g((unsigned)(((vec ? V / 8 : V) + 255) / 256), (unsigned)std::min(R, 65535));
+  auto go = [&](auto t, auto vec_c) {
+    using T = decltype(t);
+    hipLaunchKernelGGL((ce_bwd_kernel<T, decltype(vec_c)::value>), g, dim3(256), 0, st,
+                       (const T*)logits, labels, lse, work, gout, (T*)grad, R, V, Vv,
+                       smoothing, ignore_index);
+  };
+  if (f32) {
+    if (vec) go(float(), std::true_type());
+    else go(float(), std::false_type());
+  } else {
+    if (vec) go(__bf16(), std::true_type());
+    else go(__bf16(), std::false_type());
+  }
+}
+
 // ------------------------------------------------------------------------------ evaluation
 // Top-1 correct count (the reference's eval loop: argmax over classes == label, summed): one
 // wave per row, first maximal index wins (torch.argmax's tie rule), NaN counts as maximal; the
@@ -1018,10 +1168,120 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const __bf16* __rest
   }
 }
 
+// Exact-width LayerNorm: H = NC * 64 * VEC, every lane holds NC whole chunks of VEC elements
+// (BERT-base H = 768: 3 chunks of 4 per lane, where the 16-B kernel above leaves half the wave
+// idle on its second chunk behind a divergent branch), all loads issued before the first use
+// and the two row sums done with DPP instead of ds_bpermute shuffles.
+template <int VEC>
+using LnVec = std::conditional_t<VEC == 8, uint4, uint2>;
+
+int g_ln_mode = [] {
+  const char* v = getenv("MIPIPE_LN_MODE");
+  return v != nullptr ? atoi(v) : 8;
+}();
+void set_layernorm_mode(int mode) { g_ln_mode = mode; }
+int get_layernorm_mode() { return g_ln_mode; }
+
+// (VEC, chunks per lane) of the exact kernels for H, or VEC = 0 where they do not apply
+static void ln_exact_shape(int H, int& vec, int& nc) {
+  vec = nc = 0;
+  if (g_ln_mode == 0 || H > 1024) return;
+  if (H % 512 == 0) { vec = 8; nc = H / 512; }        // 512, 1024
+  else if (H % 256 == 0) { vec = 4; nc = H / 256; }   // 256, 768
+}
+
+template <bool DROP, int VEC, int NC>
+__global__ __launch_bounds__(256) void layernorm_fwd_exact_kernel(
+    const __bf16* __restrict__ x, const __bf16* __restrict__ res, const float* __restrict__ gamma,
+    const float* __restrict__ beta, __bf16* __restrict__ y, __bf16* __restrict__ xsum,
+    float* __restrict__ mean, float* __restrict__ rstd, long rows, float eps, DropArgs dr) {
+  using VT = LnVec<VEC>;
+  constexpr int H = NC * 64 * VEC;
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const __bf16* xr = x + row * H;
+  VT ux[NC], ur[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) ux[k] = reinterpret_cast<const VT*>(xr)[lane + k * 64];
+  if (res != nullptr) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) ur[k] = reinterpret_cast<const VT*>(res + row * H)[lane + k * 64];
+  }
+  const uint32_t dbase = DROP ? drop_base(dr.seed, dr.seed_dev) : 0u;
+  float v[NC][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    const int c = lane + k * 64;
+    unpackv(ux[k], v[k]);
+    if constexpr (DROP) {
+      float t[VEC];  // the standalone kernel rounds the dropped value to bf16: same here
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        t[q] = drop_keep(dbase, row * H + c * VEC + q, dr.thr) ? v[k][q] * dr.scale : 0.f;
+      unpackv(packv<VT>(t), v[k]);
+    }
+    if (res != nullptr) {
+      float r[VEC];
+      unpackv(ur[k], r);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) v[k][q] += r[q];
+      const VT sb = packv<VT>(v[k]);
+      reinterpret_cast<VT*>(xsum + row * H)[c] = sb;
+      unpackv(sb, v[k]);  // normalise the bf16-rounded sum that backward will see
+    }
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) s += v[k][q];
+  }
+  const float mu = wave_sum_dpp(s) * (1.f / (float)H);
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < NC; ++k)
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      const float d = v[k][q] - mu;
+      ss += d * d;
+    }
+  const float rs = rsqrtf(wave_sum_dpp(ss) * (1.f / (float)H) + eps);
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    const int c = lane + k * 64;
+    float o[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) o[q] = (v[k][q] - mu) * rs * gamma[c * VEC + q] + beta[c * VEC + q];
+    reinterpret_cast<VT*>(y + row * H)[c] = packv<VT>(o);
+  }
+}
+
 void layernorm_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y,
                    void* xsum, float* mean, float* rstd, long rows, int H, float eps,
                    hipStream_t st, const DropSpec* drop) {
   const DropArgs dr = drop_args(drop);
+  int vec, nc;
+  ln_exact_shape(H, vec, nc);
+  // forward: the 8-wide exact kernel measured slower than the generic one at H = 1024 (9.5 vs
+  // 8.0 us, 4096 rows, profiles/r6_layernorm_modes.txt); the 4-wide one is faster at H = 768
+  if (vec == 4) {
+    auto go = [&](auto drop_c, auto vec_c, auto nc_c) {
+      constexpr bool DROP = decltype(drop_c)::value;
+      constexpr int VEC = decltype(vec_c)::value, NC = decltype(nc_c)::value;
+      hipLaunchKernelGGL((layernorm_fwd_exact_kernel<DROP, VEC, NC>), dim3((rows + 3) / 4),
+                         dim3(256), 0, st, (const __bf16*)x, (const __bf16*)res, gamma, beta,
+                         (__bf16*)y, (__bf16*)xsum, mean, rstd, rows, eps, dr);
+    };
+    auto go_v = [&](auto drop_c) {  // (4, 1) H = 256, (4, 3) H = 768
+      if (nc == 1) go(drop_c, std::integral_constant<int, 4>(), std::integral_constant<int, 1>());
+      else go(drop_c, std::integral_constant<int, 4>(), std::integral_constant<int, 3>());
+    };
+    if (dr.thr != 0u) go_v(std::true_type());
+    else go_v(std::false_type());
+    return;
+  }
   if (dr.thr != 0u)
     hipLaunchKernelGGL(layernorm_fwd_kernel<true>, dim3((rows + 3) / 4), dim3(256), 0, st,
                        (const __bf16*)x, (const __bf16*)res, gamma, beta, (__bf16*)y,
@@ -1160,6 +1420,118 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* __rest
   }
 }
 
+// Exact-width backward (H = NC * 64 * VEC, as layernorm_fwd_exact_kernel) with W waves per block:
+// the same <= 256 blocks (one fixed-order summing pass over their partial rows) but W = 8 puts
+// 8 waves on each CU instead of 4, so the rows' loads overlap across waves rather than only
+// through the one-row prefetch.  Partials: LDS, summed over the waves in a fixed pairwise order.
+// BERT-base 4096 x 768 with dropout + bias sum: 14.6 -> 11.3 us incl. the partial-row sum
+// (W = 16: 11.5, and 23.6 at H = 1024; profiles/r6_layernorm_modes.txt).
+template <int VEC, int NC, int W, bool DROP, bool BSUM>
+__global__ __launch_bounds__(W * 64) void layernorm_bwd_exact_kernel(
+    const __bf16* __restrict__ dy, const __bf16* __restrict__ x, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ gamma, __bf16* __restrict__ dx,
+    float* __restrict__ pg, float* __restrict__ pb, long rows, int rows_per_block,
+    __bf16* __restrict__ dxd, DropArgs dr, float* __restrict__ pd) {
+  using VT = LnVec<VEC>;
+  constexpr int H = NC * 64 * VEC;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t dbase = DROP ? drop_base(dr.seed, dr.seed_dev) : 0u;
+  float accg[NC][VEC], accb[NC][VEC], accd[NC][VEC], gam[NC][VEC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k)
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      accg[k][q] = accb[k][q] = accd[k][q] = 0.f;
+      gam[k][q] = gamma[(lane + k * 64) * VEC + q];
+    }
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = min(rows, r0 + rows_per_block);
+  VT ng[NC], nx[NC];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](long row) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      ng[k] = reinterpret_cast<const VT*>(dy + row * H)[lane + k * 64];
+      nx[k] = reinterpret_cast<const VT*>(x + row * H)[lane + k * 64];
+    }
+    nmu = mean[row];
+    nrs = rstd[row];
+  };
+  if (r0 + w < r1) fetch(r0 + w);
+  for (long row = r0 + w; row < r1; row += W) {
+    const float mu = nmu, rs = nrs;
+    float g[NC][VEC], xh[NC][VEC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      unpackv(ng[k], g[k]);
+      unpackv(nx[k], xh[k]);
+    }
+    if (row + W < r1) fetch(row + W);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        xh[k][q] = (xh[k][q] - mu) * rs;
+        accg[k][q] += g[k][q] * xh[k][q];
+        accb[k][q] += g[k][q];
+        const float gg = g[k][q] * gam[k][q];
+        s1 += gg;
+        s2 += gg * xh[k][q];
+      }
+    s1 = wave_sum_dpp(s1) * (1.f / (float)H);
+    s2 = wave_sum_dpp(s2) * (1.f / (float)H);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = lane + k * 64;
+      float o[VEC];
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o[q] = rs * (g[k][q] * gam[k][q] - s1 - xh[k][q] * s2);
+      const VT ob = packv<VT>(o);
+      reinterpret_cast<VT*>(dx + row * H)[c] = ob;
+      if constexpr (DROP) {  // from the bf16-rounded dx, as the standalone kernel would see it
+        float od[VEC];
+        unpackv(ob, od);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q)
+          od[q] = drop_keep(dbase, row * H + c * VEC + q, dr.thr) ? od[q] * dr.scale : 0.f;
+        const VT odb = packv<VT>(od);
+        reinterpret_cast<VT*>(dxd + row * H)[c] = odb;
+        if constexpr (BSUM) {
+          unpackv(odb, od);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) accd[k][q] += od[q];
+        }
+      } else if constexpr (BSUM) {
+        unpackv(ob, o);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) accd[k][q] += o[q];
+      }
+    }
+  }
+  __shared__ float red[W][H];
+  for (int arr = 0; arr < (BSUM ? 3 : 2); ++arr) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        red[w][(lane + k * 64) * VEC + q] = arr == 0 ? accg[k][q] : arr == 1 ? accb[k][q] : accd[k][q];
+    __syncthreads();
+    float* dst = (arr == 0 ? pg : arr == 1 ? pb : pd) + (long)blockIdx.x * H;
+    for (int c = threadIdx.x; c < H; c += W * 64) {
+      float t[W];
+#pragma unroll
+      for (int i = 0; i < W; ++i) t[i] = red[i][c];
+#pragma unroll
+      for (int s = 1; s < W; s *= 2)
+#pragma unroll
+        for (int i = 0; i + s < W; i += 2 * s) t[i] += t[i + s];
+      dst[c] = t[0];
+    }
+  }
+}
+
 static void layernorm_bwd_grid(long rows, int& G, int& rpb) {
   // >= 16 rows (4 per wave, each next one prefetched) per block and <= 256 blocks: the partial
   // rows then take ONE fixed-order summing pass (det_sum_rows goes two-level above 256 rows;
@@ -1189,6 +1561,39 @@ void layernorm_bwd(const void* dy, const void* x, const float* mean, const float
   // register arrays sized for H: 2 chunks of 8 per lane up to H = 1024 (BERT-base), else 4
   const DropArgs dr = drop_args(drop);
   const bool dp = dr.thr != 0u && dxd != nullptr;
+  int vec, nc;
+  ln_exact_shape(H, vec, nc);
+  if (vec != 0) {
+    auto go = [&](auto vec_c, auto nc_c, auto w_c, auto drop_c, auto bsum_c) {
+      constexpr int VEC = decltype(vec_c)::value, NC = decltype(nc_c)::value;
+      constexpr int W = decltype(w_c)::value;
+      constexpr bool DROP = decltype(drop_c)::value, BSUM = decltype(bsum_c)::value;
+      hipLaunchKernelGGL((layernorm_bwd_exact_kernel<VEC, NC, W, DROP, BSUM>), dim3(G),
+                         dim3(W * 64), 0, st, (const __bf16*)dy, (const __bf16*)x, mean, rstd,
+                         gamma, (__bf16*)dx, wg, wb, rows, rpb, (__bf16*)dxd, dr, wd);
+    };
+    auto go_w = [&](auto vec_c, auto nc_c, auto drop_c, auto bsum_c) {
+      if (g_ln_mode == 4) go(vec_c, nc_c, std::integral_constant<int, 4>(), drop_c, bsum_c);
+      else if (g_ln_mode == 8) go(vec_c, nc_c, std::integral_constant<int, 8>(), drop_c, bsum_c);
+      else go(vec_c, nc_c, std::integral_constant<int, 16>(), drop_c, bsum_c);
+    };
+    auto go_s = [&](auto drop_c, auto bsum_c) {
+      using I8 = std::integral_constant<int, 8>;
+      using I4 = std::integral_constant<int, 4>;
+      if (vec == 8 && nc == 1) go_w(I8(), std::integral_constant<int, 1>(), drop_c, bsum_c);
+      else if (vec == 8) go_w(I8(), std::integral_constant<int, 2>(), drop_c, bsum_c);
+      else if (nc == 1) go_w(I4(), std::integral_constant<int, 1>(), drop_c, bsum_c);
+      else go_w(I4(), std::integral_constant<int, 3>(), drop_c, bsum_c);
+    };
+    auto go_d = [&](auto drop_c) {
+      if (wd != nullptr) go_s(drop_c, std::true_type());
+      else go_s(drop_c, std::false_type());
+    };
+    if (dp) go_d(std::true_type());
+    else go_d(std::false_type());
+    det_sum_rows(wg, wb, G, H, dgamma, dbeta, true, st, wd, dbias);
+    return;
+  }
   auto go = [&](auto nch, auto drop_c, auto bsum_c) {
     constexpr int NCH = decltype(nch)::value;
     constexpr bool DROP = decltype(drop_c)::value, BSUM = decltype(bsum_c)::value;

@@ -1101,15 +1101,32 @@ def linear(x: Tensor, weight: Tensor, w_c: Tensor, bias: Optional[Tensor], act: 
 
 # ----------------------------------------------------------------------------- loss
 class _CrossEntropyFn(Function):
+    """Native: the forward keeps the logits and per-row log-sum-exps, the backward writes the
+    scaled gradient in one pass (upstream gradient read on the device; no [R, V] gradient from
+    the forward and no separate rescale).  Fallback: fused fwd+bwd reference, rescaled."""
+
     @staticmethod
     def forward(ctx, logits, labels, label_smoothing, ignore_index, valid_cols):
-        loss, grad = K.cross_entropy_fwd_bwd(logits.contiguous(), labels.contiguous(),
-                                             label_smoothing, ignore_index, valid_cols)
+        logits, labels = logits.contiguous(), labels.contiguous()
+        ctx.args = (label_smoothing, ignore_index, valid_cols)
+        ctx.split = K.use_native(logits)
+        if ctx.split:
+            loss, work = K.native().cross_entropy_fwd(logits, labels, label_smoothing,
+                                                      ignore_index, valid_cols)
+            ctx.save_for_backward(logits, labels, work)
+            return loss
+        loss, grad = K.cross_entropy_fwd_bwd(logits, labels, label_smoothing, ignore_index,
+                                             valid_cols)
         ctx.save_for_backward(grad)
         return loss
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.split:
+            logits, labels, work = ctx.saved_tensors
+            gout = g.detach().reshape(1).to(torch.float32)
+            return (K.native().cross_entropy_bwd(logits, labels, work, gout, *ctx.args),
+                    None, None, None, None)
         (grad,) = ctx.saved_tensors
         return (grad * g.to(grad.dtype)), None, None, None, None
 

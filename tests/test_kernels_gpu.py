@@ -461,6 +461,38 @@ def test_cross_entropy(V):
         assert rel_err(grad, gr) < 1e-2
 
 
+@pytest.mark.parametrize("V,valid", [(1000, -1), (30528, 30522), (1001, -1), (10, -1)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_cross_entropy_split_fwd_bwd(V, valid, dtype):
+    """The training-step split (forward: loss + row log-sum-exps; backward: gradient from the
+    logits and a device-side upstream gradient) against the fused kernel and the fp32
+    reference — label smoothing, ignored rows, a padded vocabulary (valid columns < V), V % 8
+    != 0 (scalar path), fp32 logits, upstream gradient != 1; through mipipe's cross_entropy."""
+    from mipipe.ops.functional import cross_entropy
+    R = 131
+    logits = (torch.randn(R, V, device=dev) * 3).to(dtype)
+    labels = torch.randint(0, V if valid < 0 else valid, (R,), device=dev)
+    labels[3] = -100
+    for eps in (0.0, 0.1):
+        loss, work = native().cross_entropy_fwd(logits, labels, eps, -100, valid)
+        l0, g0 = native().cross_entropy_fwd_bwd(logits, labels, eps, -100, valid)
+        lr_, gr = _ref.cross_entropy_fwd_bwd(logits.float(), labels, eps, -100, valid)
+        assert abs(loss.item() - lr_.item()) <= 1e-4 * abs(lr_.item())
+        assert abs(loss.item() - l0.item()) <= 1e-5 * abs(l0.item())
+        assert int(work[0]) == R - 1
+        gout = torch.full((1,), 0.37, device=dev)
+        grad = native().cross_entropy_bwd(logits, labels, work, gout, eps, -100, valid)
+        assert grad.dtype == dtype
+        assert rel_err(grad, gr * 0.37) < (1e-2 if dtype == torch.bfloat16 else 1e-5)
+        assert rel_err(grad, g0.float() * 0.37) < (1e-2 if dtype == torch.bfloat16 else 1e-5)
+        if valid > 0:
+            assert not grad[:, valid:].any()
+        assert not grad[3].any()
+        x = logits.clone().requires_grad_(True)
+        (cross_entropy(x, labels, eps, valid_cols=valid) * 0.37).backward()
+        assert torch.equal(x.grad, grad)
+
+
 def test_sgd_and_adamw():
     n = 4096 * 3
     p = torch.randn(n, device=dev)
@@ -540,6 +572,44 @@ def test_layernorm_fwd_widths(H, with_res):
     assert (xs is None) == (res is None)
     if res is not None:
         assert rel_err(xs, x.float() + res.float()) < 1e-2
+
+
+@pytest.mark.parametrize("mode", [0, 4, 8, 16])
+@pytest.mark.parametrize("H", [256, 512, 768, 1024, 1032])
+@pytest.mark.parametrize("R", [37, 4100])
+def test_layernorm_kernel_modes(mode, H, R):
+    """Every LayerNorm kernel family (0: generic 16-B chunks; 4 / 8 / 16: exact-width chunks with
+    that many waves per backward block) against the fp32 reference, forward and backward, with
+    the fused residual dropout and the producing Linear's bias-gradient sum; row counts that
+    leave waves of the last block without rows.  H = 1032 takes the generic kernels in every
+    mode."""
+    old = native().get_layernorm_mode()
+    native().set_layernorm_mode(mode)
+    try:
+        torch.manual_seed(H + R)
+        x, res, dy = bf(R, H), bf(R, H), bf(R, H)
+        gbuf = torch.rand(H + 1, device=dev) + 0.5
+        gma, bta = gbuf[1:], torch.randn(H, device=dev)
+        y, mean, rstd, xs = native().layernorm_fwd(x, gma, bta, 1e-5, res)
+        yr, mr, rr, _ = _ref.layernorm_fwd(xs.float(), gma, bta, 1e-5)
+        assert rel_err(xs, x.float() + res.float()) < 1e-2
+        assert rel_err(y, yr) < 1e-2 and rel_err(mean, mr) < 1e-3 and rel_err(rstd, rr) < 1e-3
+        dx, dg, db, _ = native().layernorm_bwd(dy, xs, mean, rstd, gma)
+        dxr, dgr, dbr = _ref.layernorm_bwd(dy.float(), xs.float(), mean, rstd, gma)
+        assert rel_err(dx, dxr) < 2e-2 and rel_err(dg, dgr) < 1e-3 and rel_err(db, dbr) < 1e-3
+        # fused dropout + bias-gradient sum: the dropped branch's gradient and its column sums
+        seed = 1234
+        ydrop = native().layernorm_fwd(x, gma, bta, 1e-5, res, 0.1, seed)
+        x_d = native().dropout_fwd(x, 0.1, seed)
+        assert torch.equal(ydrop[3], (x_d.float() + res.float()).to(torch.bfloat16))
+        dacc = torch.zeros(H, device=dev)
+        gacc, bacc = torch.zeros(H, device=dev), torch.zeros(H, device=dev)
+        dx2, _, _, dxd = native().layernorm_bwd(dy, ydrop[3], ydrop[1], ydrop[2], gma, gacc,
+                                                bacc, 0.1, seed, None, dacc)
+        assert torch.equal(dxd, native().dropout_fwd(dx2, 0.1, seed))
+        assert rel_err(dacc, dxd.float().sum(0)) < 1e-3
+    finally:
+        native().set_layernorm_mode(old)
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 10, 2048), (30, 100, 512), (64, 16, 27)])
