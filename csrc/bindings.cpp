@@ -1093,7 +1093,7 @@ int* ws_tickets(const Tensor& like, long n) {
 
 Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bias,
             std::string act, at::ScalarType out_dtype, optional<Tensor> c, double beta,
-            int64_t plan, optional<Tensor> addend) {
+            int64_t plan, optional<Tensor> addend, optional<std::vector<Tensor>> prefetch) {
   check_act(a, "A");
   check_same(b, a, "B");
   c10::DeviceGuard g(a.device());
@@ -1161,6 +1161,18 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
   // Plans with kPlanWs set.  (Round 3 also timed a hipBLASLt "library plan" here; it is gone:
   // every GEMM of the training step runs on the MFMA kernels, tools/gemm_plans.py.)
   const bool ws_out0 = mode == 0 && act_i == 0 && N % 8 == 0;
+  // another GEMM's cold operands, warmed by this one's blocks (mipipe/ops/prefetch.py)
+  mipipe::TouchRanges pf;
+  if (prefetch.has_value())
+    for (const Tensor& t : *prefetch) {
+      if (pf.count == 2) break;
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.device() == a.device(),
+                  "gemm prefetch: contiguous tensors on the operands' device");
+      if (t.numel() == 0) continue;
+      pf.ptr[pf.count] = static_cast<const uint8_t*>(t.data_ptr());
+      pf.bytes[pf.count++] = (long)(t.numel() * t.element_size());
+    }
+  const mipipe::TouchRanges* pfp = pf.count > 0 ? &pf : nullptr;
   auto launch = [&](void* C, int p) {
     if (p >= 4096) p = -1;  // a round-3 table's library plan: the heuristic MFMA plan
     const bool ws_plan = p >= 0 && (p & tune::kPlanWs) != 0;
@@ -1182,7 +1194,7 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
       fin.bf16 = mode == 2 ? 0 : 1;
       mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b,
                    ws.data_ptr(), N, (int)M, (int)N, (int)K, nullptr, 0, 2, stream(), f32, cfg,
-                   sp, nullptr, true, fin.ticket != nullptr ? &fin : nullptr);
+                   sp, nullptr, true, fin.ticket != nullptr ? &fin : nullptr, nullptr, pfp);
       if (fin.ticket != nullptr) return;  // the GEMM's last split per tile summed the slices
       if (mode == 2)
         mipipe::splitk_sum(ws.data_ptr<float>(), ns, M * N, static_cast<float*>(C), stream());
@@ -1195,7 +1207,8 @@ Tensor gemm(Tensor a, Tensor b, bool trans_a, bool trans_b, optional<Tensor> bia
       return;
     }
     mipipe::gemm(a.data_ptr(), a.stride(0), !trans_a, b.data_ptr(), b.stride(0), trans_b, C, N,
-                 (int)M, (int)N, (int)K, bias_p, act_i, mode, stream(), f32, cfg, sp, add_p);
+                 (int)M, (int)N, (int)K, bias_p, act_i, mode, stream(), f32, cfg, sp, add_p,
+                 false, nullptr, nullptr, pfp);
   };
   if (plan < 0) {
     std::vector<int> cands = tune::gemm_candidates(f32, mode == 2);
@@ -1250,6 +1263,28 @@ std::tuple<Tensor, Tensor> gemm_gelu(Tensor a, Tensor b, optional<Tensor> bias, 
   }
   launch(y.data_ptr(), h.data_ptr(), (int)plan);
   return {y, h};
+}
+
+// Cache warming of GEMM operands (mipipe/ops/prefetch.py): one load per 64-B line of each
+// tensor's bytes on the current stream, nothing written.
+void touch(std::vector<Tensor> ts) {
+  mipipe::TouchRanges r;
+  for (size_t i = 0; i < ts.size(); ++i) {
+    const Tensor& t = ts[i];
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "touch: contiguous GPU tensors");
+    if (t.numel() == 0) continue;
+    r.ptr[r.count] = static_cast<const uint8_t*>(t.data_ptr());
+    r.bytes[r.count] = (long)(t.numel() * t.element_size());
+    if (++r.count == mipipe::kTouchRanges) {
+      c10::DeviceGuard g(t.device());
+      mipipe::touch(r, stream());
+      r.count = 0;
+    }
+  }
+  if (r.count > 0) {
+    c10::DeviceGuard g(ts[0].device());
+    mipipe::touch(r, stream());
+  }
 }
 
 // ------------------------------------------------------------------------------- loss / optim
@@ -2078,7 +2113,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("trans_a"), py::arg("trans_b"),
         py::arg("bias"), py::arg("act"), py::arg("out_dtype"), py::arg("c"), py::arg("beta"),
-        py::arg("plan") = -1, py::arg("addend") = py::none());
+        py::arg("plan") = -1, py::arg("addend") = py::none(),
+        py::arg("prefetch") = py::none());
+  m.def("touch", &touch, py::arg("tensors"));
   m.def("cross_entropy_fwd", &cross_entropy_fwd, py::arg("logits"), py::arg("labels"),
         py::arg("smoothing") = 0.0, py::arg("ignore_index") = -100, py::arg("valid_cols") = -1);
   m.def("cross_entropy_bwd", &cross_entropy_bwd, py::arg("logits"), py::arg("labels"),

@@ -75,6 +75,10 @@ struct EpiParams {
   // MCDenseBufBN)
   const float* in_scale;
   const float* in_bias;
+  // GEMM only: cache warming of the NEXT GEMM's cold operands (mipipe/ops/prefetch.py) — every
+  // block issues one load per 64-B line of its share of these ranges before its main loop
+  const uint8_t* pf_ptr[2];
+  uint32_t pf_lines[2];
 };
 
 // One 64 x 64 (co x ci) transpose of one tap of one parity class's flipped sub-kernel, riding in

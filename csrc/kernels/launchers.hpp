@@ -252,7 +252,10 @@ void avgpool2d_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho,
 void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc, void* C,
           long ldc, int M, int N, int K, const float* bias, int act, int out, hipStream_t st,
           bool f32 = false, int cfg = -1, int splits = -1, const void* addend = nullptr,
-          bool ws_split = false, const WsFinish* fin = nullptr, void* aux = nullptr);
+          bool ws_split = false, const WsFinish* fin = nullptr, void* aux = nullptr,
+          const struct TouchRanges* pf = nullptr);
+// pf: up to 2 byte ranges (another GEMM's cold operands) that this GEMM's blocks warm into the
+// memory-side cache beside their main loop (one load per 64-B line; mipipe/ops/prefetch.py)
 //  act 2 (GELU, bf16 output mode 0): C = gelu(A B + bias) and aux = A B + bias (the
 //  pre-activation the backward needs), both [M][ldc]
 // WsFinish tickets a gemm needs at most: one per output tile of the smallest tile config
@@ -417,6 +420,14 @@ int layernorm_bwd_blocks(long rows);  // partial rows of layernorm_bwd's work
 // 4 / 8 (default) / 16 = the exact-width kernels (chunk width picked so every lane holds whole
 // chunks, DPP wave sums) with that many waves per backward block; the generic kernels still
 // serve the widths the exact ones do not cover (and the 8-wide forward).  MIPIPE_LN_MODE.
+// Cache warming: one load per 64-B line of each range, nothing written (touch_kernel).
+constexpr int kTouchRanges = 4;
+struct TouchRanges {
+  const uint8_t* ptr[kTouchRanges];
+  long bytes[kTouchRanges];
+  int count = 0;
+};
+void touch(const TouchRanges& r, hipStream_t st);
 void set_layernorm_mode(int mode);
 int get_layernorm_mode();
 void gelu_fwd(const void* x, void* y, long n, hipStream_t st);

@@ -27,6 +27,7 @@ import torch
 from torch.autograd import Function
 
 from . import kernels as K
+from . import prefetch as _prefetch
 
 Tensor = torch.Tensor
 
@@ -1002,11 +1003,12 @@ class _LinearFn(Function):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         bk = bias if bias_c is None else bias_c  # bias_c: the kernel's (padded) bias vector
+        pf = _prefetch.before_weight_gemm(w_c)  # the next GEMM's weight, warmed by this one
         if act == "gelu":  # GELU in the GEMM epilogue (h, the pre-activation, saved)
             y, h = K.gemm_gelu(x2.contiguous(), w_c, bk)
             ctx.save_for_backward(x2, w_c, h)
         else:
-            y = K.gemm(x2, w_c, False, True, bk, act, x.dtype)
+            y = K.gemm(x2, w_c, False, True, bk, act, x.dtype, prefetch=pf)
             ctx.save_for_backward(x2, w_c, y if act == "relu" else None)
         ctx.act, ctx.shp, ctx.has_bias = act, shp, bias is not None
         ctx.weight, ctx.bias = weight, bias
@@ -1042,8 +1044,10 @@ class _LinearFn(Function):
             add = ctx.res_take.take() if ctx.res_take is not None else None
             if add is not None:
                 add = add.reshape(-1, add.shape[-1]).to(dy2.dtype).contiguous()
+            # (the weight-grad GEMM below reads the saved input next: warmed by this one)
+            pf = _prefetch.before_weight_gemm(w_c, [x2] if ctx.needs_input_grad[1] else None)
             dx = K.gemm(dy2, w_c, False, False, None, "none", dy2.dtype,
-                        addend=add).reshape(ctx.shp)
+                        addend=add, prefetch=pf).reshape(ctx.shp)
         gdt = torch.float64 if dy2.dtype == torch.float64 else torch.float32
         if ctx.needs_input_grad[1]:
             # w_c may carry more rows than the parameter (vocabulary padded to the tile width):

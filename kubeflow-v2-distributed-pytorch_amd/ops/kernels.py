@@ -308,9 +308,11 @@ def gemm_gelu(x, w, bias=None):
 
 
 def gemm(a, b, trans_a=False, trans_b=False, bias=None, act="none", out_dtype=None, c=None,
-         beta=0.0, addend=None):
+         beta=0.0, addend=None, prefetch=None):
     """act(op(a) @ op(b) + bias) [+ beta * c] [+ addend]; ``addend`` (same shape / dtype as the
-    output; a @ b form, no bias / act) is added in the GEMM epilogue."""
+    output; a @ b form, no bias / act) is added in the GEMM epilogue.  ``prefetch``: up to two
+    tensors (another GEMM's cold operands) this GEMM's blocks warm into the memory-side cache
+    (mipipe/ops/prefetch.py); a hint only, ignored off the native path."""
     if addend is not None:
         M = a.shape[1] if trans_a else a.shape[0]
         N = b.shape[0] if trans_b else b.shape[1]
@@ -321,7 +323,7 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, act="none", out_dtype=No
                    and addend.dtype == a.dtype and addend.is_contiguous())
         if fusable:
             return native().gemm(a, b, False, False, None, "none", a.dtype, None, 0.0, -1,
-                                 addend.reshape(M, N))
+                                 addend.reshape(M, N), prefetch)
         return gemm(a, b, trans_a, trans_b, bias, act, out_dtype, c, beta) + addend.reshape(M, N)
     if use_native(a):
         odt = out_dtype if out_dtype is not None else a.dtype
@@ -330,7 +332,8 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, act="none", out_dtype=No
         N = b.shape[0] if trans_b else b.shape[1]
         r8 = lambda v: (v + 7) // 8 * 8  # noqa: E731
         if M % 8 == 0 and N % 8 == 0 and Kd % 8 == 0:
-            return native().gemm(a, b, trans_a, trans_b, bias, act, odt, c, beta)
+            return native().gemm(a, b, trans_a, trans_b, bias, act, odt, c, beta, -1, None,
+                                 prefetch)
         # odd sizes (e.g. a 10-class head): zero-pad every operand dim to a multiple of 8 —
         # the kernels vectorise 16-byte rows; the pad contributes exact zeros
         Mp, Np, Kp = r8(M), r8(N), r8(Kd)

@@ -158,6 +158,8 @@ class FlatParamSpace:
                 p.grad = self.grad_view(p)
 
     def zero_grad(self) -> None:
+        from mipipe.ops import prefetch  # a step starts: GEMM operand prefetch (ops/prefetch.py)
+        prefetch.step_boundary()
         self.flat_grad.zero_()
         self.ensure_grad_views()
 
