@@ -1005,7 +1005,7 @@ class _LinearFn(Function):
         bk = bias if bias_c is None else bias_c  # bias_c: the kernel's (padded) bias vector
         pf = _prefetch.before_weight_gemm(w_c)  # the next GEMM's weight, warmed by this one
         if act == "gelu":  # GELU in the GEMM epilogue (h, the pre-activation, saved)
-            y, h = K.gemm_gelu(x2.contiguous(), w_c, bk)
+            y, h = K.gemm_gelu(x2.contiguous(), w_c, bk, prefetch=pf)
             ctx.save_for_backward(x2, w_c, h)
         else:
             y = K.gemm(x2, w_c, False, True, bk, act, x.dtype, prefetch=pf)

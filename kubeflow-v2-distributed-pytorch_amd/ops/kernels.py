@@ -298,12 +298,13 @@ def gemm_gelu_ok(x, w) -> bool:
             and x.is_contiguous() and w.is_contiguous())
 
 
-def gemm_gelu(x, w, bias=None):
+def gemm_gelu(x, w, bias=None, prefetch=None):
     """(gelu(x @ w^T + bias), x @ w^T + bias): the GELU Linear forward with the activation in
-    the GEMM epilogue (the pre-activation is the backward's saved tensor)."""
+    the GEMM epilogue (the pre-activation is the backward's saved tensor).  ``prefetch``: as
+    :func:`gemm` (the two-launch form only)."""
     if gemm_gelu_ok(x, w):
         return native().gemm_gelu(x, w, bias)
-    h = gemm(x, w, False, True, bias, "none", x.dtype)
+    h = gemm(x, w, False, True, bias, "none", x.dtype, prefetch=prefetch)
     return gelu_fwd(h), h
 
 
