@@ -81,6 +81,28 @@ struct EpiParams {
   uint32_t pf_lines[2];
 };
 
+// Cache warming (EpiParams::pf_*): block b of nb issues one 4-B load per 64-B line of its share of
+// each range, before its main loop; the returned sum goes to pf_sink after the epilogue, which
+// stores it (to LDS) only under a condition the host never sets — keeping the loads alive.
+template <int THREADS>
+__device__ __forceinline__ uint32_t pf_issue(const EpiParams& e, uint32_t b, uint32_t nb) {
+  uint32_t acc = 0;
+  if (e.pf_lines[0] != 0) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint32_t per = (e.pf_lines[r] + nb - 1) / nb;
+      const uint32_t l1 = min(e.pf_lines[r], (b + 1) * per);
+      for (uint32_t l = b * per + threadIdx.x; l < l1; l += THREADS)
+        acc += *reinterpret_cast<const uint32_t*>(e.pf_ptr[r] + ((size_t)l << 6));
+    }
+  }
+  return acc;
+}
+__device__ __forceinline__ void pf_sink(const EpiParams& e, uint32_t acc, char* smem) {
+  if (acc == 0x2545F491u && e.pf_lines[1] == 0xFFFFFFFFu)  // (lines are capped at 2^31 - 1)
+    reinterpret_cast<uint32_t*>(smem)[threadIdx.x] = acc;
+}
+
 // One 64 x 64 (co x ci) transpose of one tap of one parity class's flipped sub-kernel, riding in
 // a conv forward launch (the work of conv_dgrad.hip's conv_weight_flip_kernel).
 template <class T, int THREADS>
@@ -845,4 +867,6 @@ __device__ void epilogue_f32(char* smem, f32x4 (&acc)[BM / WM / 16][BN / WN / 16
 }
 
 }  // namespace gk
+// host: copy cache-warming ranges into a GEMM launch's params (gemm.hip)
+void set_prefetch(gk::EpiParams& e, const TouchRanges* pf);
 }  // namespace mipipe

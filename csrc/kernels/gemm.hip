@@ -34,6 +34,19 @@ long g_nt_min_bytes = [] {
   return (long)(v != nullptr ? atof(v) : 0.0) * (1l << 20);
 }();
 int g_ns1_max_k = 512;  // measured: tools/sweep_ns1.py (profiles/r1_ns1_sweep.jsonl)
+// (e.pf_lines[1] == 0xFFFFFFFF would enable pf_sink's store: lines are capped below it)
+void set_prefetch(gk::EpiParams& e, const TouchRanges* pf) {
+  if (pf == nullptr) return;
+  for (int r = 0; r < 2 && r < pf->count; ++r) {
+    e.pf_ptr[r] = pf->ptr[r];
+    e.pf_lines[r] = (uint32_t)std::min<long>(pf->bytes[r] >> 6, 0x7FFFFFFF);
+  }
+  if (e.pf_lines[0] == 0) {  // keep "range 0 empty" meaning "no prefetch"
+    e.pf_ptr[0] = e.pf_ptr[1];
+    e.pf_lines[0] = e.pf_lines[1];
+    e.pf_lines[1] = 0;
+  }
+}
 namespace gk {
 
 __device__ __attribute__((aligned(64))) uint4 g_gemm_zero[8];
@@ -63,19 +76,9 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void gemm_dense_ker
   const int kt1 = min(nk, kt0 + kt_per_split);
   auto ia = [&](auto& a, uint32_t origin) { a.init(A, lda, e.M, K, origin, wave, lane, g_gemm_zero); };
   auto ib = [&](auto& b, uint32_t origin) { b.init(B, ldb, e.N, K, origin, wave, lane, g_gemm_zero); };
-  // cache warming for the next GEMM (e.pf_*): issued first, so the loads overlap this block's
-  // main loop; their sum is stored only under an impossible condition (keeps them alive)
-  uint32_t pf_acc = 0;
-  if (e.pf_lines[0] != 0) {
-    const uint32_t nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const uint32_t per = (e.pf_lines[r] + nb - 1) / nb;
-      const uint32_t l1 = min(e.pf_lines[r], (b + 1) * per);
-      for (uint32_t l = b * per + threadIdx.x; l < l1; l += C::THREADS)
-        pf_acc += *reinterpret_cast<const uint32_t*>(e.pf_ptr[r] + ((size_t)l << 6));
-    }
-  }
+  // cache warming for the next GEMM (e.pf_*): issued first, so the loads overlap the main loop
+  const uint32_t pf_acc =
+      pf_issue<C::THREADS>(e, blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   f32x4 acc[BM / C::WM / 16][BN / C::WN / 16];
   run_main_loop<T, C, PA, PB, kGemmLoop>(smem, ia, ib, m0, n0, kt0, kt1, acc, wave, lane);
   if constexpr (OUT == 0)
@@ -84,8 +87,7 @@ __global__ __launch_bounds__(C::THREADS, (conv_occ<T, C>())) void gemm_dense_ker
     epilogue_out<BM, BN, true, T, C::WM, C::WN, false, C::PP>(smem, acc, e, m0, n0, 0, wave, lane);
   else
     epilogue_f32<BM, BN, OUT == 2, C::WM, C::WN, C::PP>(smem, acc, e, m0, n0, wave, lane);
-  if (pf_acc == 0x2545F491u && e.pf_lines[1] == 0xFFFFFFFFu)
-    reinterpret_cast<uint32_t*>(smem)[threadIdx.x] = pf_acc;
+  pf_sink(e, pf_acc, smem);
 }
 
 }  // namespace gk
@@ -187,17 +189,7 @@ void gemm(const void* A, long lda, bool a_kc, const void* B, long ldb, bool b_kc
           bool f32, int cfg, int splits, const void* addend, bool ws_split, const WsFinish* fin,
           void* aux, const TouchRanges* pf) {
   EpiParams e{};
-  if (pf != nullptr) {  // (e.pf_lines[1] == 0xFFFFFFFF would enable the sink store: capped)
-    for (int r = 0; r < 2 && r < pf->count; ++r) {
-      e.pf_ptr[r] = pf->ptr[r];
-      e.pf_lines[r] = (uint32_t)std::min<long>(pf->bytes[r] >> 6, 0x7FFFFFFF);
-    }
-    if (e.pf_lines[0] == 0) {  // keep "range 0 empty" meaning "no prefetch"
-      e.pf_ptr[0] = e.pf_ptr[1];
-      e.pf_lines[0] = e.pf_lines[1];
-      e.pf_lines[1] = 0;
-    }
-  }
+  set_prefetch(e, pf);
   e.C = C; e.ldc = ldc; e.M = (uint32_t)M; e.N = (uint32_t)N; e.bias = bias; e.act = act;
   if (act == 2) {  // GELU: bf16 activation output with the pre-activation in aux
     e.act = 0;
