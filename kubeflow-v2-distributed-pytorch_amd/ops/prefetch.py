@@ -18,6 +18,11 @@ a new recording.  Same-stream and in-kernel: no fork / join, so nothing changes 
 capture.  (A side-stream touch kernel was tried first: ROCm serialised the graph's branches and
 BERT-base lost 17 %, ``profiles/r6_prefetch_side_stream_negative.txt``.)
 
+Handing saved tensors forward as well (the GELU pre-activation, the attention's packed q/k/v, a
+LayerNorm's input, each warmed by the weight-grad GEMM that runs right before its backward) made
+those hosting GEMMs slower than the backward kernels gained: 4,720 vs 4,849 seq/s without it, same
+box (``profiles/r6_prefetch_handover_negative.txt``).
+
 ``MIPIPE_PREFETCH=0`` disables it.
 """
 from __future__ import annotations
@@ -92,8 +97,9 @@ def before_weight_gemm(w: torch.Tensor,
     _S.cursor = i + 1
     if not enabled() or not w.is_cuda:
         return None
-    nxt = list(also) if also else []
+    nxt = list(also) if also and _MODE != "w0" else []  # ("w0": weights only, for A/Bs)
     if i + 1 < len(_S.order) and i + 1 not in _S.volatile:
         nxt.append(_S.order[i + 1])
     nxt = [t for t in nxt if t is not None and t.is_contiguous() and t.numel()]
     return nxt[:2] or None
+
