@@ -152,14 +152,36 @@ int select_from(const std::string& k, const std::vector<int>& cands, F&& run) {
   int best = -1;
   float best_ms = 1e30f;
   std::string log;
+  // MIPIPE_TUNE_COLD=1: time every launch after a 512 MB sweep of the caches (operands as cold as
+  // in a training step, where most were last touched a pass earlier) instead of back-to-back
+  static const bool cold = [] {
+    const char* v = getenv("MIPIPE_TUNE_COLD");
+    return v != nullptr && atoi(v) != 0;
+  }();
+  static void* sweep = nullptr;
+  constexpr size_t kSweep = 512u << 20;
+  if (cold && sweep == nullptr && hipMalloc(&sweep, kSweep) != hipSuccess) sweep = nullptr;
   for (int cfg : cands) {
     run(cfg);  // warm (first launch of a kernel object loads its code)
-    hipEventRecord(e0, st);
-    for (int r = 0; r < g_reps; ++r) run(cfg);
-    hipEventRecord(e1, st);
-    hipEventSynchronize(e1);
     float ms = 0.f;
-    hipEventElapsedTime(&ms, e0, e1);
+    if (cold && sweep != nullptr) {
+      for (int r = 0; r < g_reps; ++r) {
+        hipMemsetAsync(sweep, r, kSweep, st);
+        hipEventRecord(e0, st);
+        run(cfg);
+        hipEventRecord(e1, st);
+        hipEventSynchronize(e1);
+        float t = 0.f;
+        hipEventElapsedTime(&t, e0, e1);
+        ms += t;
+      }
+    } else {
+      hipEventRecord(e0, st);
+      for (int r = 0; r < g_reps; ++r) run(cfg);
+      hipEventRecord(e1, st);
+      hipEventSynchronize(e1);
+      hipEventElapsedTime(&ms, e0, e1);
+    }
     ms /= (float)g_reps;
     if (g_verbose) log += " " + std::to_string(cfg) + ":" + std::to_string(ms * 1e3f).substr(0, 7);
     if (ms < best_ms) {
