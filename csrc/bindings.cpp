@@ -1618,7 +1618,9 @@ Tensor embedding_bwd(Tensor dy, Tensor idx, int64_t num_rows, optional<Tensor> o
   const bool pre = sorted_ids.has_value();
   const bool det = ordered || mipipe::g_deterministic || pre;
   TORCH_CHECK(scale == 1.0 || det, "embedding_bwd: scale needs the ordered path");
-  if (det && n > 0) {
+  // tables of <= 8 rows: per-block partial tables summed in block order, in every mode (cheaper
+  // than 256 blocks' atomics onto the same few rows, and deterministic anyway)
+  if ((det || num_rows <= 8) && n > 0) {
     auto dyc = dy.contiguous();
     if (num_rows <= 8 && !pre) {
       auto part = torch::empty({mipipe::embedding_bwd_small_blocks(n), num_rows * H},

@@ -1034,8 +1034,74 @@ __global__ __launch_bounds__(256) void embedding_bwd_sorted_fix_kernel(
   emb_add_row<NC>(out + id * H, acc, lane, nch, scale);
 }
 
+// Tables of <= kEmbSmallRows rows (BERT's token types: 2) with H % 8 == 0: each thread owns one
+// 8-column chunk of every table row in registers and walks its token stream (tokens t0 + s,
+// t0 + s + S, ...: 256 / (H/8) streams per block) with 16-B loads — no LDS atomics — then the
+// streams are added into the block's table in stream order (deterministic) and written out as
+// in embedding_bwd_small_kernel.  BERT-base 4096 x 768: 36.4 us (LDS atomics) -> 14.7 us with
+// 128 blocks (profiles/r6_bert_emb_tiny.txt).
+__global__ __launch_bounds__(256) void embedding_bwd_tiny_kernel(
+    const __bf16* __restrict__ dy, const int64_t* __restrict__ idx, float* __restrict__ out,
+    long n, int H, int rows, long tok_per_block, float* __restrict__ partial) {
+  extern __shared__ float tab[];  // [rows][H]
+  const int nc8 = H / 8, S = 256 / nc8;
+  const int s = threadIdx.x / nc8, c8 = threadIdx.x - s * nc8;
+  const bool act = s < S;
+  float acc[kEmbSmallRows][8];
+#pragma unroll
+  for (int r = 0; r < kEmbSmallRows; ++r)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[r][q] = 0.f;
+  const long t0 = (long)blockIdx.x * tok_per_block, t1 = min(n, t0 + tok_per_block);
+  if (act) {
+    long t = t0 + s;
+    for (; t + S < t1; t += 2 * S) {  // two tokens' loads in flight
+      const long r0 = idx[t], r1 = idx[t + S];
+      const uint4 u0 = *reinterpret_cast<const uint4*>(dy + t * H + c8 * 8);
+      const uint4 u1 = *reinterpret_cast<const uint4*>(dy + (t + S) * H + c8 * 8);
+      float v0[8], v1[8];
+      unpack8(u0, v0);
+      unpack8(u1, v1);
+#pragma unroll
+      for (int rr = 0; rr < kEmbSmallRows; ++rr)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          acc[rr][q] += r0 == rr ? v0[q] : 0.f;
+          acc[rr][q] += r1 == rr ? v1[q] : 0.f;
+        }
+    }
+    if (t < t1) {
+      const long r = idx[t];
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + t * H + c8 * 8), v);
+#pragma unroll
+      for (int rr = 0; rr < kEmbSmallRows; ++rr)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[rr][q] += r == rr ? v[q] : 0.f;
+    }
+  }
+  for (int i = threadIdx.x; i < rows * H; i += 256) tab[i] = 0.f;
+  __syncthreads();
+  for (int ss = 0; ss < S; ++ss) {  // streams added in order
+    if (act && s == ss) {
+#pragma unroll
+      for (int rr = 0; rr < kEmbSmallRows; ++rr)
+        if (rr < rows)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) tab[rr * H + c8 * 8 + q] += acc[rr][q];
+    }
+    __syncthreads();
+  }
+  if (partial != nullptr) {
+    float* dst = partial + (long)blockIdx.x * rows * H;
+    for (int i = threadIdx.x; i < rows * H; i += 256) dst[i] = tab[i];
+  } else {
+    for (int i = threadIdx.x; i < rows * H; i += 256) atomicAdd(out + i, tab[i]);
+  }
+}
+
 int embedding_bwd_small_blocks(long n) {
-  const long G = std::max<long>(1, std::min<long>(256, (n + 31) / 32));
+  const long G = std::max<long>(1, std::min<long>(256, (n + 15) / 16));
   const long per = (n + G - 1) / G;
   return (int)((n + per - 1) / per);
 }
@@ -1045,9 +1111,14 @@ void embedding_bwd(const void* dy, const int64_t* idx, float* out, long n, int H
   if (rows > 0 && rows <= kEmbSmallRows) {
     const int G = embedding_bwd_small_blocks(n);
     const long per = (n + G - 1) / G;
-    hipLaunchKernelGGL(embedding_bwd_small_kernel, dim3((unsigned)G), dim3(256),
-                       (size_t)rows * H * 4, st, (const __bf16*)dy, idx, out, n, H, rows, per,
-                       partial);
+    if (H % 8 == 0 && H / 8 <= 256)
+      hipLaunchKernelGGL(embedding_bwd_tiny_kernel, dim3((unsigned)G), dim3(256),
+                         (size_t)rows * H * 4, st, (const __bf16*)dy, idx, out, n, H, rows, per,
+                         partial);
+    else
+      hipLaunchKernelGGL(embedding_bwd_small_kernel, dim3((unsigned)G), dim3(256),
+                         (size_t)rows * H * 4, st, (const __bf16*)dy, idx, out, n, H, rows, per,
+                         partial);
     if (partial != nullptr) det_sum_rows(partial, nullptr, G, rows * H, out, nullptr, true, st);
     return;
   }
