@@ -245,8 +245,14 @@ class BertForMaskedLM(tnn.Module):
             return _seed(base, self._step, site)
 
         ids = input_ids.reshape(-1)
-        pos = torch.arange(S, device=ids.device).repeat(B)
-        tt = torch.zeros_like(ids) if token_type_ids is None else token_type_ids.reshape(-1)
+        # position / default token-type ids per batch shape, made once (3 fewer launches a step)
+        key = (B, S, ids.device)
+        pc = getattr(self, "_ids_cache", None)
+        if pc is None or pc[0] != key:
+            pc = (key, torch.arange(S, device=ids.device).repeat(B), torch.zeros_like(ids))
+            self._ids_cache = pc
+        pos = pc[1]
+        tt = pc[2] if token_type_ids is None else token_type_ids.reshape(-1)
         w = emb.word_embeddings(ids, dt)
         pt = emb.position_embeddings(pos, dt) + emb.token_type_embeddings(tt, dt)
         h = emb.LayerNorm(w, residual=pt)
