@@ -92,8 +92,12 @@ def before_weight_gemm(w: torch.Tensor,
         return None
     if o.data_ptr() != w.data_ptr():
         # a weight operand made per step (a cast of a parameter outside the flat space): the
-        # slot stays, never prefetched
+        # slot stays, never prefetched.  Most slots moving means another model of the same
+        # shapes: record again (and drop the old weights)
         _S.volatile.add(i)
+        if len(_S.volatile) > len(_S.order) // 2:
+            _S.armed, _S.order, _S.volatile = False, [], set()
+            return None
     _S.cursor = i + 1
     if not enabled() or not w.is_cuda:
         return None

@@ -98,6 +98,8 @@ class FlatParamSpace:
             _REGISTRY[id(p)] = self
         self._synced_version = -1
         self.refresh_shadow()
+        from mipipe.ops import prefetch  # a new model: its GEMM weight order is recorded anew
+        prefetch.reset()
         self._bound_modules: List[weakref.ref] = []
         self._ready_listeners: List = []
 

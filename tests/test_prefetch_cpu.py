@@ -57,3 +57,19 @@ def test_disabled_mode_still_keeps_the_order(monkeypatch):
     _step(ws)
     _step(ws)
     assert not prefetch.enabled() and prefetch._S.armed
+
+
+def test_new_flat_space_and_moved_weights_rerecord():
+    from mipipe.optim.flat import FlatParamSpace
+    ws = [torch.zeros(4, 8), torch.zeros(8, 8), torch.zeros(8, 2)]
+    _step(ws)
+    _step(ws)
+    assert prefetch._S.armed
+    FlatParamSpace([torch.nn.Parameter(torch.zeros(3))])  # another model's optimizer
+    assert not prefetch._S.armed and prefetch._S.order == []
+    _step(ws)
+    _step(ws)
+    assert prefetch._S.armed
+    # the same shapes at new addresses (another model): most slots move -> record again
+    _step([torch.zeros(4, 8), torch.zeros(8, 8), torch.zeros(8, 2)])
+    assert not prefetch._S.armed and prefetch._S.order == []
