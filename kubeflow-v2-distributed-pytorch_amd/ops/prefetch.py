@@ -104,6 +104,8 @@ def before_weight_gemm(w: torch.Tensor,
     nxt = list(also) if also and _MODE != "w0" else []  # ("w0": weights only, for A/Bs)
     if i + 1 < len(_S.order) and i + 1 not in _S.volatile:
         nxt.append(_S.order[i + 1])
-    nxt = [t for t in nxt if t is not None and t.is_contiguous() and t.numel()]
+    # (a model split over devices: only tensors on this GEMM's device can be warmed by it)
+    nxt = [t for t in nxt
+           if t is not None and t.device == w.device and t.is_contiguous() and t.numel()]
     return nxt[:2] or None
 
